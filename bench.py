@@ -1,0 +1,235 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X path tracer on BASELINE.json's headline config.
+
+Metric: Mrays/s at 1920x1080, 8 bounces (C2: Cornell box, 5 quads + 2 spheres, 64 spp per frame),
+with the per-pixel RMSE vs the CPU oracle (reference semantics) reported beside it.
+
+One step = one 64-spp frame of C2 rendered by the HIP megakernel (one launch per GPU) — the pixel
+rows are dealt cyclically over the N ranks (one process per GPU) and, for N > 1, the float4
+accumulators are gathered to rank 0 over RCCL (torch.distributed "nccl") and de-interleaved.
+Total work is the fixed 1080p frame, so scaling is strong. value = closest-hit queries traced by all
+ranks in the K timed steps / the max over ranks of the timed wall time.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--config c2]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO / "path-tracer-and-rasterizer-engine_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import iqpt  # noqa: E402
+from iqpt import dist as iqdist  # noqa: E402
+from iqpt.scene import CONFIGS, Scene, make_camera, packet_stats  # noqa: E402
+
+FP32_PEAK_TFLOPS = 157.3        # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="c2")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--verify-rows", type=int, default=16)
+    ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r01_pmc_traffic.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(cfg, pk, cam, seconds: float) -> dict:
+    """The oracle (reference restated as a host loop, OpenMP) on the same scene: full-frame 1-spp
+    passes until `seconds` of wall time (Mrays/s does not depend on spp)."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle  # cpu_baseline leg only
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    fr = oracle.OracleFrame(cfg.width, cfg.height, max_depth=cfg.max_depth)
+    rays = 0
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        rays += fr.render(pk, cam, 1, threads=threads)
+        passes += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            break
+    return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"{passes} full {cfg.width}x{cfg.height} 1-spp passes of {cfg.preset} "
+                      f"(max_depth {cfg.max_depth}) in {dt:.1f} s, {rays} rays"}
+
+
+def verify_vs_oracle(cfg, pk, cam, lin_rank, rank, world, nrows) -> dict:
+    """After the first 64-spp frame: compare a band of this rank's rows with the oracle."""
+    sys.path.insert(0, str(REPO / "oracle"))
+    import oracle
+    y_band = int(cfg.height * 0.46)                     # through both spheres
+    first = y_band + ((rank - y_band) % world)          # first row >= y_band owned by this rank
+    k0 = (first - rank) // world
+    ps = iqpt.pixel_set(cfg.width, cfg.height, 0, cfg.width, first, world, nrows)
+    fr = oracle.OracleFrame(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
+    fr.render(pk, cam, cfg.spp)
+    mine = lin_rank.reshape(-1, cfg.width, 4)[k0:k0 + nrows].reshape(-1, 4)
+    a = mine[:, :3].astype(np.float64)
+    b = fr.lin[:, :3].astype(np.float64)
+    rmse = float(np.sqrt(np.mean((a - b) ** 2)))
+    same = np.all(mine[:, :3].view(np.uint32) == fr.lin[:, :3].view(np.uint32), axis=1)
+    return {"rmse": rmse, "bitexact_frac": float(same.mean()), "pixels": int(mine.shape[0])}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    cfg = CONFIGS[args.config]
+    scene = Scene()
+    scene.add_preset(cfg.preset)
+    pk = scene.build_packet()
+    stats = packet_stats(pk)
+    cam = make_camera(cfg.width, cfg.height)
+    ps = iqdist.pixel_set_for_rank(cfg.width, cfg.height, rank, world)
+    pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth, device=local_rank)
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+
+    max_px = iqdist.max_rows(cfg.height, world) * cfg.width
+    accum = torch.zeros((max_px, 4), dtype=torch.float32, device="cuda") if world > 1 else None
+    gather_list = ([torch.empty_like(accum) for _ in range(world)] if (world > 1 and rank == 0) else None)
+    frame = None
+
+    def step():
+        nonlocal frame
+        pt.render(cfg.spp)
+        if world > 1:
+            pt.copy_accum_device(accum.data_ptr(), accum.numel() * 4)
+            dist.gather(accum, gather_list, dst=0)
+            if rank == 0:
+                frame = iqdist.assemble(gather_list, cfg.width, cfg.height, world)
+
+    # warmup (the first frame is also checked against the oracle)
+    verify = None
+    for i in range(max(1, args.warmup)):
+        step()
+        if i == 0 and args.verify_rows > 0:
+            lin, _ = pt.read()
+            verify = verify_vs_oracle(cfg, pk, cam, lin, rank, world, min(args.verify_rows, ps.nrows))
+    torch.cuda.synchronize()
+    barrier()
+    rays0 = pt.rays()
+    pt.kernel_time()                                   # discard warmup timings
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    pt.sync()
+    torch.cuda.synchronize()
+    barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    rays = pt.rays() - rays0
+    kern_ms, launches = pt.kernel_time()
+
+    vals = torch.tensor([elapsed, float(rays), kern_ms / max(1, launches), verify["rmse"] if verify else 0.0,
+                         verify["bitexact_frac"] if verify else 1.0], dtype=torch.float64, device="cuda")
+    if world > 1:
+        t_max = vals[0:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        tot = vals[1:2].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        kmax = vals[2:3].clone()
+        dist.all_reduce(kmax, op=dist.ReduceOp.MAX)
+        rmse = vals[3:4].clone()
+        dist.all_reduce(rmse, op=dist.ReduceOp.MAX)
+        bx = vals[4:5].clone()
+        dist.all_reduce(bx, op=dist.ReduceOp.MIN)
+        elapsed, total_rays, kern_avg_ms = t_max.item(), tot.item(), kmax.item()
+        rmse_v, bitexact = rmse.item(), bx.item()
+    else:
+        total_rays, kern_avg_ms = float(rays), kern_ms / max(1, launches)
+        rmse_v, bitexact = (verify["rmse"], verify["bitexact_frac"]) if verify else (None, None)
+
+    if rank == 0:
+        mrays = total_rays / elapsed / 1e6
+        rays_per_launch = float(rays) / max(1, args.steps)           # rank 0's kernel
+        f_ray = cfg.flops_per_ray
+        achieved_tflops = f_ray * rays_per_launch / (kern_avg_ms * 1e-3) / 1e12 if kern_avg_ms > 0 else 0.0
+        traffic = None
+        pmc_path = Path(args.pmc_json)
+        if pmc_path.exists():
+            try:
+                pmc = json.loads(pmc_path.read_text())
+                if pmc.get("config") == cfg.name and world == 1:
+                    traffic = pmc.get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        samples = cfg.width * cfg.height * cfg.spp * args.steps
+        out = {
+            "metric": "Mrays/sec at 1920x1080 8-bounce; per-pixel RMSE vs reference",
+            "value": round(mrays, 3),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural Cornell-box scene of SURVEY.md §8d, seed 1984)",
+            "config": {"workload": f"{cfg.name}:{cfg.preset}", "width": cfg.width, "height": cfg.height,
+                       "spp_per_step": cfg.spp, "max_depth": cfg.max_depth, "triangles": stats["triangles"],
+                       "spheres": stats["spheres"], "partition": f"cyclic rows x{world}",
+                       "collective": "rccl gather of float4 accumulators" if world > 1 else "none"},
+            "msamples_per_s": round(samples / elapsed / 1e6, 3),
+            "rays_per_sample": round(total_rays / samples, 5),
+            "rmse_vs_oracle": rmse_v,
+            "bitexact_frac_vs_oracle": bitexact,
+            "roofline": {
+                "bound": "valu",
+                "achieved": round(achieved_tflops, 4),
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 5),
+                "traffic": traffic,
+                "kernel": iqpt.kernel_name(),
+                "kernel_avg_ms": round(kern_avg_ms, 4),
+                "flops_per_ray": f_ray,
+                "note": "algorithmic FLOPs F_ray = 52 T + 19 S (SURVEY.md §8d) x rays per launch / HIP-event "
+                        "kernel time; FP32 vector peak (no MFMA: nothing here is a dense contraction)",
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(cfg, pk, cam, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    pt.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,523 @@
+// iqpt_kernels.hip — the MI355X (gfx950, CDNA4, wave64) path-tracing megakernel and RNG init.
+//
+// Replaces render_kernel + path_tracer::ray_color + renderer_init_kernel of IoniqRE
+// (path_tracer.cu:36-46, 231-366) and the device code they inline (camera.cu:20-43,
+// shape.cu:13-103, material.cu:5-57, onb.h, random.cu:66-107, cuRAND XORWOW).
+//
+// Design:
+//  * Persistent grid, one lane = one pixel at a time. A lane runs ALL of its pixel's samples of
+//    the launch back to back (a pixel's samples are sequential in its XORWOW stream: each sample
+//    consumes a data-dependent number of draws), regenerating a camera ray as soon as a path ends,
+//    so every iteration of the loop traces one ray per live lane and the intersection loop never
+//    idles on dead paths. Lanes that finish their pixel refill from a global pixel queue: one
+//    atomic per 64-pixel chunk per wave, handed out to the empty lanes with a wave64
+//    __ballot + mbcnt prefix sum (compaction of live work across waves and pixels).
+//  * The scene is pre-transformed to world space at upload (the six per-ray transforms and the
+//    per-drawcall normal-matrix inverse of path_tracer.cu:257-270 are ray-independent); the
+//    triangles (48 B: v0, e1, e2) and spheres (16 B) are staged in LDS and read by broadcast. When
+//    the scene exceeds the LDS budget it is streamed in batches behind workgroup barriers.
+//  * The reference's scatter_record stack (path_tracer.cu:243, 321-324) is a register shift
+//    register: under the reference materials every non-terminal record is an Oren-Nayar scatter
+//    whose (attenuation * cos/pdf) is the same in x, y and z, so a record is one float and the
+//    backward product keeps its exact evaluation order.
+//  * Every floating-point operation follows the reference's order with contraction off
+//    (-ffp-contract=off) and the shared transcendentals of iq_fp.h: results are bit-identical to
+//    the CPU oracle (tests/test_gpu_parity.py).
+#include <hip/hip_runtime.h>
+
+#include "iq_fp.h"
+#include "iq_xorwow.h"
+#include "iqpt_internal.hpp"
+
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
+namespace iqpt {
+namespace {
+
+constexpr float kTMin = 0.000001f;       // path_tracer.cu:241
+constexpr float kTMax = 999.99f;
+constexpr int kHitNone = 0, kHitTri = 1, kHitSphere = 2;
+
+struct rng6 {
+    uint32_t v0, v1, v2, v3, v4, d;
+};
+
+__device__ __forceinline__ uint32_t xorwow_next(rng6& s) {     // cuRAND curand() (iq_xorwow.h)
+    const uint32_t t = s.v0 ^ (s.v0 >> 2);
+    s.v0 = s.v1;
+    s.v1 = s.v2;
+    s.v2 = s.v3;
+    s.v3 = s.v4;
+    s.v4 = (s.v4 ^ (s.v4 << 4)) ^ (t ^ (t << 1));
+    s.d += IQ_XORWOW_WEYL;
+    return s.v4 + s.d;
+}
+
+// random::real(state, lo, hi) (random.cu:66-70): u * (hi - lo) + lo with u = curand / 2^32.
+__device__ __forceinline__ float rand_real(rng6& s, float lo, float hi) {
+    const float u = iq_u32_to_unit(xorwow_next(s));
+    return u * (hi - lo) + lo;
+}
+
+// dot4(v, column c of M) of iqvec::transformed (vector.h:371-383); M row-major m[r][c].
+__device__ __forceinline__ float dot_col(float x, float y, float z, float w, const float* M, int c) {
+    return ((x * M[c] + y * M[4 + c]) + z * M[8 + c]) + w * M[12 + c];
+}
+
+// normalized3 (vector.h:239-244) in place.
+__device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
+    if (iq_fabsf(x) < 0.00001f && iq_fabsf(y) < 0.00001f && iq_fabsf(z) < 0.00001f) {
+        x = 0.0f;
+        y = 0.0f;
+        z = 0.0f;
+        return;
+    }
+    const float len = iq_sqrtf((x * x + y * y) + z * z);
+    const float inv = 1.0f / len;
+    x = x * inv;
+    y = y * inv;
+    z = z * inv;
+}
+
+struct ray3 {
+    float ox, oy, oz, dx, dy, dz;
+};
+
+// camera::get_ray (camera.cu:20-43): x jitter drawn first, then y.
+__device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_t y, rng6& s, ray3& r) {
+    const float jx = rand_real(s, -0.5f, 0.5f);
+    const float x_ndc = (((float)x + jx) / (float)p.width) * 2.0f - 1.0f;
+    const float jy = rand_real(s, -0.5f, 0.5f);
+    const float y_ndc = 1.0f - (((float)y + jy) / (float)p.height) * 2.0f;
+    const float* P = p.inv_proj;
+    const float* Vw = p.inv_view;
+    // near point (x, y, 0, 1) and far point (x, y, 1, 1) through inv_proj, then /w (vector.h:100-103)
+    float nx = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 0);
+    float ny = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 1);
+    float nz = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 2);
+    const float nw = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 3);
+    const float ninv = 1.0f / nw;
+    nx = nx * ninv;
+    ny = ny * ninv;
+    nz = nz * ninv;
+    float fx = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 0);
+    float fy = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 1);
+    float fz = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 2);
+    const float fw = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 3);
+    const float finv = 1.0f / fw;
+    fx = fx * finv;
+    fy = fy * finv;
+    fz = fz * finv;
+    // to world space: usage POINT forces w = 1 (vector.h:374)
+    const float wnx = dot_col(nx, ny, nz, 1.0f, Vw, 0);
+    const float wny = dot_col(nx, ny, nz, 1.0f, Vw, 1);
+    const float wnz = dot_col(nx, ny, nz, 1.0f, Vw, 2);
+    const float wfx = dot_col(fx, fy, fz, 1.0f, Vw, 0);
+    const float wfy = dot_col(fx, fy, fz, 1.0f, Vw, 1);
+    const float wfz = dot_col(fx, fy, fz, 1.0f, Vw, 2);
+    float dx = wfx - wnx, dy = wfy - wny, dz = wfz - wnz;
+    normalize3(dx, dy, dz);
+    r.ox = wnx;
+    r.oy = wny;
+    r.oz = wnz;
+    r.dx = dx;
+    r.dy = dy;
+    r.dz = dz;
+}
+
+// CUDA float -> uint8_t: NaN -> 0, saturating, truncating (path_tracer.cu:361-363).
+__device__ __forceinline__ uint32_t to_u8(float f) {
+    if (!(f > 0.0f)) return 0u;
+    if (f >= 255.0f) return 255u;
+    return (uint32_t)f;
+}
+
+// Möller–Trumbore of shape.cu:62-103 with the hit bookkeeping reduced to (t, index); every reject
+// test is the reference's condition, negated, so NaN behaves identically.
+__device__ __forceinline__ void test_triangle(const float4 a, const float4 b, const float4 c,
+                                              const ray3& r, float& closest, int& kind,
+                                              uint32_t& idx, uint32_t k) {
+    const float e1x = a.w, e1y = b.x, e1z = b.y;
+    const float e2x = b.z, e2y = b.w, e2z = c.x;
+    const float px = r.dy * e2z - r.dz * e2y;                   // dir x v0v2
+    const float py = r.dz * e2x - r.dx * e2z;
+    const float pz = r.dx * e2y - r.dy * e2x;
+    const float det = (e1x * px + e1y * py) + e1z * pz;
+    if (iq_fabsf(det) < 0.000001f) return;                      // is_zero(fabs(det))
+    const float inv = 1.0f / det;
+    const float tx = r.ox - a.x, ty = r.oy - a.y, tz = r.oz - a.z;
+    const float u = ((tx * px + ty * py) + tz * pz) * inv;
+    if (u < 0.0f || u > 1.0f) return;
+    const float qx = ty * e1z - tz * e1y;                       // tvec x v0v1
+    const float qy = tz * e1x - tx * e1z;
+    const float qz = tx * e1y - ty * e1x;
+    const float v = ((r.dx * qx + r.dy * qy) + r.dz * qz) * inv;
+    if (v < 0.0f || u + v > 1.0f) return;
+    const float t = ((e2x * qx + e2y * qy) + e2z * qz) * inv;
+    if (t < kTMin || closest < t) return;
+    closest = t;
+    kind = kHitTri;
+    idx = k;
+}
+
+// sphere::intersect (shape.cu:13-46), far root not checked against t_max (reference quirk).
+__device__ __forceinline__ void test_sphere(const float4 s, const ray3& r, float& closest, int& kind,
+                                            uint32_t& idx, uint32_t k) {
+    const float ocx = s.x - r.ox, ocy = s.y - r.oy, ocz = s.z - r.oz;
+    const float halfb = (r.dx * ocx + r.dy * ocy) + r.dz * ocz;
+    const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.w * s.w;
+    const float delta = halfb * halfb - cc;
+    if (delta < 0.0f) return;
+    float t = halfb - iq_sqrtf(delta);
+    if (closest < t) return;
+    if (t < kTMin) {
+        t = halfb + iq_sqrtf(delta);
+        if (t < kTMin) return;
+    }
+    closest = t;
+    kind = kHitSphere;
+    idx = k;
+}
+
+// oren_nayar(albedo .5, sigma 1).scatter (material.cu:5-43) at the closest sphere hit. Writes the
+// continuation ray into r and returns the record's scalar (attenuation * cos / pdf).
+__device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, ray3& r, rng6& s) {
+    // hit point and outward normal (shape.cu:36-44)
+    const float hx = r.ox + t * r.dx, hy = r.oy + t * r.dy, hz = r.oz + t * r.dz;
+    const float rinv = 1.0f / sph.w;
+    float nx = (hx - sph.x) * rinv, ny = (hy - sph.y) * rinv, nz = (hz - sph.z) * rinv;
+    if (!((r.dx * nx + r.dy * ny) + r.dz * nz < 0.0f)) {
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+    }
+    // onb (onb.h:7-12)
+    float wx = nx, wy = ny, wz = nz;
+    normalize3(wx, wy, wz);
+    float ax, ay, az;
+    if (iq_fabsf(wx) > 0.9f) { ax = 0.0f; ay = 1.0f; az = 0.0f; }
+    else { ax = 1.0f; ay = 0.0f; az = 0.0f; }
+    float vx = wy * az - wz * ay, vy = wz * ax - wx * az, vz = wx * ay - wy * ax;
+    normalize3(vx, vy, vz);
+    const float ux = vy * wz - vz * wy, uy = vz * wx - vx * wz, uz = vx * wy - vy * wx;
+    // cosine_weighted (random.cu:96-107)
+    const float u1 = rand_real(s, 0.0f, 1.0f);
+    const float u2 = rand_real(s, 0.0f, 1.0f);
+    const float phi = (2.0f * IQ_PI) * u1;
+    const float su2 = iq_sqrtf(u2);
+    const float lx = iq_cosf(phi) * su2;
+    const float ly = iq_sinf(phi) * su2;
+    const float lz = iq_sqrtf(1.0f - u2);
+    float dx = (ux * lx + vx * ly) + wx * lz;                    // onb::transform_to_world
+    float dy = (uy * lx + vy * ly) + wy * lz;
+    float dz = (uz * lx + vz * ly) + wz * lz;
+    const float wox = -r.dx, woy = -r.dy, woz = -r.dz;
+    float pdf = ((nx * dx + ny * dy) + nz * dz) / IQ_PI;         // oren_nayar::pdf (material.cu:45-48)
+    if (pdf < 0.00001f) {
+        dx = nx;
+        dy = ny;
+        dz = nz;
+        pdf = 1.0f / IQ_PI;
+    }
+    const float cosw = iq_fmaxf(0.0f, (nx * dx + ny * dy) + nz * dz);
+    const float sigma2 = 1.0f * 1.0f;
+    const float A = 1.0f - 0.5f * sigma2 / (sigma2 + 0.33f);
+    const float B = 0.45f * sigma2 / (sigma2 + 0.09f);
+    const float phi_o = iq_atan2f(woy, wox);
+    const float phi_i = iq_atan2f(dy, dx);
+    const float cto = iq_fmaxf(0.0f, (wox * nx + woy * ny) + woz * nz);
+    const float theta_o = cto > 1.0f ? 0.0f : iq_acosf(cto);
+    const float cti = iq_fmaxf(0.0f, (dx * nx + dy * ny) + dz * nz);
+    const float theta_i = cti > 1.0f ? 0.0f : iq_acosf(cti);
+    const float alpha = iq_fmaxf(theta_i, theta_o);
+    const float beta = iq_fminf(theta_i, theta_o);
+    const float coeff = A + B * iq_cosf(phi_i - phi_o) * iq_sinf(alpha) * iq_tanf(beta);
+    const float att = (0.5f * coeff) * (1.0f / IQ_PI);           // m_albedo * coeff / pi
+    r.ox = hx + nx * 0.0001f;                                    // hr.p + 0.0001f * hr.n
+    r.oy = hy + ny * 0.0001f;
+    r.oz = hz + nz * 0.0001f;
+    r.dx = dx;
+    r.dy = dy;
+    r.dz = dz;
+    return att * (cosw / pdf);
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// ------------------------------------------------------------------------------------------------
+// The megakernel. MAXD bounds max_depth (register stack size); STREAM selects LDS batch streaming
+// (scene larger than one LDS batch) with workgroup-uniform iteration.
+template <int MAXD, bool STREAM>
+__global__ __launch_bounds__(kRenderBlock) void iqpt_render_kernel(const kparams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    float4* lds_tri = lds;
+    float4* lds_sph = lds + (size_t)p.tri_batch * kTriFloat4;
+    const float4* __restrict__ g_tri = reinterpret_cast<const float4*>(p.tris);
+    const float4* __restrict__ g_sph = reinterpret_cast<const float4*>(p.spheres);
+
+    if (!STREAM) {
+        // whole scene resident in LDS for the lifetime of the block
+        for (uint32_t i = threadIdx.x; i < p.ntri * kTriFloat4; i += kRenderBlock) lds_tri[i] = g_tri[i];
+        for (uint32_t i = threadIdx.x; i < p.nsph; i += kRenderBlock) lds_sph[i] = g_sph[i];
+        __syncthreads();
+    }
+
+    const uint32_t lane = lane_id();
+    // ---- per-lane state
+    bool active = false;
+    uint32_t pix = 0, px = 0, py = 0;
+    uint32_t done = 0;                 // samples finished for the current pixel
+    rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
+    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    int depth = 0;
+    float stk[MAXD];
+#pragma unroll
+    for (int i = 0; i < MAXD; ++i) stk[i] = 1.0f;
+    uint32_t nrays = 0;
+    // ---- wave-uniform chunk state
+    uint32_t chunk_next = 0, chunk_end = 0;
+    bool exhausted = false;
+
+    auto refill = [&]() {
+        uint64_t need = __ballot(!active);
+        while (need != 0ull && !exhausted) {
+            if (chunk_next >= chunk_end) {
+                uint32_t base = 0;
+                if (lane == 0) base = atomicAdd(p.queue, kQueueChunk);
+                base = __shfl(base, 0);
+                if (base >= p.npix) {
+                    exhausted = true;
+                    break;
+                }
+                chunk_next = base;
+                chunk_end = min(base + kQueueChunk, p.npix);
+            }
+            const uint32_t avail = chunk_end - chunk_next;
+            const uint32_t rank = prefix_below(need);
+            if (!active && rank < avail) {
+                pix = chunk_next + rank;
+                const uint32_t col = pix % p.ncols, row = pix / p.ncols;
+                px = p.x0 + col;
+                py = p.y0 + row * p.ystep;
+                st.v0 = p.rng[pix];
+                st.v1 = p.rng[(size_t)p.npix + pix];
+                st.v2 = p.rng[2 * (size_t)p.npix + pix];
+                st.v3 = p.rng[3 * (size_t)p.npix + pix];
+                st.v4 = p.rng[4 * (size_t)p.npix + pix];
+                st.d = p.rng[5 * (size_t)p.npix + pix];
+                const float4_storage a = p.lin[pix];
+                acc = make_float4(a.x, a.y, a.z, a.w);
+                done = 0;
+                depth = 0;
+                camera_ray(p, px, py, st, ray);
+                active = true;
+            }
+            const uint32_t cnt = (uint32_t)__popcll(need);
+            chunk_next += cnt < avail ? cnt : avail;
+            need = __ballot(!active);
+        }
+    };
+
+    if (p.spp > 0) refill();
+
+    while (true) {
+        if (STREAM) {
+            if (!__syncthreads_or(active ? 1 : 0)) break;
+        } else {
+            if (!__any(active)) break;
+        }
+
+        // ------------------------------------------------ closest hit (path_tracer.cu:253-295)
+        float closest = kTMax;
+        int kind = kHitNone;
+        uint32_t hidx = 0;
+        if (STREAM) {
+            for (uint32_t base = 0; base < p.ntri; base += p.tri_batch) {
+                const uint32_t n = min(p.tri_batch, p.ntri - base);
+                __syncthreads();
+                for (uint32_t i = threadIdx.x; i < n * kTriFloat4; i += kRenderBlock)
+                    lds_tri[i] = g_tri[(size_t)base * kTriFloat4 + i];
+                __syncthreads();
+                if (active) {
+                    for (uint32_t k = 0; k < n; ++k)
+                        test_triangle(lds_tri[3 * k], lds_tri[3 * k + 1], lds_tri[3 * k + 2], ray, closest, kind,
+                                      hidx, base + k);
+                }
+            }
+            for (uint32_t base = 0; base < p.nsph; base += p.sph_batch) {
+                const uint32_t n = min(p.sph_batch, p.nsph - base);
+                __syncthreads();
+                for (uint32_t i = threadIdx.x; i < n; i += kRenderBlock) lds_sph[i] = g_sph[base + i];
+                __syncthreads();
+                if (active) {
+                    for (uint32_t k = 0; k < n; ++k) test_sphere(lds_sph[k], ray, closest, kind, hidx, base + k);
+                }
+            }
+        } else if (active) {
+            for (uint32_t k = 0; k < p.ntri; ++k)
+                test_triangle(lds_tri[3 * k], lds_tri[3 * k + 1], lds_tri[3 * k + 2], ray, closest, kind, hidx, k);
+            for (uint32_t k = 0; k < p.nsph; ++k) test_sphere(lds_sph[k], ray, closest, kind, hidx, k);
+        }
+
+        // ------------------------------------------------ shade (path_tracer.cu:297-316)
+        if (active) {
+            ++nrays;
+            bool term;
+            float Lx, Ly, Lz;
+            if (kind == kHitSphere) {
+                const float s = oren_nayar_scatter(g_sph[hidx], closest, ray, st);
+                if (depth + 1 >= p.max_depth) {
+                    term = true;                 // the last record is this scatter (biased, :252)
+                    Lx = s;
+                    Ly = s;
+                    Lz = s;
+                } else {
+                    term = false;
+#pragma unroll
+                    for (int i = MAXD - 1; i > 0; --i) stk[i] = stk[i - 1];
+                    stk[0] = s;
+                    ++depth;
+                }
+            } else if (kind == kHitTri) {
+                term = true;                     // emissive(1, 10): att 10, cos = pdf = 1
+                Lx = 10.0f;
+                Ly = 10.0f;
+                Lz = 10.0f;
+            } else {
+                term = true;                     // sky gradient, :308-313
+                const float a = (ray.dy + 1.0f) * 0.5f;
+                const float one_a = 1.0f - a;
+                Lx = one_a + a * 0.5f;
+                Ly = one_a + a * 0.7f;
+                Lz = one_a + a * 1.0f;
+            }
+            if (term) {
+                // backward product over the stacked records, newest first (:321-324)
+                float cx = Lx, cy = Ly, cz = Lz;
+#pragma unroll
+                for (int i = 0; i < MAXD; ++i) {
+                    if (i < depth) {
+                        cx = cx * stk[i];
+                        cy = cy * stk[i];
+                        cz = cz * stk[i];
+                    }
+                }
+                // clamp (:345-347), path_color = 0 + color (:341,348), running mean (:356-358)
+                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                cx = 0.0f + cx;
+                cy = 0.0f + cy;
+                cz = 0.0f + cz;
+                const uint64_t n = p.frame0 + done + 1;
+                const float nf = (float)n;
+                const float keep = (float)(n - 1) / nf;
+                acc.x = cx / nf + acc.x * keep;
+                acc.y = cy / nf + acc.y * keep;
+                acc.z = cz / nf + acc.z * keep;
+                ++done;
+                depth = 0;
+                if (done == p.spp) {
+                    // pixel complete: BGRA8 (:360-365), accumulator and RNG state back to HBM
+                    const uint32_t r8 = to_u8(255.0f * iq_sqrtf(acc.x));
+                    const uint32_t g8 = to_u8(255.0f * iq_sqrtf(acc.y));
+                    const uint32_t b8 = to_u8(255.0f * iq_sqrtf(acc.z));
+                    p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+                    float4_storage o;
+                    o.x = acc.x;
+                    o.y = acc.y;
+                    o.z = acc.z;
+                    o.w = acc.w;
+                    p.lin[pix] = o;
+                    p.rng[pix] = st.v0;
+                    p.rng[(size_t)p.npix + pix] = st.v1;
+                    p.rng[2 * (size_t)p.npix + pix] = st.v2;
+                    p.rng[3 * (size_t)p.npix + pix] = st.v3;
+                    p.rng[4 * (size_t)p.npix + pix] = st.v4;
+                    p.rng[5 * (size_t)p.npix + pix] = st.d;
+                    active = false;
+                } else {
+                    camera_ray(p, px, py, st, ray);
+                }
+            }
+        }
+        if (!exhausted && __any(!active)) refill();
+    }
+
+    // closest-hit query count: wave reduction, one atomic per wave
+    uint32_t sum = nrays;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+    if (lane == 0 && sum) atomicAdd(p.rays, (unsigned long long)sum);
+}
+
+// curand_init(seed, global pixel id, 0) per owned pixel (renderer_init_kernel, path_tracer.cu:36-46).
+__global__ __launch_bounds__(256) void iqpt_rng_init_kernel(uint32_t width, uint32_t x0, uint32_t ncols,
+                                                            uint32_t y0, uint32_t ystep, uint32_t npix,
+                                                            uint64_t seed, const uint32_t* __restrict__ tables,
+                                                            uint32_t* __restrict__ rng) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= npix) return;
+    const uint32_t x = x0 + p % ncols;
+    const uint32_t y = y0 + (p / ncols) * ystep;
+    const uint64_t pid = (uint64_t)y * width + x;
+    iq_xorwow_state s;
+    iq_xorwow_seed(seed, &s);
+    uint64_t sub = pid;
+    for (int i = 0; i < 32 && sub; ++i, sub >>= 1) {
+        if (sub & 1u) iq_gf2_matvec(tables + i * IQ_XORWOW_MAT_WORDS, s.v);
+    }
+    rng[p] = s.v[0];
+    rng[(size_t)npix + p] = s.v[1];
+    rng[2 * (size_t)npix + p] = s.v[2];
+    rng[3 * (size_t)npix + p] = s.v[3];
+    rng[4 * (size_t)npix + p] = s.v[4];
+    rng[5 * (size_t)npix + p] = s.d;
+}
+
+template <int MAXD, bool STREAM>
+int launch_render_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
+    hipLaunchKernelGGL((iqpt_render_kernel<MAXD, STREAM>), dim3(grid), dim3(kRenderBlock), lds, stream, p);
+    return (int)hipGetLastError();
+}
+
+template <int MAXD, bool STREAM>
+int occupancy_t(uint32_t lds, int* blocks) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_render_kernel<MAXD, STREAM>,
+                                                             kRenderBlock, lds);
+}
+
+}  // namespace
+
+int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, uint32_t y0, uint32_t ystep,
+                    uint32_t npix, uint64_t seed, const uint32_t* tables, uint32_t* rng) {
+    if (npix == 0) return 0;
+    const uint32_t grid = (npix + 255) / 256;
+    hipLaunchKernelGGL(iqpt_rng_init_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, width, x0, ncols,
+                       y0, ystep, npix, seed, tables, rng);
+    return (int)hipGetLastError();
+}
+
+int launch_render(void* stream, const kparams& p, uint32_t grid, uint32_t lds, bool stream_batches) {
+    hipStream_t s = (hipStream_t)stream;
+    if (p.max_depth <= 8) {
+        return stream_batches ? launch_render_t<8, true>(s, p, grid, lds) : launch_render_t<8, false>(s, p, grid, lds);
+    }
+    return stream_batches ? launch_render_t<16, true>(s, p, grid, lds) : launch_render_t<16, false>(s, p, grid, lds);
+}
+
+int render_occupancy(int max_depth, bool stream_batches, uint32_t lds, int* blocks) {
+    if (max_depth <= 8) return stream_batches ? occupancy_t<8, true>(lds, blocks) : occupancy_t<8, false>(lds, blocks);
+    return stream_batches ? occupancy_t<16, true>(lds, blocks) : occupancy_t<16, false>(lds, blocks);
+}
+
+const char* render_kernel_name() { return "iqpt_render_kernel"; }
+
+}  // namespace iqpt

@@ -1,0 +1,483 @@
+// iqpt_runtime.cpp — the C ABI of include/iqpt.h over HIP: render contexts, packet relayout,
+// launches, readback, timing and errors.
+//
+// Replaces the CUDA side of path_tracer (IoniqRE/path_tracer.cu:48-164, 368-404) and the upload
+// half of scene::build_packet / free_packet (IoniqRE/scene.cu:183-264).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "iq_host_math.hpp"
+#include "iq_xorwow.h"
+#include "iqpt.h"
+#include "iqpt_internal.hpp"
+
+namespace iqpt {
+
+namespace {
+thread_local std::string g_last_error;
+
+// LDS budget under which the whole scene stays resident per block (no barriers in the loop).
+constexpr uint32_t kLdsResidentBytes = 32 * 1024;
+// Batch sizes when the scene is streamed through LDS (24 KB + 8 KB).
+constexpr uint32_t kTriBatch = 512;
+constexpr uint32_t kSphBatch = 512;
+
+std::once_flag g_tables_once;
+std::vector<uint32_t> g_tables;  // A^(2^(67+i)), i < 32
+
+const std::vector<uint32_t>& xorwow_tables() {
+    std::call_once(g_tables_once, [] {
+        g_tables.resize(32 * IQ_XORWOW_MAT_WORDS);
+        iq_xorwow_subseq_tables(g_tables.data(), 32);
+    });
+    return g_tables;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(IQPT_ERR_HIP, std::string(what) + ": " + hipGetErrorName(e) + " (" + hipGetErrorString(e) + ")");
+}
+}  // namespace
+
+void set_last_error(const std::string& msg) { g_last_error = msg; }
+int fail(int status, const std::string& msg) {
+    g_last_error = msg;
+    return status;
+}
+
+}  // namespace iqpt
+
+#define IQPT_HIP(call)                                                  \
+    do {                                                                \
+        hipError_t e_ = (call);                                         \
+        if (e_ != hipSuccess) return iqpt::hip_fail(e_, #call);         \
+    } while (0)
+
+using iqpt::float4_storage;
+
+struct iqpt_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t width = 0, height = 0;
+    iqpt_pixel_set set{};
+    uint32_t ncols = 0, npix = 0;
+    uint64_t seed = 0;
+    int max_depth = 0;
+    uint64_t frame = 0;
+    int num_cus = 0;
+    bool have_camera = false, have_packet = false;
+    iqpt_camera cam{};
+    // pixel state (compact over the owned set)
+    float4_storage* d_lin = nullptr;
+    uint32_t* d_bgra = nullptr;
+    uint32_t* d_rng = nullptr;
+    unsigned long long* d_rays = nullptr;
+    uint32_t* d_queue = nullptr;
+    // scene (world space)
+    float4_storage* d_tris = nullptr;
+    float4_storage* d_tri_shade = nullptr;
+    float4_storage* d_sph = nullptr;
+    uint32_t ntri = 0, nsph = 0;
+    // timing
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
+    std::vector<hipEvent_t> event_pool;
+};
+
+namespace {
+
+int use_device(const iqpt_ctx* c) {
+    IQPT_HIP(hipSetDevice(c->device));
+    return IQPT_OK;
+}
+
+void free_scene(iqpt_ctx* c) {
+    if (c->d_tris) (void)hipFree(c->d_tris);
+    if (c->d_tri_shade) (void)hipFree(c->d_tri_shade);
+    if (c->d_sph) (void)hipFree(c->d_sph);
+    c->d_tris = c->d_tri_shade = c->d_sph = nullptr;
+    c->ntri = c->nsph = 0;
+}
+
+hipEvent_t take_event(iqpt_ctx* c) {
+    if (!c->event_pool.empty()) {
+        hipEvent_t e = c->event_pool.back();
+        c->event_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    return e;
+}
+
+}  // namespace
+
+extern "C" {
+
+int iqpt_abi_version(void) { return IQPT_ABI_VERSION; }
+
+const char* iqpt_error_string(int status) {
+    switch (status) {
+    case IQPT_OK: return "IQPT_OK";
+    case IQPT_ERR_INVALID_ARG: return "IQPT_ERR_INVALID_ARG";
+    case IQPT_ERR_HIP: return "IQPT_ERR_HIP";
+    case IQPT_ERR_OUT_OF_MEMORY: return "IQPT_ERR_OUT_OF_MEMORY";
+    case IQPT_ERR_NO_DEVICE: return "IQPT_ERR_NO_DEVICE";
+    case IQPT_ERR_NOT_READY: return "IQPT_ERR_NOT_READY";
+    case IQPT_ERR_UNSUPPORTED: return "IQPT_ERR_UNSUPPORTED";
+    default: return "IQPT_ERR_UNKNOWN";
+    }
+}
+
+const char* iqpt_last_error(void) { return iqpt::g_last_error.c_str(); }
+
+const char* iqpt_kernel_name(void) { return iqpt::render_kernel_name(); }
+
+int iqpt_create(int device, uint32_t width, uint32_t height, const iqpt_pixel_set* pixels, uint64_t seed,
+                int max_depth, iqpt_ctx** out) {
+    if (!out) return iqpt::fail(IQPT_ERR_INVALID_ARG, "out is NULL");
+    *out = nullptr;
+    if (width == 0 || height == 0 || width > 65535 || height > 65535)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "frame must be 1..65535 pixels per side (camera stores uint16)");
+    if (max_depth < 1) return iqpt::fail(IQPT_ERR_INVALID_ARG, "max_depth must be >= 1");
+    if (max_depth > IQPT_MAX_DEPTH_LIMIT)
+        return iqpt::fail(IQPT_ERR_UNSUPPORTED, "max_depth above IQPT_MAX_DEPTH_LIMIT");
+    iqpt_pixel_set ps = pixels ? *pixels : iqpt_pixel_set{0, width, 0, 1, height};
+    if (ps.x1 <= ps.x0 || ps.x1 > width || ps.nrows == 0 || ps.ystep == 0 ||
+        (uint64_t)ps.y0 + (uint64_t)(ps.nrows - 1) * ps.ystep >= height)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "pixel set outside the frame");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0)
+        return iqpt::fail(IQPT_ERR_NO_DEVICE, "no HIP device visible");
+    if (device < 0 || device >= count) return iqpt::fail(IQPT_ERR_NO_DEVICE, "device index out of range");
+
+    iqpt_ctx* c = new iqpt_ctx();
+    c->device = device;
+    c->width = width;
+    c->height = height;
+    c->set = ps;
+    c->ncols = ps.x1 - ps.x0;
+    c->npix = c->ncols * ps.nrows;
+    c->seed = seed;
+    c->max_depth = max_depth;
+    auto cleanup = [&](int st) {
+        iqpt_destroy(c);
+        return st;
+    };
+    int st = use_device(c);
+    if (st) return cleanup(st);
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return cleanup(iqpt::fail(IQPT_ERR_HIP, "hipGetDeviceProperties"));
+    c->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+        return cleanup(iqpt::fail(IQPT_ERR_HIP, "hipStreamCreate"));
+    const size_t n = c->npix;
+    if (hipMalloc(&c->d_lin, n * sizeof(float4_storage)) != hipSuccess ||
+        hipMalloc(&c->d_bgra, n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_rng, 6 * n * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_rays, sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_queue, sizeof(uint32_t)) != hipSuccess)
+        return cleanup(iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "device allocation of the frame state failed"));
+    // path_tracer.cu:134-135: both buffers start at zero
+    if (hipMemsetAsync(c->d_lin, 0, n * sizeof(float4_storage), c->stream) != hipSuccess ||
+        hipMemsetAsync(c->d_bgra, 0, n * sizeof(uint32_t), c->stream) != hipSuccess ||
+        hipMemsetAsync(c->d_rays, 0, sizeof(unsigned long long), c->stream) != hipSuccess)
+        return cleanup(iqpt::fail(IQPT_ERR_HIP, "hipMemsetAsync"));
+    // renderer_init_kernel (path_tracer.cu:139): curand_init(seed, pixelid, 0)
+    const std::vector<uint32_t>& tables = iqpt::xorwow_tables();
+    uint32_t* d_tables = nullptr;
+    if (hipMalloc(&d_tables, tables.size() * sizeof(uint32_t)) != hipSuccess)
+        return cleanup(iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "jump tables"));
+    hipError_t e = hipMemcpyAsync(d_tables, tables.data(), tables.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream);
+    int lst = e == hipSuccess ? iqpt::launch_rng_init(c->stream, width, ps.x0, c->ncols, ps.y0, ps.ystep, c->npix,
+                                                      seed, d_tables, c->d_rng)
+                              : (int)e;
+    hipError_t se = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_tables);
+    if (lst != 0) return cleanup(iqpt::hip_fail((hipError_t)lst, "rng init kernel"));
+    if (se != hipSuccess) return cleanup(iqpt::hip_fail(se, "rng init sync"));
+    *out = c;
+    return IQPT_OK;
+}
+
+int iqpt_destroy(iqpt_ctx* c) {
+    if (!c) return IQPT_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    free_scene(c);
+    if (c->d_lin) (void)hipFree(c->d_lin);
+    if (c->d_bgra) (void)hipFree(c->d_bgra);
+    if (c->d_rng) (void)hipFree(c->d_rng);
+    if (c->d_rays) (void)hipFree(c->d_rays);
+    if (c->d_queue) (void)hipFree(c->d_queue);
+    for (auto& pr : c->timed) {
+        (void)hipEventDestroy(pr.first);
+        (void)hipEventDestroy(pr.second);
+    }
+    for (hipEvent_t ev : c->event_pool) (void)hipEventDestroy(ev);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return IQPT_OK;
+}
+
+int iqpt_set_camera(iqpt_ctx* c, const iqpt_camera* cam) {
+    if (!c || !cam) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (cam->width != c->width || cam->height != c->height)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "camera size differs from the context frame");
+    c->cam = *cam;   // passed by value to every launch: no device copy to race with
+    c->have_camera = true;
+    return IQPT_OK;
+}
+
+int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
+    if (!c || !pk) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    const uint32_t ntdc = pk->num_drawcalls[IQPT_MESH_TRIANGLES];
+    const uint32_t nsdc = pk->num_drawcalls[IQPT_MESH_SPHERES];
+    if ((ntdc && !pk->tri_mesh_dcs) || (nsdc && !pk->sphere_dcs) || (pk->num_tri_meshes && !pk->tri_meshes))
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "packet array is NULL");
+    // world-space relayout (the ray-independent part of path_tracer.cu:257-270)
+    std::vector<float4_storage> tris, shade, sph;
+    uint64_t total = 0;
+    for (uint32_t i = 0; i < ntdc; ++i) {
+        const uint32_t id = pk->tri_mesh_dcs[i].mesh_id;
+        if (id >= pk->num_tri_meshes)
+            return iqpt::fail(IQPT_ERR_INVALID_ARG, "tri drawcall " + std::to_string(i) + ": mesh_id out of range");
+        const iqpt_tri_mesh& m = pk->tri_meshes[id];
+        if (m.num_indices % 3 != 0)
+            return iqpt::fail(IQPT_ERR_INVALID_ARG, "mesh " + std::to_string(id) + ": num_indices not a multiple of 3");
+        if (m.num_indices && (!m.indices || !m.vertices))
+            return iqpt::fail(IQPT_ERR_INVALID_ARG, "mesh " + std::to_string(id) + ": NULL arrays");
+        total += m.num_indices / 3;
+    }
+    if (total > 0xffffffffull / 4) return iqpt::fail(IQPT_ERR_INVALID_ARG, "too many triangles");
+    tris.reserve(total * iqpt::kTriFloat4);
+    shade.reserve(total * 3);
+    for (uint32_t i = 0; i < ntdc; ++i) {
+        const iqpt_tri_mesh_drawcall& dc = pk->tri_mesh_dcs[i];
+        const iq::mat4 M = iq::mat4::from(dc.transform);
+        const iq::mat4 N = iq::normal_matrix(M);                     // path_tracer.cu:260
+        const iqpt_tri_mesh& m = pk->tri_meshes[dc.mesh_id];
+        for (uint32_t j = 0; j < m.num_indices; j += 3) {
+            const uint32_t ia = m.indices[j], ib = m.indices[j + 1], ic = m.indices[j + 2];
+            if (ia >= m.num_vertices || ib >= m.num_vertices || ic >= m.num_vertices)
+                return iqpt::fail(IQPT_ERR_INVALID_ARG, "mesh " + std::to_string(dc.mesh_id) + ": index out of range");
+            const iqpt_vertex& a = m.vertices[ia];
+            const iqpt_vertex& b = m.vertices[ib];
+            const iqpt_vertex& cc = m.vertices[ic];
+            const iq::vec4 v0 = iq::transformed(iq::load3(a.pos, iq::usage::POINT), M);
+            const iq::vec4 v1 = iq::transformed(iq::load3(b.pos, iq::usage::POINT), M);
+            const iq::vec4 v2 = iq::transformed(iq::load3(cc.pos, iq::usage::POINT), M);
+            const iq::vec4 n0 = iq::transformed(iq::load3(a.normal, iq::usage::DIRECTION), N);
+            const iq::vec4 n1 = iq::transformed(iq::load3(b.normal, iq::usage::DIRECTION), N);
+            const iq::vec4 n2 = iq::transformed(iq::load3(cc.normal, iq::usage::DIRECTION), N);
+            const iq::vec4 e1 = v1 - v0, e2 = v2 - v0;               // shape.cu:65-66
+            const iq::vec4 ng = iq::cross3(e1, e2);                  // shape.cu:98
+            tris.push_back({v0.x, v0.y, v0.z, e1.x});
+            tris.push_back({e1.y, e1.z, e2.x, e2.y});
+            tris.push_back({e2.z, 0.0f, 0.0f, 0.0f});
+            shade.push_back({n0.x, n0.y, n0.z, ng.x});
+            shade.push_back({n1.x, n1.y, n1.z, ng.y});
+            shade.push_back({n2.x, n2.y, n2.z, ng.z});
+        }
+    }
+    for (uint32_t i = 0; i < nsdc; ++i) {
+        const iqpt_sphere_drawcall& s = pk->sphere_dcs[i];
+        sph.push_back({s.center[0], s.center[1], s.center[2], s.radius});
+    }
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
+    free_scene(c);
+    c->have_packet = false;
+    auto upload = [&](const std::vector<float4_storage>& v, float4_storage** dst) -> int {
+        if (v.empty()) return IQPT_OK;
+        if (hipMalloc(dst, v.size() * sizeof(float4_storage)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "scene allocation");
+        IQPT_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(float4_storage), hipMemcpyHostToDevice));
+        return IQPT_OK;
+    };
+    if ((st = upload(tris, &c->d_tris)) || (st = upload(shade, &c->d_tri_shade)) || (st = upload(sph, &c->d_sph))) {
+        free_scene(c);
+        return st;
+    }
+    c->ntri = (uint32_t)total;
+    c->nsph = nsdc;
+    c->have_packet = true;
+    return IQPT_OK;
+}
+
+int iqpt_render(iqpt_ctx* c, uint32_t spp) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    if (!c->have_camera || !c->have_packet) return iqpt::fail(IQPT_ERR_NOT_READY, "camera and packet must be set");
+    if (spp == 0) return IQPT_OK;
+    int st = use_device(c);
+    if (st) return st;
+    iqpt::kparams p;
+    std::memset(&p, 0, sizeof p);
+    p.width = c->width;
+    p.height = c->height;
+    p.x0 = c->set.x0;
+    p.ncols = c->ncols;
+    p.y0 = c->set.y0;
+    p.ystep = c->set.ystep;
+    p.nrows = c->set.nrows;
+    p.npix = c->npix;
+    p.frame0 = c->frame;
+    p.spp = spp;
+    p.max_depth = c->max_depth;
+    std::memcpy(p.inv_proj, c->cam.inv_proj, sizeof p.inv_proj);
+    std::memcpy(p.inv_view, c->cam.inv_view, sizeof p.inv_view);
+    p.tris = c->d_tris;
+    p.ntri = c->ntri;
+    p.spheres = c->d_sph;
+    p.nsph = c->nsph;
+    const uint64_t resident = (uint64_t)c->ntri * iqpt::kTriFloat4 * 16 + (uint64_t)c->nsph * 16;
+    const bool stream_batches = resident > iqpt::kLdsResidentBytes;
+    if (stream_batches) {
+        p.tri_batch = iqpt::kTriBatch;
+        p.sph_batch = iqpt::kSphBatch;
+    } else {
+        p.tri_batch = c->ntri;
+        p.sph_batch = c->nsph;
+    }
+    const uint32_t lds = std::max<uint32_t>(16u, p.tri_batch * iqpt::kTriFloat4 * 16 + p.sph_batch * 16);
+    p.lin = c->d_lin;
+    p.bgra = c->d_bgra;
+    p.rng = c->d_rng;
+    p.rays = c->d_rays;
+    p.queue = c->d_queue;
+    int occ = 0;
+    if (iqpt::render_occupancy(c->max_depth, stream_batches, lds, &occ) != 0 || occ < 1) occ = 1;
+    const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
+    IQPT_HIP(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), c->stream));
+    hipEvent_t e0 = take_event(c), e1 = take_event(c);
+    if (e0) (void)hipEventRecord(e0, c->stream);
+    int le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches);
+    if (e1) (void)hipEventRecord(e1, c->stream);
+    if (e0 && e1) c->timed.emplace_back(e0, e1);
+    if (le != 0) return iqpt::hip_fail((hipError_t)le, "render kernel launch");
+    c->frame += spp;
+    return IQPT_OK;
+}
+
+int iqpt_sync(iqpt_ctx* c) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    return IQPT_OK;
+}
+
+int iqpt_reset(iqpt_ctx* c) {                                       // path_tracer.cu:394-400
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    IQPT_HIP(hipMemsetAsync(c->d_bgra, 0, (size_t)c->npix * sizeof(uint32_t), c->stream));
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    c->frame = 0;
+    return IQPT_OK;
+}
+
+int iqpt_read(iqpt_ctx* c, float* lin_rgba, uint8_t* bgra) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    if (lin_rgba)
+        IQPT_HIP(hipMemcpy(lin_rgba, c->d_lin, (size_t)c->npix * sizeof(float4_storage), hipMemcpyDeviceToHost));
+    if (bgra) IQPT_HIP(hipMemcpy(bgra, c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    return IQPT_OK;
+}
+
+int iqpt_read_rng(iqpt_ctx* c, uint32_t* states) {
+    if (!c || !states) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    std::vector<uint32_t> planes((size_t)c->npix * 6);
+    IQPT_HIP(hipMemcpy(planes.data(), c->d_rng, planes.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (size_t p = 0; p < c->npix; ++p)
+        for (int k = 0; k < 6; ++k) states[p * 6 + k] = planes[(size_t)k * c->npix + p];
+    return IQPT_OK;
+}
+
+int iqpt_copy_accum_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
+    if (!c || !dst_device) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (bytes < (size_t)c->npix * sizeof(float4_storage)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipMemcpyAsync(dst_device, c->d_lin, (size_t)c->npix * sizeof(float4_storage), hipMemcpyDeviceToDevice,
+                            c->stream));
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    return IQPT_OK;
+}
+
+int iqpt_num_pixels(const iqpt_ctx* c, uint64_t* npix) {
+    if (!c || !npix) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *npix = c->npix;
+    return IQPT_OK;
+}
+
+int iqpt_frame_count(const iqpt_ctx* c, uint64_t* frames) {
+    if (!c || !frames) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *frames = c->frame;
+    return IQPT_OK;
+}
+
+int iqpt_rays_traced(iqpt_ctx* c, uint64_t* rays) {
+    if (!c || !rays) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    unsigned long long v = 0;
+    IQPT_HIP(hipMemcpy(&v, c->d_rays, sizeof v, hipMemcpyDeviceToHost));
+    *rays = v;
+    return IQPT_OK;
+}
+
+int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
+    if (!c || !total_ms || !launches) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    double sum = 0.0;
+    for (auto& pr : c->timed) {
+        float ms = 0.0f;
+        IQPT_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+        sum += ms;
+        c->event_pool.push_back(pr.first);
+        c->event_pool.push_back(pr.second);
+    }
+    *total_ms = sum;
+    *launches = c->timed.size();
+    c->timed.clear();
+    return IQPT_OK;
+}
+
+int iqpt_write_ppm(const char* path, uint32_t width, uint32_t height, const uint8_t* bgra) {
+    if (!path || !bgra || !width || !height) return iqpt::fail(IQPT_ERR_INVALID_ARG, "bad PPM arguments");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return iqpt::fail(IQPT_ERR_INVALID_ARG, std::string("cannot open ") + path);
+    std::fprintf(f, "P6\n%u %u\n255\n", width, height);
+    std::vector<uint8_t> row((size_t)width * 3);
+    for (uint32_t y = 0; y < height; ++y) {
+        const uint8_t* src = bgra + (size_t)y * width * 4;
+        for (uint32_t x = 0; x < width; ++x) {
+            row[x * 3 + 0] = src[x * 4 + 2];
+            row[x * 3 + 1] = src[x * 4 + 1];
+            row[x * 3 + 2] = src[x * 4 + 0];
+        }
+        std::fwrite(row.data(), 1, row.size(), f);
+    }
+    std::fclose(f);
+    return IQPT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,112 @@
+"""Render-context binding: ``PathTracer`` owns one iqpt_ctx (one GPU, one owned pixel set)."""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import Camera, PacketDesc, PixelSet, check
+
+
+def pixel_set(width: int, height: int, x0: int = 0, x1: int | None = None, y0: int = 0, ystep: int = 1,
+              nrows: int | None = None) -> PixelSet:
+    x1 = width if x1 is None else x1
+    if nrows is None:
+        nrows = (height - y0 + ystep - 1) // ystep
+    return PixelSet(x0, x1, y0, ystep, nrows)
+
+
+class PathTracer:
+    """The MI355X render context (iqpt_create .. iqpt_destroy). Raises IqptError on failure."""
+
+    def __init__(self, width: int, height: int, pixels: PixelSet | None = None, seed: int = _lib.DEFAULT_SEED,
+                 max_depth: int = _lib.DEFAULT_MAX_DEPTH, device: int = 0):
+        self._lib = _lib.load()
+        h = C.c_void_p()
+        ps = C.byref(pixels) if pixels is not None else None
+        check(self._lib.iqpt_create(device, width, height, ps, seed, max_depth, C.byref(h)), "iqpt_create")
+        self._h = h
+        self.width, self.height = width, height
+        self.pixels = pixels if pixels is not None else pixel_set(width, height)
+        n = C.c_uint64()
+        check(self._lib.iqpt_num_pixels(self._h, C.byref(n)), "iqpt_num_pixels")
+        self.npix = n.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self._lib.iqpt_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def set_camera(self, cam: Camera):
+        check(self._lib.iqpt_set_camera(self._h, C.byref(cam)), "iqpt_set_camera")
+
+    def upload_packet(self, pk: PacketDesc):
+        check(self._lib.iqpt_upload_packet(self._h, C.byref(pk)), "iqpt_upload_packet")
+
+    def render(self, spp: int):
+        check(self._lib.iqpt_render(self._h, spp), "iqpt_render")
+
+    def sync(self):
+        check(self._lib.iqpt_sync(self._h), "iqpt_sync")
+
+    def reset(self):
+        check(self._lib.iqpt_reset(self._h), "iqpt_reset")
+
+    def read(self) -> tuple[np.ndarray, np.ndarray]:
+        """(lin [npix,4] float32, bgra [npix,4] uint8) in the owned set's compact order."""
+        lin = np.empty((self.npix, 4), dtype=np.float32)
+        bgra = np.empty((self.npix, 4), dtype=np.uint8)
+        check(self._lib.iqpt_read(self._h, lin.ctypes.data_as(C.POINTER(C.c_float)),
+                                  bgra.ctypes.data_as(C.POINTER(C.c_uint8))), "iqpt_read")
+        return lin, bgra
+
+    def read_rng(self) -> np.ndarray:
+        st = np.empty((self.npix, 6), dtype=np.uint32)
+        check(self._lib.iqpt_read_rng(self._h, st.ctypes.data_as(C.POINTER(C.c_uint32))), "iqpt_read_rng")
+        return st
+
+    def copy_accum_device(self, dst_ptr: int, nbytes: int):
+        check(self._lib.iqpt_copy_accum_device(self._h, C.c_void_p(dst_ptr), nbytes), "iqpt_copy_accum_device")
+
+    def frames(self) -> int:
+        f = C.c_uint64()
+        check(self._lib.iqpt_frame_count(self._h, C.byref(f)), "iqpt_frame_count")
+        return f.value
+
+    def rays(self) -> int:
+        r = C.c_uint64()
+        check(self._lib.iqpt_rays_traced(self._h, C.byref(r)), "iqpt_rays_traced")
+        return r.value
+
+    def kernel_time(self) -> tuple[float, int]:
+        ms = C.c_double()
+        n = C.c_uint64()
+        check(self._lib.iqpt_kernel_time(self._h, C.byref(ms), C.byref(n)), "iqpt_kernel_time")
+        return ms.value, n.value
+
+
+def kernel_name() -> str:
+    return _lib.load().iqpt_kernel_name().decode()
+
+
+def write_ppm(path: str, width: int, height: int, bgra: np.ndarray):
+    b = np.ascontiguousarray(bgra, dtype=np.uint8)
+    check(_lib.load().iqpt_write_ppm(str(path).encode(), width, height, b.ctypes.data_as(C.POINTER(C.c_uint8))),
+          "iqpt_write_ppm")

@@ -1,0 +1,8 @@
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/t2.log 2>&1 || { echo TESTS_FAILED; tail -30 gpurun_out/t2.log; exit 1; }
+tail -3 gpurun_out/t2.log
+timeout -k 10 300 python bench.py > gpurun_out/bench1.json 2> gpurun_out/bench1.err || { echo BENCH_FAILED; tail -30 gpurun_out/bench1.err; exit 1; }
+cat gpurun_out/bench1.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof1 -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/bench_prof1.json 2> gpurun_out/prof1.err || { echo PROF_FAILED; tail -20 gpurun_out/prof1.err; exit 1; }
+find gpurun_out/prof1 -name "*stats*" | head; 
