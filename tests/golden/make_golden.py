@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Generates the golden fixtures of tests/golden/ from the CPU oracle (oracle/iqpt_oracle.c).
+
+The reference ships no golden data (IoniqRE/image.ppm is 0 bytes) and cannot be built here, so the
+fixtures pin the oracle's own output: they guard the restatement against regressions and give the
+GPU tests a CPU-free comparison. Run from the repo root:  python tests/golden/make_golden.py
+"""
+import hashlib
+import sys
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+sys.path[:0] = [str(REPO / "path-tracer-and-rasterizer-engine_amd"), str(REPO / "oracle")]
+
+import oracle  # noqa: E402
+from iqpt import Scene, make_camera  # noqa: E402
+
+# name: (preset, W, H, spp launches, max_depth, crop (x0, x1, y0, ystep, nrows) or None)
+CASES = {
+    "c1_full": ("c1_plumbing", 256, 256, [1], 2, None),
+    "cornell_crop": ("cornell", 1920, 1080, [4, 4], 8, (928, 992, 520, 1, 24)),
+    "mesh10k_crop": ("mesh10k", 1920, 1080, [2], 8, (944, 976, 400, 2, 12)),
+    "mixed_crop": ("mixed", 3840, 2160, [1], 8, (1908, 1932, 1150, 1, 8)),
+    "app_full": ("app_default", 96, 54, [4], 5, None),
+}
+
+
+def render(preset, w, h, launches, depth, crop):
+    sc = Scene()
+    sc.add_preset(preset)
+    pk = sc.build_packet()
+    cam = make_camera(w, h)
+    ps = oracle.pixel_set(w, h, *crop) if crop else None
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=depth)
+    for s in launches:
+        fr.render(pk, cam, s)
+    return fr
+
+
+def main():
+    for name, (preset, w, h, launches, depth, crop) in CASES.items():
+        fr = render(preset, w, h, launches, depth, crop)
+        np.savez_compressed(
+            HERE / f"{name}.npz", lin=fr.lin, bgra=fr.bgra, rays=fr.rays.astype(np.uint16),
+            states_sha256=np.frombuffer(hashlib.sha256(fr.states.tobytes()).digest(), dtype=np.uint8),
+            states_head=fr.states[:64], meta=np.array([w, h, depth, sum(launches)], dtype=np.int64))
+        print(name, fr.npix, "pixels", int(fr.rays.sum()), "rays")
+    # RNG KATs: curand_init(1984, pid, 0) for pid in {0, 1, 2^16, W*H-1} at 1080p and 4K
+    import ctypes as C
+    lib = oracle.load()
+    kat = []
+    for w, h in ((1920, 1080), (3840, 2160)):
+        for pid in (0, 1, 1 << 16, w * h - 1):
+            ps = oracle.pixel_set(w, h, pid % w, pid % w + 1, pid // w, 1, 1)
+            st = np.zeros((1, 6), dtype=np.uint32)
+            lib.iqo_rng_init(w, C.byref(ps), 1984, st.ctypes.data_as(C.POINTER(C.c_uint32)))
+            kat.append([w, h, pid, *st[0].tolist()])
+    np.savez_compressed(HERE / "rng_kat.npz", kat=np.array(kat, dtype=np.uint64))
+
+
+if __name__ == "__main__":
+    main()
