@@ -143,6 +143,25 @@ IQ_INLINE float iq_cosf(float x) {
     return sign < 0.0f ? -y : y;
 }
 
+/* sin and cos of one argument with one shared reduction; bit-identical to iq_sinf / iq_cosf. */
+IQ_INLINE void iq_sincosf(float x, float* s_out, float* c_out) {
+    if (iq_isnan(x) || iq_isinf(x)) { *s_out = iq_nanf(); *c_out = iq_nanf(); return; }
+    float ax = iq_fabsf(x);
+    if (ax > 1.0e18f) { *s_out = 0.0f; *c_out = 1.0f; return; }
+    int j;
+    float r = ax <= IQ_TRIG_MAX ? iq__reduce_octant(ax, &j) : iq__reduce_big(ax, &j);
+    float ssign = (iq_f2u(x) >> 31) ? -1.0f : 1.0f;
+    float csign = 1.0f;
+    if (j > 3) { ssign = -ssign; csign = -csign; j -= 4; }
+    if (j > 1) csign = -csign;
+    float z = r * r;
+    float ps = iq__sin_poly(r, z), pc = iq__cos_poly(z);
+    int swap = (j == 1 || j == 2);
+    float sy = swap ? pc : ps, cy = swap ? ps : pc;
+    *s_out = ssign < 0.0f ? -sy : sy;
+    *c_out = csign < 0.0f ? -cy : cy;
+}
+
 IQ_INLINE float iq_tanf(float x) {
     if (iq_isnan(x) || iq_isinf(x)) return iq_nanf();
     float ax = iq_fabsf(x);

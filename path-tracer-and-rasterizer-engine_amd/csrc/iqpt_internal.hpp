@@ -19,14 +19,25 @@ struct alignas(16) float4_storage {
     float x, y, z, w;
 };
 
-// Device layout of one triangle for the intersection loop: 3 x float4 = 48 B,
-//   t0 = (v0.x, v0.y, v0.z, e1.x), t1 = (e1.y, e1.z, e2.x, e2.y), t2 = (e2.z, 0, 0, 0)
-// where v0 is the world-space first vertex and e1 = v1 - v0, e2 = v2 - v0 (shape.cu:65-66).
+// Device layout of the scene (world space, built once per packet upload):
+//  * single triangles, 3 x float4 = 48 B:
+//      (v0.x, v0.y, v0.z, e1.x), (e1.y, e1.z, e2.x, e2.y), (e2.z, 0, 0, 0)
+//    with v0 the world-space first vertex and e1 = v1 - v0, e2 = v2 - v0 (shape.cu:65-66);
+//  * triangle PAIRS (2k, 2k+1), SoA inside the pair, 5 x float4 = 80 B, so that one packed
+//    (v_pk_*_f32) instruction advances both Möller–Trumbore tests and every operand pair lands in
+//    an aligned VGPR pair straight from one ds_read_b128:
+//      (v0x_a, v0x_b, v0y_a, v0y_b), (v0z_a, v0z_b, e1x_a, e1x_b), (e1y_a, e1y_b, e1z_a, e1z_b),
+//      (e2x_a, e2x_b, e2y_a, e2y_b), (e2z_a, e2z_b, 0, 0)
+//    an odd last triangle is paired with a zero triangle that is masked out;
+//  * spheres: (center.xyz, radius) float4, and sphere pairs 2 x float4 = 32 B:
+//      (cx_a, cx_b, cy_a, cy_b), (cz_a, cz_b, r_a, r_b).
 constexpr int kTriFloat4 = 3;
+constexpr int kTriPairFloat4 = 5;
+constexpr int kSphPairFloat4 = 2;
 // Shading record per triangle (only read for the closest hit): world normals n0, n1, n2 and the
-// geometric normal e1 x e2 (shape.cu:96-101) packed in the w lanes — 3 x float4. Not read under the reference's
-// hard-wired materials (every triangle is emissive, path_tracer.cu:278), kept for the
-// per-primitive material table.
+// geometric normal e1 x e2 (shape.cu:96-101) packed in the w lanes — 3 x float4. Not read under
+// the reference's hard-wired materials (every triangle is emissive, path_tracer.cu:278), kept for
+// the per-primitive material table.
 constexpr int kTriShadeFloat4 = 3;
 
 // Kernel parameters (passed by value; lands in SGPRs / the kernarg segment).
@@ -40,27 +51,47 @@ struct kparams {
     int32_t max_depth;
     float inv_proj[16];              // camera.h:30-31 (row-major m[r][c])
     float inv_view[16];
-    const float4_storage* tris;      // ntri * kTriFloat4
-    uint32_t ntri;
-    const float4_storage* spheres;   // nsph * (center.xyz, radius)
-    uint32_t nsph;
-    uint32_t tri_batch;              // triangles staged in LDS per batch
-    uint32_t sph_batch;              // spheres staged in LDS per batch
+    uint32_t cam_const;              // inverse projection has constant w (see camera_ray)
+    float cam_near_rw, cam_far_rw;   // 1 / w_near, 1 / w_far when cam_const
+    uint32_t acc_tab;                // build the per-launch (1/n, (n-1)/n) table in LDS
+    const float4_storage* tris;      // ntri * kTriFloat4 (single layout)
+    const float4_storage* tri_pairs; // ntri_pairs * kTriPairFloat4 (pair layout)
+    uint32_t ntri, ntri_pairs;
+    const float4_storage* spheres;   // nsph (center.xyz, radius)
+    const float4_storage* sph_pairs; // nsph_pairs * kSphPairFloat4
+    uint32_t nsph, nsph_pairs;
+    uint32_t tri_batch;              // LDS batch (triangles or triangle pairs, by layout)
+    uint32_t sph_batch;              // LDS batch (spheres or sphere pairs, by layout)
     float4_storage* lin;             // npix
     uint32_t* bgra;                  // npix
     uint32_t* rng;                   // 6 planes of npix words: v0..v4, d
     unsigned long long* rays;        // closest-hit query counter
     uint32_t* queue;                 // pixel dequeue head (zeroed before every launch)
+    unsigned long long* stats;       // kOptStats counters (8 x u64) or null
 };
+
+// Kernel option bits (all exact: each shortcut reproduces the reference's bits, see the kernel).
+constexpr int kOptCamConst = 1 << 0;   // launch-constant 1/w of the inverse projection
+constexpr int kOptAccTable = 1 << 1;   // running-mean 1/n, (n-1)/n table; c in {0,1} without a division
+constexpr int kOptPair = 1 << 2;       // packed two-primitive intersection (pair layout)
+constexpr int kOptLB5 = 1 << 3;        // __launch_bounds__ min 5 waves/SIMD (<= 96 VGPRs)
+constexpr int kOptLB6 = 1 << 4;        // __launch_bounds__ min 6 waves/SIMD (<= 80 VGPRs)
+constexpr int kOptSinCos = 1 << 5;     // shared reduction for cos(phi), sin(phi)
+constexpr int kOptBranchless = 1 << 6; // pair MT without early exits (small resident scenes)
+constexpr int kOptStats = 1 << 7;      // wave-level counters (diagnostic builds)
+constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5;
+constexpr uint32_t kAccTableMax = 4096;  // spp per launch covered by the LDS table
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.
 int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, uint32_t y0,
                     uint32_t ystep, uint32_t npix, uint64_t seed, const uint32_t* tables,
                     uint32_t* rng);
-// grid_blocks = persistent grid size; lds_bytes dynamic LDS; stream = hipStream_t.
-int launch_render(void* stream, const kparams& p, uint32_t grid_blocks, uint32_t lds_bytes, bool stream_batches);
+// grid_blocks = persistent grid size; lds_bytes dynamic LDS; stream = hipStream_t; opt = kOpt* mask.
+int launch_render(void* stream, const kparams& p, uint32_t grid_blocks, uint32_t lds_bytes, bool stream_batches,
+                  int opt);
 // Max resident blocks per CU of the render kernel for the given dynamic LDS (occupancy query).
-int render_occupancy(int max_depth, bool stream_batches, uint32_t lds_bytes, int* blocks_per_cu);
+int render_occupancy(int max_depth, bool stream_batches, int opt, uint32_t lds_bytes, int* blocks_per_cu);
+bool render_variant_exists(int max_depth, bool stream_batches, int opt);
 constexpr int kRenderBlock = 256;
 constexpr uint32_t kQueueChunk = 64;
 const char* render_kernel_name();

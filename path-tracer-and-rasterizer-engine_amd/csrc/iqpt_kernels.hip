@@ -8,21 +8,24 @@
 //  * Persistent grid, one lane = one pixel at a time. A lane runs ALL of its pixel's samples of
 //    the launch back to back (a pixel's samples are sequential in its XORWOW stream: each sample
 //    consumes a data-dependent number of draws), regenerating a camera ray as soon as a path ends,
-//    so every iteration of the loop traces one ray per live lane and the intersection loop never
-//    idles on dead paths. Lanes that finish their pixel refill from a global pixel queue: one
-//    atomic per 64-pixel chunk per wave, handed out to the empty lanes with a wave64
-//    __ballot + mbcnt prefix sum (compaction of live work across waves and pixels).
-//  * The scene is pre-transformed to world space at upload (the six per-ray transforms and the
-//    per-drawcall normal-matrix inverse of path_tracer.cu:257-270 are ray-independent); the
-//    triangles (48 B: v0, e1, e2) and spheres (16 B) are staged in LDS and read by broadcast. When
-//    the scene exceeds the LDS budget it is streamed in batches behind workgroup barriers.
-//  * The reference's scatter_record stack (path_tracer.cu:243, 321-324) is a register shift
-//    register: under the reference materials every non-terminal record is an Oren-Nayar scatter
-//    whose (attenuation * cos/pdf) is the same in x, y and z, so a record is one float and the
-//    backward product keeps its exact evaluation order.
+//    so every iteration traces one ray per live lane. Lanes that finish their pixel refill from a
+//    global pixel queue: one atomic per 64-pixel chunk per wave, handed to the empty lanes with a
+//    wave64 __ballot + mbcnt prefix sum.
+//  * The scene is pre-transformed to world space at upload (the per-ray transforms and the
+//    per-drawcall normal-matrix inverse of path_tracer.cu:257-270 are ray-independent) and laid out
+//    as SoA primitive PAIRS: one packed v_pk_{mul,add}_f32 instruction advances two Möller–Trumbore
+//    (or two sphere) tests, with operand pairs arriving in aligned VGPR pairs from ds_read_b128.
+//    Packed FP32 ops round each element exactly like the scalar op, and the closest-hit updates of
+//    the two primitives stay sequential, so results are unchanged bit for bit.
+//  * Small scenes stay resident in LDS for the whole launch; large scenes are streamed through LDS
+//    in batches behind workgroup barriers (workgroup-uniform loop).
+//  * The scatter_record stack (path_tracer.cu:243, 321-324) is a register shift register: under
+//    the reference materials every non-terminal record is an Oren–Nayar scatter whose
+//    (attenuation * cos/pdf) is the same in x, y and z, so a record is one float and the backward
+//    product keeps its exact evaluation order.
 //  * Every floating-point operation follows the reference's order with contraction off
-//    (-ffp-contract=off) and the shared transcendentals of iq_fp.h: results are bit-identical to
-//    the CPU oracle (tests/test_gpu_parity.py).
+//    (-ffp-contract=off) and the shared transcendentals of iq_fp.h; every shortcut below is exact
+//    (argued where it is taken). Results are bit-identical to the CPU oracle.
 #include <hip/hip_runtime.h>
 
 #include "iq_fp.h"
@@ -39,6 +42,8 @@ namespace {
 constexpr float kTMin = 0.000001f;       // path_tracer.cu:241
 constexpr float kTMax = 999.99f;
 constexpr int kHitNone = 0, kHitTri = 1, kHitSphere = 2;
+
+typedef float f2 __attribute__((ext_vector_type(2)));
 
 struct rng6 {
     uint32_t v0, v1, v2, v3, v4, d;
@@ -86,6 +91,11 @@ struct ray3 {
 };
 
 // camera::get_ray (camera.cu:20-43): x jitter drawn first, then y.
+// kOptCamConst: when the inverse projection has m[0][3] = m[1][3] = 0 and finite non-zero m[2][3],
+// m[3][3] (checked exactly on the host), w_near = ((x*0 + y*0) + 0*m23) + m33 = m33 and
+// w_far = ((x*0 + y*0) + m23) + m33 = fl(m23 + m33) for every finite x, y, so 1/w are launch
+// constants computed by the same IEEE division on the host (p.cam_near_rw / p.cam_far_rw).
+template <int OPT>
 __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_t y, rng6& s, ray3& r) {
     const float jx = rand_real(s, -0.5f, 0.5f);
     const float x_ndc = (((float)x + jx) / (float)p.width) * 2.0f - 1.0f;
@@ -93,20 +103,23 @@ __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_
     const float y_ndc = 1.0f - (((float)y + jy) / (float)p.height) * 2.0f;
     const float* P = p.inv_proj;
     const float* Vw = p.inv_view;
-    // near point (x, y, 0, 1) and far point (x, y, 1, 1) through inv_proj, then /w (vector.h:100-103)
     float nx = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 0);
     float ny = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 1);
     float nz = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 2);
-    const float nw = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 3);
-    const float ninv = 1.0f / nw;
-    nx = nx * ninv;
-    ny = ny * ninv;
-    nz = nz * ninv;
     float fx = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 0);
     float fy = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 1);
     float fz = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 2);
-    const float fw = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 3);
-    const float finv = 1.0f / fw;
+    float ninv, finv;
+    if ((OPT & kOptCamConst) && p.cam_const) {
+        ninv = p.cam_near_rw;
+        finv = p.cam_far_rw;
+    } else {
+        ninv = 1.0f / dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 3);
+        finv = 1.0f / dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 3);
+    }
+    nx = nx * ninv;
+    ny = ny * ninv;
+    nz = nz * ninv;
     fx = fx * finv;
     fy = fy * finv;
     fz = fz * finv;
@@ -136,9 +149,8 @@ __device__ __forceinline__ uint32_t to_u8(float f) {
 
 // Möller–Trumbore of shape.cu:62-103 with the hit bookkeeping reduced to (t, index); every reject
 // test is the reference's condition, negated, so NaN behaves identically.
-__device__ __forceinline__ void test_triangle(const float4 a, const float4 b, const float4 c,
-                                              const ray3& r, float& closest, int& kind,
-                                              uint32_t& idx, uint32_t k) {
+__device__ __forceinline__ void test_triangle(const float4 a, const float4 b, const float4 c, const ray3 r,
+                                              float& closest, int& kind, uint32_t& idx, uint32_t k) {
     const float e1x = a.w, e1y = b.x, e1z = b.y;
     const float e2x = b.z, e2y = b.w, e2z = c.x;
     const float px = r.dy * e2z - r.dz * e2y;                   // dir x v0v2
@@ -162,14 +174,90 @@ __device__ __forceinline__ void test_triangle(const float4 a, const float4 b, co
     idx = k;
 }
 
+// The same Möller–Trumbore for the pair (k, k+1), both in flight in packed registers. Each
+// element sees exactly the scalar operation sequence above; `alive` masks the odd tail. The t
+// test against the running closest hit is sequential (k first), as in the reference's loop.
+// Branchless form (kOptBranchless): all stages always evaluated, the reference's reject tests
+// folded into the two `alive` masks; same per-element operations, so the same bits.
+__device__ __forceinline__ void test_triangle_pair_nb(const float4 q0, const float4 q1, const float4 q2,
+                                                      const float4 q3, const float4 q4, const ray3 r,
+                                                      float& closest, int& kind, uint32_t& idx, uint32_t k,
+                                                      bool second) {
+    const f2 v0x = {q0.x, q0.y}, v0y = {q0.z, q0.w}, v0z = {q1.x, q1.y};
+    const f2 e1x = {q1.z, q1.w}, e1y = {q2.x, q2.y}, e1z = {q2.z, q2.w};
+    const f2 e2x = {q3.x, q3.y}, e2y = {q3.z, q3.w}, e2z = {q4.x, q4.y};
+    const f2 px = r.dy * e2z - r.dz * e2y;
+    const f2 py = r.dz * e2x - r.dx * e2z;
+    const f2 pz = r.dx * e2y - r.dy * e2x;
+    const f2 det = (e1x * px + e1y * py) + e1z * pz;
+    const f2 inv = {1.0f / det.x, 1.0f / det.y};
+    const f2 tx = r.ox - v0x, ty = r.oy - v0y, tz = r.oz - v0z;
+    const f2 u = ((tx * px + ty * py) + tz * pz) * inv;
+    const f2 qx = ty * e1z - tz * e1y;
+    const f2 qy = tz * e1x - tx * e1z;
+    const f2 qz = tx * e1y - ty * e1x;
+    const f2 v = ((r.dx * qx + r.dy * qy) + r.dz * qz) * inv;
+    const f2 uv = u + v;
+    const f2 t = ((e2x * qx + e2y * qy) + e2z * qz) * inv;
+    const bool a0 = !(iq_fabsf(det.x) < 0.000001f) && !(u.x < 0.0f || u.x > 1.0f) &&
+                    !(v.x < 0.0f || uv.x > 1.0f) && !(t.x < kTMin);
+    const bool a1 = second && !(iq_fabsf(det.y) < 0.000001f) && !(u.y < 0.0f || u.y > 1.0f) &&
+                    !(v.y < 0.0f || uv.y > 1.0f) && !(t.y < kTMin);
+    if (a0 && !(closest < t.x)) {
+        closest = t.x;
+        kind = kHitTri;
+        idx = k;
+    }
+    if (a1 && !(closest < t.y)) {
+        closest = t.y;
+        kind = kHitTri;
+        idx = k + 1;
+    }
+}
+
+__device__ __forceinline__ void test_triangle_pair(const float4 q0, const float4 q1, const float4 q2,
+                                                   const float4 q3, const float4 q4, const ray3 r, float& closest,
+                                                   int& kind, uint32_t& idx, uint32_t k, bool second) {
+    const f2 v0x = {q0.x, q0.y}, v0y = {q0.z, q0.w}, v0z = {q1.x, q1.y};
+    const f2 e1x = {q1.z, q1.w}, e1y = {q2.x, q2.y}, e1z = {q2.z, q2.w};
+    const f2 e2x = {q3.x, q3.y}, e2y = {q3.z, q3.w}, e2z = {q4.x, q4.y};
+    const f2 px = r.dy * e2z - r.dz * e2y;
+    const f2 py = r.dz * e2x - r.dx * e2z;
+    const f2 pz = r.dx * e2y - r.dy * e2x;
+    const f2 det = (e1x * px + e1y * py) + e1z * pz;
+    bool a0 = !(iq_fabsf(det.x) < 0.000001f);
+    bool a1 = second && !(iq_fabsf(det.y) < 0.000001f);
+    if (!(a0 || a1)) return;
+    const f2 inv = {1.0f / det.x, 1.0f / det.y};
+    const f2 tx = r.ox - v0x, ty = r.oy - v0y, tz = r.oz - v0z;
+    const f2 u = ((tx * px + ty * py) + tz * pz) * inv;
+    a0 = a0 && !(u.x < 0.0f || u.x > 1.0f);
+    a1 = a1 && !(u.y < 0.0f || u.y > 1.0f);
+    if (!(a0 || a1)) return;
+    const f2 qx = ty * e1z - tz * e1y;
+    const f2 qy = tz * e1x - tx * e1z;
+    const f2 qz = tx * e1y - ty * e1x;
+    const f2 v = ((r.dx * qx + r.dy * qy) + r.dz * qz) * inv;
+    const f2 uv = u + v;
+    a0 = a0 && !(v.x < 0.0f || uv.x > 1.0f);
+    a1 = a1 && !(v.y < 0.0f || uv.y > 1.0f);
+    if (!(a0 || a1)) return;
+    const f2 t = ((e2x * qx + e2y * qy) + e2z * qz) * inv;
+    if (a0 && !(t.x < kTMin || closest < t.x)) {
+        closest = t.x;
+        kind = kHitTri;
+        idx = k;
+    }
+    if (a1 && !(t.y < kTMin || closest < t.y)) {
+        closest = t.y;
+        kind = kHitTri;
+        idx = k + 1;
+    }
+}
+
 // sphere::intersect (shape.cu:13-46), far root not checked against t_max (reference quirk).
-__device__ __forceinline__ void test_sphere(const float4 s, const ray3& r, float& closest, int& kind,
-                                            uint32_t& idx, uint32_t k) {
-    const float ocx = s.x - r.ox, ocy = s.y - r.oy, ocz = s.z - r.oz;
-    const float halfb = (r.dx * ocx + r.dy * ocy) + r.dz * ocz;
-    const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.w * s.w;
-    const float delta = halfb * halfb - cc;
-    if (delta < 0.0f) return;
+__device__ __forceinline__ void sphere_roots(float halfb, float delta, float& closest, int& kind, uint32_t& idx,
+                                             uint32_t k) {
     float t = halfb - iq_sqrtf(delta);
     if (closest < t) return;
     if (t < kTMin) {
@@ -181,8 +269,33 @@ __device__ __forceinline__ void test_sphere(const float4 s, const ray3& r, float
     idx = k;
 }
 
+__device__ __forceinline__ void test_sphere(const float4 s, const ray3 r, float& closest, int& kind,
+                                            uint32_t& idx, uint32_t k) {
+    const float ocx = s.x - r.ox, ocy = s.y - r.oy, ocz = s.z - r.oz;
+    const float halfb = (r.dx * ocx + r.dy * ocy) + r.dz * ocz;
+    const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.w * s.w;
+    const float delta = halfb * halfb - cc;
+    if (delta < 0.0f) return;
+    sphere_roots(halfb, delta, closest, kind, idx, k);
+}
+
+// Two spheres (k, k+1) with the quadratic set up in packed registers, roots tested in order.
+__device__ __forceinline__ void test_sphere_pair(const float4 s0, const float4 s1, const ray3 r, float& closest,
+                                                 int& kind, uint32_t& idx, uint32_t k, bool second) {
+    const f2 cx = {s0.x, s0.y}, cy = {s0.z, s0.w}, cz = {s1.x, s1.y}, rad = {s1.z, s1.w};
+    const f2 ocx = cx - r.ox, ocy = cy - r.oy, ocz = cz - r.oz;
+    const f2 halfb = (r.dx * ocx + r.dy * ocy) + r.dz * ocz;
+    const f2 cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - rad * rad;
+    const f2 delta = halfb * halfb - cc;
+    const bool a0 = !(delta.x < 0.0f);
+    const bool a1 = second && !(delta.y < 0.0f);
+    if (a0) sphere_roots(halfb.x, delta.x, closest, kind, idx, k);
+    if (a1) sphere_roots(halfb.y, delta.y, closest, kind, idx, k + 1);
+}
+
 // oren_nayar(albedo .5, sigma 1).scatter (material.cu:5-43) at the closest sphere hit. Writes the
 // continuation ray into r and returns the record's scalar (attenuation * cos / pdf).
+template <int OPT>
 __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, ray3& r, rng6& s) {
     // hit point and outward normal (shape.cu:36-44)
     const float hx = r.ox + t * r.dx, hy = r.oy + t * r.dy, hz = r.oz + t * r.dz;
@@ -207,8 +320,15 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     const float u2 = rand_real(s, 0.0f, 1.0f);
     const float phi = (2.0f * IQ_PI) * u1;
     const float su2 = iq_sqrtf(u2);
-    const float lx = iq_cosf(phi) * su2;
-    const float ly = iq_sinf(phi) * su2;
+    float sphi, cphi;
+    if (OPT & kOptSinCos) {
+        iq_sincosf(phi, &sphi, &cphi);
+    } else {
+        cphi = iq_cosf(phi);
+        sphi = iq_sinf(phi);
+    }
+    const float lx = cphi * su2;
+    const float ly = sphi * su2;
     const float lz = iq_sqrtf(1.0f - u2);
     float dx = (ux * lx + vx * ly) + wx * lz;                    // onb::transform_to_world
     float dy = (uy * lx + vy * ly) + wy * lz;
@@ -244,31 +364,94 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     return att * (cosw / pdf);
 }
 
-__device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
-
 __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// c / n of the running mean (path_tracer.cu:356-358). kOptAccTable: 1/n is read from a per-launch
+// table built with the same IEEE division (so c = 1 gives the identical bits) and 0/n = +0 (c is
+// never -0 here: path_color = 0 + color).
+template <int OPT>
+__device__ __forceinline__ float mean_term(float c, float nf, float rc) {
+    if (OPT & kOptAccTable) {
+        if (c == 1.0f) return rc;
+        if (c == 0.0f) return 0.0f;
+    }
+    return c / nf;
+}
+
+// Closest hit over the primitives in [tri0, tri1) / [sph0, sph1) of the given base arrays (LDS),
+// in the reference's order: triangles of every drawcall first, then spheres (path_tracer.cu:257-295).
+template <int OPT>
+__device__ __forceinline__ void intersect_range(const float4* tri, uint32_t tri_first, uint32_t ntri_local,
+                                                const float4* sph, uint32_t sph_first, uint32_t nsph_local,
+                                                const ray3 ray, float& closest, int& kind, uint32_t& hidx) {
+    if (OPT & kOptPair) {
+        // tri points at pair records; tri_first / sph_first are even primitive indices
+        const uint32_t tp = (ntri_local + 1) / 2;
+        for (uint32_t j = 0; j < tp; ++j) {
+            const float4* q = tri + (size_t)j * kTriPairFloat4;
+            if (OPT & kOptBranchless)
+                test_triangle_pair_nb(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, tri_first + 2 * j,
+                                      2 * j + 1 < ntri_local);
+            else
+                test_triangle_pair(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, tri_first + 2 * j,
+                                   2 * j + 1 < ntri_local);
+        }
+        const uint32_t sp = (nsph_local + 1) / 2;
+        for (uint32_t j = 0; j < sp; ++j) {
+            const float4* q = sph + (size_t)j * kSphPairFloat4;
+            test_sphere_pair(q[0], q[1], ray, closest, kind, hidx, sph_first + 2 * j, 2 * j + 1 < nsph_local);
+        }
+    } else {
+        for (uint32_t k = 0; k < ntri_local; ++k) {
+            const float4* q = tri + (size_t)k * kTriFloat4;
+            test_triangle(q[0], q[1], q[2], ray, closest, kind, hidx, tri_first + k);
+        }
+        for (uint32_t k = 0; k < nsph_local; ++k) test_sphere(sph[k], ray, closest, kind, hidx, sph_first + k);
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // The megakernel. MAXD bounds max_depth (register stack size); STREAM selects LDS batch streaming
-// (scene larger than one LDS batch) with workgroup-uniform iteration.
-template <int MAXD, bool STREAM>
-__global__ __launch_bounds__(kRenderBlock) void iqpt_render_kernel(const kparams p) {
+// (scene larger than the resident budget) with workgroup-uniform iteration; OPT is the kOpt* mask.
+template <int OPT>
+constexpr int min_waves_per_simd() {
+    return (OPT & kOptLB6) ? 6 : ((OPT & kOptLB5) ? 5 : 1);
+}
+
+template <int MAXD, bool STREAM, int OPT>
+__global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_render_kernel(const kparams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    constexpr bool kPair = (OPT & kOptPair) != 0;
+    constexpr int kTriRec = kPair ? kTriPairFloat4 : kTriFloat4;   // float4 per LDS record
+    constexpr int kSphRec = kPair ? kSphPairFloat4 : 1;
+    constexpr uint32_t kTriPer = kPair ? 2u : 1u;                   // primitives per record
+    constexpr uint32_t kSphPer = kPair ? 2u : 1u;
+    const float4* __restrict__ g_tri = reinterpret_cast<const float4*>(kPair ? p.tri_pairs : p.tris);
+    const float4* __restrict__ g_sph = reinterpret_cast<const float4*>(kPair ? p.sph_pairs : p.spheres);
+    const float4* __restrict__ g_sph_plain = reinterpret_cast<const float4*>(p.spheres);
+    const uint32_t tri_recs = kPair ? p.ntri_pairs : p.ntri;
+    const uint32_t sph_recs = kPair ? p.nsph_pairs : p.nsph;
     float4* lds_tri = lds;
-    float4* lds_sph = lds + (size_t)p.tri_batch * kTriFloat4;
-    const float4* __restrict__ g_tri = reinterpret_cast<const float4*>(p.tris);
-    const float4* __restrict__ g_sph = reinterpret_cast<const float4*>(p.spheres);
+    float4* lds_sph = lds + (size_t)p.tri_batch * kTriRec;
+    float2* lds_tab = reinterpret_cast<float2*>(lds_sph + (size_t)p.sph_batch * kSphRec);
+    const bool use_tab = (OPT & kOptAccTable) && p.acc_tab;
 
     if (!STREAM) {
-        // whole scene resident in LDS for the lifetime of the block
-        for (uint32_t i = threadIdx.x; i < p.ntri * kTriFloat4; i += kRenderBlock) lds_tri[i] = g_tri[i];
-        for (uint32_t i = threadIdx.x; i < p.nsph; i += kRenderBlock) lds_sph[i] = g_sph[i];
-        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < tri_recs * kTriRec; i += kRenderBlock) lds_tri[i] = g_tri[i];
+        for (uint32_t i = threadIdx.x; i < sph_recs * kSphRec; i += kRenderBlock) lds_sph[i] = g_sph[i];
     }
+    if (use_tab) {
+        // (1/n, (n-1)/n) of sample s of this launch: the reference's own divisions, once per block
+        for (uint32_t s = threadIdx.x; s < p.spp; s += kRenderBlock) {
+            const uint64_t n = p.frame0 + s + 1;
+            lds_tab[s] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
+        }
+    }
+    __syncthreads();
 
-    const uint32_t lane = lane_id();
+    const uint32_t lane = __lane_id();
     // ---- per-lane state
     bool active = false;
     uint32_t pix = 0, px = 0, py = 0;
@@ -284,6 +467,9 @@ __global__ __launch_bounds__(kRenderBlock) void iqpt_render_kernel(const kparams
     // ---- wave-uniform chunk state
     uint32_t chunk_next = 0, chunk_end = 0;
     bool exhausted = false;
+    // ---- stats (kOptStats): wave-level counters
+    unsigned long long s_iter = 0, s_ready = 0, s_scatter_exec = 0, s_scatter_lanes = 0, s_term_exec = 0,
+                       s_term_lanes = 0;
 
     auto refill = [&]() {
         uint64_t need = __ballot(!active);
@@ -316,7 +502,7 @@ __global__ __launch_bounds__(kRenderBlock) void iqpt_render_kernel(const kparams
                 acc = make_float4(a.x, a.y, a.z, a.w);
                 done = 0;
                 depth = 0;
-                camera_ray(p, px, py, st, ray);
+                camera_ray<OPT>(p, px, py, st, ray);
                 active = true;
             }
             const uint32_t cnt = (uint32_t)__popcll(need);
@@ -333,53 +519,58 @@ __global__ __launch_bounds__(kRenderBlock) void iqpt_render_kernel(const kparams
         } else {
             if (!__any(active)) break;
         }
+        if (OPT & kOptStats) {
+            ++s_iter;
+            s_ready += (unsigned long long)__popcll(__ballot(active));
+        }
 
         // ------------------------------------------------ closest hit (path_tracer.cu:253-295)
         float closest = kTMax;
         int kind = kHitNone;
         uint32_t hidx = 0;
         if (STREAM) {
-            for (uint32_t base = 0; base < p.ntri; base += p.tri_batch) {
-                const uint32_t n = min(p.tri_batch, p.ntri - base);
+            for (uint32_t base = 0; base < tri_recs; base += p.tri_batch) {
+                const uint32_t n = min(p.tri_batch, tri_recs - base);
                 __syncthreads();
-                for (uint32_t i = threadIdx.x; i < n * kTriFloat4; i += kRenderBlock)
-                    lds_tri[i] = g_tri[(size_t)base * kTriFloat4 + i];
+                for (uint32_t i = threadIdx.x; i < n * kTriRec; i += kRenderBlock)
+                    lds_tri[i] = g_tri[(size_t)base * kTriRec + i];
                 __syncthreads();
                 if (active) {
-                    for (uint32_t k = 0; k < n; ++k)
-                        test_triangle(lds_tri[3 * k], lds_tri[3 * k + 1], lds_tri[3 * k + 2], ray, closest, kind,
-                                      hidx, base + k);
+                    const uint32_t first = base * kTriPer;
+                    const uint32_t cnt = min(n * kTriPer, p.ntri - first);
+                    intersect_range<OPT>(lds_tri, first, cnt, lds_sph, 0, 0, ray, closest, kind, hidx);
                 }
             }
-            for (uint32_t base = 0; base < p.nsph; base += p.sph_batch) {
-                const uint32_t n = min(p.sph_batch, p.nsph - base);
+            for (uint32_t base = 0; base < sph_recs; base += p.sph_batch) {
+                const uint32_t n = min(p.sph_batch, sph_recs - base);
                 __syncthreads();
-                for (uint32_t i = threadIdx.x; i < n; i += kRenderBlock) lds_sph[i] = g_sph[base + i];
+                for (uint32_t i = threadIdx.x; i < n * kSphRec; i += kRenderBlock)
+                    lds_sph[i] = g_sph[(size_t)base * kSphRec + i];
                 __syncthreads();
                 if (active) {
-                    for (uint32_t k = 0; k < n; ++k) test_sphere(lds_sph[k], ray, closest, kind, hidx, base + k);
+                    const uint32_t first = base * kSphPer;
+                    const uint32_t cnt = min(n * kSphPer, p.nsph - first);
+                    intersect_range<OPT>(lds_tri, 0, 0, lds_sph, first, cnt, ray, closest, kind, hidx);
                 }
             }
         } else if (active) {
-            for (uint32_t k = 0; k < p.ntri; ++k)
-                test_triangle(lds_tri[3 * k], lds_tri[3 * k + 1], lds_tri[3 * k + 2], ray, closest, kind, hidx, k);
-            for (uint32_t k = 0; k < p.nsph; ++k) test_sphere(lds_sph[k], ray, closest, kind, hidx, k);
+            intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
         }
 
         // ------------------------------------------------ shade (path_tracer.cu:297-316)
+        bool term = false;
+        float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
         if (active) {
             ++nrays;
-            bool term;
-            float Lx, Ly, Lz;
             if (kind == kHitSphere) {
-                const float s = oren_nayar_scatter(g_sph[hidx], closest, ray, st);
+                if (OPT & kOptStats) ++s_scatter_lanes;
+                const float s = oren_nayar_scatter<OPT>(g_sph_plain[hidx], closest, ray, st);
                 if (depth + 1 >= p.max_depth) {
                     term = true;                 // the last record is this scatter (biased, :252)
                     Lx = s;
                     Ly = s;
                     Lz = s;
                 } else {
-                    term = false;
 #pragma unroll
                     for (int i = MAXD - 1; i > 0; --i) stk[i] = stk[i - 1];
                     stk[0] = s;
@@ -398,9 +589,21 @@ __global__ __launch_bounds__(kRenderBlock) void iqpt_render_kernel(const kparams
                 Ly = one_a + a * 0.7f;
                 Lz = one_a + a * 1.0f;
             }
-            if (term) {
-                // backward product over the stacked records, newest first (:321-324)
-                float cx = Lx, cy = Ly, cz = Lz;
+        }
+        if (OPT & kOptStats) {
+            if (__ballot(active && kind == kHitSphere)) ++s_scatter_exec;
+            const uint64_t tm = __ballot(term);
+            if (tm) {
+                ++s_term_exec;
+                s_term_lanes += (unsigned long long)__popcll(tm);
+            }
+        }
+
+        // ------------------------------------------------ path end: product, clamp, running mean
+        if (term) {
+            // backward product over the stacked records, newest first (:321-324)
+            float cx = Lx, cy = Ly, cz = Lz;
+            if (depth > 0) {                     // most paths end on their first ray
 #pragma unroll
                 for (int i = 0; i < MAXD; ++i) {
                     if (i < depth) {
@@ -409,43 +612,50 @@ __global__ __launch_bounds__(kRenderBlock) void iqpt_render_kernel(const kparams
                         cz = cz * stk[i];
                     }
                 }
-                // clamp (:345-347), path_color = 0 + color (:341,348), running mean (:356-358)
-                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                cx = 0.0f + cx;
-                cy = 0.0f + cy;
-                cz = 0.0f + cz;
-                const uint64_t n = p.frame0 + done + 1;
-                const float nf = (float)n;
-                const float keep = (float)(n - 1) / nf;
-                acc.x = cx / nf + acc.x * keep;
-                acc.y = cy / nf + acc.y * keep;
-                acc.z = cz / nf + acc.z * keep;
-                ++done;
-                depth = 0;
-                if (done == p.spp) {
-                    // pixel complete: BGRA8 (:360-365), accumulator and RNG state back to HBM
-                    const uint32_t r8 = to_u8(255.0f * iq_sqrtf(acc.x));
-                    const uint32_t g8 = to_u8(255.0f * iq_sqrtf(acc.y));
-                    const uint32_t b8 = to_u8(255.0f * iq_sqrtf(acc.z));
-                    p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
-                    float4_storage o;
-                    o.x = acc.x;
-                    o.y = acc.y;
-                    o.z = acc.z;
-                    o.w = acc.w;
-                    p.lin[pix] = o;
-                    p.rng[pix] = st.v0;
-                    p.rng[(size_t)p.npix + pix] = st.v1;
-                    p.rng[2 * (size_t)p.npix + pix] = st.v2;
-                    p.rng[3 * (size_t)p.npix + pix] = st.v3;
-                    p.rng[4 * (size_t)p.npix + pix] = st.v4;
-                    p.rng[5 * (size_t)p.npix + pix] = st.d;
-                    active = false;
-                } else {
-                    camera_ray(p, px, py, st, ray);
-                }
+            }
+            // clamp (:345-347), path_color = 0 + color (:341,348), running mean (:356-358)
+            cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+            cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+            cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+            cx = 0.0f + cx;
+            cy = 0.0f + cy;
+            cz = 0.0f + cz;
+            const uint64_t n = p.frame0 + done + 1;
+            const float nf = (float)n;
+            float keep, rc = 0.0f;
+            if (use_tab) {
+                const float2 tv = lds_tab[done];
+                rc = tv.x;
+                keep = tv.y;
+            } else {
+                keep = (float)(n - 1) / nf;
+            }
+            acc.x = mean_term<OPT>(cx, nf, rc) + acc.x * keep;
+            acc.y = mean_term<OPT>(cy, nf, rc) + acc.y * keep;
+            acc.z = mean_term<OPT>(cz, nf, rc) + acc.z * keep;
+            ++done;
+            depth = 0;
+            if (done == p.spp) {
+                // pixel complete: BGRA8 (:360-365), accumulator and RNG state back to HBM
+                const uint32_t r8 = to_u8(255.0f * iq_sqrtf(acc.x));
+                const uint32_t g8 = to_u8(255.0f * iq_sqrtf(acc.y));
+                const uint32_t b8 = to_u8(255.0f * iq_sqrtf(acc.z));
+                p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+                float4_storage o;
+                o.x = acc.x;
+                o.y = acc.y;
+                o.z = acc.z;
+                o.w = acc.w;
+                p.lin[pix] = o;
+                p.rng[pix] = st.v0;
+                p.rng[(size_t)p.npix + pix] = st.v1;
+                p.rng[2 * (size_t)p.npix + pix] = st.v2;
+                p.rng[3 * (size_t)p.npix + pix] = st.v3;
+                p.rng[4 * (size_t)p.npix + pix] = st.v4;
+                p.rng[5 * (size_t)p.npix + pix] = st.d;
+                active = false;
+            } else {
+                camera_ray<OPT>(p, px, py, st, ray);
             }
         }
         if (!exhausted && __any(!active)) refill();
@@ -456,6 +666,21 @@ __global__ __launch_bounds__(kRenderBlock) void iqpt_render_kernel(const kparams
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
     if (lane == 0 && sum) atomicAdd(p.rays, (unsigned long long)sum);
+    if (OPT & kOptStats) {
+        unsigned long long scat = s_scatter_lanes;
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) scat += __shfl_xor(scat, off);
+        if (lane == 0 && p.stats) {
+            atomicAdd(p.stats + 0, s_iter);
+            atomicAdd(p.stats + 1, s_ready);
+            atomicAdd(p.stats + 2, s_ready);
+            atomicAdd(p.stats + 3, s_scatter_exec);
+            atomicAdd(p.stats + 4, scat);
+            atomicAdd(p.stats + 5, s_term_exec);
+            atomicAdd(p.stats + 6, s_term_lanes);
+            atomicAdd(p.stats + 7, 1ull);
+        }
+    }
 }
 
 // curand_init(seed, global pixel id, 0) per owned pixel (renderer_init_kernel, path_tracer.cu:36-46).
@@ -482,16 +707,54 @@ __global__ __launch_bounds__(256) void iqpt_rng_init_kernel(uint32_t width, uint
     rng[5 * (size_t)npix + p] = s.d;
 }
 
-template <int MAXD, bool STREAM>
-int launch_render_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_render_kernel<MAXD, STREAM>), dim3(grid), dim3(kRenderBlock), lds, stream, p);
+template <int MAXD, bool STREAM, int OPT>
+int launch_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
+    hipLaunchKernelGGL((iqpt_render_kernel<MAXD, STREAM, OPT>), dim3(grid), dim3(kRenderBlock), lds, stream, p);
     return (int)hipGetLastError();
 }
-
-template <int MAXD, bool STREAM>
-int occupancy_t(uint32_t lds, int* blocks) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_render_kernel<MAXD, STREAM>,
+template <int MAXD, bool STREAM, int OPT>
+int occ_t(uint32_t lds, int* blocks) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_render_kernel<MAXD, STREAM, OPT>,
                                                              kRenderBlock, lds);
+}
+
+// Variant table: the production option set for every (MAXD, STREAM), plus (in IQPT_AB_VARIANTS
+// builds) the A/B set used by tools/ab_kernel.py.
+struct variant {
+    int maxd;
+    bool stream;
+    int opt;
+    int (*launch)(hipStream_t, const kparams&, uint32_t, uint32_t);
+    int (*occ)(uint32_t, int*);
+};
+#define IQPT_V(M, S, O) {M, S, O, launch_t<M, S, O>, occ_t<M, S, O>}
+const variant kVariants[] = {
+    // MAXD 16 would spill under the 96-VGPR bound of kOptLB5 (16 stack registers): 4 waves/SIMD
+    IQPT_V(8, false, kOptDefault), IQPT_V(8, true, kOptDefault),
+    IQPT_V(16, false, kOptDefault & ~kOptLB5), IQPT_V(16, true, kOptDefault & ~kOptLB5),
+#if defined(IQPT_AB_VARIANTS)
+    IQPT_V(8, false, 0),
+    IQPT_V(8, true, 0),
+    IQPT_V(8, false, kOptDefault & ~kOptPair),
+    IQPT_V(8, true, kOptDefault & ~kOptPair),
+    IQPT_V(8, false, kOptDefault & ~kOptSinCos),
+    IQPT_V(8, false, kOptDefault | kOptLB5),
+    IQPT_V(8, false, kOptDefault | kOptLB6),
+    IQPT_V(8, false, kOptDefault | kOptBranchless),
+    IQPT_V(8, false, kOptDefault | kOptBranchless | kOptLB5),
+    IQPT_V(8, false, (kOptDefault & ~kOptPair) | kOptLB6),
+    IQPT_V(8, true, kOptDefault | kOptLB5),
+    IQPT_V(8, false, kOptDefault | kOptStats),
+    IQPT_V(8, true, kOptDefault | kOptStats),
+#endif
+};
+#undef IQPT_V
+
+const variant* find_variant(int max_depth, bool stream, int opt) {
+    const int maxd = max_depth <= 8 ? 8 : 16;
+    for (const variant& v : kVariants)
+        if (v.maxd == maxd && v.stream == stream && v.opt == opt) return &v;
+    return nullptr;
 }
 
 }  // namespace
@@ -505,17 +768,20 @@ int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, u
     return (int)hipGetLastError();
 }
 
-int launch_render(void* stream, const kparams& p, uint32_t grid, uint32_t lds, bool stream_batches) {
-    hipStream_t s = (hipStream_t)stream;
-    if (p.max_depth <= 8) {
-        return stream_batches ? launch_render_t<8, true>(s, p, grid, lds) : launch_render_t<8, false>(s, p, grid, lds);
-    }
-    return stream_batches ? launch_render_t<16, true>(s, p, grid, lds) : launch_render_t<16, false>(s, p, grid, lds);
+int launch_render(void* stream, const kparams& p, uint32_t grid, uint32_t lds, bool stream_batches, int opt) {
+    const variant* v = find_variant(p.max_depth, stream_batches, opt);
+    if (!v) return (int)hipErrorInvalidDeviceFunction;
+    return v->launch((hipStream_t)stream, p, grid, lds);
 }
 
-int render_occupancy(int max_depth, bool stream_batches, uint32_t lds, int* blocks) {
-    if (max_depth <= 8) return stream_batches ? occupancy_t<8, true>(lds, blocks) : occupancy_t<8, false>(lds, blocks);
-    return stream_batches ? occupancy_t<16, true>(lds, blocks) : occupancy_t<16, false>(lds, blocks);
+int render_occupancy(int max_depth, bool stream_batches, int opt, uint32_t lds, int* blocks) {
+    const variant* v = find_variant(max_depth, stream_batches, opt);
+    if (!v) return (int)hipErrorInvalidDeviceFunction;
+    return v->occ(lds, blocks);
+}
+
+bool render_variant_exists(int max_depth, bool stream_batches, int opt) {
+    return find_variant(max_depth, stream_batches, opt) != nullptr;
 }
 
 const char* render_kernel_name() { return "iqpt_render_kernel"; }

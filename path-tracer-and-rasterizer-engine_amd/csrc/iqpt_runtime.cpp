@@ -6,7 +6,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -71,6 +73,7 @@ struct iqpt_ctx {
     int max_depth = 0;
     uint64_t frame = 0;
     int num_cus = 0;
+    int opt = iqpt::kOptDefault;
     bool have_camera = false, have_packet = false;
     iqpt_camera cam{};
     // pixel state (compact over the owned set)
@@ -79,10 +82,13 @@ struct iqpt_ctx {
     uint32_t* d_rng = nullptr;
     unsigned long long* d_rays = nullptr;
     uint32_t* d_queue = nullptr;
+    unsigned long long* d_stats = nullptr;   // kOptStats counters (diagnostic variants)
     // scene (world space)
     float4_storage* d_tris = nullptr;
+    float4_storage* d_tri_pairs = nullptr;
     float4_storage* d_tri_shade = nullptr;
     float4_storage* d_sph = nullptr;
+    float4_storage* d_sph_pairs = nullptr;
     uint32_t ntri = 0, nsph = 0;
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
@@ -97,10 +103,10 @@ int use_device(const iqpt_ctx* c) {
 }
 
 void free_scene(iqpt_ctx* c) {
-    if (c->d_tris) (void)hipFree(c->d_tris);
-    if (c->d_tri_shade) (void)hipFree(c->d_tri_shade);
-    if (c->d_sph) (void)hipFree(c->d_sph);
-    c->d_tris = c->d_tri_shade = c->d_sph = nullptr;
+    for (float4_storage** b : {&c->d_tris, &c->d_tri_pairs, &c->d_tri_shade, &c->d_sph, &c->d_sph_pairs}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
     c->ntri = c->nsph = 0;
 }
 
@@ -215,6 +221,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->d_rng) (void)hipFree(c->d_rng);
     if (c->d_rays) (void)hipFree(c->d_rays);
     if (c->d_queue) (void)hipFree(c->d_queue);
+    if (c->d_stats) (void)hipFree(c->d_stats);
     for (auto& pr : c->timed) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -289,6 +296,22 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         const iqpt_sphere_drawcall& s = pk->sphere_dcs[i];
         sph.push_back({s.center[0], s.center[1], s.center[2], s.radius});
     }
+    // pair layouts (iqpt_internal.hpp): SoA inside each pair of consecutive primitives
+    std::vector<float4_storage> tri_pairs, sph_pairs;
+    const size_t ntp = (total + 1) / 2, nsp = ((size_t)nsdc + 1) / 2;
+    tri_pairs.resize(ntp * iqpt::kTriPairFloat4, float4_storage{0.0f, 0.0f, 0.0f, 0.0f});
+    for (size_t k = 0; k < total; ++k) {
+        const float4_storage* t = &tris[k * iqpt::kTriFloat4];
+        const float f[9] = {t[0].x, t[0].y, t[0].z, t[0].w, t[1].x, t[1].y, t[1].z, t[1].w, t[2].x};
+        float* dst = &tri_pairs[(k / 2) * iqpt::kTriPairFloat4].x;     // 20 floats, component c at 2c + (k & 1)
+        for (int comp = 0; comp < 9; ++comp) dst[2 * comp + (k & 1)] = f[comp];
+    }
+    sph_pairs.resize(nsp * iqpt::kSphPairFloat4, float4_storage{0.0f, 0.0f, 0.0f, 0.0f});
+    for (size_t k = 0; k < nsdc; ++k) {
+        const float f[4] = {sph[k].x, sph[k].y, sph[k].z, sph[k].w};
+        float* dst = &sph_pairs[(k / 2) * iqpt::kSphPairFloat4].x;
+        for (int comp = 0; comp < 4; ++comp) dst[2 * comp + (k & 1)] = f[comp];
+    }
     int st = use_device(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
@@ -301,7 +324,9 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         IQPT_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(float4_storage), hipMemcpyHostToDevice));
         return IQPT_OK;
     };
-    if ((st = upload(tris, &c->d_tris)) || (st = upload(shade, &c->d_tri_shade)) || (st = upload(sph, &c->d_sph))) {
+    if ((st = upload(tris, &c->d_tris)) || (st = upload(tri_pairs, &c->d_tri_pairs)) ||
+        (st = upload(shade, &c->d_tri_shade)) || (st = upload(sph, &c->d_sph)) ||
+        (st = upload(sph_pairs, &c->d_sph_pairs))) {
         free_scene(c);
         return st;
     }
@@ -332,33 +357,59 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     p.max_depth = c->max_depth;
     std::memcpy(p.inv_proj, c->cam.inv_proj, sizeof p.inv_proj);
     std::memcpy(p.inv_view, c->cam.inv_view, sizeof p.inv_view);
+    {
+        // w of the unprojected near/far points is a launch constant when the perspective row of
+        // the inverse projection is (0, 0, m23, m33) with finite non-zero m23, m33 (camera_ray).
+        const float* P = c->cam.inv_proj;
+        const float wf = P[11] + P[15];
+        const bool fin = std::isfinite(P[11]) && std::isfinite(P[15]) && std::isfinite(wf);
+        if (P[3] == 0.0f && P[7] == 0.0f && fin && P[11] != 0.0f && P[15] != 0.0f && wf != 0.0f) {
+            p.cam_const = 1;
+            p.cam_near_rw = 1.0f / P[15];
+            p.cam_far_rw = 1.0f / wf;
+        }
+    }
+    p.acc_tab = spp <= iqpt::kAccTableMax ? 1u : 0u;
     p.tris = c->d_tris;
+    p.tri_pairs = c->d_tri_pairs;
     p.ntri = c->ntri;
+    p.ntri_pairs = (c->ntri + 1) / 2;
     p.spheres = c->d_sph;
+    p.sph_pairs = c->d_sph_pairs;
     p.nsph = c->nsph;
-    const uint64_t resident = (uint64_t)c->ntri * iqpt::kTriFloat4 * 16 + (uint64_t)c->nsph * 16;
+    p.nsph_pairs = (c->nsph + 1) / 2;
+    // the production variant for max_depth > 8 carries 16 stack registers and no 5-wave bound
+    const int opt = (c->max_depth > 8 && c->opt == iqpt::kOptDefault) ? (c->opt & ~iqpt::kOptLB5) : c->opt;
+    const bool pair = (opt & iqpt::kOptPair) != 0;
+    const uint32_t tri_rec = pair ? iqpt::kTriPairFloat4 * 16 : iqpt::kTriFloat4 * 16;   // bytes per LDS record
+    const uint32_t sph_rec = pair ? iqpt::kSphPairFloat4 * 16 : 16;
+    const uint32_t tri_recs = pair ? p.ntri_pairs : p.ntri;
+    const uint32_t sph_recs = pair ? p.nsph_pairs : p.nsph;
+    const uint64_t resident = (uint64_t)tri_recs * tri_rec + (uint64_t)sph_recs * sph_rec;
     const bool stream_batches = resident > iqpt::kLdsResidentBytes;
     if (stream_batches) {
-        p.tri_batch = iqpt::kTriBatch;
-        p.sph_batch = iqpt::kSphBatch;
+        p.tri_batch = pair ? iqpt::kTriBatch / 2 : iqpt::kTriBatch;   // records
+        p.sph_batch = pair ? iqpt::kSphBatch / 2 : iqpt::kSphBatch;
     } else {
-        p.tri_batch = c->ntri;
-        p.sph_batch = c->nsph;
+        p.tri_batch = tri_recs;
+        p.sph_batch = sph_recs;
     }
-    const uint32_t lds = std::max<uint32_t>(16u, p.tri_batch * iqpt::kTriFloat4 * 16 + p.sph_batch * 16);
+    const uint32_t lds = std::max<uint32_t>(16u, p.tri_batch * tri_rec + p.sph_batch * sph_rec +
+                                                     (p.acc_tab ? spp * 8u : 0u));
     p.lin = c->d_lin;
     p.bgra = c->d_bgra;
     p.rng = c->d_rng;
     p.rays = c->d_rays;
     p.queue = c->d_queue;
+    p.stats = c->d_stats;
     int occ = 0;
-    if (iqpt::render_occupancy(c->max_depth, stream_batches, lds, &occ) != 0 || occ < 1) occ = 1;
+    if (iqpt::render_occupancy(c->max_depth, stream_batches, opt, lds, &occ) != 0 || occ < 1) occ = 1;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
     IQPT_HIP(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), c->stream));
     hipEvent_t e0 = take_event(c), e1 = take_event(c);
     if (e0) (void)hipEventRecord(e0, c->stream);
-    int le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches);
+    int le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
     if (e1) (void)hipEventRecord(e1, c->stream);
     if (e0 && e1) c->timed.emplace_back(e0, e1);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "render kernel launch");
@@ -458,6 +509,37 @@ int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
     *total_ms = sum;
     *launches = c->timed.size();
     c->timed.clear();
+    return IQPT_OK;
+}
+
+/* Internal (tools/ab_kernel.py): select the kernel option mask of a context and read the
+ * diagnostic counters of kOptStats variants. Not part of include/iqpt.h. */
+int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    if (!iqpt::render_variant_exists(c->max_depth, false, opt) && !iqpt::render_variant_exists(c->max_depth, true, opt))
+        return iqpt::fail(IQPT_ERR_UNSUPPORTED, "kernel option set not compiled into this build");
+    int st = use_device(c);
+    if (st) return st;
+    if ((opt & iqpt::kOptStats) && !c->d_stats) {
+        if (hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "stats");
+        IQPT_HIP(hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
+    }
+    c->opt = opt;
+    return IQPT_OK;
+}
+
+int iqpt_debug_read_stats(iqpt_ctx* c, unsigned long long* out8) {
+    if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    if (!c->d_stats) {
+        std::memset(out8, 0, 8 * sizeof(unsigned long long));
+        return IQPT_OK;
+    }
+    IQPT_HIP(hipMemcpy(out8, c->d_stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    IQPT_HIP(hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
     return IQPT_OK;
 }
 

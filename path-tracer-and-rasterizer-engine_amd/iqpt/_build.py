@@ -26,6 +26,7 @@ ORACLE_DIR = REPO / "oracle"
 BUILD_DIR = PROJ_DIR / "build"
 
 LIB_PATH = PKG_DIR / "libiqpt.so"
+AB_LIB_PATH = PKG_DIR / "libiqpt_ab.so"        # + A/B kernel variants (tools/ab_kernel.py)
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 ORACLE_GLIBC_LIB = ORACLE_DIR / "liboracle_glibc.so"
 CLI_PATH = PKG_DIR / "iqpt_cli"
@@ -61,25 +62,27 @@ def _headers() -> list[Path]:
     return sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("*.hpp")) + sorted(INCLUDE.glob("*.h"))
 
 
-def build_lib(force: bool = False) -> Path:
-    """Compile the HIP kernels + runtime into libiqpt.so (gfx950)."""
+def build_lib(force: bool = False, ab: bool = False) -> Path:
+    """Compile the HIP kernels + runtime into libiqpt.so (gfx950); ab=True adds the A/B variants."""
+    target = AB_LIB_PATH if ab else LIB_PATH
     srcs = [CSRC / s for s in LIB_SOURCES]
-    if not force and _newer(LIB_PATH, srcs + _headers() + [Path(__file__)]):
-        return LIB_PATH
-    BUILD_DIR.mkdir(parents=True, exist_ok=True)
+    if not force and _newer(target, srcs + _headers() + [Path(__file__)]):
+        return target
+    bdir = BUILD_DIR / ("ab" if ab else "prod")
+    bdir.mkdir(parents=True, exist_ok=True)
     objs = []
     cmds = []
+    extra = ["-DIQPT_AB_VARIANTS"] if ab else []
     for s in srcs:
-        o = BUILD_DIR / (s.name + ".o")
-        lang = ["-x", "hip"] if s.suffix in (".hip",) else ["-x", "hip"]
-        cmds.append([HIPCC, *HIP_FLAGS, *lang, "-c", str(s), "-o", str(o)])
+        o = bdir / (s.name + ".o")
+        cmds.append([HIPCC, *HIP_FLAGS, *extra, "-x", "hip", "-c", str(s), "-o", str(o)])
         objs.append(o)
     with ThreadPoolExecutor(max_workers=min(4, len(cmds))) as ex:
         list(ex.map(_run, cmds))
-    tmp = LIB_PATH.with_suffix(".so.tmp")
+    tmp = target.with_suffix(".so.tmp")
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp)])
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+    os.replace(tmp, target)
+    return target
 
 
 def build_tools(force: bool = False) -> list[Path]:
