@@ -54,6 +54,7 @@ struct kparams {
     uint32_t cam_const;              // inverse projection has constant w (see camera_ray)
     float cam_near_rw, cam_far_rw;   // 1 / w_near, 1 / w_far when cam_const
     uint32_t acc_tab;                // build the per-launch (1/n, (n-1)/n) table in LDS
+    uint32_t frames32;               // frame0 + spp < 2^32: 32-bit frame-counter conversions
     const float4_storage* tris;      // ntri * kTriFloat4 (single layout)
     const float4_storage* tri_pairs; // ntri_pairs * kTriPairFloat4 (pair layout)
     uint32_t ntri, ntri_pairs;
@@ -80,7 +81,7 @@ constexpr int kOptSinCos = 1 << 5;     // shared reduction for cos(phi), sin(phi
 constexpr int kOptBranchless = 1 << 6; // pair MT without early exits (small resident scenes)
 constexpr int kOptStats = 1 << 7;      // wave-level counters (diagnostic builds)
 constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5;
-constexpr uint32_t kAccTableMax = 4096;  // spp per launch covered by the LDS table
+constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.
 int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, uint32_t y0,

@@ -371,9 +371,9 @@ __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
 // c / n of the running mean (path_tracer.cu:356-358). kOptAccTable: 1/n is read from a per-launch
 // table built with the same IEEE division (so c = 1 gives the identical bits) and 0/n = +0 (c is
 // never -0 here: path_color = 0 + color).
-template <int OPT>
-__device__ __forceinline__ float mean_term(float c, float nf, float rc) {
-    if (OPT & kOptAccTable) {
+// `tab` is false when the launch has more samples than the table holds (rc is then not set).
+__device__ __forceinline__ float mean_term(float c, float nf, float rc, bool tab) {
+    if (tab) {
         if (c == 1.0f) return rc;
         if (c == 0.0f) return 0.0f;
     }
@@ -621,18 +621,20 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
             cy = 0.0f + cy;
             cz = 0.0f + cz;
             const uint64_t n = p.frame0 + done + 1;
-            const float nf = (float)n;
+            // (float)n of the 64-bit frame counter; when every frame of the launch fits 32 bits the
+            // 32-bit conversion is the same correctly rounded value (one v_cvt_f32_u32)
+            const float nf = p.frames32 ? (float)(uint32_t)n : (float)n;
             float keep, rc = 0.0f;
             if (use_tab) {
                 const float2 tv = lds_tab[done];
                 rc = tv.x;
                 keep = tv.y;
             } else {
-                keep = (float)(n - 1) / nf;
+                keep = (p.frames32 ? (float)(uint32_t)(n - 1) : (float)(n - 1)) / nf;
             }
-            acc.x = mean_term<OPT>(cx, nf, rc) + acc.x * keep;
-            acc.y = mean_term<OPT>(cy, nf, rc) + acc.y * keep;
-            acc.z = mean_term<OPT>(cz, nf, rc) + acc.z * keep;
+            acc.x = mean_term(cx, nf, rc, use_tab) + acc.x * keep;
+            acc.y = mean_term(cy, nf, rc, use_tab) + acc.y * keep;
+            acc.z = mean_term(cz, nf, rc, use_tab) + acc.z * keep;
             ++done;
             depth = 0;
             if (done == p.spp) {

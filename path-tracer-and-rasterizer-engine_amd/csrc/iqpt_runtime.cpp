@@ -370,6 +370,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
         }
     }
     p.acc_tab = spp <= iqpt::kAccTableMax ? 1u : 0u;
+    p.frames32 = (c->frame + (uint64_t)spp) < (1ull << 32) ? 1u : 0u;
     p.tris = c->d_tris;
     p.tri_pairs = c->d_tri_pairs;
     p.ntri = c->ntri;
