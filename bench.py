@@ -47,6 +47,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--verify-rows", type=int, default=16)
     ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r01_pmc_traffic.json"))
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo = rehearsal)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="all ranks on GPU 0 (multi-rank rehearsal on a 1-GPU box; use with --backend gloo)")
+    ap.add_argument("--save-frame", default="", help="rank 0 writes the assembled float frame (.npy)")
     return ap.parse_args()
 
 
@@ -97,9 +102,15 @@ def main():
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
+    # Rehearsal of the multi-rank path on a 1-GPU box: every rank on device 0 and the gather over
+    # gloo through host memory (RCCL refuses two ranks on one GPU). The driver's runs use nccl.
+    device = 0 if args.one_device else local_rank
+    torch.cuda.set_device(device)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+        else:
+            dist.init_process_group("gloo")
 
     def barrier():
         if world > 1:
@@ -112,12 +123,14 @@ def main():
     stats = packet_stats(pk)
     cam = make_camera(cfg.width, cfg.height)
     ps = iqdist.pixel_set_for_rank(cfg.width, cfg.height, rank, world)
-    pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth, device=local_rank)
+    pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth, device=device)
     pt.set_camera(cam)
     pt.upload_packet(pk)
 
     max_px = iqdist.max_rows(cfg.height, world) * cfg.width
-    accum = torch.zeros((max_px, 4), dtype=torch.float32, device="cuda") if world > 1 else None
+    on_gpu = args.backend == "nccl"
+    accum = (torch.zeros((max_px, 4), dtype=torch.float32, device="cuda" if on_gpu else "cpu")
+             if world > 1 else None)
     gather_list = ([torch.empty_like(accum) for _ in range(world)] if (world > 1 and rank == 0) else None)
     frame = None
 
@@ -125,7 +138,11 @@ def main():
         nonlocal frame
         pt.render(cfg.spp)
         if world > 1:
-            pt.copy_accum_device(accum.data_ptr(), accum.numel() * 4)
+            if on_gpu:
+                pt.copy_accum_device(accum.data_ptr(), accum.numel() * 4)     # D2D, then RCCL
+            else:
+                lin_host, _ = pt.read()
+                accum[: lin_host.shape[0]] = torch.from_numpy(lin_host)
             dist.gather(accum, gather_list, dst=0)
             if rank == 0:
                 frame = iqdist.assemble(gather_list, cfg.width, cfg.height, world)
@@ -155,7 +172,8 @@ def main():
     kern_ms, launches = pt.kernel_time()
 
     vals = torch.tensor([elapsed, float(rays), kern_ms / max(1, launches), verify["rmse"] if verify else 0.0,
-                         verify["bitexact_frac"] if verify else 1.0], dtype=torch.float64, device="cuda")
+                         verify["bitexact_frac"] if verify else 1.0], dtype=torch.float64,
+                        device="cuda" if on_gpu else "cpu")
     if world > 1:
         t_max = vals[0:1].clone()
         dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
@@ -204,7 +222,9 @@ def main():
             "config": {"workload": f"{cfg.name}:{cfg.preset}", "width": cfg.width, "height": cfg.height,
                        "spp_per_step": cfg.spp, "max_depth": cfg.max_depth, "triangles": stats["triangles"],
                        "spheres": stats["spheres"], "partition": f"cyclic rows x{world}",
-                       "collective": "rccl gather of float4 accumulators" if world > 1 else "none"},
+                       "collective": ("none" if world == 1 else
+                                      "rccl gather of float4 accumulators" if on_gpu else
+                                      "gloo gather via host (rehearsal)")},
             "msamples_per_s": round(samples / elapsed / 1e6, 3),
             "rays_per_sample": round(total_rays / samples, 5),
             "rmse_vs_oracle": rmse_v,
@@ -225,6 +245,10 @@ def main():
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, pk, cam, args.cpu_seconds)
+        if args.save_frame:
+            if frame is None:
+                frame = torch.from_numpy(pt.read()[0])
+            np.save(args.save_frame, frame.cpu().numpy() if hasattr(frame, "cpu") else frame)
         print(json.dumps(out), flush=True)
     pt.close()
     if world > 1:
