@@ -37,6 +37,22 @@
 
 #define IQ_INLINE static inline IQ_HD
 
+/* Divisions inside the functions below. In the GPU pass of a TU that opts in (IQ_FP_FASTDIV) they
+ * use the short correctly rounded forms of iq_fastdiv.h (bit-identical to IEEE division, verified
+ * exhaustively / on 2^36 pairs per class by tools/fastdiv_check.hip); everywhere else plain IEEE
+ * division. IQ_RCP and IQ_DIV are exact for every operand; IQ_DIV_N needs |a| in {0} U
+ * [2^-100, 2^100], |b| in [2^-100, 2^100] and a normal quotient (stated where it is used). */
+#if defined(__HIP_DEVICE_COMPILE__) && defined(IQ_FP_FASTDIV)
+#include "iq_fastdiv.h"
+#define IQ_RCP(x) iq_rcp_guarded(x)
+#define IQ_DIV(a, b) iq_div((a), (b))
+#define IQ_DIV_N(a, b) iq_div_pre((a), (b), iq_rcp(b))
+#else
+#define IQ_RCP(x) (1.0f / (x))
+#define IQ_DIV(a, b) ((a) / (b))
+#define IQ_DIV_N(a, b) ((a) / (b))
+#endif
+
 /* constants of IoniqRE/iqmath.h:6-11 */
 #define IQ_PI        3.1415926535897932384626433832795f
 #define IQ_TAU       6.283185307179586476925286766559f
@@ -184,7 +200,7 @@ IQ_INLINE float iq_tanf(float x) {
     } else {
         y = r;
     }
-    if (j & 2) y = -1.0f / y;
+    if (j & 2) y = -IQ_RCP(y);
     return (iq_f2u(x) >> 31) ? -y : y;
 }
 
@@ -221,8 +237,9 @@ IQ_INLINE float iq_atanf(float x) {
     if (iq_isnan(x)) return x;
     float ax = iq_fabsf(x);
     float y, r;
-    if (ax > 2.414213562373095f) { y = IQ_PI_DIV_2; r = -(1.0f / ax); }
-    else if (ax > 0.4142135623730950f) { y = IQ_PI_DIV_4; r = (ax - 1.0f) / (ax + 1.0f); }
+    /* (ax - 1) is 0 or in [2^-24, 1.5) and (ax + 1) in (1.4, 3.5): inside IQ_DIV_N's range */
+    if (ax > 2.414213562373095f) { y = IQ_PI_DIV_2; r = -IQ_RCP(ax); }
+    else if (ax > 0.4142135623730950f) { y = IQ_PI_DIV_4; r = IQ_DIV_N(ax - 1.0f, ax + 1.0f); }
     else { y = 0.0f; r = ax; }
     float z = r * r;
     y = y + ((((8.05374449538e-2f * z - 1.38776856032e-1f) * z + 1.99777106478e-1f) * z
@@ -247,7 +264,7 @@ IQ_INLINE float iq_atan2f(float y, float x) {
         res = xsign ? IQ_PI : 0.0f;
     } else {
         float ay = iq_fabsf(y);
-        float z = iq_atanf(ay / iq_fabsf(x));
+        float z = iq_atanf(IQ_DIV(ay, iq_fabsf(x)));
         res = xsign ? IQ_PI - z : z;
     }
     return ysign ? -res : res;

@@ -53,6 +53,7 @@ struct kparams {
     float inv_view[16];
     uint32_t cam_const;              // inverse projection has constant w (see camera_ray)
     float cam_near_rw, cam_far_rw;   // 1 / w_near, 1 / w_far when cam_const
+    float rcp_width, rcp_height;     // RN(1 / W), RN(1 / H) (kOptFastDiv camera divisions)
     uint32_t acc_tab;                // build the per-launch (1/n, (n-1)/n) table in LDS
     uint32_t frames32;               // frame0 + spp < 2^32: 32-bit frame-counter conversions
     const float4_storage* tris;      // ntri * kTriFloat4 (single layout)
@@ -80,7 +81,8 @@ constexpr int kOptLB6 = 1 << 4;        // __launch_bounds__ min 6 waves/SIMD (<=
 constexpr int kOptSinCos = 1 << 5;     // shared reduction for cos(phi), sin(phi)
 constexpr int kOptBranchless = 1 << 6; // pair MT without early exits (small resident scenes)
 constexpr int kOptStats = 1 << 7;      // wave-level counters (diagnostic builds)
-constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5;
+constexpr int kOptFastDiv = 1 << 8;    // short exact reciprocal / division forms (iq_fastdiv.h)
+constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.

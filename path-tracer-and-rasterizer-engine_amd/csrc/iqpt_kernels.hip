@@ -28,6 +28,7 @@
 //    (argued where it is taken). Results are bit-identical to the CPU oracle.
 #include <hip/hip_runtime.h>
 
+#include "iq_fastdiv.h"
 #include "iq_fp.h"
 #include "iq_xorwow.h"
 #include "iqpt_internal.hpp"
@@ -42,6 +43,8 @@ namespace {
 constexpr float kTMin = 0.000001f;       // path_tracer.cu:241
 constexpr float kTMax = 999.99f;
 constexpr int kHitNone = 0, kHitTri = 1, kHitSphere = 2;
+constexpr float kRcpPi = 0x1.45f306p-2f;   // RN(1 / IQ_PI) of the float IQ_PI
+static_assert(1.0f / IQ_PI == kRcpPi, "kRcpPi must be the correctly rounded reciprocal of the float pi");
 
 typedef float f2 __attribute__((ext_vector_type(2)));
 
@@ -66,12 +69,29 @@ __device__ __forceinline__ float rand_real(rng6& s, float lo, float hi) {
     return u * (hi - lo) + lo;
 }
 
+// IEEE 1/x under kOptFastDiv (iq_fastdiv.h), the generic expansion otherwise.
+// rcp_scene: x is a Möller–Trumbore determinant with |det| >= 1e-6 or a sphere radius; the runtime
+// launches kOptFastDiv variants only when every edge component and radius of the packet is within
+// 2^60 (radii 0 or >= 2^-60), so |det| <= |e1| |e2| |dir| < 2^126 and 1/r is in iq_rcp's exact range.
+template <int OPT>
+__device__ __forceinline__ float rcp_scene(float x) {
+    if (OPT & kOptFastDiv) return iq_rcp(x);
+    return 1.0f / x;
+}
+// rcp_any: no range known (a rarely taken branch keeps the generic expansion outside iq_rcp's range).
+template <int OPT>
+__device__ __forceinline__ float rcp_any(float x) {
+    if (OPT & kOptFastDiv) return iq_rcp_guarded(x);
+    return 1.0f / x;
+}
+
 // dot4(v, column c of M) of iqvec::transformed (vector.h:371-383); M row-major m[r][c].
 __device__ __forceinline__ float dot_col(float x, float y, float z, float w, const float* M, int c) {
     return ((x * M[c] + y * M[4 + c]) + z * M[8 + c]) + w * M[12 + c];
 }
 
 // normalized3 (vector.h:239-244) in place.
+template <int OPT>
 __device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
     if (iq_fabsf(x) < 0.00001f && iq_fabsf(y) < 0.00001f && iq_fabsf(z) < 0.00001f) {
         x = 0.0f;
@@ -80,7 +100,7 @@ __device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
         return;
     }
     const float len = iq_sqrtf((x * x + y * y) + z * z);
-    const float inv = 1.0f / len;
+    const float inv = rcp_any<OPT>(len);
     x = x * inv;
     y = y * inv;
     z = z * inv;
@@ -98,9 +118,15 @@ struct ray3 {
 template <int OPT>
 __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_t y, rng6& s, ray3& r) {
     const float jx = rand_real(s, -0.5f, 0.5f);
-    const float x_ndc = (((float)x + jx) / (float)p.width) * 2.0f - 1.0f;
+    // (x + jx) / W: under kOptFastDiv Markstein's correction of (x + jx) * RN(1/W) (RN(1/W) from the
+    // host); exact here since x + jx is 0 or in [2^-32, 2^24] and W in [1, 2^24] (iq_fastdiv.h)
+    const float xs = (float)x + jx;
+    const float x_ndc = ((OPT & kOptFastDiv) ? iq_div_pre(xs, (float)p.width, p.rcp_width)
+                                             : xs / (float)p.width) * 2.0f - 1.0f;
     const float jy = rand_real(s, -0.5f, 0.5f);
-    const float y_ndc = 1.0f - (((float)y + jy) / (float)p.height) * 2.0f;
+    const float ys = (float)y + jy;
+    const float y_ndc = 1.0f - ((OPT & kOptFastDiv) ? iq_div_pre(ys, (float)p.height, p.rcp_height)
+                                                    : ys / (float)p.height) * 2.0f;
     const float* P = p.inv_proj;
     const float* Vw = p.inv_view;
     float nx = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 0);
@@ -114,8 +140,8 @@ __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_
         ninv = p.cam_near_rw;
         finv = p.cam_far_rw;
     } else {
-        ninv = 1.0f / dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 3);
-        finv = 1.0f / dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 3);
+        ninv = rcp_any<OPT>(dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 3));
+        finv = rcp_any<OPT>(dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 3));
     }
     nx = nx * ninv;
     ny = ny * ninv;
@@ -131,7 +157,7 @@ __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_
     const float wfy = dot_col(fx, fy, fz, 1.0f, Vw, 1);
     const float wfz = dot_col(fx, fy, fz, 1.0f, Vw, 2);
     float dx = wfx - wnx, dy = wfy - wny, dz = wfz - wnz;
-    normalize3(dx, dy, dz);
+    normalize3<OPT>(dx, dy, dz);
     r.ox = wnx;
     r.oy = wny;
     r.oz = wnz;
@@ -149,6 +175,7 @@ __device__ __forceinline__ uint32_t to_u8(float f) {
 
 // Möller–Trumbore of shape.cu:62-103 with the hit bookkeeping reduced to (t, index); every reject
 // test is the reference's condition, negated, so NaN behaves identically.
+template <int OPT>
 __device__ __forceinline__ void test_triangle(const float4 a, const float4 b, const float4 c, const ray3 r,
                                               float& closest, int& kind, uint32_t& idx, uint32_t k) {
     const float e1x = a.w, e1y = b.x, e1z = b.y;
@@ -158,7 +185,7 @@ __device__ __forceinline__ void test_triangle(const float4 a, const float4 b, co
     const float pz = r.dx * e2y - r.dy * e2x;
     const float det = (e1x * px + e1y * py) + e1z * pz;
     if (iq_fabsf(det) < 0.000001f) return;                      // is_zero(fabs(det))
-    const float inv = 1.0f / det;
+    const float inv = rcp_scene<OPT>(det);
     const float tx = r.ox - a.x, ty = r.oy - a.y, tz = r.oz - a.z;
     const float u = ((tx * px + ty * py) + tz * pz) * inv;
     if (u < 0.0f || u > 1.0f) return;
@@ -179,6 +206,7 @@ __device__ __forceinline__ void test_triangle(const float4 a, const float4 b, co
 // test against the running closest hit is sequential (k first), as in the reference's loop.
 // Branchless form (kOptBranchless): all stages always evaluated, the reference's reject tests
 // folded into the two `alive` masks; same per-element operations, so the same bits.
+template <int OPT>
 __device__ __forceinline__ void test_triangle_pair_nb(const float4 q0, const float4 q1, const float4 q2,
                                                       const float4 q3, const float4 q4, const ray3 r,
                                                       float& closest, int& kind, uint32_t& idx, uint32_t k,
@@ -190,7 +218,7 @@ __device__ __forceinline__ void test_triangle_pair_nb(const float4 q0, const flo
     const f2 py = r.dz * e2x - r.dx * e2z;
     const f2 pz = r.dx * e2y - r.dy * e2x;
     const f2 det = (e1x * px + e1y * py) + e1z * pz;
-    const f2 inv = {1.0f / det.x, 1.0f / det.y};
+    const f2 inv = {rcp_scene<OPT>(det.x), rcp_scene<OPT>(det.y)};
     const f2 tx = r.ox - v0x, ty = r.oy - v0y, tz = r.oz - v0z;
     const f2 u = ((tx * px + ty * py) + tz * pz) * inv;
     const f2 qx = ty * e1z - tz * e1y;
@@ -215,6 +243,7 @@ __device__ __forceinline__ void test_triangle_pair_nb(const float4 q0, const flo
     }
 }
 
+template <int OPT>
 __device__ __forceinline__ void test_triangle_pair(const float4 q0, const float4 q1, const float4 q2,
                                                    const float4 q3, const float4 q4, const ray3 r, float& closest,
                                                    int& kind, uint32_t& idx, uint32_t k, bool second) {
@@ -228,7 +257,7 @@ __device__ __forceinline__ void test_triangle_pair(const float4 q0, const float4
     bool a0 = !(iq_fabsf(det.x) < 0.000001f);
     bool a1 = second && !(iq_fabsf(det.y) < 0.000001f);
     if (!(a0 || a1)) return;
-    const f2 inv = {1.0f / det.x, 1.0f / det.y};
+    const f2 inv = {rcp_scene<OPT>(det.x), rcp_scene<OPT>(det.y)};
     const f2 tx = r.ox - v0x, ty = r.oy - v0y, tz = r.oz - v0z;
     const f2 u = ((tx * px + ty * py) + tz * pz) * inv;
     a0 = a0 && !(u.x < 0.0f || u.x > 1.0f);
@@ -299,7 +328,7 @@ template <int OPT>
 __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, ray3& r, rng6& s) {
     // hit point and outward normal (shape.cu:36-44)
     const float hx = r.ox + t * r.dx, hy = r.oy + t * r.dy, hz = r.oz + t * r.dz;
-    const float rinv = 1.0f / sph.w;
+    const float rinv = rcp_scene<OPT>(sph.w);
     float nx = (hx - sph.x) * rinv, ny = (hy - sph.y) * rinv, nz = (hz - sph.z) * rinv;
     if (!((r.dx * nx + r.dy * ny) + r.dz * nz < 0.0f)) {
         nx = -nx;
@@ -308,12 +337,12 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     }
     // onb (onb.h:7-12)
     float wx = nx, wy = ny, wz = nz;
-    normalize3(wx, wy, wz);
+    normalize3<OPT>(wx, wy, wz);
     float ax, ay, az;
     if (iq_fabsf(wx) > 0.9f) { ax = 0.0f; ay = 1.0f; az = 0.0f; }
     else { ax = 1.0f; ay = 0.0f; az = 0.0f; }
     float vx = wy * az - wz * ay, vy = wz * ax - wx * az, vz = wx * ay - wy * ax;
-    normalize3(vx, vy, vz);
+    normalize3<OPT>(vx, vy, vz);
     const float ux = vy * wz - vz * wy, uy = vz * wx - vx * wz, uz = vx * wy - vy * wx;
     // cosine_weighted (random.cu:96-107)
     const float u1 = rand_real(s, 0.0f, 1.0f);
@@ -334,7 +363,11 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     float dy = (uy * lx + vy * ly) + wy * lz;
     float dz = (uz * lx + vz * ly) + wz * lz;
     const float wox = -r.dx, woy = -r.dy, woz = -r.dz;
-    float pdf = ((nx * dx + ny * dy) + nz * dz) / IQ_PI;         // oren_nayar::pdf (material.cu:45-48)
+    // oren_nayar::pdf (material.cu:45-48). Under kOptFastDiv the dot is divided by Markstein's
+    // correction with RN(1/pi): exact for |dot| in {0} U [2^-100, 2^100]; below 2^-100 both the IEEE
+    // and the short quotient are < 1e-5 and the pdf is replaced by 1/pi on both paths.
+    const float pdot = (nx * dx + ny * dy) + nz * dz;
+    float pdf = (OPT & kOptFastDiv) ? iq_div_pre(pdot, IQ_PI, kRcpPi) : pdot / IQ_PI;
     if (pdf < 0.00001f) {
         dx = nx;
         dy = ny;
@@ -361,7 +394,9 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     r.dx = dx;
     r.dy = dy;
     r.dz = dz;
-    return att * (cosw / pdf);
+    // pdf is NaN, 1/pi or in [1e-5, 1/pi] and cosw = max(0, dot) >= pi * 1e-5 when the pdf was not
+    // replaced (|n|^2 otherwise): inside the exact range of iq_div_pre
+    return att * ((OPT & kOptFastDiv) ? iq_div_pre(cosw, pdf, iq_rcp(pdf)) : cosw / pdf);
 }
 
 __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
@@ -372,10 +407,14 @@ __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
 // table built with the same IEEE division (so c = 1 gives the identical bits) and 0/n = +0 (c is
 // never -0 here: path_color = 0 + color).
 // `tab` is false when the launch has more samples than the table holds (rc is then not set).
+// kOptFastDiv: for c in [2^-90, 1) (c is clamped to [0, 1] or NaN) and n < 2^32 the quotient is
+// normal and Markstein's correction of c * rc, rc = RN(1/n) from the table, is exact (iq_fastdiv.h).
+template <int OPT>
 __device__ __forceinline__ float mean_term(float c, float nf, float rc, bool tab) {
     if (tab) {
         if (c == 1.0f) return rc;
         if (c == 0.0f) return 0.0f;
+        if ((OPT & kOptFastDiv) && c >= 0x1p-90f) return iq_div_pre(c, nf, rc);
     }
     return c / nf;
 }
@@ -392,10 +431,10 @@ __device__ __forceinline__ void intersect_range(const float4* tri, uint32_t tri_
         for (uint32_t j = 0; j < tp; ++j) {
             const float4* q = tri + (size_t)j * kTriPairFloat4;
             if (OPT & kOptBranchless)
-                test_triangle_pair_nb(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, tri_first + 2 * j,
+                test_triangle_pair_nb<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, tri_first + 2 * j,
                                       2 * j + 1 < ntri_local);
             else
-                test_triangle_pair(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, tri_first + 2 * j,
+                test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, tri_first + 2 * j,
                                    2 * j + 1 < ntri_local);
         }
         const uint32_t sp = (nsph_local + 1) / 2;
@@ -406,7 +445,7 @@ __device__ __forceinline__ void intersect_range(const float4* tri, uint32_t tri_
     } else {
         for (uint32_t k = 0; k < ntri_local; ++k) {
             const float4* q = tri + (size_t)k * kTriFloat4;
-            test_triangle(q[0], q[1], q[2], ray, closest, kind, hidx, tri_first + k);
+            test_triangle<OPT>(q[0], q[1], q[2], ray, closest, kind, hidx, tri_first + k);
         }
         for (uint32_t k = 0; k < nsph_local; ++k) test_sphere(sph[k], ray, closest, kind, hidx, sph_first + k);
     }
@@ -632,9 +671,9 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
             } else {
                 keep = (p.frames32 ? (float)(uint32_t)(n - 1) : (float)(n - 1)) / nf;
             }
-            acc.x = mean_term(cx, nf, rc, use_tab) + acc.x * keep;
-            acc.y = mean_term(cy, nf, rc, use_tab) + acc.y * keep;
-            acc.z = mean_term(cz, nf, rc, use_tab) + acc.z * keep;
+            acc.x = mean_term<OPT>(cx, nf, rc, use_tab) + acc.x * keep;
+            acc.y = mean_term<OPT>(cy, nf, rc, use_tab) + acc.y * keep;
+            acc.z = mean_term<OPT>(cz, nf, rc, use_tab) + acc.z * keep;
             ++done;
             depth = 0;
             if (done == p.spp) {
@@ -734,6 +773,9 @@ const variant kVariants[] = {
     // MAXD 16 would spill under the 96-VGPR bound of kOptLB5 (16 stack registers): 4 waves/SIMD
     IQPT_V(8, false, kOptDefault), IQPT_V(8, true, kOptDefault),
     IQPT_V(16, false, kOptDefault & ~kOptLB5), IQPT_V(16, true, kOptDefault & ~kOptLB5),
+    // packets outside the kOptFastDiv range (iqpt_upload_packet)
+    IQPT_V(8, false, kOptDefault & ~kOptFastDiv), IQPT_V(8, true, kOptDefault & ~kOptFastDiv),
+    IQPT_V(16, false, kOptDefault & ~kOptLB5 & ~kOptFastDiv), IQPT_V(16, true, kOptDefault & ~kOptLB5 & ~kOptFastDiv),
 #if defined(IQPT_AB_VARIANTS)
     IQPT_V(8, false, 0),
     IQPT_V(8, true, 0),
@@ -748,6 +790,7 @@ const variant kVariants[] = {
     IQPT_V(8, true, kOptDefault | kOptLB5),
     IQPT_V(8, false, kOptDefault | kOptStats),
     IQPT_V(8, true, kOptDefault | kOptStats),
+    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptStats),
 #endif
 };
 #undef IQPT_V

@@ -90,6 +90,7 @@ struct iqpt_ctx {
     float4_storage* d_sph = nullptr;
     float4_storage* d_sph_pairs = nullptr;
     uint32_t ntri = 0, nsph = 0;
+    bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
     std::vector<hipEvent_t> event_pool;
@@ -296,6 +297,20 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         const iqpt_sphere_drawcall& s = pk->sphere_dcs[i];
         sph.push_back({s.center[0], s.center[1], s.center[2], s.radius});
     }
+    // kOptFastDiv (iq_fastdiv.h): iq_rcp is exact for |x| in [2^-126, 2^126) and for 0, inf, NaN.
+    // Möller–Trumbore determinants are |e1 . (dir x e2)| <= |e1| |e2| (|dir| = 1) < 2^126 when every
+    // finite edge component is within 2^60 (a non-finite component makes det inf or NaN), and sphere
+    // radii must be 0, non-finite or in [2^-126, 2^126).
+    bool fast_rcp_ok = true;
+    auto big = [](float v) { return std::isfinite(v) && std::fabs(v) > 0x1p60f; };
+    for (uint64_t k = 0; k < total && fast_rcp_ok; ++k) {
+        const float4_storage* t = &tris[k * iqpt::kTriFloat4];
+        fast_rcp_ok = !(big(t[0].w) || big(t[1].x) || big(t[1].y) || big(t[1].z) || big(t[1].w) || big(t[2].x));
+    }
+    for (const float4_storage& s : sph) {
+        const float r = std::fabs(s.w);
+        if (std::isfinite(r) && r != 0.0f && (r < 0x1p-126f || r >= 0x1p126f)) fast_rcp_ok = false;
+    }
     // pair layouts (iqpt_internal.hpp): SoA inside each pair of consecutive primitives
     std::vector<float4_storage> tri_pairs, sph_pairs;
     const size_t ntp = (total + 1) / 2, nsp = ((size_t)nsdc + 1) / 2;
@@ -332,6 +347,7 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
     }
     c->ntri = (uint32_t)total;
     c->nsph = nsdc;
+    c->fast_rcp_ok = fast_rcp_ok;
     c->have_packet = true;
     return IQPT_OK;
 }
@@ -379,8 +395,14 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     p.sph_pairs = c->d_sph_pairs;
     p.nsph = c->nsph;
     p.nsph_pairs = (c->nsph + 1) / 2;
-    // the production variant for max_depth > 8 carries 16 stack registers and no 5-wave bound
-    const int opt = (c->max_depth > 8 && c->opt == iqpt::kOptDefault) ? (c->opt & ~iqpt::kOptLB5) : c->opt;
+    // the production variant for max_depth > 8 carries 16 stack registers and no 5-wave bound;
+    // kOptFastDiv only for packets inside its range (upload) and frames up to 2^24 wide / high
+    // (camera_ray divides by W and H with the pre-rounded reciprocals below)
+    int opt = (c->max_depth > 8 && (c->opt & ~iqpt::kOptFastDiv) == (iqpt::kOptDefault & ~iqpt::kOptFastDiv))
+                  ? (c->opt & ~iqpt::kOptLB5) : c->opt;
+    if (!c->fast_rcp_ok || c->width > (1u << 24) || c->height > (1u << 24)) opt &= ~iqpt::kOptFastDiv;
+    p.rcp_width = 1.0f / (float)c->width;
+    p.rcp_height = 1.0f / (float)c->height;
     const bool pair = (opt & iqpt::kOptPair) != 0;
     const uint32_t tri_rec = pair ? iqpt::kTriPairFloat4 * 16 : iqpt::kTriFloat4 * 16;   // bytes per LDS record
     const uint32_t sph_rec = pair ? iqpt::kSphPairFloat4 * 16 : 16;

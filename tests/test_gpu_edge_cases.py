@@ -96,3 +96,21 @@ def test_singular_normal_matrix_and_empty_scene(require_gpu):
     sc.add_model("wall", "q", 3.0, 0.0, (0.0, 0.5, 1.0))
     run_both(sc, 64, 48, [2], 5)
     run_both(Scene(), 48, 32, [3], 5)
+
+
+@pytest.mark.parametrize("case", ["edges_2^59", "edges_2^61", "denormal_radius", "huge_radius"])
+def test_fast_division_range(require_gpu, case):
+    """kOptFastDiv (iq_fastdiv.h) is exact only for reciprocals in [2^-126, 2^126): packets whose edge
+    components stay within 2^60 keep the fast variant (here with determinants near 2^118), larger
+    edges or radii outside the range switch the launch to the generic-division variant. Both must
+    match the oracle bit for bit."""
+    sc = odd_scene(2)
+    if case.startswith("edges"):
+        s = 2.0 ** (59 if case.endswith("59") else 61)
+        sc.add_model("giant", "b_quad", (s, s, 1.0), 0.0, (0.0, 0.0, 2.0 ** 62))
+        sc.add_model("near", "b_quad", (s, s, 1.0), (0.3, 0.2, 0.0), (0.0, 0.5, 3.0))
+    elif case == "denormal_radius":
+        sc.add_model("dust", "sphere", 1e-40, 0.0, (0.0, 0.5, 0.5))
+    else:
+        sc.add_model("shell", "sphere", 2.0 ** 126, 0.0, (0.0, 0.0, 0.0))
+    run_both(sc, 80, 60, [3], 8)
