@@ -58,3 +58,27 @@ __device__ __forceinline__ float iq_rcp_guarded(float x) {
     if (__builtin_expect(ax >= 0x1p-126f && ax < 0x1p126f, 1)) return iq_rcp(x);
     return 1.0f / x;
 }
+
+// RN(sqrt(x)) for x = +-0, x in [2^-96, +inf], negative normals / -inf (NaN) and NaN (verified on
+// all such inputs by
+// tools/fastdiv_check.hip): v_sqrt_f32 is within 1 ulp, so the correctly rounded root is one of
+// s - 1ulp, s, s + 1ulp, picked by the signs of the residuals x - s'*s (one FMA each). Below 2^-96
+// the residuals underflow and the pick can be wrong; the generic expansion pre-scales such x by
+// 2^32 and adds a class test for 0 / inf on top. Negative denormals give -0 (v_sqrt_f32 flushes
+// them), not NaN.
+__device__ __forceinline__ float iq_sqrt_n(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float s_dn = __uint_as_float(__float_as_uint(s) - 1u);
+    const float s_up = __uint_as_float(__float_as_uint(s) + 1u);
+    const float r_dn = __builtin_fmaf(-s_dn, s, x);
+    const float r_up = __builtin_fmaf(-s_up, s, x);
+    float t = r_dn <= 0.0f ? s_dn : s;
+    t = r_up > 0.0f ? s_up : t;
+    return t;
+}
+
+// RN(sqrt(x)) for every x (a rarely taken branch for 0 < |x| < 2^-96).
+__device__ __forceinline__ float iq_sqrt_guarded(float x) {
+    if (__builtin_expect(__builtin_fabsf(x) < 0x1p-96f && x != 0.0f, 0)) return __builtin_sqrtf(x);
+    return iq_sqrt_n(x);
+}

@@ -41,16 +41,19 @@
  * use the short correctly rounded forms of iq_fastdiv.h (bit-identical to IEEE division, verified
  * exhaustively / on 2^36 pairs per class by tools/fastdiv_check.hip); everywhere else plain IEEE
  * division. IQ_RCP and IQ_DIV are exact for every operand; IQ_DIV_N needs |a| in {0} U
- * [2^-100, 2^100], |b| in [2^-100, 2^100] and a normal quotient (stated where it is used). */
+ * [2^-100, 2^100], |b| in [2^-100, 2^100] and a normal quotient, IQ_SQRT_N an argument that is
+ * 0 or >= 2^-96 (stated where they are used). */
 #if defined(__HIP_DEVICE_COMPILE__) && defined(IQ_FP_FASTDIV)
 #include "iq_fastdiv.h"
 #define IQ_RCP(x) iq_rcp_guarded(x)
 #define IQ_DIV(a, b) iq_div((a), (b))
 #define IQ_DIV_N(a, b) iq_div_pre((a), (b), iq_rcp(b))
+#define IQ_SQRT_N(x) iq_sqrt_n(x)
 #else
 #define IQ_RCP(x) (1.0f / (x))
 #define IQ_DIV(a, b) ((a) / (b))
 #define IQ_DIV_N(a, b) ((a) / (b))
+#define IQ_SQRT_N(x) iq_sqrtf(x)
 #endif
 
 /* constants of IoniqRE/iqmath.h:6-11 */
@@ -215,7 +218,8 @@ IQ_INLINE float iq_asinf(float x) {
     } else {
         float r, zz;
         int flag;
-        if (a > 0.5f) { zz = 0.5f * (1.0f - a); r = iq_sqrtf(zz); flag = 1; }
+        /* 1 - a is 0 or >= 2^-24 (a <= 1): zz is 0 or normal */
+        if (a > 0.5f) { zz = 0.5f * (1.0f - a); r = IQ_SQRT_N(zz); flag = 1; }
         else { r = a; zz = r * r; flag = 0; }
         z = ((((4.2163199048e-2f * zz + 2.4181311049e-2f) * zz + 4.5470025998e-2f) * zz
               + 7.4953002686e-2f) * zz + 1.6666752422e-1f) * zz * r + r;
@@ -227,8 +231,9 @@ IQ_INLINE float iq_asinf(float x) {
 IQ_INLINE float iq_acosf(float x) {
     if (iq_isnan(x)) return x;
     if (x < -1.0f || x > 1.0f) return iq_nanf();
-    if (x < -0.5f) return IQ_PI - 2.0f * iq_asinf(iq_sqrtf(0.5f * (1.0f + x)));
-    if (x > 0.5f) return 2.0f * iq_asinf(iq_sqrtf(0.5f * (1.0f - x)));
+    /* 1 +- x is 0 or >= 2^-24 here: the root's argument is 0 or normal */
+    if (x < -0.5f) return IQ_PI - 2.0f * iq_asinf(IQ_SQRT_N(0.5f * (1.0f + x)));
+    if (x > 0.5f) return 2.0f * iq_asinf(IQ_SQRT_N(0.5f * (1.0f - x)));
     return IQ_PI_DIV_2 - iq_asinf(x);
 }
 

@@ -89,6 +89,8 @@ constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS ta
 int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, uint32_t y0,
                     uint32_t ystep, uint32_t npix, uint64_t seed, const uint32_t* tables,
                     uint32_t* rng);
+// Device probe of the shared math (iqpt_debug_libm).
+int launch_libm(void* stream, int fn, const float* a, const float* b, float* out, uint32_t n);
 // grid_blocks = persistent grid size; lds_bytes dynamic LDS; stream = hipStream_t; opt = kOpt* mask.
 int launch_render(void* stream, const kparams& p, uint32_t grid_blocks, uint32_t lds_bytes, bool stream_batches,
                   int opt);

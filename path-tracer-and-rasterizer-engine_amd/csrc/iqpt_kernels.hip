@@ -28,6 +28,8 @@
 //    (argued where it is taken). Results are bit-identical to the CPU oracle.
 #include <hip/hip_runtime.h>
 
+// the transcendentals of iq_fp.h use the short exact division forms in this TU's GPU pass
+#define IQ_FP_FASTDIV 1
 #include "iq_fastdiv.h"
 #include "iq_fp.h"
 #include "iq_xorwow.h"
@@ -85,6 +87,19 @@ __device__ __forceinline__ float rcp_any(float x) {
     return 1.0f / x;
 }
 
+// IEEE sqrt: iq_sqrt_n (iq_fastdiv.h) where the argument is known to be 0, >= 2^-96, inf or NaN
+// (sqrt_n), the guarded form elsewhere (sqrt_any).
+template <int OPT>
+__device__ __forceinline__ float sqrt_n(float x) {
+    if (OPT & kOptFastDiv) return iq_sqrt_n(x);
+    return iq_sqrtf(x);
+}
+template <int OPT>
+__device__ __forceinline__ float sqrt_any(float x) {
+    if (OPT & kOptFastDiv) return iq_sqrt_guarded(x);
+    return iq_sqrtf(x);
+}
+
 // dot4(v, column c of M) of iqvec::transformed (vector.h:371-383); M row-major m[r][c].
 __device__ __forceinline__ float dot_col(float x, float y, float z, float w, const float* M, int c) {
     return ((x * M[c] + y * M[4 + c]) + z * M[8 + c]) + w * M[12 + c];
@@ -99,7 +114,8 @@ __device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
         z = 0.0f;
         return;
     }
-    const float len = iq_sqrtf((x * x + y * y) + z * z);
+    // one component is >= 1e-5 in magnitude, so len^2 >= 1e-10 (or inf / NaN): sqrt_n's domain
+    const float len = sqrt_n<OPT>((x * x + y * y) + z * z);
     const float inv = rcp_any<OPT>(len);
     x = x * inv;
     y = y * inv;
@@ -285,12 +301,14 @@ __device__ __forceinline__ void test_triangle_pair(const float4 q0, const float4
 }
 
 // sphere::intersect (shape.cu:13-46), far root not checked against t_max (reference quirk).
+template <int OPT>
 __device__ __forceinline__ void sphere_roots(float halfb, float delta, float& closest, int& kind, uint32_t& idx,
                                              uint32_t k) {
-    float t = halfb - iq_sqrtf(delta);
+    const float sd = sqrt_any<OPT>(delta);      // delta >= 0 may be tiny (grazing rays)
+    float t = halfb - sd;
     if (closest < t) return;
     if (t < kTMin) {
-        t = halfb + iq_sqrtf(delta);
+        t = halfb + sd;
         if (t < kTMin) return;
     }
     closest = t;
@@ -298,6 +316,7 @@ __device__ __forceinline__ void sphere_roots(float halfb, float delta, float& cl
     idx = k;
 }
 
+template <int OPT>
 __device__ __forceinline__ void test_sphere(const float4 s, const ray3 r, float& closest, int& kind,
                                             uint32_t& idx, uint32_t k) {
     const float ocx = s.x - r.ox, ocy = s.y - r.oy, ocz = s.z - r.oz;
@@ -305,10 +324,11 @@ __device__ __forceinline__ void test_sphere(const float4 s, const ray3 r, float&
     const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.w * s.w;
     const float delta = halfb * halfb - cc;
     if (delta < 0.0f) return;
-    sphere_roots(halfb, delta, closest, kind, idx, k);
+    sphere_roots<OPT>(halfb, delta, closest, kind, idx, k);
 }
 
 // Two spheres (k, k+1) with the quadratic set up in packed registers, roots tested in order.
+template <int OPT>
 __device__ __forceinline__ void test_sphere_pair(const float4 s0, const float4 s1, const ray3 r, float& closest,
                                                  int& kind, uint32_t& idx, uint32_t k, bool second) {
     const f2 cx = {s0.x, s0.y}, cy = {s0.z, s0.w}, cz = {s1.x, s1.y}, rad = {s1.z, s1.w};
@@ -318,8 +338,8 @@ __device__ __forceinline__ void test_sphere_pair(const float4 s0, const float4 s
     const f2 delta = halfb * halfb - cc;
     const bool a0 = !(delta.x < 0.0f);
     const bool a1 = second && !(delta.y < 0.0f);
-    if (a0) sphere_roots(halfb.x, delta.x, closest, kind, idx, k);
-    if (a1) sphere_roots(halfb.y, delta.y, closest, kind, idx, k + 1);
+    if (a0) sphere_roots<OPT>(halfb.x, delta.x, closest, kind, idx, k);
+    if (a1) sphere_roots<OPT>(halfb.y, delta.y, closest, kind, idx, k + 1);
 }
 
 // oren_nayar(albedo .5, sigma 1).scatter (material.cu:5-43) at the closest sphere hit. Writes the
@@ -348,7 +368,7 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     const float u1 = rand_real(s, 0.0f, 1.0f);
     const float u2 = rand_real(s, 0.0f, 1.0f);
     const float phi = (2.0f * IQ_PI) * u1;
-    const float su2 = iq_sqrtf(u2);
+    const float su2 = sqrt_n<OPT>(u2);                          // u2 = k 2^-32: 0 or >= 2^-32
     float sphi, cphi;
     if (OPT & kOptSinCos) {
         iq_sincosf(phi, &sphi, &cphi);
@@ -358,7 +378,7 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     }
     const float lx = cphi * su2;
     const float ly = sphi * su2;
-    const float lz = iq_sqrtf(1.0f - u2);
+    const float lz = sqrt_n<OPT>(1.0f - u2);                    // 1 - u2: 0 or >= 2^-24
     float dx = (ux * lx + vx * ly) + wx * lz;                    // onb::transform_to_world
     float dy = (uy * lx + vy * ly) + wy * lz;
     float dz = (uz * lx + vz * ly) + wz * lz;
@@ -440,14 +460,14 @@ __device__ __forceinline__ void intersect_range(const float4* tri, uint32_t tri_
         const uint32_t sp = (nsph_local + 1) / 2;
         for (uint32_t j = 0; j < sp; ++j) {
             const float4* q = sph + (size_t)j * kSphPairFloat4;
-            test_sphere_pair(q[0], q[1], ray, closest, kind, hidx, sph_first + 2 * j, 2 * j + 1 < nsph_local);
+            test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, sph_first + 2 * j, 2 * j + 1 < nsph_local);
         }
     } else {
         for (uint32_t k = 0; k < ntri_local; ++k) {
             const float4* q = tri + (size_t)k * kTriFloat4;
             test_triangle<OPT>(q[0], q[1], q[2], ray, closest, kind, hidx, tri_first + k);
         }
-        for (uint32_t k = 0; k < nsph_local; ++k) test_sphere(sph[k], ray, closest, kind, hidx, sph_first + k);
+        for (uint32_t k = 0; k < nsph_local; ++k) test_sphere<OPT>(sph[k], ray, closest, kind, hidx, sph_first + k);
     }
 }
 
@@ -724,6 +744,34 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
     }
 }
 
+// Device probe of the shared transcendentals and division forms exactly as the render kernel
+// compiles them (tests/test_gpu_libm.py compares them with the oracle's host build, bit for bit).
+// fn: 0 sin, 1 cos, 2 tan, 3 acos, 4 atan2(a, b), 5 asin, 6 atan (the oracle's iqo_libm_batch
+// numbering), 7 / 8 sin / cos of iq_sincosf, 9 iq_sqrt_guarded, 10 iq_rcp_guarded, 11 iq_div.
+__global__ __launch_bounds__(256) void iqpt_libm_kernel(int fn, const float* a, const float* b, float* out,
+                                                        uint32_t n) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const float x = a[i], y = b[i];
+    float r = 0.0f, s2, c2;
+    switch (fn) {
+    case 0: r = iq_sinf(x); break;
+    case 1: r = iq_cosf(x); break;
+    case 2: r = iq_tanf(x); break;
+    case 3: r = iq_acosf(x); break;
+    case 4: r = iq_atan2f(x, y); break;
+    case 5: r = iq_asinf(x); break;
+    case 6: r = iq_atanf(x); break;
+    case 7: iq_sincosf(x, &s2, &c2); r = s2; break;
+    case 8: iq_sincosf(x, &s2, &c2); r = c2; break;
+    case 9: r = iq_sqrt_guarded(x); break;
+    case 10: r = iq_rcp_guarded(x); break;
+    case 11: r = iq_div(x, y); break;
+    default: break;
+    }
+    out[i] = r;
+}
+
 // curand_init(seed, global pixel id, 0) per owned pixel (renderer_init_kernel, path_tracer.cu:36-46).
 __global__ __launch_bounds__(256) void iqpt_rng_init_kernel(uint32_t width, uint32_t x0, uint32_t ncols,
                                                             uint32_t y0, uint32_t ystep, uint32_t npix,
@@ -810,6 +858,12 @@ int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, u
     const uint32_t grid = (npix + 255) / 256;
     hipLaunchKernelGGL(iqpt_rng_init_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, width, x0, ncols,
                        y0, ystep, npix, seed, tables, rng);
+    return (int)hipGetLastError();
+}
+
+int launch_libm(void* stream, int fn, const float* a, const float* b, float* out, uint32_t n) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(iqpt_libm_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, a, b, out, n);
     return (int)hipGetLastError();
 }
 

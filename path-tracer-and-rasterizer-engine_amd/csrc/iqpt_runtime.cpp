@@ -552,6 +552,31 @@ int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
     return IQPT_OK;
 }
 
+/* Internal (tests/test_gpu_libm.py): evaluate the device build of the shared math on n inputs on
+ * the current device (synchronous). */
+int iqpt_debug_libm(int fn, const float* a, const float* b, float* out, uint64_t n) {
+    if (!a || !b || !out) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (n == 0) return IQPT_OK;
+    if (n > (1ull << 28)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "n too large");
+    float *da = nullptr, *db = nullptr, *dout = nullptr;
+    const size_t bytes = (size_t)n * sizeof(float);
+    int st = IQPT_OK;
+    if (hipMalloc(&da, bytes) != hipSuccess || hipMalloc(&db, bytes) != hipSuccess ||
+        hipMalloc(&dout, bytes) != hipSuccess) {
+        st = iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "libm probe buffers");
+    } else {
+        hipError_t e = hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = (hipError_t)iqpt::launch_libm(nullptr, fn, da, db, dout, (uint32_t)n);
+        if (e == hipSuccess) e = hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) st = iqpt::hip_fail(e, "libm probe");
+    }
+    (void)hipFree(da);
+    (void)hipFree(db);
+    (void)hipFree(dout);
+    return st;
+}
+
 int iqpt_debug_read_stats(iqpt_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     int st = use_device(c);

@@ -30,6 +30,9 @@
 
 struct counters {
     unsigned long long n[8];
+    unsigned long long sqrt_bad;   // iq_sqrt_n mismatches on its domain
+    unsigned long long sqrt_guarded_bad;   // iq_sqrt_guarded mismatches over all inputs
+    uint32_t sqrt_worst_below;     // largest failing positive input below the domain
     uint32_t ex_a[16], ex_b[16], ex_got[16], ex_ref[16];
     uint32_t nex;
 };
@@ -60,7 +63,7 @@ __device__ void record(counters* c, uint32_t a, uint32_t b, float got, float ref
 // mismatches (x >= 0), n[4] inputs tested, n[5] mismatches with |x| in [2^-126, 2^126) (the
 // documented exact range), n[6] mismatches on zeros / infinities / NaN
 __global__ void rcp_all(counters* c, uint64_t base, uint64_t count) {
-    unsigned long long m0 = 0, m1 = 0, m2 = 0, m3 = 0, m5 = 0, m6 = 0, m7 = 0, t = 0;
+    unsigned long long m0 = 0, m1 = 0, m2 = 0, m3 = 0, m5 = 0, m6 = 0, m7 = 0, m8 = 0, m9 = 0, t = 0;
     for (uint64_t i = base + blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < base + count;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t u = (uint32_t)i;
@@ -83,6 +86,21 @@ __global__ void rcp_all(counters* c, uint64_t base, uint64_t count) {
         if (cmp(iq_rcp_guarded(x), ref) == 2) ++m7;
         if (cmp(__builtin_amdgcn_rcpf(x), ref) == 2) ++m2;
         if (!(u >> 31) && cmp(__builtin_amdgcn_sqrtf(x), __builtin_sqrtf(x)) == 2) ++m3;
+        // iq_sqrt_n on its documented domain: +-0, [2^-96, +inf], negative normals / -inf and NaN;
+        // below it (positive) only the largest failing input is recorded, to show where the short
+        // form stops being exact. Negative denormals are outside (v_sqrt_f32 flushes them to -0).
+        {
+            const uint32_t mag = u & 0x7fffffffu;
+            const bool in_domain = mag == 0u || mag >= 0x0f800000u || ((u >> 31) && mag >= 0x00800000u);
+            const int k2 = cmp(iq_sqrt_n(x), __builtin_sqrtf(x));
+            if (in_domain && k2 == 2) {
+                ++m8;
+                record(c, u, 1, iq_sqrt_n(x), __builtin_sqrtf(x));
+            } else if (!in_domain && !(u >> 31) && k2 == 2) {
+                atomicMax(&c->sqrt_worst_below, u);
+            }
+            if (cmp(iq_sqrt_guarded(x), __builtin_sqrtf(x)) == 2) ++m9;
+        }
         ++t;
     }
     atomicAdd(&c->n[0], m0);
@@ -93,6 +111,8 @@ __global__ void rcp_all(counters* c, uint64_t base, uint64_t count) {
     atomicAdd(&c->n[5], m5);
     atomicAdd(&c->n[6], m6);
     atomicAdd(&c->n[7], m7);
+    atomicAdd(&c->sqrt_bad, m8);
+    atomicAdd(&c->sqrt_guarded_bad, m9);
 }
 
 __device__ __forceinline__ uint32_t xs32(uint32_t& s) {
@@ -191,7 +211,10 @@ int main(int argc, char** argv) {
     CHECK(hipDeviceSynchronize());
     CHECK(hipMemcpy(&h, d, sizeof(h), hipMemcpyDeviceToHost));
     report("iq_rcp vs 1/x (all 2^32 inputs)", h);
-    fails += h.n[5] != 0 || h.n[6] != 0 || h.n[7] != 0 || h.n[4] != (1ull << 32);
+    printf("iq_sqrt_n vs sqrtf on its domain: mismatches %llu (largest failing positive input below 2^-96: "
+           "%08x); iq_sqrt_guarded on all 2^32 inputs: mismatches %llu\n",
+           h.sqrt_bad, h.sqrt_worst_below, h.sqrt_guarded_bad);
+    fails += h.n[5] != 0 || h.n[6] != 0 || h.n[7] != 0 || h.n[4] != (1ull << 32) || h.sqrt_bad != 0 || h.sqrt_guarded_bad != 0;
 
     const char* names[7] = {"iq_div_pre |a|,|b| in [2^-62,2^62]", "iq_div_pre near-midpoint",
                             "iq_div random bit patterns", "iq_div_pre b mantissa 0/all-ones",
