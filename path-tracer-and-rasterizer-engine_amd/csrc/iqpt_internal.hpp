@@ -70,7 +70,26 @@ struct kparams {
     unsigned long long* rays;        // closest-hit query counter
     uint32_t* queue;                 // pixel dequeue head (zeroed before every launch)
     unsigned long long* stats;       // kOptStats counters (8 x u64) or null
+    // kOptCull: per screen tile of kCullTile x kCullTile owned pixels (columns x owned rows), one bit
+    // per triangle pair (words [0, cull_wt)) and per sphere pair (words [cull_wt, cull_stride)) that
+    // camera rays of the tile may hit (iq_interval.h); null = no culling for this launch
+    const uint32_t* cull;
+    uint32_t cull_ntx, cull_wt, cull_stride;
 };
+
+// Binning launch (iqpt_bin_kernel): the camera and pixel set of the context, the world-space scene.
+struct kbin {
+    uint32_t width, height, x0, ncols, y0, ystep, nrows;
+    float inv_proj[16], inv_view[16];
+    uint32_t cam_const;
+    float cam_near_rw, cam_far_rw;
+    const float4_storage* tris;      // single layout, ntri * kTriFloat4
+    const float4_storage* spheres;   // nsph
+    uint32_t ntri, nsph;
+    uint32_t ntx, nty, wt, stride;
+    uint32_t* cull;                  // ntx * nty * stride words
+};
+constexpr uint32_t kCullTile = 8;
 
 // Kernel option bits (all exact: each shortcut reproduces the reference's bits, see the kernel).
 constexpr int kOptCamConst = 1 << 0;   // launch-constant 1/w of the inverse projection
@@ -82,13 +101,16 @@ constexpr int kOptSinCos = 1 << 5;     // shared reduction for cos(phi), sin(phi
 constexpr int kOptBranchless = 1 << 6; // pair MT without early exits (small resident scenes)
 constexpr int kOptStats = 1 << 7;      // wave-level counters (diagnostic builds)
 constexpr int kOptFastDiv = 1 << 8;    // short exact reciprocal / division forms (iq_fastdiv.h)
-constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv;
+constexpr int kOptCull = 1 << 9;       // camera rays test only the pairs of their tile's mask (pair layout)
+constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.
 int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, uint32_t y0,
                     uint32_t ystep, uint32_t npix, uint64_t seed, const uint32_t* tables,
                     uint32_t* rng);
+// Tile masks for kOptCull (one thread per tile word).
+int launch_bin(void* stream, const kbin& b);
 // Device probe of the shared math (iqpt_debug_libm).
 int launch_libm(void* stream, int fn, const float* a, const float* b, float* out, uint32_t n);
 // grid_blocks = persistent grid size; lds_bytes dynamic LDS; stream = hipStream_t; opt = kOpt* mask.

@@ -32,6 +32,7 @@
 #define IQ_FP_FASTDIV 1
 #include "iq_fastdiv.h"
 #include "iq_fp.h"
+#include "iq_interval.h"
 #include "iq_xorwow.h"
 #include "iqpt_internal.hpp"
 
@@ -471,6 +472,53 @@ __device__ __forceinline__ void intersect_range(const float4* tri, uint32_t tri_
     }
 }
 
+// OR of a 32-bit value over the 64 lanes of the wave (all lanes must be executing): DPP within
+// each 16-lane row, then the four row results read as scalars.
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);    // quad_perm [1,0,3,2]
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);    // quad_perm [2,3,0,1]
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);   // row_shr:4
+    v |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);   // row_shr:8
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 15) | (uint32_t)__builtin_amdgcn_readlane((int)v, 31) |
+           (uint32_t)__builtin_amdgcn_readlane((int)v, 47) | (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
+// kOptCull, LDS-resident scene: the closest hit over the pairs whose bit is set in the wave's OR of
+// the lanes' tile masks (camera rays, iq_interval.h) — or over every pair when some lane traces a
+// secondary ray. Skipped pairs are rejected by the reference's own tests for every camera ray of
+// the tile, and the remaining pairs are visited in index order, so results are unchanged. Called by
+// all lanes of the wave (wave_or); only active lanes test.
+template <int OPT>
+__device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntri, const float4* sph, uint32_t nsph,
+                                                 const uint32_t* lane_mask, bool all, bool active, const ray3 ray,
+                                                 float& closest, int& kind, uint32_t& hidx, uint32_t wt) {
+    const uint32_t tp = (ntri + 1) / 2, sp = (nsph + 1) / 2;
+    for (uint32_t w = 0; w * 32u < tp; ++w) {
+        uint32_t m = all ? ~0u : wave_or(lane_mask ? lane_mask[w] : 0u);
+        while (m) {
+            const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            if (j >= tp) break;
+            if (active) {
+                const float4* q = tri + (size_t)j * kTriPairFloat4;
+                test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j, 2 * j + 1 < ntri);
+            }
+        }
+    }
+    for (uint32_t w = 0; w * 32u < sp; ++w) {
+        uint32_t m = all ? ~0u : wave_or(lane_mask ? lane_mask[wt + w] : 0u);
+        while (m) {
+            const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
+            m &= m - 1u;
+            if (j >= sp) break;
+            if (active) {
+                const float4* q = sph + (size_t)j * kSphPairFloat4;
+                test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, 2 * j, 2 * j + 1 < nsph);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------------------------------------
 // The megakernel. MAXD bounds max_depth (register stack size); STREAM selects LDS batch streaming
 // (scene larger than the resident budget) with workgroup-uniform iteration; OPT is the kOpt* mask.
@@ -514,6 +562,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
     // ---- per-lane state
     bool active = false;
     uint32_t pix = 0, px = 0, py = 0;
+    uint32_t tile = 0;                 // kOptCull: the pixel's screen tile
     uint32_t done = 0;                 // samples finished for the current pixel
     rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
     float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
@@ -551,6 +600,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                 const uint32_t col = pix % p.ncols, row = pix / p.ncols;
                 px = p.x0 + col;
                 py = p.y0 + row * p.ystep;
+                if (OPT & kOptCull) tile = col / kCullTile + (row / kCullTile) * p.cull_ntx;
                 st.v0 = p.rng[pix];
                 st.v1 = p.rng[(size_t)p.npix + pix];
                 st.v2 = p.rng[2 * (size_t)p.npix + pix];
@@ -587,31 +637,102 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
         float closest = kTMax;
         int kind = kHitNone;
         uint32_t hidx = 0;
+        // kOptCull: camera rays (depth 0) test only the pairs of their tile's mask; one secondary ray
+        // in the wave makes it test everything
+        constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
+        const bool cull = kCull && p.cull != nullptr && !__any(active && depth != 0);
+        const uint32_t* lane_mask =
+            (cull && active) ? p.cull + (size_t)tile * p.cull_stride : nullptr;   // null: contributes 0
         if (STREAM) {
             for (uint32_t base = 0; base < tri_recs; base += p.tri_batch) {
                 const uint32_t n = min(p.tri_batch, tri_recs - base);
-                __syncthreads();
+                uint32_t wm[kCull ? 8 : 1];
+                bool any = true;
+                if (kCull) {
+                    // the batch's mask words (tri_batch is 256 pairs when culling: 8 aligned words)
+                    any = false;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint32_t w = base / 32u + (uint32_t)i;
+                        wm[i] = 0u;
+                        if ((uint32_t)i * 32u < n)
+                            wm[i] = cull ? wave_or(lane_mask ? lane_mask[w] : 0u) : ~0u;
+                        any = any || wm[i] != 0u;
+                    }
+                    // the barrier also orders this batch's LDS writes after the previous batch's reads
+                    if (!__syncthreads_or(any ? 1 : 0)) continue;
+                } else {
+                    __syncthreads();
+                }
                 for (uint32_t i = threadIdx.x; i < n * kTriRec; i += kRenderBlock)
                     lds_tri[i] = g_tri[(size_t)base * kTriRec + i];
                 __syncthreads();
                 if (active) {
                     const uint32_t first = base * kTriPer;
                     const uint32_t cnt = min(n * kTriPer, p.ntri - first);
-                    intersect_range<OPT>(lds_tri, first, cnt, lds_sph, 0, 0, ray, closest, kind, hidx);
+                    if (kCull) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            uint32_t m = wm[i];
+                            while (m) {
+                                const uint32_t j = (uint32_t)i * 32u + (uint32_t)__builtin_ctz(m);   // local pair
+                                m &= m - 1u;
+                                if (j >= n) break;
+                                const float4* q = lds_tri + (size_t)j * kTriPairFloat4;
+                                test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx,
+                                                        first + 2 * j, 2 * j + 1 < cnt);
+                            }
+                        }
+                    } else {
+                        intersect_range<OPT>(lds_tri, first, cnt, lds_sph, 0, 0, ray, closest, kind, hidx);
+                    }
                 }
             }
             for (uint32_t base = 0; base < sph_recs; base += p.sph_batch) {
                 const uint32_t n = min(p.sph_batch, sph_recs - base);
-                __syncthreads();
+                uint32_t wm[kCull ? 8 : 1];
+                bool any = true;
+                if (kCull) {
+                    any = false;
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const uint32_t w = p.cull_wt + base / 32u + (uint32_t)i;
+                        wm[i] = 0u;
+                        if ((uint32_t)i * 32u < n)
+                            wm[i] = cull ? wave_or(lane_mask ? lane_mask[w] : 0u) : ~0u;
+                        any = any || wm[i] != 0u;
+                    }
+                    if (!__syncthreads_or(any ? 1 : 0)) continue;
+                } else {
+                    __syncthreads();
+                }
                 for (uint32_t i = threadIdx.x; i < n * kSphRec; i += kRenderBlock)
                     lds_sph[i] = g_sph[(size_t)base * kSphRec + i];
                 __syncthreads();
                 if (active) {
                     const uint32_t first = base * kSphPer;
                     const uint32_t cnt = min(n * kSphPer, p.nsph - first);
-                    intersect_range<OPT>(lds_tri, 0, 0, lds_sph, first, cnt, ray, closest, kind, hidx);
+                    if (kCull) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            uint32_t m = wm[i];
+                            while (m) {
+                                const uint32_t j = (uint32_t)i * 32u + (uint32_t)__builtin_ctz(m);
+                                m &= m - 1u;
+                                if (j >= n) break;
+                                const float4* q = lds_sph + (size_t)j * kSphPairFloat4;
+                                test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, first + 2 * j,
+                                                      2 * j + 1 < cnt);
+                            }
+                        }
+                    } else {
+                        intersect_range<OPT>(lds_tri, 0, 0, lds_sph, first, cnt, ray, closest, kind, hidx);
+                    }
                 }
             }
+        } else if (kCull && p.cull != nullptr) {
+            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, !cull, active, ray, closest, kind,
+                                  hidx, p.cull_wt);
         } else if (active) {
             intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
         }
@@ -772,6 +893,64 @@ __global__ __launch_bounds__(256) void iqpt_libm_kernel(int fn, const float* a, 
     out[i] = r;
 }
 
+// kOptCull tile masks: one thread per (tile, mask word), 32 primitive pairs per word. A pair's bit
+// is cleared only if iq_interval.h proves that the reference's tests reject both of its primitives
+// for every camera ray of the tile (every pixel, every jitter).
+__global__ __launch_bounds__(256) void iqpt_bin_kernel(const kbin b) {
+    const uint64_t gid = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    const uint64_t ntiles = (uint64_t)b.ntx * b.nty;
+    if (gid >= ntiles * b.stride) return;
+    const uint32_t w = (uint32_t)(gid % b.stride);
+    const uint32_t tile = (uint32_t)(gid / b.stride);
+    const uint32_t tx = tile % b.ntx, ty = tile / b.ntx;
+    const uint32_t c0 = tx * kCullTile, c1 = min(c0 + kCullTile, b.ncols) - 1u;
+    const uint32_t k0 = ty * kCullTile, k1 = min(k0 + kCullTile, b.nrows) - 1u;
+    iqiv::camera_in ci;
+    ci.width = b.width;
+    ci.height = b.height;
+    ci.rcp_width = 0.0f;
+    ci.rcp_height = 0.0f;
+    ci.inv_proj = b.inv_proj;
+    ci.inv_view = b.inv_view;
+    ci.cam_const = (int)b.cam_const;
+    ci.near_rw = b.cam_near_rw;
+    ci.far_rw = b.cam_far_rw;
+    const iqiv::bundle bd = iqiv::camera_bundle(ci, b.x0 + c0, b.x0 + c1, b.y0 + k0 * b.ystep, b.y0 + k1 * b.ystep);
+    uint32_t bits = 0u;
+    if (w < b.wt) {
+        for (uint32_t i = 0; i < 32u; ++i) {
+            const uint32_t j = w * 32u + i;
+            if (2u * j >= b.ntri) break;
+            bool culled = bd.ok;
+            for (uint32_t e = 0; e < 2u && culled; ++e) {
+                const uint32_t k = 2u * j + e;
+                if (k >= b.ntri) break;
+                const float4_storage* t = b.tris + (size_t)k * kTriFloat4;
+                const float v0[3] = {t[0].x, t[0].y, t[0].z};
+                const float e1[3] = {t[0].w, t[1].x, t[1].y};
+                const float e2[3] = {t[1].z, t[1].w, t[2].x};
+                culled = iqiv::tri_culled(bd, v0, e1, e2);
+            }
+            if (!culled) bits |= 1u << i;
+        }
+    } else {
+        for (uint32_t i = 0; i < 32u; ++i) {
+            const uint32_t j = (w - b.wt) * 32u + i;
+            if (2u * j >= b.nsph) break;
+            bool culled = bd.ok;
+            for (uint32_t e = 0; e < 2u && culled; ++e) {
+                const uint32_t k = 2u * j + e;
+                if (k >= b.nsph) break;
+                const float4_storage s = b.spheres[k];
+                const float c[3] = {s.x, s.y, s.z};
+                culled = iqiv::sphere_culled(bd, c, s.w);
+            }
+            if (!culled) bits |= 1u << i;
+        }
+    }
+    b.cull[gid] = bits;
+}
+
 // curand_init(seed, global pixel id, 0) per owned pixel (renderer_init_kernel, path_tracer.cu:36-46).
 __global__ __launch_bounds__(256) void iqpt_rng_init_kernel(uint32_t width, uint32_t x0, uint32_t ncols,
                                                             uint32_t y0, uint32_t ystep, uint32_t npix,
@@ -839,6 +1018,9 @@ const variant kVariants[] = {
     IQPT_V(8, false, kOptDefault | kOptStats),
     IQPT_V(8, true, kOptDefault | kOptStats),
     IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptStats),
+    IQPT_V(8, false, kOptDefault & ~kOptCull),
+    IQPT_V(8, true, kOptDefault & ~kOptCull),
+    IQPT_V(8, false, kOptDefault & ~kOptCull & ~kOptFastDiv),
 #endif
 };
 #undef IQPT_V
@@ -864,6 +1046,14 @@ int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, u
 int launch_libm(void* stream, int fn, const float* a, const float* b, float* out, uint32_t n) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(iqpt_libm_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, a, b, out, n);
+    return (int)hipGetLastError();
+}
+
+int launch_bin(void* stream, const kbin& b) {
+    const uint64_t n = (uint64_t)b.ntx * b.nty * b.stride;
+    if (n == 0) return 0;
+    if (n > 0xffffffffull * 256ull) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(iqpt_bin_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, b);
     return (int)hipGetLastError();
 }
 

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "iq_host_math.hpp"
+#include "iq_interval.h"
 #include "iq_xorwow.h"
 #include "iqpt.h"
 #include "iqpt_internal.hpp"
@@ -91,6 +92,11 @@ struct iqpt_ctx {
     float4_storage* d_sph_pairs = nullptr;
     uint32_t ntri = 0, nsph = 0;
     bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
+    // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
+    uint32_t* d_cull = nullptr;
+    size_t cull_cap = 0;       // words allocated
+    bool cull_valid = false;
+    uint32_t cull_ntx = 0, cull_nty = 0, cull_wt = 0, cull_stride = 0;
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
     std::vector<hipEvent_t> event_pool;
@@ -103,12 +109,81 @@ int use_device(const iqpt_ctx* c) {
     return IQPT_OK;
 }
 
+void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, float* far_rw);
+
 void free_scene(iqpt_ctx* c) {
     for (float4_storage** b : {&c->d_tris, &c->d_tri_pairs, &c->d_tri_shade, &c->d_sph, &c->d_sph_pairs}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
     c->ntri = c->nsph = 0;
+    c->cull_valid = false;
+}
+
+// (Re)build the kOptCull tile masks of the current camera and packet on the context's stream.
+int build_cull(iqpt_ctx* c) {
+    const uint32_t ntp = (c->ntri + 1) / 2, nsp = (c->nsph + 1) / 2;
+    c->cull_ntx = (c->ncols + iqpt::kCullTile - 1) / iqpt::kCullTile;
+    c->cull_nty = (c->set.nrows + iqpt::kCullTile - 1) / iqpt::kCullTile;
+    c->cull_wt = (ntp + 31) / 32;
+    c->cull_stride = c->cull_wt + (nsp + 31) / 32;
+    const size_t words = (size_t)c->cull_ntx * c->cull_nty * c->cull_stride;
+    if (words == 0) {
+        c->cull_valid = true;
+        return IQPT_OK;
+    }
+    if (words > c->cull_cap) {
+        if (c->d_cull) {
+            IQPT_HIP(hipStreamSynchronize(c->stream));
+            (void)hipFree(c->d_cull);
+            c->d_cull = nullptr;
+            c->cull_cap = 0;
+        }
+        if (hipMalloc(&c->d_cull, words * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "cull masks");
+        c->cull_cap = words;
+    }
+    iqpt::kbin b;
+    std::memset(&b, 0, sizeof b);
+    b.width = c->width;
+    b.height = c->height;
+    b.x0 = c->set.x0;
+    b.ncols = c->ncols;
+    b.y0 = c->set.y0;
+    b.ystep = c->set.ystep;
+    b.nrows = c->set.nrows;
+    std::memcpy(b.inv_proj, c->cam.inv_proj, sizeof b.inv_proj);
+    std::memcpy(b.inv_view, c->cam.inv_view, sizeof b.inv_view);
+    cam_constants(c->cam, &b.cam_const, &b.cam_near_rw, &b.cam_far_rw);
+    b.tris = c->d_tris;
+    b.spheres = c->d_sph;
+    b.ntri = c->ntri;
+    b.nsph = c->nsph;
+    b.ntx = c->cull_ntx;
+    b.nty = c->cull_nty;
+    b.wt = c->cull_wt;
+    b.stride = c->cull_stride;
+    b.cull = c->d_cull;
+    const int le = iqpt::launch_bin(c->stream, b);
+    if (le != 0) return iqpt::hip_fail((hipError_t)le, "cull binning kernel");
+    c->cull_valid = true;
+    return IQPT_OK;
+}
+
+// w of the unprojected near/far points is a launch constant when the perspective row of the
+// inverse projection is (0, 0, m23, m33) with finite non-zero m23, m33 (camera_ray).
+void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, float* far_rw) {
+    const float* P = cam.inv_proj;
+    const float wf = P[11] + P[15];
+    const bool fin = std::isfinite(P[11]) && std::isfinite(P[15]) && std::isfinite(wf);
+    *is_const = 0;
+    *near_rw = 0.0f;
+    *far_rw = 0.0f;
+    if (P[3] == 0.0f && P[7] == 0.0f && fin && P[11] != 0.0f && P[15] != 0.0f && wf != 0.0f) {
+        *is_const = 1;
+        *near_rw = 1.0f / P[15];
+        *far_rw = 1.0f / wf;
+    }
 }
 
 hipEvent_t take_event(iqpt_ctx* c) {
@@ -223,6 +298,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->d_rays) (void)hipFree(c->d_rays);
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_stats) (void)hipFree(c->d_stats);
+    if (c->d_cull) (void)hipFree(c->d_cull);
     for (auto& pr : c->timed) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -239,6 +315,7 @@ int iqpt_set_camera(iqpt_ctx* c, const iqpt_camera* cam) {
         return iqpt::fail(IQPT_ERR_INVALID_ARG, "camera size differs from the context frame");
     c->cam = *cam;   // passed by value to every launch: no device copy to race with
     c->have_camera = true;
+    c->cull_valid = false;
     return IQPT_OK;
 }
 
@@ -373,18 +450,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     p.max_depth = c->max_depth;
     std::memcpy(p.inv_proj, c->cam.inv_proj, sizeof p.inv_proj);
     std::memcpy(p.inv_view, c->cam.inv_view, sizeof p.inv_view);
-    {
-        // w of the unprojected near/far points is a launch constant when the perspective row of
-        // the inverse projection is (0, 0, m23, m33) with finite non-zero m23, m33 (camera_ray).
-        const float* P = c->cam.inv_proj;
-        const float wf = P[11] + P[15];
-        const bool fin = std::isfinite(P[11]) && std::isfinite(P[15]) && std::isfinite(wf);
-        if (P[3] == 0.0f && P[7] == 0.0f && fin && P[11] != 0.0f && P[15] != 0.0f && wf != 0.0f) {
-            p.cam_const = 1;
-            p.cam_near_rw = 1.0f / P[15];
-            p.cam_far_rw = 1.0f / wf;
-        }
-    }
+    cam_constants(c->cam, &p.cam_const, &p.cam_near_rw, &p.cam_far_rw);
     p.acc_tab = spp <= iqpt::kAccTableMax ? 1u : 0u;
     p.frames32 = (c->frame + (uint64_t)spp) < (1ull << 32) ? 1u : 0u;
     p.tris = c->d_tris;
@@ -401,6 +467,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     int opt = (c->max_depth > 8 && (c->opt & ~iqpt::kOptFastDiv) == (iqpt::kOptDefault & ~iqpt::kOptFastDiv))
                   ? (c->opt & ~iqpt::kOptLB5) : c->opt;
     if (!c->fast_rcp_ok || c->width > (1u << 24) || c->height > (1u << 24)) opt &= ~iqpt::kOptFastDiv;
+    if (!(opt & iqpt::kOptPair)) opt &= ~iqpt::kOptCull;       // masks are per primitive pair
     p.rcp_width = 1.0f / (float)c->width;
     p.rcp_height = 1.0f / (float)c->height;
     const bool pair = (opt & iqpt::kOptPair) != 0;
@@ -419,6 +486,13 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     }
     const uint32_t lds = std::max<uint32_t>(16u, p.tri_batch * tri_rec + p.sph_batch * sph_rec +
                                                      (p.acc_tab ? spp * 8u : 0u));
+    if ((opt & iqpt::kOptCull) && (c->ntri + c->nsph) > 0) {
+        if (!c->cull_valid && (st = build_cull(c)) != IQPT_OK) return st;
+        p.cull = c->d_cull;
+        p.cull_ntx = c->cull_ntx;
+        p.cull_wt = c->cull_wt;
+        p.cull_stride = c->cull_stride;
+    }
     p.lin = c->d_lin;
     p.bgra = c->d_bgra;
     p.rng = c->d_rng;
@@ -550,6 +624,35 @@ int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
     }
     c->opt = opt;
     return IQPT_OK;
+}
+
+/* Internal (tests/test_cull.py): the host build of iq_interval.h for one tile of camera rays,
+ * x in [xa, xb], y in [ya, yb]. tris: ntri x 9 floats (v0, e1, e2 world space); spheres: nsph x 4
+ * (center, radius). Writes 1 per culled primitive; returns 0 with all flags 0 if the bundle is
+ * unbounded (nothing can be culled). */
+int iqpt_debug_cull_tile(const iqpt_camera* cam, uint32_t xa, uint32_t xb, uint32_t ya, uint32_t yb,
+                         const float* tris, uint32_t ntri, const float* spheres, uint32_t nsph,
+                         uint8_t* tri_culled, uint8_t* sph_culled) {
+    if (!cam || (ntri && (!tris || !tri_culled)) || (nsph && (!spheres || !sph_culled)))
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    iqiv::camera_in ci;
+    ci.width = cam->width;
+    ci.height = cam->height;
+    ci.rcp_width = 0.0f;
+    ci.rcp_height = 0.0f;
+    ci.inv_proj = cam->inv_proj;
+    ci.inv_view = cam->inv_view;
+    uint32_t cc = 0;
+    cam_constants(*cam, &cc, &ci.near_rw, &ci.far_rw);
+    ci.cam_const = (int)cc;
+    const iqiv::bundle b = iqiv::camera_bundle(ci, xa, xb, ya, yb);
+    for (uint32_t k = 0; k < ntri; ++k)
+        tri_culled[k] = b.ok && iqiv::tri_culled(b, tris + 9 * k, tris + 9 * k + 3, tris + 9 * k + 6) ? 1 : 0;
+    for (uint32_t k = 0; k < nsph; ++k) {
+        const float* sp = spheres + 4 * k;
+        sph_culled[k] = b.ok && iqiv::sphere_culled(b, sp, sp[3]) ? 1 : 0;
+    }
+    return b.ok ? 1 : 0;
 }
 
 /* Internal (tests/test_gpu_libm.py): evaluate the device build of the shared math on n inputs on

@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 from iqpt import _build, _lib  # noqa: E402
 
 OPT = {"cam": 1, "acc": 2, "pair": 4, "sincos": 32, "stats": 128}
-DEFAULT = 1 | 2 | 4 | 8 | 32 | 256
+DEFAULT = 1 | 2 | 4 | 8 | 32 | 256 | 512
 
 
 def main():
@@ -60,8 +60,8 @@ def main():
         sc.add_preset(args.scene or cfg.preset)
     pk = sc.build_packet()
     cam = iqpt.make_camera(cfg.width, cfg.height)
-    variants = {"default": DEFAULT, "none": 0, "-fastdiv": DEFAULT & ~256, "-pair": DEFAULT & ~4,
-                "-sincos": DEFAULT & ~32}
+    variants = {"default": DEFAULT, "none": 0, "-cull": DEFAULT & ~512, "-fastdiv": DEFAULT & ~256,
+                "-pair": DEFAULT & ~4, "-sincos": DEFAULT & ~32}
     if args.variants:
         variants = {kv.split("=")[0]: int(kv.split("=")[1], 0) for kv in args.variants.split(",")}
     ps = None

@@ -1,0 +1,18 @@
+# round-1 GPU run 16: exact camera-ray culling (kOptCull) — parity, A/B, bench
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/t16.log 2>&1 || { echo TESTS_FAILED; tail -40 gpurun_out/t16.log; exit 1; }
+tail -2 gpurun_out/t16.log
+timeout -k 10 600 python tools/ab_kernel.py --config c2 --rounds 9 --variants "default=815,nocull=303" --out gpurun_out/ab16_c2.json > gpurun_out/ab16_c2.log 2>&1 || { echo AB1_FAILED; tail -30 gpurun_out/ab16_c2.log; exit 1; }
+timeout -k 10 600 python tools/ab_kernel.py --config c4 --spp 2 --rounds 3 --crop 0,1920,400,1,256 --variants "default=815,nocull=303" --out gpurun_out/ab16_c4.json > gpurun_out/ab16_c4.log 2>&1 || { echo AB2_FAILED; tail -30 gpurun_out/ab16_c4.log; exit 1; }
+timeout -k 10 600 python tools/ab_kernel.py --config c5 --spp 1 --rounds 3 --crop 0,3840,1000,1,64 --variants "default=815,nocull=303" --out gpurun_out/ab16_c5.json > gpurun_out/ab16_c5.log 2>&1 || { echo AB3_FAILED; tail -30 gpurun_out/ab16_c5.log; exit 1; }
+python - <<'PY'
+import json
+for n in ("c2","c4","c5"):
+    d=json.load(open(f"gpurun_out/ab16_{n}.json"))
+    print(n, {k:(v["median_ms"], v["vs_default"], v["bitexact"]) for k,v in d["variants"].items()})
+PY
+timeout -k 10 400 python bench.py > gpurun_out/r16_bench.json 2> gpurun_out/r16_bench.err || { echo BENCH_FAILED; tail -30 gpurun_out/r16_bench.err; exit 1; }
+cat gpurun_out/r16_bench.json
+echo DONE
