@@ -4,11 +4,20 @@
 Metric: Mrays/s at 1920x1080, 8 bounces (C2: Cornell box, 5 quads + 2 spheres, 64 spp per frame),
 with the per-pixel RMSE vs the CPU oracle (reference semantics) reported beside it.
 
-One step = one 64-spp frame of C2 rendered by the HIP megakernel (one launch per GPU) — the pixel
-rows are dealt cyclically over the N ranks (one process per GPU) and, for N > 1, the float4
-accumulators are gathered to rank 0 over RCCL (torch.distributed "nccl") and de-interleaved.
-Total work is the fixed 1080p frame, so scaling is strong. value = closest-hit queries traced by all
-ranks in the K timed steps / the max over ranks of the timed wall time.
+One step = one 64-spp C2 frame per GPU rendered by the HIP megakernel (one launch per GPU, one
+process per GPU). Two multi-GPU modes:
+
+* --scaling weak (default): every rank renders the full 1080p frame with its own RNG
+  streams (seed 1984 + rank; rank 0 is the reference's own seed), so per-GPU work is fixed and the
+  job grows with N — N independent 64-spp estimates of the same view. No collective in the timed
+  region; after timing, the N accumulators are averaged onto rank 0 with one RCCL reduce (the
+  N x 64-spp image).
+* --scaling strong: the pixel rows of ONE frame are dealt cyclically over the ranks and the float4
+  accumulators are gathered to rank 0 over RCCL inside every step (bit-identical to the 1-GPU
+  frame).
+
+value = closest-hit queries traced by all ranks in the K timed steps / the max over ranks of the
+timed wall time.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--config c2]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
@@ -52,6 +61,8 @@ def parse():
     ap.add_argument("--one-device", action="store_true",
                     help="all ranks on GPU 0 (multi-rank rehearsal on a 1-GPU box; use with --backend gloo)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the assembled float frame (.npy)")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: every rank renders the full frame with seed 1984+rank; strong: rows of one frame")
     return ap.parse_args()
 
 
@@ -76,15 +87,16 @@ def cpu_baseline(cfg, pk, cam, seconds: float) -> dict:
                       f"(max_depth {cfg.max_depth}) in {dt:.1f} s, {rays} rays"}
 
 
-def verify_vs_oracle(cfg, pk, cam, lin_rank, rank, world, nrows) -> dict:
-    """After the first 64-spp frame: compare a band of this rank's rows with the oracle."""
+def verify_vs_oracle(cfg, pk, cam, lin_rank, rank, world, nrows, seed=1984) -> dict:
+    """After the first 64-spp frame: compare a band of this rank's rows with the oracle. `rank` and
+    `world` describe the row partition (world 1 = the rank owns the whole frame)."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle
     y_band = int(cfg.height * 0.46)                     # through both spheres
     first = y_band + ((rank - y_band) % world)          # first row >= y_band owned by this rank
     k0 = (first - rank) // world
     ps = iqpt.pixel_set(cfg.width, cfg.height, 0, cfg.width, first, world, nrows)
-    fr = oracle.OracleFrame(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
+    fr = oracle.OracleFrame(cfg.width, cfg.height, pixels=ps, seed=seed, max_depth=cfg.max_depth)
     fr.render(pk, cam, cfg.spp)
     mine = lin_rank.reshape(-1, cfg.width, 4)[k0:k0 + nrows].reshape(-1, 4)
     a = mine[:, :3].astype(np.float64)
@@ -122,27 +134,35 @@ def main():
     pk = scene.build_packet()
     stats = packet_stats(pk)
     cam = make_camera(cfg.width, cfg.height)
-    ps = iqdist.pixel_set_for_rank(cfg.width, cfg.height, rank, world)
-    pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth, device=device)
+    weak = args.scaling == "weak"
+    # weak: the whole frame per rank, RNG streams of seed 1984 + rank; strong: cyclic rows of one frame
+    part_rank, part_world = (0, 1) if weak else (rank, world)
+    seed = iqpt.DEFAULT_SEED + (rank if weak else 0)
+    ps = iqdist.pixel_set_for_rank(cfg.width, cfg.height, part_rank, part_world)
+    pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, seed=seed, max_depth=cfg.max_depth, device=device)
     pt.set_camera(cam)
     pt.upload_packet(pk)
 
-    max_px = iqdist.max_rows(cfg.height, world) * cfg.width
     on_gpu = args.backend == "nccl"
-    accum = (torch.zeros((max_px, 4), dtype=torch.float32, device="cuda" if on_gpu else "cpu")
-             if world > 1 else None)
-    gather_list = ([torch.empty_like(accum) for _ in range(world)] if (world > 1 and rank == 0) else None)
+    tdev = "cuda" if on_gpu else "cpu"
+    max_px = iqdist.max_rows(cfg.height, part_world) * cfg.width
+    accum = torch.zeros((max_px, 4), dtype=torch.float32, device=tdev) if world > 1 else None
+    gather_list = ([torch.empty_like(accum) for _ in range(world)]
+                   if (world > 1 and rank == 0 and not weak) else None)
     frame = None
+
+    def fetch_accum():
+        if on_gpu:
+            pt.copy_accum_device(accum.data_ptr(), accum.numel() * 4)     # D2D, then RCCL
+        else:
+            lin_host, _ = pt.read()
+            accum[: lin_host.shape[0]] = torch.from_numpy(lin_host)
 
     def step():
         nonlocal frame
         pt.render(cfg.spp)
-        if world > 1:
-            if on_gpu:
-                pt.copy_accum_device(accum.data_ptr(), accum.numel() * 4)     # D2D, then RCCL
-            else:
-                lin_host, _ = pt.read()
-                accum[: lin_host.shape[0]] = torch.from_numpy(lin_host)
+        if world > 1 and not weak:
+            fetch_accum()
             dist.gather(accum, gather_list, dst=0)
             if rank == 0:
                 frame = iqdist.assemble(gather_list, cfg.width, cfg.height, world)
@@ -153,7 +173,8 @@ def main():
         step()
         if i == 0 and args.verify_rows > 0:
             lin, _ = pt.read()
-            verify = verify_vs_oracle(cfg, pk, cam, lin, rank, world, min(args.verify_rows, ps.nrows))
+            verify = verify_vs_oracle(cfg, pk, cam, lin, part_rank, part_world, min(args.verify_rows, ps.nrows),
+                                      seed=seed)
     torch.cuda.synchronize()
     barrier()
     rays0 = pt.rays()
@@ -170,6 +191,12 @@ def main():
     elapsed = t1 - t0
     rays = pt.rays() - rays0
     kern_ms, launches = pt.kernel_time()
+    if weak and world > 1:
+        # after timing: the N independent estimates averaged onto rank 0 (the N x spp image)
+        fetch_accum()
+        dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)
+        if rank == 0:
+            frame = accum / float(world)
 
     vals = torch.tensor([elapsed, float(rays), kern_ms / max(1, launches), verify["rmse"] if verify else 0.0,
                          verify["bitexact_frac"] if verify else 1.0], dtype=torch.float64,
@@ -215,16 +242,20 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": "synthetic (procedural Cornell-box scene of SURVEY.md §8d, seed 1984)",
+            "data": ("synthetic (procedural Cornell-box scene of SURVEY.md §8d, seed 1984"
+                     + (", rank r: seed 1984+r)" if weak and world > 1 else ")")),
             "config": {"workload": f"{cfg.name}:{cfg.preset}", "width": cfg.width, "height": cfg.height,
                        "spp_per_step": cfg.spp, "max_depth": cfg.max_depth, "triangles": stats["triangles"],
-                       "spheres": stats["spheres"], "partition": f"cyclic rows x{world}",
+                       "spheres": stats["spheres"],
+                       "partition": (f"full frame per rank x{world} (seed 1984+rank)" if weak
+                                     else f"cyclic rows x{world}"),
                        "collective": ("none" if world == 1 else
-                                      "rccl gather of float4 accumulators" if on_gpu else
-                                      "gloo gather via host (rehearsal)")},
+                                      ("none in the timed region; one reduce of the accumulators after it"
+                                       if weak else "gather of float4 accumulators every step")
+                                      + (" (rccl)" if on_gpu else " (gloo via host, rehearsal)"))},
             "msamples_per_s": round(samples / elapsed / 1e6, 3),
             "rays_per_sample": round(total_rays / samples, 5),
             "rmse_vs_oracle": rmse_v,

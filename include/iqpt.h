@@ -175,6 +175,16 @@ int iqpt_kernel_time(iqpt_ctx* ctx, double* total_ms, uint64_t* launches);
 /* Name of the render kernel as it appears in rocprofv3 traces. */
 const char* iqpt_kernel_name(void);
 
+/* Checkpoint / resume of the progressive accumulation (the reference keeps this
+ * state only in device memory, path_tracer.cu:129-141). The file holds everything a context carries
+ * between launches — accumulator, BGRA frame, XORWOW states, frame counter, rays traced — so that
+ * render(a); checkpoint_save; ... checkpoint_load into a context created with the same frame size,
+ * pixel set, seed and max_depth; render(b) is bit-identical to render(a + b) in one context.
+ * Save synchronises and writes atomically (temporary file + rename); load validates the header, the
+ * sizes and an FNV-1a checksum before touching the context (IQPT_ERR_INVALID_ARG otherwise). */
+int iqpt_checkpoint_save(iqpt_ctx* ctx, const char* path);
+int iqpt_checkpoint_load(iqpt_ctx* ctx, const char* path);
+
 /* Headless replacement of the D3D11 present path: writes a binary PPM (P6) from BGRA8 pixels. */
 int iqpt_write_ppm(const char* path, uint32_t width, uint32_t height, const uint8_t* bgra);
 

@@ -488,13 +488,15 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 // secondary ray. Skipped pairs are rejected by the reference's own tests for every camera ray of
 // the tile, and the remaining pairs are visited in index order, so results are unchanged. Called by
 // all lanes of the wave (wave_or); only active lanes test.
+// Word 0 of each mask comes from the lane's registers (cm_t, cm_s: loaded with the pixel).
 template <int OPT>
 __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntri, const float4* sph, uint32_t nsph,
-                                                 const uint32_t* lane_mask, bool all, bool active, const ray3 ray,
-                                                 float& closest, int& kind, uint32_t& hidx, uint32_t wt) {
+                                                 const uint32_t* lane_mask, uint32_t cm_t, uint32_t cm_s, bool all,
+                                                 bool active, const ray3 ray, float& closest, int& kind,
+                                                 uint32_t& hidx, uint32_t wt) {
     const uint32_t tp = (ntri + 1) / 2, sp = (nsph + 1) / 2;
     for (uint32_t w = 0; w * 32u < tp; ++w) {
-        uint32_t m = all ? ~0u : wave_or(lane_mask ? lane_mask[w] : 0u);
+        uint32_t m = all ? ~0u : wave_or(lane_mask ? (w == 0 ? cm_t : lane_mask[w]) : 0u);
         while (m) {
             const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
@@ -506,7 +508,7 @@ __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntr
         }
     }
     for (uint32_t w = 0; w * 32u < sp; ++w) {
-        uint32_t m = all ? ~0u : wave_or(lane_mask ? lane_mask[wt + w] : 0u);
+        uint32_t m = all ? ~0u : wave_or(lane_mask ? (w == 0 ? cm_s : lane_mask[wt + w]) : 0u);
         while (m) {
             const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
@@ -519,8 +521,11 @@ __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntr
     }
 }
 
+// The running-mean table occupies spp float2 of dynamic LDS when the launch builds it.
+__device__ __forceinline__ bool use_tab_lds(const kparams& p) { return p.acc_tab != 0u; }
+
 // ------------------------------------------------------------------------------------------------
-// The megakernel. MAXD bounds max_depth (register stack size); STREAM selects LDS batch streaming
+// The megakernel. MAXD bounds max_depth (variant selection; the scatter stack lives in LDS); STREAM selects LDS batch streaming
 // (scene larger than the resident budget) with workgroup-uniform iteration; OPT is the kOpt* mask.
 template <int OPT>
 constexpr int min_waves_per_simd() {
@@ -543,7 +548,10 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
     float4* lds_tri = lds;
     float4* lds_sph = lds + (size_t)p.tri_batch * kTriRec;
     float2* lds_tab = reinterpret_cast<float2*>(lds_sph + (size_t)p.sph_batch * kSphRec);
+    // kOptCull: one (mask word 0 of triangles, of spheres, tile, -) slot per thread, 16-B aligned
+    uint4* lds_cm = reinterpret_cast<uint4*>(lds_tab + (use_tab_lds(p) ? ((p.spp + 1u) & ~1u) : 0u));
     const bool use_tab = (OPT & kOptAccTable) && p.acc_tab;
+    constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
 
     if (!STREAM) {
         for (uint32_t i = threadIdx.x; i < tri_recs * kTriRec; i += kRenderBlock) lds_tri[i] = g_tri[i];
@@ -560,18 +568,19 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
 
     const uint32_t lane = __lane_id();
     // ---- per-lane state
+    // (the compact pixel index, the tile and the mask words live in LDS / are recomputed at the
+    // pixel's end, and the accumulator's untouched w is never loaded: registers are the limit at
+    // 5 waves/SIMD)
     bool active = false;
-    uint32_t pix = 0, px = 0, py = 0;
-    uint32_t tile = 0;                 // kOptCull: the pixel's screen tile
+    uint32_t px = 0, py = 0;
     uint32_t done = 0;                 // samples finished for the current pixel
     rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
-    float4 acc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    float3 acc = make_float3(0.0f, 0.0f, 0.0f);
     ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
     int depth = 0;
-    float stk[MAXD];
-#pragma unroll
-    for (int i = 0; i < MAXD; ++i) stk[i] = 1.0f;
-    uint32_t nrays = 0;
+    // scatter-record stack (path_tracer.cu:243): record k of the current path at lds_stk[k][thread]
+    float* lds_stk = reinterpret_cast<float*>(lds_cm + ((OPT & kOptCull) ? kRenderBlock : 0));
+    uint64_t wave_rays = 0;            // closest-hit queries of this wave (wave-uniform)
     // ---- wave-uniform chunk state
     uint32_t chunk_next = 0, chunk_end = 0;
     bool exhausted = false;
@@ -596,22 +605,28 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
             const uint32_t avail = chunk_end - chunk_next;
             const uint32_t rank = prefix_below(need);
             if (!active && rank < avail) {
-                pix = chunk_next + rank;
+                const uint32_t pix = chunk_next + rank;
                 const uint32_t col = pix % p.ncols, row = pix / p.ncols;
                 px = p.x0 + col;
                 py = p.y0 + row * p.ystep;
-                if (OPT & kOptCull) tile = col / kCullTile + (row / kCullTile) * p.cull_ntx;
                 st.v0 = p.rng[pix];
                 st.v1 = p.rng[(size_t)p.npix + pix];
                 st.v2 = p.rng[2 * (size_t)p.npix + pix];
                 st.v3 = p.rng[3 * (size_t)p.npix + pix];
                 st.v4 = p.rng[4 * (size_t)p.npix + pix];
                 st.d = p.rng[5 * (size_t)p.npix + pix];
-                const float4_storage a = p.lin[pix];
-                acc = make_float4(a.x, a.y, a.z, a.w);
+                const float* a = reinterpret_cast<const float*>(p.lin + pix);
+                acc = make_float3(a[0], a[1], a[2]);
                 done = 0;
                 depth = 0;
                 camera_ray<OPT>(p, px, py, st, ray);
+                if (kCull && p.cull) {
+                    // the tile and word 0 of its triangle / sphere masks, kept in this lane's LDS slot for
+                    // the pixel's lifetime (the global load latency is paid once per pixel, not per ray)
+                    const uint32_t tile = col / kCullTile + (row / kCullTile) * p.cull_ntx;
+                    lds_cm[threadIdx.x] = make_uint4(p.cull[(size_t)tile * p.cull_stride],
+                                                     p.cull[(size_t)tile * p.cull_stride + p.cull_wt], tile, 0u);
+                }
                 active = true;
             }
             const uint32_t cnt = (uint32_t)__popcll(need);
@@ -639,17 +654,16 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
         uint32_t hidx = 0;
         // kOptCull: camera rays (depth 0) test only the pairs of their tile's mask; one secondary ray
         // in the wave makes it test everything
-        constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
         const bool cull = kCull && p.cull != nullptr && !__any(active && depth != 0);
         const uint32_t* lane_mask =
-            (cull && active) ? p.cull + (size_t)tile * p.cull_stride : nullptr;   // null: contributes 0
+            (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;   // null: 0
         if (STREAM) {
             for (uint32_t base = 0; base < tri_recs; base += p.tri_batch) {
                 const uint32_t n = min(p.tri_batch, tri_recs - base);
                 uint32_t wm[kCull ? 8 : 1];
                 bool any = true;
                 if (kCull) {
-                    // the batch's mask words (tri_batch is 256 pairs when culling: 8 aligned words)
+                    // the batch's mask words (a batch is at most 256 pairs, a multiple of 32: <= 8 aligned words)
                     any = false;
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
@@ -731,8 +745,9 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                 }
             }
         } else if (kCull && p.cull != nullptr) {
-            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, !cull, active, ray, closest, kind,
-                                  hidx, p.cull_wt);
+            const uint4 cm = lds_cm[threadIdx.x];
+            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray,
+                                  closest, kind, hidx, p.cull_wt);
         } else if (active) {
             intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
         }
@@ -740,20 +755,27 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
         // ------------------------------------------------ shade (path_tracer.cu:297-316)
         bool term = false;
         float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
+        wave_rays += (uint64_t)__popcll(__ballot(active));
         if (active) {
-            ++nrays;
             if (kind == kHitSphere) {
                 if (OPT & kOptStats) ++s_scatter_lanes;
-                const float s = oren_nayar_scatter<OPT>(g_sph_plain[hidx], closest, ray, st);
+                float4 sphr;
+                if (!STREAM && kPair) {
+                    // the pair record in LDS: (cx_a, cx_b, cy_a, cy_b), (cz_a, cz_b, r_a, r_b)
+                    const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) +
+                                     (hidx & 1u);
+                    sphr = make_float4(q[0], q[2], q[4], q[6]);
+                } else {
+                    sphr = g_sph_plain[hidx];
+                }
+                const float s = oren_nayar_scatter<OPT>(sphr, closest, ray, st);
                 if (depth + 1 >= p.max_depth) {
                     term = true;                 // the last record is this scatter (biased, :252)
                     Lx = s;
                     Ly = s;
                     Lz = s;
                 } else {
-#pragma unroll
-                    for (int i = MAXD - 1; i > 0; --i) stk[i] = stk[i - 1];
-                    stk[0] = s;
+                    lds_stk[(uint32_t)depth * kRenderBlock + threadIdx.x] = s;
                     ++depth;
                 }
             } else if (kind == kHitTri) {
@@ -783,15 +805,12 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
         if (term) {
             // backward product over the stacked records, newest first (:321-324)
             float cx = Lx, cy = Ly, cz = Lz;
-            if (depth > 0) {                     // most paths end on their first ray
-#pragma unroll
-                for (int i = 0; i < MAXD; ++i) {
-                    if (i < depth) {
-                        cx = cx * stk[i];
-                        cy = cy * stk[i];
-                        cz = cz * stk[i];
-                    }
-                }
+            // most paths end on their first ray (depth 0: no records)
+            for (int i = depth - 1; i >= 0; --i) {
+                const float r = lds_stk[(uint32_t)i * kRenderBlock + threadIdx.x];
+                cx = cx * r;
+                cy = cy * r;
+                cz = cz * r;
             }
             // clamp (:345-347), path_color = 0 + color (:341,348), running mean (:356-358)
             cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
@@ -822,13 +841,12 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                 const uint32_t r8 = to_u8(255.0f * iq_sqrtf(acc.x));
                 const uint32_t g8 = to_u8(255.0f * iq_sqrtf(acc.y));
                 const uint32_t b8 = to_u8(255.0f * iq_sqrtf(acc.z));
+                const uint32_t pix = ((py - p.y0) / p.ystep) * p.ncols + (px - p.x0);
                 p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
-                float4_storage o;
-                o.x = acc.x;
-                o.y = acc.y;
-                o.z = acc.z;
-                o.w = acc.w;
-                p.lin[pix] = o;
+                float* o = reinterpret_cast<float*>(p.lin + pix);          // w is never written
+                o[0] = acc.x;
+                o[1] = acc.y;
+                o[2] = acc.z;
                 p.rng[pix] = st.v0;
                 p.rng[(size_t)p.npix + pix] = st.v1;
                 p.rng[2 * (size_t)p.npix + pix] = st.v2;
@@ -843,11 +861,8 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
         if (!exhausted && __any(!active)) refill();
     }
 
-    // closest-hit query count: wave reduction, one atomic per wave
-    uint32_t sum = nrays;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
-    if (lane == 0 && sum) atomicAdd(p.rays, (unsigned long long)sum);
+    // closest-hit query count: one atomic per wave
+    if (lane == 0 && wave_rays) atomicAdd(p.rays, (unsigned long long)wave_rays);
     if (OPT & kOptStats) {
         unsigned long long scat = s_scatter_lanes;
 #pragma unroll
@@ -997,12 +1012,12 @@ struct variant {
 };
 #define IQPT_V(M, S, O) {M, S, O, launch_t<M, S, O>, occ_t<M, S, O>}
 const variant kVariants[] = {
-    // MAXD 16 would spill under the 96-VGPR bound of kOptLB5 (16 stack registers): 4 waves/SIMD
+    // MAXD 16 (max_depth 9-16) differs only in the LDS stack size the runtime reserves
     IQPT_V(8, false, kOptDefault), IQPT_V(8, true, kOptDefault),
-    IQPT_V(16, false, kOptDefault & ~kOptLB5), IQPT_V(16, true, kOptDefault & ~kOptLB5),
+    IQPT_V(16, false, kOptDefault), IQPT_V(16, true, kOptDefault),
     // packets outside the kOptFastDiv range (iqpt_upload_packet)
     IQPT_V(8, false, kOptDefault & ~kOptFastDiv), IQPT_V(8, true, kOptDefault & ~kOptFastDiv),
-    IQPT_V(16, false, kOptDefault & ~kOptLB5 & ~kOptFastDiv), IQPT_V(16, true, kOptDefault & ~kOptLB5 & ~kOptFastDiv),
+    IQPT_V(16, false, kOptDefault & ~kOptFastDiv), IQPT_V(16, true, kOptDefault & ~kOptFastDiv),
 #if defined(IQPT_AB_VARIANTS)
     IQPT_V(8, false, 0),
     IQPT_V(8, true, 0),

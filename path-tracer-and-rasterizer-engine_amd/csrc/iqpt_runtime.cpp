@@ -28,9 +28,10 @@ thread_local std::string g_last_error;
 
 // LDS budget under which the whole scene stays resident per block (no barriers in the loop).
 constexpr uint32_t kLdsResidentBytes = 32 * 1024;
-// Batch sizes when the scene is streamed through LDS (24 KB + 8 KB).
-constexpr uint32_t kTriBatch = 512;
-constexpr uint32_t kSphBatch = 512;
+// Batch sizes when the scene is streamed through LDS (pairs: 10 KB + 4 KB; with the table, mask
+// slots and scatter stack a block stays under 32 KB, so 5 blocks fit a CU).
+constexpr uint32_t kTriBatch = 256;   // primitives per LDS batch (128 pairs = 10 KB)
+constexpr uint32_t kSphBatch = 256;
 
 std::once_flag g_tables_once;
 std::vector<uint32_t> g_tables;  // A^(2^(67+i)), i < 32
@@ -461,11 +462,9 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     p.sph_pairs = c->d_sph_pairs;
     p.nsph = c->nsph;
     p.nsph_pairs = (c->nsph + 1) / 2;
-    // the production variant for max_depth > 8 carries 16 stack registers and no 5-wave bound;
     // kOptFastDiv only for packets inside its range (upload) and frames up to 2^24 wide / high
     // (camera_ray divides by W and H with the pre-rounded reciprocals below)
-    int opt = (c->max_depth > 8 && (c->opt & ~iqpt::kOptFastDiv) == (iqpt::kOptDefault & ~iqpt::kOptFastDiv))
-                  ? (c->opt & ~iqpt::kOptLB5) : c->opt;
+    int opt = c->opt;
     if (!c->fast_rcp_ok || c->width > (1u << 24) || c->height > (1u << 24)) opt &= ~iqpt::kOptFastDiv;
     if (!(opt & iqpt::kOptPair)) opt &= ~iqpt::kOptCull;       // masks are per primitive pair
     p.rcp_width = 1.0f / (float)c->width;
@@ -484,8 +483,12 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
         p.tri_batch = tri_recs;
         p.sph_batch = sph_recs;
     }
-    const uint32_t lds = std::max<uint32_t>(16u, p.tri_batch * tri_rec + p.sph_batch * sph_rec +
-                                                     (p.acc_tab ? spp * 8u : 0u));
+    // scene batch + running-mean table (padded to 16 B) + (kOptCull) one uint4 slot per thread +
+    // the scatter-record stack (max_depth - 1 records per thread; one float each)
+    const uint32_t lds = p.tri_batch * tri_rec + p.sph_batch * sph_rec +
+                         (p.acc_tab ? ((spp + 1u) & ~1u) * 8u : 0u) +
+                         ((opt & iqpt::kOptCull) ? iqpt::kRenderBlock * 16u : 0u) +
+                         (uint32_t)std::max(c->max_depth, 1) * iqpt::kRenderBlock * 4u;
     if ((opt & iqpt::kOptCull) && (c->ntri + c->nsph) > 0) {
         if (!c->cull_valid && (st = build_cull(c)) != IQPT_OK) return st;
         p.cull = c->d_cull;
@@ -564,6 +567,120 @@ int iqpt_copy_accum_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
     IQPT_HIP(hipMemcpyAsync(dst_device, c->d_lin, (size_t)c->npix * sizeof(float4_storage), hipMemcpyDeviceToDevice,
                             c->stream));
     IQPT_HIP(hipStreamSynchronize(c->stream));
+    return IQPT_OK;
+}
+
+namespace {
+// Checkpoint file: header, then accumulator (npix float4), BGRA (npix u32), RNG (6 planes of npix u32).
+struct ckpt_header {
+    char magic[8];            // "IQPTCKP1"
+    uint32_t version;         // 1
+    uint32_t width, height;
+    uint32_t x0, x1, y0, ystep, nrows;
+    int32_t max_depth;
+    uint64_t seed;
+    uint64_t frame;
+    uint64_t rays;
+    uint64_t npix;
+    uint64_t checksum;        // FNV-1a 64 over the payload
+};
+constexpr char kCkptMagic[8] = {'I', 'Q', 'P', 'T', 'C', 'K', 'P', '1'};
+
+uint64_t fnv1a(const void* data, size_t n, uint64_t h = 1469598103934665603ull) {
+    const unsigned char* b = static_cast<const unsigned char*>(data);
+    for (size_t i = 0; i < n; ++i) {
+        h ^= b[i];
+        h *= 1099511628211ull;
+    }
+    return h;
+}
+}  // namespace
+
+int iqpt_checkpoint_save(iqpt_ctx* c, const char* path) {
+    if (!c || !path) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    const size_t n = c->npix;
+    std::vector<float4_storage> lin(n);
+    std::vector<uint32_t> bgra(n), rng(n * 6);
+    unsigned long long rays = 0;
+    IQPT_HIP(hipMemcpy(lin.data(), c->d_lin, n * sizeof(float4_storage), hipMemcpyDeviceToHost));
+    IQPT_HIP(hipMemcpy(bgra.data(), c->d_bgra, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    IQPT_HIP(hipMemcpy(rng.data(), c->d_rng, n * 6 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    IQPT_HIP(hipMemcpy(&rays, c->d_rays, sizeof rays, hipMemcpyDeviceToHost));
+    ckpt_header h;
+    std::memset(&h, 0, sizeof h);
+    std::memcpy(h.magic, kCkptMagic, 8);
+    h.version = 1;
+    h.width = c->width;
+    h.height = c->height;
+    h.x0 = c->set.x0;
+    h.x1 = c->set.x1;
+    h.y0 = c->set.y0;
+    h.ystep = c->set.ystep;
+    h.nrows = c->set.nrows;
+    h.max_depth = c->max_depth;
+    h.seed = c->seed;
+    h.frame = c->frame;
+    h.rays = rays;
+    h.npix = n;
+    uint64_t sum = fnv1a(lin.data(), n * sizeof(float4_storage));
+    sum = fnv1a(bgra.data(), n * sizeof(uint32_t), sum);
+    h.checksum = fnv1a(rng.data(), n * 6 * sizeof(uint32_t), sum);
+    const std::string tmp = std::string(path) + ".tmp";
+    FILE* f = std::fopen(tmp.c_str(), "wb");
+    if (!f) return iqpt::fail(IQPT_ERR_INVALID_ARG, "cannot open " + tmp);
+    bool ok = std::fwrite(&h, sizeof h, 1, f) == 1 &&
+              std::fwrite(lin.data(), sizeof(float4_storage), n, f) == n &&
+              std::fwrite(bgra.data(), sizeof(uint32_t), n, f) == n &&
+              std::fwrite(rng.data(), sizeof(uint32_t), n * 6, f) == n * 6;
+    ok = (std::fclose(f) == 0) && ok;
+    if (!ok || std::rename(tmp.c_str(), path) != 0) {
+        std::remove(tmp.c_str());
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, std::string("cannot write ") + path);
+    }
+    return IQPT_OK;
+}
+
+int iqpt_checkpoint_load(iqpt_ctx* c, const char* path) {
+    if (!c || !path) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    FILE* f = std::fopen(path, "rb");
+    if (!f) return iqpt::fail(IQPT_ERR_INVALID_ARG, std::string("cannot open ") + path);
+    ckpt_header h;
+    const size_t n = c->npix;
+    std::vector<float4_storage> lin(n);
+    std::vector<uint32_t> bgra(n), rng(n * 6);
+    bool ok = std::fread(&h, sizeof h, 1, f) == 1;
+    std::string why;
+    if (!ok || std::memcmp(h.magic, kCkptMagic, 8) != 0 || h.version != 1) why = "not an iqpt checkpoint (v1)";
+    else if (h.width != c->width || h.height != c->height || h.x0 != c->set.x0 || h.x1 != c->set.x1 ||
+             h.y0 != c->set.y0 || h.ystep != c->set.ystep || h.nrows != c->set.nrows || h.npix != n)
+        why = "frame size / pixel set differ from the context";
+    else if (h.seed != c->seed || h.max_depth != c->max_depth) why = "seed / max_depth differ from the context";
+    if (why.empty()) {
+        ok = std::fread(lin.data(), sizeof(float4_storage), n, f) == n &&
+             std::fread(bgra.data(), sizeof(uint32_t), n, f) == n &&
+             std::fread(rng.data(), sizeof(uint32_t), n * 6, f) == n * 6;
+        unsigned char extra;
+        if (!ok || std::fread(&extra, 1, 1, f) != 0) why = "truncated or oversized checkpoint";
+    }
+    std::fclose(f);
+    if (why.empty()) {
+        uint64_t sum = fnv1a(lin.data(), n * sizeof(float4_storage));
+        sum = fnv1a(bgra.data(), n * sizeof(uint32_t), sum);
+        if (fnv1a(rng.data(), n * 6 * sizeof(uint32_t), sum) != h.checksum) why = "checksum mismatch";
+    }
+    if (!why.empty()) return iqpt::fail(IQPT_ERR_INVALID_ARG, std::string(path) + ": " + why);
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    const unsigned long long rays = h.rays;
+    IQPT_HIP(hipMemcpy(c->d_lin, lin.data(), n * sizeof(float4_storage), hipMemcpyHostToDevice));
+    IQPT_HIP(hipMemcpy(c->d_bgra, bgra.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    IQPT_HIP(hipMemcpy(c->d_rng, rng.data(), n * 6 * sizeof(uint32_t), hipMemcpyHostToDevice));
+    IQPT_HIP(hipMemcpy(c->d_rays, &rays, sizeof rays, hipMemcpyHostToDevice));
+    c->frame = h.frame;
     return IQPT_OK;
 }
 

@@ -118,4 +118,13 @@ void path_tracer::read_linear(std::vector<float>& rgba) const {
     IQPT_THROW_FAILED(iqpt_read(m_ctx, rgba.data(), nullptr));
 }
 
+void path_tracer::save_checkpoint(const std::string& path) const {
+    IQPT_THROW_FAILED(iqpt_checkpoint_save(m_ctx, path.c_str()));
+}
+
+void path_tracer::load_checkpoint(const std::string& path) {
+    IQPT_THROW_FAILED(iqpt_checkpoint_load(m_ctx, path.c_str()));
+    m_pending_reset = false;       // the loaded state replaces any reset not yet applied
+}
+
 }  // namespace iqpt

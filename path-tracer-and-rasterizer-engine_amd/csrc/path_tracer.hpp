@@ -114,6 +114,9 @@ public:
     uint64_t frames() const;
     uint64_t rays_traced() const;
     void read_linear(std::vector<float>& rgba) const;
+    // progressive accumulation checkpoint / resume (iqpt_checkpoint_save / _load)
+    void save_checkpoint(const std::string& path) const;
+    void load_checkpoint(const std::string& path);
     iqpt_ctx* context() const { return m_ctx; }
 
 private:

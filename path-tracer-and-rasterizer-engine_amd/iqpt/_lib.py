@@ -86,6 +86,8 @@ SIGNATURES = [
     ("iqpt_rays_traced", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("iqpt_kernel_time", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     ("iqpt_kernel_name", C.c_char_p, []),
+    ("iqpt_checkpoint_save", C.c_int, [_P, C.c_char_p]),
+    ("iqpt_checkpoint_load", C.c_int, [_P, C.c_char_p]),
     ("iqpt_write_ppm", C.c_int, [C.c_char_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint8)]),
     ("iqpt_error_string", C.c_char_p, [C.c_int]),
     ("iqpt_last_error", C.c_char_p, []),

@@ -82,6 +82,14 @@ class PathTracer:
         check(self._lib.iqpt_read_rng(self._h, st.ctypes.data_as(C.POINTER(C.c_uint32))), "iqpt_read_rng")
         return st
 
+    def checkpoint_save(self, path) -> None:
+        """Accumulator, frame, RNG states, frame counter and ray count to `path` (iqpt_checkpoint_save)."""
+        check(self._lib.iqpt_checkpoint_save(self._h, str(path).encode()), "iqpt_checkpoint_save")
+
+    def checkpoint_load(self, path) -> None:
+        """Resume from a checkpoint of a context with the same frame, pixel set, seed and max_depth."""
+        check(self._lib.iqpt_checkpoint_load(self._h, str(path).encode()), "iqpt_checkpoint_load")
+
     def copy_accum_device(self, dst_ptr: int, nbytes: int):
         check(self._lib.iqpt_copy_accum_device(self._h, C.c_void_p(dst_ptr), nbytes), "iqpt_copy_accum_device")
 
