@@ -75,6 +75,9 @@ struct kparams {
     // camera rays of the tile may hit (iq_interval.h); null = no culling for this launch
     const uint32_t* cull;
     uint32_t cull_ntx, cull_wt, cull_stride;
+    // queue order: queue position q -> compact pixel index perm[q] (null = identity). Built with the
+    // masks: whole 8x8 tiles, most expensive first (longest-processing-time order, shorter tail)
+    const uint32_t* perm;
 };
 
 // Binning launch (iqpt_bin_kernel): the camera and pixel set of the context, the world-space scene.
@@ -111,6 +114,9 @@ int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, u
                     uint32_t* rng);
 // Tile masks for kOptCull (one thread per tile word).
 int launch_bin(void* stream, const kbin& b);
+// Per-tile cost estimate from the masks: set triangle-pair bits + 8 x set sphere-pair bits.
+int launch_tile_cost(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
+                     uint32_t* cost);
 // Device probe of the shared math (iqpt_debug_libm).
 int launch_libm(void* stream, int fn, const float* a, const float* b, float* out, uint32_t n);
 // grid_blocks = persistent grid size; lds_bytes dynamic LDS; stream = hipStream_t; opt = kOpt* mask.

@@ -605,7 +605,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
             const uint32_t avail = chunk_end - chunk_next;
             const uint32_t rank = prefix_below(need);
             if (!active && rank < avail) {
-                const uint32_t pix = chunk_next + rank;
+                const uint32_t pix = p.perm ? p.perm[chunk_next + rank] : chunk_next + rank;
                 const uint32_t col = pix % p.ncols, row = pix / p.ncols;
                 px = p.x0 + col;
                 py = p.y0 + row * p.ystep;
@@ -966,6 +966,18 @@ __global__ __launch_bounds__(256) void iqpt_bin_kernel(const kbin b) {
     b.cull[gid] = bits;
 }
 
+// Cost estimate per tile for the queue order: candidate triangle pairs + 8 x candidate sphere pairs
+// (a camera ray that can hit a sphere starts an Oren-Nayar path: more rays and the scatter shading).
+__global__ __launch_bounds__(256) void iqpt_tile_cost_kernel(const uint32_t* cull, uint32_t ntiles, uint32_t wt,
+                                                             uint32_t stride, uint32_t* cost) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint32_t* m = cull + (size_t)t * stride;
+    uint32_t c = 0;
+    for (uint32_t w = 0; w < stride; ++w) c += (uint32_t)__popc(m[w]) * (w < wt ? 1u : 8u);
+    cost[t] = c;
+}
+
 // curand_init(seed, global pixel id, 0) per owned pixel (renderer_init_kernel, path_tracer.cu:36-46).
 __global__ __launch_bounds__(256) void iqpt_rng_init_kernel(uint32_t width, uint32_t x0, uint32_t ncols,
                                                             uint32_t y0, uint32_t ystep, uint32_t npix,
@@ -1069,6 +1081,14 @@ int launch_bin(void* stream, const kbin& b) {
     if (n == 0) return 0;
     if (n > 0xffffffffull * 256ull) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(iqpt_bin_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, b);
+    return (int)hipGetLastError();
+}
+
+int launch_tile_cost(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
+                     uint32_t* cost) {
+    if (ntiles == 0) return 0;
+    hipLaunchKernelGGL(iqpt_tile_cost_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, cull,
+                       ntiles, wt, stride, cost);
     return (int)hipGetLastError();
 }
 

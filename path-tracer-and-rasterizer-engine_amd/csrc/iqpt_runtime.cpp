@@ -95,6 +95,7 @@ struct iqpt_ctx {
     bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
     // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
     uint32_t* d_cull = nullptr;
+    uint32_t* d_perm = nullptr;   // queue order built with the masks (npix)
     size_t cull_cap = 0;       // words allocated
     bool cull_valid = false;
     uint32_t cull_ntx = 0, cull_nty = 0, cull_wt = 0, cull_stride = 0;
@@ -167,6 +168,33 @@ int build_cull(iqpt_ctx* c) {
     b.cull = c->d_cull;
     const int le = iqpt::launch_bin(c->stream, b);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "cull binning kernel");
+    // queue order: whole tiles, most expensive first (a chunk of the queue is then one tile, and the
+    // pixels that set the end of the launch are cheap ones)
+    const uint32_t ntiles = c->cull_ntx * c->cull_nty;
+    uint32_t* d_cost = nullptr;
+    IQPT_HIP(hipMalloc(&d_cost, (size_t)ntiles * sizeof(uint32_t)));
+    std::vector<uint32_t> cost(ntiles);
+    const int lc = iqpt::launch_tile_cost(c->stream, c->d_cull, ntiles, c->cull_wt, c->cull_stride, d_cost);
+    hipError_t e = lc ? (hipError_t)lc : hipMemcpyAsync(cost.data(), d_cost, (size_t)ntiles * sizeof(uint32_t),
+                                                        hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(d_cost);
+    if (e != hipSuccess) return iqpt::hip_fail(e, "tile cost");
+    std::vector<uint32_t> order(ntiles);
+    for (uint32_t t = 0; t < ntiles; ++t) order[t] = t;
+    std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    std::vector<uint32_t> perm;
+    perm.reserve(c->npix);
+    for (uint32_t t : order) {
+        const uint32_t tx = t % c->cull_ntx, ty = t / c->cull_ntx;
+        for (uint32_t r = ty * iqpt::kCullTile; r < std::min((ty + 1) * iqpt::kCullTile, c->set.nrows); ++r)
+            for (uint32_t q = tx * iqpt::kCullTile; q < std::min((tx + 1) * iqpt::kCullTile, c->ncols); ++q)
+                perm.push_back(r * c->ncols + q);
+    }
+    if (perm.size() != c->npix) return iqpt::fail(IQPT_ERR_INVALID_ARG, "queue order does not cover the pixel set");
+    if (!c->d_perm && hipMalloc(&c->d_perm, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess)
+        return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "queue order");
+    IQPT_HIP(hipMemcpy(c->d_perm, perm.data(), perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->cull_valid = true;
     return IQPT_OK;
 }
@@ -300,6 +328,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
+    if (c->d_perm) (void)hipFree(c->d_perm);
     for (auto& pr : c->timed) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -492,6 +521,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     if ((opt & iqpt::kOptCull) && (c->ntri + c->nsph) > 0) {
         if (!c->cull_valid && (st = build_cull(c)) != IQPT_OK) return st;
         p.cull = c->d_cull;
+        p.perm = c->d_perm;
         p.cull_ntx = c->cull_ntx;
         p.cull_wt = c->cull_wt;
         p.cull_stride = c->cull_stride;
