@@ -68,16 +68,17 @@ struct kparams {
     uint32_t* bgra;                  // npix
     uint32_t* rng;                   // 6 planes of npix words: v0..v4, d
     unsigned long long* rays;        // closest-hit query counter
-    uint32_t* queue;                 // pixel dequeue head (zeroed before every launch)
+    uint32_t* queue;                 // tile dequeue head (zeroed before every launch)
     unsigned long long* stats;       // kOptStats counters (8 x u64) or null
     // kOptCull: per screen tile of kCullTile x kCullTile owned pixels (columns x owned rows), one bit
     // per triangle pair (words [0, cull_wt)) and per sphere pair (words [cull_wt, cull_stride)) that
     // camera rays of the tile may hit (iq_interval.h); null = no culling for this launch
     const uint32_t* cull;
     uint32_t cull_ntx, cull_wt, cull_stride;
-    // queue order: queue position q -> compact pixel index perm[q] (null = identity). Built with the
-    // masks: whole 8x8 tiles, most expensive first (longest-processing-time order, shorter tail)
-    const uint32_t* perm;
+    // work queue over tiles: queue position q -> tile tile_order[q] (null = identity); built with the
+    // masks, most expensive tiles first (longest-processing-time order: a shorter launch tail)
+    const uint32_t* tile_order;
+    uint32_t ntx, ntiles;            // tiles of the owned set (kCullTile x kCullTile)
 };
 
 // Binning launch (iqpt_bin_kernel): the camera and pixel set of the context, the world-space scene.
@@ -93,6 +94,28 @@ struct kbin {
     uint32_t* cull;                  // ntx * nty * stride words
 };
 constexpr uint32_t kCullTile = 8;
+
+// Pixel state (accumulator, BGRA, RNG planes) is stored TILE-MAJOR over the owned set: 8x8 tiles
+// of (column, owned row) in row-major tile order, pixels row-major inside a tile; tiles of the last
+// tile column / row are narrower / shorter. A work-queue chunk is one tile, so a wave's loads and
+// stores of pixel state are contiguous. The C ABI converts to the compact row-major order on the
+// way in and out (iqpt_read, iqpt_read_rng, iqpt_copy_accum_device, checkpoints).
+__host__ __device__ inline uint32_t tile_store_index(uint32_t col, uint32_t row, uint32_t ncols, uint32_t nrows) {
+    const uint32_t tx = col / kCullTile, ty = row / kCullTile;
+    const uint32_t th = nrows - ty * kCullTile < kCullTile ? nrows - ty * kCullTile : kCullTile;
+    const uint32_t tw = ncols - tx * kCullTile < kCullTile ? ncols - tx * kCullTile : kCullTile;
+    return ty * kCullTile * ncols + tx * kCullTile * th + (row % kCullTile) * tw + col % kCullTile;
+}
+__host__ __device__ inline void tile_decode(uint32_t s, uint32_t ncols, uint32_t nrows, uint32_t* col, uint32_t* row) {
+    const uint32_t ty = s / (kCullTile * ncols);
+    const uint32_t rem = s - ty * kCullTile * ncols;
+    const uint32_t th = nrows - ty * kCullTile < kCullTile ? nrows - ty * kCullTile : kCullTile;
+    const uint32_t tx = rem / (kCullTile * th);
+    const uint32_t w = rem - tx * kCullTile * th;
+    const uint32_t tw = ncols - tx * kCullTile < kCullTile ? ncols - tx * kCullTile : kCullTile;
+    *col = tx * kCullTile + w % tw;
+    *row = ty * kCullTile + w / tw;
+}
 
 // Kernel option bits (all exact: each shortcut reproduces the reference's bits, see the kernel).
 constexpr int kOptCamConst = 1 << 0;   // launch-constant 1/w of the inverse projection
@@ -110,8 +133,13 @@ constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS ta
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.
 int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, uint32_t y0,
-                    uint32_t ystep, uint32_t npix, uint64_t seed, const uint32_t* tables,
+                    uint32_t ystep, uint32_t nrows, uint64_t seed, const uint32_t* tables,
                     uint32_t* rng);
+// Reorder `planes` planes of npix 32-bit words between tile-major storage and compact row-major
+// order (to_compact: dst[compact] = src[storage]; else dst[storage] = src[compact]). `words` is the
+// element width in 32-bit words (4 for the accumulator), the planes are npix * words apart.
+int launch_relayout(void* stream, const uint32_t* src, uint32_t* dst, uint32_t ncols, uint32_t nrows,
+                    uint32_t words, uint32_t planes, bool to_compact);
 // Tile masks for kOptCull (one thread per tile word).
 int launch_bin(void* stream, const kbin& b);
 // Per-tile cost estimate from the masks: set triangle-pair bits + 8 x set sphere-pair bits.

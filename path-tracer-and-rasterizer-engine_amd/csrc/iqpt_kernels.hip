@@ -588,25 +588,33 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
     unsigned long long s_iter = 0, s_ready = 0, s_scatter_exec = 0, s_scatter_lanes = 0, s_term_exec = 0,
                        s_term_lanes = 0;
 
+    // ---- wave-uniform chunk state: the current tile [chunk_next, chunk_end) of tile-major storage
+    uint32_t chunk_tile = 0;
     auto refill = [&]() {
         uint64_t need = __ballot(!active);
         while (need != 0ull && !exhausted) {
             if (chunk_next >= chunk_end) {
-                uint32_t base = 0;
-                if (lane == 0) base = atomicAdd(p.queue, kQueueChunk);
-                base = __shfl(base, 0);
-                if (base >= p.npix) {
+                uint32_t q = 0;
+                if (lane == 0) q = atomicAdd(p.queue, 1u);
+                q = __shfl(q, 0);
+                if (q >= p.ntiles) {
                     exhausted = true;
                     break;
                 }
-                chunk_next = base;
-                chunk_end = min(base + kQueueChunk, p.npix);
+                const uint32_t t = p.tile_order ? p.tile_order[q] : q;
+                chunk_tile = t;
+                const uint32_t tx = t % p.ntx, ty = t / p.ntx;
+                const uint32_t th = min(kCullTile, p.nrows - ty * kCullTile);
+                const uint32_t tw = min(kCullTile, p.ncols - tx * kCullTile);
+                chunk_next = ty * kCullTile * p.ncols + tx * kCullTile * th;
+                chunk_end = chunk_next + tw * th;
             }
             const uint32_t avail = chunk_end - chunk_next;
             const uint32_t rank = prefix_below(need);
             if (!active && rank < avail) {
-                const uint32_t pix = p.perm ? p.perm[chunk_next + rank] : chunk_next + rank;
-                const uint32_t col = pix % p.ncols, row = pix / p.ncols;
+                const uint32_t pix = chunk_next + rank;            // tile-major storage index
+                uint32_t col, row;
+                tile_decode(pix, p.ncols, p.nrows, &col, &row);
                 px = p.x0 + col;
                 py = p.y0 + row * p.ystep;
                 st.v0 = p.rng[pix];
@@ -623,7 +631,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                 if (kCull && p.cull) {
                     // the tile and word 0 of its triangle / sphere masks, kept in this lane's LDS slot for
                     // the pixel's lifetime (the global load latency is paid once per pixel, not per ray)
-                    const uint32_t tile = col / kCullTile + (row / kCullTile) * p.cull_ntx;
+                    const uint32_t tile = chunk_tile;
                     lds_cm[threadIdx.x] = make_uint4(p.cull[(size_t)tile * p.cull_stride],
                                                      p.cull[(size_t)tile * p.cull_stride + p.cull_wt], tile, 0u);
                 }
@@ -841,7 +849,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                 const uint32_t r8 = to_u8(255.0f * iq_sqrtf(acc.x));
                 const uint32_t g8 = to_u8(255.0f * iq_sqrtf(acc.y));
                 const uint32_t b8 = to_u8(255.0f * iq_sqrtf(acc.z));
-                const uint32_t pix = ((py - p.y0) / p.ystep) * p.ncols + (px - p.x0);
+                const uint32_t pix = tile_store_index(px - p.x0, (py - p.y0) / p.ystep, p.ncols, p.nrows);
                 p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
                 float* o = reinterpret_cast<float*>(p.lin + pix);          // w is never written
                 o[0] = acc.x;
@@ -978,15 +986,35 @@ __global__ __launch_bounds__(256) void iqpt_tile_cost_kernel(const uint32_t* cul
     cost[t] = c;
 }
 
+// Compact row-major <-> tile-major reorder of pixel-state planes (one thread per 32-bit word).
+__global__ __launch_bounds__(256) void iqpt_relayout_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                            uint32_t ncols, uint32_t nrows, uint32_t words,
+                                                            uint32_t planes, int to_compact) {
+    const uint64_t npix = (uint64_t)ncols * nrows;
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= npix * words * planes) return;
+    const uint64_t plane = i / (npix * words);
+    const uint64_t e = i - plane * npix * words;
+    const uint32_t c = (uint32_t)(e / words), k = (uint32_t)(e % words);   // compact pixel, word
+    const uint32_t s = tile_store_index(c % ncols, c / ncols, ncols, nrows);
+    const uint64_t ci = plane * npix * words + (uint64_t)c * words + k;
+    const uint64_t si = plane * npix * words + (uint64_t)s * words + k;
+    if (to_compact) dst[ci] = src[si];
+    else dst[si] = src[ci];
+}
+
 // curand_init(seed, global pixel id, 0) per owned pixel (renderer_init_kernel, path_tracer.cu:36-46).
 __global__ __launch_bounds__(256) void iqpt_rng_init_kernel(uint32_t width, uint32_t x0, uint32_t ncols,
-                                                            uint32_t y0, uint32_t ystep, uint32_t npix,
+                                                            uint32_t y0, uint32_t ystep, uint32_t nrows,
                                                             uint64_t seed, const uint32_t* __restrict__ tables,
                                                             uint32_t* __restrict__ rng) {
-    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t npix = ncols * nrows;
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;     // tile-major storage index
     if (p >= npix) return;
-    const uint32_t x = x0 + p % ncols;
-    const uint32_t y = y0 + (p / ncols) * ystep;
+    uint32_t col, row;
+    tile_decode(p, ncols, nrows, &col, &row);
+    const uint32_t x = x0 + col;
+    const uint32_t y = y0 + row * ystep;
     const uint64_t pid = (uint64_t)y * width + x;
     iq_xorwow_state s;
     iq_xorwow_seed(seed, &s);
@@ -1062,11 +1090,21 @@ const variant* find_variant(int max_depth, bool stream, int opt) {
 }  // namespace
 
 int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, uint32_t y0, uint32_t ystep,
-                    uint32_t npix, uint64_t seed, const uint32_t* tables, uint32_t* rng) {
+                    uint32_t nrows, uint64_t seed, const uint32_t* tables, uint32_t* rng) {
+    const uint32_t npix = ncols * nrows;
     if (npix == 0) return 0;
     const uint32_t grid = (npix + 255) / 256;
     hipLaunchKernelGGL(iqpt_rng_init_kernel, dim3(grid), dim3(256), 0, (hipStream_t)stream, width, x0, ncols,
-                       y0, ystep, npix, seed, tables, rng);
+                       y0, ystep, nrows, seed, tables, rng);
+    return (int)hipGetLastError();
+}
+
+int launch_relayout(void* stream, const uint32_t* src, uint32_t* dst, uint32_t ncols, uint32_t nrows, uint32_t words,
+                    uint32_t planes, bool to_compact) {
+    const uint64_t n = (uint64_t)ncols * nrows * words * planes;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(iqpt_relayout_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       src, dst, ncols, nrows, words, planes, to_compact ? 1 : 0);
     return (int)hipGetLastError();
 }
 

@@ -95,7 +95,7 @@ struct iqpt_ctx {
     bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
     // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
     uint32_t* d_cull = nullptr;
-    uint32_t* d_perm = nullptr;   // queue order built with the masks (npix)
+    uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
     size_t cull_cap = 0;       // words allocated
     bool cull_valid = false;
     uint32_t cull_ntx = 0, cull_nty = 0, cull_wt = 0, cull_stride = 0;
@@ -168,8 +168,8 @@ int build_cull(iqpt_ctx* c) {
     b.cull = c->d_cull;
     const int le = iqpt::launch_bin(c->stream, b);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "cull binning kernel");
-    // queue order: whole tiles, most expensive first (a chunk of the queue is then one tile, and the
-    // pixels that set the end of the launch are cheap ones)
+    // queue order over tiles (a queue chunk is one tile): most expensive first, so the pixels that set
+    // the end of the launch are cheap ones
     const uint32_t ntiles = c->cull_ntx * c->cull_nty;
     uint32_t* d_cost = nullptr;
     IQPT_HIP(hipMalloc(&d_cost, (size_t)ntiles * sizeof(uint32_t)));
@@ -183,18 +183,9 @@ int build_cull(iqpt_ctx* c) {
     std::vector<uint32_t> order(ntiles);
     for (uint32_t t = 0; t < ntiles; ++t) order[t] = t;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
-    std::vector<uint32_t> perm;
-    perm.reserve(c->npix);
-    for (uint32_t t : order) {
-        const uint32_t tx = t % c->cull_ntx, ty = t / c->cull_ntx;
-        for (uint32_t r = ty * iqpt::kCullTile; r < std::min((ty + 1) * iqpt::kCullTile, c->set.nrows); ++r)
-            for (uint32_t q = tx * iqpt::kCullTile; q < std::min((tx + 1) * iqpt::kCullTile, c->ncols); ++q)
-                perm.push_back(r * c->ncols + q);
-    }
-    if (perm.size() != c->npix) return iqpt::fail(IQPT_ERR_INVALID_ARG, "queue order does not cover the pixel set");
-    if (!c->d_perm && hipMalloc(&c->d_perm, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess)
-        return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "queue order");
-    IQPT_HIP(hipMemcpy(c->d_perm, perm.data(), perm.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if (!c->d_tile_order && hipMalloc(&c->d_tile_order, (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
+        return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "tile order");
+    IQPT_HIP(hipMemcpy(c->d_tile_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->cull_valid = true;
     return IQPT_OK;
 }
@@ -213,6 +204,36 @@ void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, f
         *near_rw = 1.0f / P[15];
         *far_rw = 1.0f / wf;
     }
+}
+
+// Pixel-state planes between device tile-major storage and host compact row-major order
+// (iqpt_internal.hpp): a device reorder into a temporary buffer plus one copy. Synchronises.
+int fetch_compact(iqpt_ctx* c, const void* dev, uint32_t words, uint32_t planes, void* host) {
+    const size_t bytes = (size_t)c->npix * words * planes * sizeof(uint32_t);
+    if (bytes == 0) return IQPT_OK;
+    void* tmp = nullptr;
+    if (hipMalloc(&tmp, bytes) != hipSuccess) return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "readback buffer");
+    hipError_t e = (hipError_t)iqpt::launch_relayout(c->stream, static_cast<const uint32_t*>(dev),
+                                                      static_cast<uint32_t*>(tmp), c->ncols, c->set.nrows, words,
+                                                      planes, true);
+    if (e == hipSuccess) e = hipMemcpyAsync(host, tmp, bytes, hipMemcpyDeviceToHost, c->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(tmp);
+    return e == hipSuccess ? IQPT_OK : iqpt::hip_fail(e, "readback");
+}
+
+int store_compact(iqpt_ctx* c, const void* host, uint32_t words, uint32_t planes, void* dev) {
+    const size_t bytes = (size_t)c->npix * words * planes * sizeof(uint32_t);
+    if (bytes == 0) return IQPT_OK;
+    void* tmp = nullptr;
+    if (hipMalloc(&tmp, bytes) != hipSuccess) return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "upload buffer");
+    hipError_t e = hipMemcpyAsync(tmp, host, bytes, hipMemcpyHostToDevice, c->stream);
+    if (e == hipSuccess)
+        e = (hipError_t)iqpt::launch_relayout(c->stream, static_cast<const uint32_t*>(tmp), static_cast<uint32_t*>(dev),
+                                              c->ncols, c->set.nrows, words, planes, false);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    (void)hipFree(tmp);
+    return e == hipSuccess ? IQPT_OK : iqpt::hip_fail(e, "upload");
 }
 
 hipEvent_t take_event(iqpt_ctx* c) {
@@ -305,7 +326,7 @@ int iqpt_create(int device, uint32_t width, uint32_t height, const iqpt_pixel_se
     if (hipMalloc(&d_tables, tables.size() * sizeof(uint32_t)) != hipSuccess)
         return cleanup(iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "jump tables"));
     hipError_t e = hipMemcpyAsync(d_tables, tables.data(), tables.size() * sizeof(uint32_t), hipMemcpyHostToDevice, c->stream);
-    int lst = e == hipSuccess ? iqpt::launch_rng_init(c->stream, width, ps.x0, c->ncols, ps.y0, ps.ystep, c->npix,
+    int lst = e == hipSuccess ? iqpt::launch_rng_init(c->stream, width, ps.x0, c->ncols, ps.y0, ps.ystep, ps.nrows,
                                                       seed, d_tables, c->d_rng)
                               : (int)e;
     hipError_t se = hipStreamSynchronize(c->stream);
@@ -328,7 +349,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->d_queue) (void)hipFree(c->d_queue);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
-    if (c->d_perm) (void)hipFree(c->d_perm);
+    if (c->d_tile_order) (void)hipFree(c->d_tile_order);
     for (auto& pr : c->timed) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -521,11 +542,13 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     if ((opt & iqpt::kOptCull) && (c->ntri + c->nsph) > 0) {
         if (!c->cull_valid && (st = build_cull(c)) != IQPT_OK) return st;
         p.cull = c->d_cull;
-        p.perm = c->d_perm;
+        p.tile_order = c->d_tile_order;
         p.cull_ntx = c->cull_ntx;
         p.cull_wt = c->cull_wt;
         p.cull_stride = c->cull_stride;
     }
+    p.ntx = (c->ncols + iqpt::kCullTile - 1) / iqpt::kCullTile;
+    p.ntiles = p.ntx * ((c->set.nrows + iqpt::kCullTile - 1) / iqpt::kCullTile);
     p.lin = c->d_lin;
     p.bgra = c->d_bgra;
     p.rng = c->d_rng;
@@ -570,10 +593,8 @@ int iqpt_read(iqpt_ctx* c, float* lin_rgba, uint8_t* bgra) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     int st = use_device(c);
     if (st) return st;
-    IQPT_HIP(hipStreamSynchronize(c->stream));
-    if (lin_rgba)
-        IQPT_HIP(hipMemcpy(lin_rgba, c->d_lin, (size_t)c->npix * sizeof(float4_storage), hipMemcpyDeviceToHost));
-    if (bgra) IQPT_HIP(hipMemcpy(bgra, c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if (lin_rgba && (st = fetch_compact(c, c->d_lin, 4, 1, lin_rgba)) != IQPT_OK) return st;
+    if (bgra && (st = fetch_compact(c, c->d_bgra, 1, 1, bgra)) != IQPT_OK) return st;
     return IQPT_OK;
 }
 
@@ -581,9 +602,8 @@ int iqpt_read_rng(iqpt_ctx* c, uint32_t* states) {
     if (!c || !states) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     int st = use_device(c);
     if (st) return st;
-    IQPT_HIP(hipStreamSynchronize(c->stream));
     std::vector<uint32_t> planes((size_t)c->npix * 6);
-    IQPT_HIP(hipMemcpy(planes.data(), c->d_rng, planes.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    if ((st = fetch_compact(c, c->d_rng, 1, 6, planes.data())) != IQPT_OK) return st;
     for (size_t p = 0; p < c->npix; ++p)
         for (int k = 0; k < 6; ++k) states[p * 6 + k] = planes[(size_t)k * c->npix + p];
     return IQPT_OK;
@@ -594,8 +614,9 @@ int iqpt_copy_accum_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
     if (bytes < (size_t)c->npix * sizeof(float4_storage)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
     int st = use_device(c);
     if (st) return st;
-    IQPT_HIP(hipMemcpyAsync(dst_device, c->d_lin, (size_t)c->npix * sizeof(float4_storage), hipMemcpyDeviceToDevice,
-                            c->stream));
+    const int le = iqpt::launch_relayout(c->stream, reinterpret_cast<const uint32_t*>(c->d_lin),
+                                         static_cast<uint32_t*>(dst_device), c->ncols, c->set.nrows, 4, 1, true);
+    if (le != 0) return iqpt::hip_fail((hipError_t)le, "accumulator reorder");
     IQPT_HIP(hipStreamSynchronize(c->stream));
     return IQPT_OK;
 }
@@ -635,9 +656,11 @@ int iqpt_checkpoint_save(iqpt_ctx* c, const char* path) {
     std::vector<float4_storage> lin(n);
     std::vector<uint32_t> bgra(n), rng(n * 6);
     unsigned long long rays = 0;
-    IQPT_HIP(hipMemcpy(lin.data(), c->d_lin, n * sizeof(float4_storage), hipMemcpyDeviceToHost));
-    IQPT_HIP(hipMemcpy(bgra.data(), c->d_bgra, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    IQPT_HIP(hipMemcpy(rng.data(), c->d_rng, n * 6 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    // the file holds the compact row-major order (independent of the device layout)
+    if ((st = fetch_compact(c, c->d_lin, 4, 1, lin.data())) != IQPT_OK ||
+        (st = fetch_compact(c, c->d_bgra, 1, 1, bgra.data())) != IQPT_OK ||
+        (st = fetch_compact(c, c->d_rng, 1, 6, rng.data())) != IQPT_OK)
+        return st;
     IQPT_HIP(hipMemcpy(&rays, c->d_rays, sizeof rays, hipMemcpyDeviceToHost));
     ckpt_header h;
     std::memset(&h, 0, sizeof h);
@@ -706,9 +729,10 @@ int iqpt_checkpoint_load(iqpt_ctx* c, const char* path) {
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     const unsigned long long rays = h.rays;
-    IQPT_HIP(hipMemcpy(c->d_lin, lin.data(), n * sizeof(float4_storage), hipMemcpyHostToDevice));
-    IQPT_HIP(hipMemcpy(c->d_bgra, bgra.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));
-    IQPT_HIP(hipMemcpy(c->d_rng, rng.data(), n * 6 * sizeof(uint32_t), hipMemcpyHostToDevice));
+    if ((st = store_compact(c, lin.data(), 4, 1, c->d_lin)) != IQPT_OK ||
+        (st = store_compact(c, bgra.data(), 1, 1, c->d_bgra)) != IQPT_OK ||
+        (st = store_compact(c, rng.data(), 1, 6, c->d_rng)) != IQPT_OK)
+        return st;
     IQPT_HIP(hipMemcpy(c->d_rays, &rays, sizeof rays, hipMemcpyHostToDevice));
     c->frame = h.frame;
     return IQPT_OK;
