@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define IQPT_ABI_VERSION 1
+#define IQPT_ABI_VERSION 2
 
 typedef enum iqpt_status {
     IQPT_OK = 0,
@@ -86,13 +86,34 @@ typedef struct iqpt_sphere_drawcall {
     float radius;
 } iqpt_sphere_drawcall;
 
-/* scene.h:21-45 `scene::gpu_packet` with host pointers. */
+/* Per-primitive material table (README.txt:66-72 "planned"). The reference hard-wires
+ * emissive(white, 10) on every triangle and oren_nayar(0.5, sigma 1) on every sphere
+ * (path_tracer.cu:248-249, 278, 292); a packet without a table keeps exactly that. With a table,
+ * every drawcall names one material, with the reference's two material classes (material.h:21-62):
+ *   IQPT_MAT_EMISSIVE:   scatter = (albedo * param, cos 1, pdf 1), path ends (material.cu:50-57);
+ *   IQPT_MAT_OREN_NAYAR: albedo, param = roughness sigma, clamped to [0, 1] like the constructor
+ *                        (material.h:25-29); scatter as material.cu:5-48. On a triangle the hit normal
+ *                        is the interpolated vertex normal, flipped to face the ray (shape.cu:93-101). */
+#define IQPT_MAT_EMISSIVE 0u
+#define IQPT_MAT_OREN_NAYAR 1u
+typedef struct iqpt_material {
+    uint32_t type;                /* IQPT_MAT_* */
+    float albedo[4];              /* iqvec color (w unused by the output) */
+    float param;                  /* emissive: strength; Oren-Nayar: roughness sigma */
+} iqpt_material;
+
+/* scene.h:21-45 `scene::gpu_packet` with host pointers, plus the optional material table. */
 typedef struct iqpt_packet_desc {
     uint32_t num_drawcalls[2];    /* [IQPT_MESH_TRIANGLES], [IQPT_MESH_SPHERES] */
     uint32_t num_tri_meshes;
     const iqpt_tri_mesh* tri_meshes;
     const iqpt_tri_mesh_drawcall* tri_mesh_dcs;
     const iqpt_sphere_drawcall* sphere_dcs;
+    /* NULL = the reference's materials. Otherwise num_materials entries and one index per drawcall. */
+    const iqpt_material* materials;
+    uint32_t num_materials;
+    const uint32_t* tri_dc_material;      /* [num_drawcalls[IQPT_MESH_TRIANGLES]] */
+    const uint32_t* sphere_dc_material;   /* [num_drawcalls[IQPT_MESH_SPHERES]] */
 } iqpt_packet_desc;
 
 /* camera.h:22-32 `camera` layout (uint16 size, fov, position/forward, 4 matrices). */
@@ -222,6 +243,12 @@ int iqpt_scene_num_meshes(const iqpt_scene* s, uint32_t* n);
 /* Scenes of BASELINE.json's configs, built with the calls above:
  *   "app_default" application.cu:25-34, "c1_plumbing" C1, "cornell" C2/C3, "mesh10k" C4, "mixed" C5. */
 int iqpt_scene_add_preset(iqpt_scene* s, const char* preset);
+/* Material table of the scene builder: add a material (its index is returned) and assign it to a
+ * model; the packet carries a table as soon as one material was added (models without an assignment
+ * then get the reference's default for their mesh type: emissive(white, 10) for triangle meshes,
+ * oren_nayar(0.5, 1) for spheres). */
+int iqpt_scene_add_material(iqpt_scene* s, const iqpt_material* m, uint32_t* index);
+int iqpt_scene_set_model_material(iqpt_scene* s, const char* model, uint32_t material);
 /* Builds the packet into arrays owned by the scene (valid until the next build or destroy). */
 int iqpt_scene_build_packet(iqpt_scene* s, iqpt_packet_desc* out);
 

@@ -178,7 +178,9 @@ typedef struct { vec4 o, d; } ray_t;                                            
 static inline vec4 ray_at(const ray_t* r, float t) { return vadd(r->o, vmul(r->d, t)); }
 
 enum { MAT_NONE = 0, MAT_EMISSIVE = 1, MAT_OREN_NAYAR = 2 };
-typedef struct { vec4 p, n; float t; int front_face; int mat; } hit_record;       /* shape.h:7-14 */
+/* mat: MAT_*; albedo / param of the hit primitive's material (param: emissive strength or the
+ * clamped Oren-Nayar sigma) */
+typedef struct { vec4 p, n; float t; int front_face; int mat; vec4 albedo; float param; } hit_record;  /* shape.h:7-14 */
 
 static int triangle_intersect(vec4 v0, vec4 v1, vec4 v2, vec4 n0, vec4 n1, vec4 n2,
                               const ray_t* r, float t_min, float t_max, hit_record* hr) {
@@ -242,9 +244,36 @@ static vec4 onb_to_world(const onb_t* b, vec4 v) {
     return vadd(vadd(vmul(b->w_[0], v.x), vmul(b->w_[1], v.y)), vmul(b->w_[2], v.z));
 }
 
-/* oren_nayar(iqvec(.5,.5,.5,0), 1.0) (path_tracer.cu:248; material.h:23-29 clamps sigma) */
+/* The reference's materials (path_tracer.cu:248-249): oren_nayar(iqvec(.5,.5,.5,0), 1.0) on every
+ * sphere, emissive(iqvec(1.0f), 10.0f) on every triangle. A packet may carry a material table instead
+ * (iqpt.h). */
 static const vec4 ON_ALBEDO = {0.5f, 0.5f, 0.5f, 0.0f};
 static const float ON_SIGMA = 1.0f;
+static const vec4 EM_ALBEDO = {1.0f, 1.0f, 1.0f, 1.0f};
+static const float EM_STRENGTH = 10.0f;
+
+/* oren_nayar::oren_nayar clamps the roughness to [0, 1] (material.h:25-29) */
+static float clamp_sigma(float r) { return r < 0.0f ? 0.0f : (r > 1.0f ? 1.0f : r); }
+
+/* material of drawcall i of the given kind, into the hit record */
+static void set_material(hit_record* hr, const iqpt_packet_desc* pk, int kind, uint32_t i) {
+    if (!pk->materials) {
+        hr->mat = kind == IQPT_MESH_TRIANGLES ? MAT_EMISSIVE : MAT_OREN_NAYAR;
+        hr->albedo = kind == IQPT_MESH_TRIANGLES ? EM_ALBEDO : ON_ALBEDO;
+        hr->param = kind == IQPT_MESH_TRIANGLES ? EM_STRENGTH : ON_SIGMA;
+        return;
+    }
+    const uint32_t k = kind == IQPT_MESH_TRIANGLES ? pk->tri_dc_material[i] : pk->sphere_dc_material[i];
+    const iqpt_material* m = &pk->materials[k];
+    memcpy(&hr->albedo, m->albedo, sizeof hr->albedo);
+    if (m->type == IQPT_MAT_EMISSIVE) {
+        hr->mat = MAT_EMISSIVE;
+        hr->param = m->param;
+    } else {
+        hr->mat = MAT_OREN_NAYAR;
+        hr->param = clamp_sigma(m->param);
+    }
+}
 
 static int oren_nayar_scatter(const ray_t* r_in, const hit_record* hr, scatter_record* srec,
                               ray_t* r_out, iq_xorwow_state* st) {
@@ -260,7 +289,7 @@ static int oren_nayar_scatter(const ray_t* r_in, const hit_record* hr, scatter_r
     }
     srec->cos_law_weight = O_FMAXF(0.0f, dot3(hr->n, r_out->d));
     const vec4 wi = r_out->d;
-    const float sigma2 = ON_SIGMA * ON_SIGMA;
+    const float sigma2 = hr->param * hr->param;
     const float A = 1.0f - 0.5f * sigma2 / (sigma2 + 0.33f);
     const float B = 0.45f * sigma2 / (sigma2 + 0.09f);
     const float phi_o = O_ATAN2F(wo.y, wo.x);
@@ -272,13 +301,13 @@ static int oren_nayar_scatter(const ray_t* r_in, const hit_record* hr, scatter_r
     const float alpha = O_FMAXF(theta_i, theta_o);
     const float beta = O_FMINF(theta_i, theta_o);
     const float coeff = A + B * O_COSF(phi_i - phi_o) * O_SINF(alpha) * O_TANF(beta);
-    srec->attenuation = vdiv(vmul(ON_ALBEDO, coeff), IQ_PI);
+    srec->attenuation = vdiv(vmul(hr->albedo, coeff), IQ_PI);
     return 1;
 }
 
-/* emissive(1.0f, 10.0f) (path_tracer.cu:249; material.cu:50-57) */
-static int emissive_scatter(scatter_record* srec) {
-    srec->attenuation = vmul(vsplat(1.0f), 10.0f);
+/* emissive::scatter (material.cu:50-57): m_strength * m_albedo */
+static int emissive_scatter(const hit_record* hr, scatter_record* srec) {
+    srec->attenuation = vmul(hr->albedo, hr->param);
     srec->cos_law_weight = 1.0f;
     srec->pdf_val = 1.0f;
     return 0;
@@ -339,7 +368,7 @@ static vec4 ray_color(const ray_t* r0, const iqpt_packet_desc* pk, const mat4* n
                 if (triangle_intersect(v0, v1, v2, n0, n1, n2, &crt_ray, t_min, closest_hit, &hr)) {
                     closest_hit = hr.t;
                     final_hr = hr;
-                    final_hr.mat = MAT_EMISSIVE;
+                    set_material(&final_hr, pk, IQPT_MESH_TRIANGLES, i);
                     hit = 1;
                 }
             }
@@ -351,7 +380,7 @@ static vec4 ray_color(const ray_t* r0, const iqpt_packet_desc* pk, const mat4* n
             if (sphere_intersect(center, pk->sphere_dcs[i].radius, &crt_ray, t_min, closest_hit, &hr)) {
                 closest_hit = hr.t;
                 final_hr = hr;
-                final_hr.mat = MAT_OREN_NAYAR;
+                set_material(&final_hr, pk, IQPT_MESH_SPHERES, i);
                 hit = 1;
             }
         }
@@ -359,7 +388,7 @@ static vec4 ray_color(const ray_t* r0, const iqpt_packet_desc* pk, const mat4* n
             ray_t r_out;
             int cont = final_hr.mat == MAT_OREN_NAYAR
                            ? oren_nayar_scatter(&crt_ray, &final_hr, &ray_stack[crt_depth], &r_out, st)
-                           : emissive_scatter(&ray_stack[crt_depth]);
+                           : emissive_scatter(&final_hr, &ray_stack[crt_depth]);
             if (cont) {
                 crt_ray = r_out;
             } else {
@@ -406,6 +435,17 @@ static int check_packet(const iqpt_packet_desc* pk) {
         if (m->num_indices % 3) return IQPT_ERR_INVALID_ARG;
         for (uint32_t j = 0; j < m->num_indices; j++)
             if (m->indices[j] >= m->num_vertices) return IQPT_ERR_INVALID_ARG;
+    }
+    if (pk->materials) {
+        for (int kind = 0; kind < 2; ++kind) {
+            const uint32_t* idx = kind == IQPT_MESH_TRIANGLES ? pk->tri_dc_material : pk->sphere_dc_material;
+            if (pk->num_drawcalls[kind] && !idx) return IQPT_ERR_INVALID_ARG;
+            for (uint32_t i = 0; i < pk->num_drawcalls[kind]; i++)
+                if (idx[i] >= pk->num_materials) return IQPT_ERR_INVALID_ARG;
+        }
+        for (uint32_t k = 0; k < pk->num_materials; k++)
+            if (pk->materials[k].type != IQPT_MAT_EMISSIVE && pk->materials[k].type != IQPT_MAT_OREN_NAYAR)
+                return IQPT_ERR_INVALID_ARG;
     }
     return IQPT_OK;
 }
@@ -570,6 +610,9 @@ void iqo_oren_nayar(const float* p4, const float* n4, const float* din4, uint32_
     memset(&hr, 0, sizeof hr);
     memcpy(&hr.p, p4, 16);
     memcpy(&hr.n, n4, 16);
+    hr.mat = MAT_OREN_NAYAR;
+    hr.albedo = ON_ALBEDO;
+    hr.param = ON_SIGMA;
     iq_xorwow_state s;
     for (int q = 0; q < 5; ++q) s.v[q] = state6[q];
     s.d = state6[5];

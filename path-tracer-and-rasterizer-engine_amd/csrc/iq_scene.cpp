@@ -168,6 +168,7 @@ struct model {
     vec4 scale_v{1.0f}, rotation{0.0f}, translation{0.0f};
     mat4 transform;
     uint64_t order = 0;                         // insertion order: tie-break of scene.h:58-67
+    int64_t material = -1;                      // material table index (-1: the reference default)
     void recompute() {                                                          // model.cu:11-18
         mat4 s = iq::scale(scale_v);
         mat4 r = iq::rotation_x(rotation.x) * iq::rotation_y(rotation.y) * iq::rotation_z(rotation.z);
@@ -182,10 +183,13 @@ struct iqpt_scene {
     std::map<std::string, mesh> meshes;
     std::map<std::string, model> models;
     uint64_t next_order = 0;
+    std::vector<iqpt_material> materials;      // §8f.3 material table (empty: reference materials)
     // storage of the last built packet
     std::vector<iqpt_tri_mesh> pk_meshes;
     std::vector<iqpt_tri_mesh_drawcall> pk_tri_dcs;
     std::vector<iqpt_sphere_drawcall> pk_sph_dcs;
+    std::vector<iqpt_material> pk_mats;
+    std::vector<uint32_t> pk_tri_mat, pk_sph_mat;
 };
 
 namespace {
@@ -251,6 +255,25 @@ int iqpt_scene_add_model(iqpt_scene* s, const char* name, const char* mesh_name,
     return IQPT_OK;
 }
 
+int iqpt_scene_add_material(iqpt_scene* s, const iqpt_material* m, uint32_t* index) {
+    if (!s || !m) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (m->type != IQPT_MAT_EMISSIVE && m->type != IQPT_MAT_OREN_NAYAR)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "unknown material type");
+    if (s->materials.size() >= 0xffff) return iqpt::fail(IQPT_ERR_INVALID_ARG, "too many materials");
+    s->materials.push_back(*m);
+    if (index) *index = (uint32_t)(s->materials.size() - 1);
+    return IQPT_OK;
+}
+
+int iqpt_scene_set_model_material(iqpt_scene* s, const char* model_name, uint32_t material) {
+    if (!s || !model_name) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    auto it = s->models.find(model_name);
+    if (it == s->models.end()) return iqpt::fail(IQPT_ERR_INVALID_ARG, std::string("no model ") + model_name);
+    if (material >= s->materials.size()) return iqpt::fail(IQPT_ERR_INVALID_ARG, "material index out of range");
+    it->second.material = material;
+    return IQPT_OK;
+}
+
 int iqpt_scene_num_meshes(const iqpt_scene* s, uint32_t* n) {
     if (!s || !n) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     *n = (uint32_t)s->meshes.size();
@@ -265,6 +288,18 @@ int iqpt_scene_build_packet(iqpt_scene* s, iqpt_packet_desc* out) {            /
     s->pk_meshes.clear();
     s->pk_tri_dcs.clear();
     s->pk_sph_dcs.clear();
+    s->pk_tri_mat.clear();
+    s->pk_sph_mat.clear();
+    // the table, followed by the reference's two materials for models without an assignment
+    // (path_tracer.cu:248-249: oren_nayar(iqvec(.5,.5,.5,0), 1), emissive(iqvec(1), 10))
+    const bool with_table = !s->materials.empty();
+    s->pk_mats = s->materials;
+    const uint32_t def_emissive = (uint32_t)s->pk_mats.size();
+    const uint32_t def_oren_nayar = def_emissive + 1;
+    if (with_table) {
+        s->pk_mats.push_back(iqpt_material{IQPT_MAT_EMISSIVE, {1.0f, 1.0f, 1.0f, 1.0f}, 10.0f});
+        s->pk_mats.push_back(iqpt_material{IQPT_MAT_OREN_NAYAR, {0.5f, 0.5f, 0.5f, 0.0f}, 1.0f});
+    }
     for (const auto& n : names) {
         const mesh& m = s->meshes.at(n);
         if (m.type != IQPT_MESH_TRIANGLES) continue;
@@ -299,12 +334,14 @@ int iqpt_scene_build_packet(iqpt_scene* s, iqpt_packet_desc* out) {            /
             std::memcpy(dc.transform, pm->transform.m, sizeof dc.transform);
             dc.mesh_id = mesh_id;
             s->pk_tri_dcs.push_back(dc);
+            s->pk_tri_mat.push_back(pm->material >= 0 ? (uint32_t)pm->material : def_emissive);
         } else {
             iqpt_sphere_drawcall dc;
             dc.center[0] = pm->translation.x; dc.center[1] = pm->translation.y;
             dc.center[2] = pm->translation.z; dc.center[3] = pm->translation.w;
             dc.radius = pm->scale_v.x;
             s->pk_sph_dcs.push_back(dc);
+            s->pk_sph_mat.push_back(pm->material >= 0 ? (uint32_t)pm->material : def_oren_nayar);
         }
     }
     out->num_drawcalls[IQPT_MESH_TRIANGLES] = (uint32_t)s->pk_tri_dcs.size();
@@ -313,6 +350,10 @@ int iqpt_scene_build_packet(iqpt_scene* s, iqpt_packet_desc* out) {            /
     out->tri_meshes = s->pk_meshes.empty() ? nullptr : s->pk_meshes.data();
     out->tri_mesh_dcs = s->pk_tri_dcs.empty() ? nullptr : s->pk_tri_dcs.data();
     out->sphere_dcs = s->pk_sph_dcs.empty() ? nullptr : s->pk_sph_dcs.data();
+    out->materials = with_table ? s->pk_mats.data() : nullptr;
+    out->num_materials = with_table ? (uint32_t)s->pk_mats.size() : 0u;
+    out->tri_dc_material = with_table && !s->pk_tri_mat.empty() ? s->pk_tri_mat.data() : nullptr;
+    out->sphere_dc_material = with_table && !s->pk_sph_mat.empty() ? s->pk_sph_mat.data() : nullptr;
     return IQPT_OK;
 }
 
@@ -352,6 +393,36 @@ int iqpt_scene_add_preset(iqpt_scene* s, const char* preset) {
         add("right", "quad", wall, vec4(0.0f, -IQ_PI_DIV_2, 0.0f, 0.0f), vec4(1.0f, 0.5f, 0.0f, 0.0f));
         add("sphere_big", "sphere", vec4(0.35f), zero, vec4(-0.4f, -0.15f, 0.2f, 0.0f));
         add("sphere_small", "sphere", vec4(0.25f), zero, vec4(0.45f, -0.25f, -0.2f, 0.0f));
+        return IQPT_OK;
+    }
+    if (name == "cornell_lit") {
+        // §8f.3: the C2 geometry with a material table — Oren–Nayar walls (white, red, green), a small
+        // emissive ceiling panel, diffuse spheres — a lit Cornell box instead of the reference's
+        // all-emissive walls
+        iqpt_scene_add_mesh_quad(s, "quad");
+        iqpt_scene_add_mesh_uv_sphere(s, "sphere", 0, 32, 16, IQPT_MESH_SPHERES);
+        const vec4 wall(2.0f, 2.0f, 1.0f, 1.0f);
+        add("back", "quad", wall, zero, vec4(0.0f, 0.5f, 1.0f, 0.0f));
+        add("floor", "quad", wall, vec4(IQ_PI_DIV_2, 0.0f, 0.0f, 0.0f), vec4(0.0f, -0.5f, 0.0f, 0.0f));
+        add("ceiling", "quad", wall, vec4(-IQ_PI_DIV_2, 0.0f, 0.0f, 0.0f), vec4(0.0f, 1.5f, 0.0f, 0.0f));
+        add("left", "quad", wall, vec4(0.0f, IQ_PI_DIV_2, 0.0f, 0.0f), vec4(-1.0f, 0.5f, 0.0f, 0.0f));
+        add("right", "quad", wall, vec4(0.0f, -IQ_PI_DIV_2, 0.0f, 0.0f), vec4(1.0f, 0.5f, 0.0f, 0.0f));
+        add("light", "quad", vec4(0.6f, 0.6f, 1.0f, 1.0f), vec4(-IQ_PI_DIV_2, 0.0f, 0.0f, 0.0f),
+            vec4(0.0f, 1.49f, 0.0f, 0.0f));
+        add("sphere_big", "sphere", vec4(0.35f), zero, vec4(-0.4f, -0.15f, 0.2f, 0.0f));
+        add("sphere_small", "sphere", vec4(0.25f), zero, vec4(0.45f, -0.25f, -0.2f, 0.0f));
+        const iqpt_material mats[] = {
+            {IQPT_MAT_OREN_NAYAR, {0.73f, 0.73f, 0.73f, 0.0f}, 0.5f},   // 0 white walls
+            {IQPT_MAT_OREN_NAYAR, {0.65f, 0.05f, 0.05f, 0.0f}, 0.5f},   // 1 red
+            {IQPT_MAT_OREN_NAYAR, {0.12f, 0.45f, 0.15f, 0.0f}, 0.5f},   // 2 green
+            {IQPT_MAT_EMISSIVE, {1.0f, 0.9f, 0.75f, 1.0f}, 12.0f},      // 3 light
+            {IQPT_MAT_OREN_NAYAR, {0.8f, 0.8f, 0.8f, 0.0f}, 0.2f},      // 4 big sphere
+            {IQPT_MAT_OREN_NAYAR, {0.9f, 0.6f, 0.2f, 0.0f}, 1.0f},      // 5 small sphere
+        };
+        for (const iqpt_material& m : mats) iqpt_scene_add_material(s, &m, nullptr);
+        const char* assign[][2] = {{"back", "0"}, {"floor", "0"}, {"ceiling", "0"}, {"left", "1"}, {"right", "2"},
+                                   {"light", "3"}, {"sphere_big", "4"}, {"sphere_small", "5"}};
+        for (const auto& a : assign) iqpt_scene_set_model_material(s, a[0], (uint32_t)(a[1][0] - '0'));
         return IQPT_OK;
     }
     if (name == "mesh10k") {

@@ -79,6 +79,13 @@ struct kparams {
     // masks, most expensive tiles first (longest-processing-time order: a shorter launch tail)
     const uint32_t* tile_order;
     uint32_t ntx, ntiles;            // tiles of the owned set (kCullTile x kCullTile)
+    // kOptMaterials (packet material table): material index per triangle / sphere, the material
+    // records (2 x float4 each: (albedo.rgb, type bits), (strength | sigma, A, B, 0)) and the
+    // triangle shading records (kTriShadeFloat4 per triangle)
+    const uint32_t* tri_mat;
+    const uint32_t* sph_mat;
+    const float4_storage* mats;
+    const float4_storage* tri_shade;
 };
 
 // Binning launch (iqpt_bin_kernel): the camera and pixel set of the context, the world-space scene.
@@ -128,6 +135,7 @@ constexpr int kOptBranchless = 1 << 6; // pair MT without early exits (small res
 constexpr int kOptStats = 1 << 7;      // wave-level counters (diagnostic builds)
 constexpr int kOptFastDiv = 1 << 8;    // short exact reciprocal / division forms (iq_fastdiv.h)
 constexpr int kOptCull = 1 << 9;       // camera rays test only the pairs of their tile's mask (pair layout)
+constexpr int kOptMaterials = 1 << 10; // per-primitive material table (RGB scatter records)
 constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 

@@ -343,19 +343,31 @@ __device__ __forceinline__ void test_sphere_pair(const float4 s0, const float4 s
     if (a1) sphere_roots<OPT>(halfb.y, delta.y, closest, kind, idx, k + 1);
 }
 
-// oren_nayar(albedo .5, sigma 1).scatter (material.cu:5-43) at the closest sphere hit. Writes the
-// continuation ray into r and returns the record's scalar (attenuation * cos / pdf).
+// Sphere hit record (shape.cu:36-44): hit point h = o + t d and the normal (h - c) / r (reciprocal
+// multiply), flipped to face the ray.
 template <int OPT>
-__device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, ray3& r, rng6& s) {
-    // hit point and outward normal (shape.cu:36-44)
-    const float hx = r.ox + t * r.dx, hy = r.oy + t * r.dy, hz = r.oz + t * r.dz;
+__device__ __forceinline__ void sphere_hit(const float4 sph, float t, const ray3& r, float& hx, float& hy, float& hz,
+                                           float& nx, float& ny, float& nz) {
+    hx = r.ox + t * r.dx;
+    hy = r.oy + t * r.dy;
+    hz = r.oz + t * r.dz;
     const float rinv = rcp_scene<OPT>(sph.w);
-    float nx = (hx - sph.x) * rinv, ny = (hy - sph.y) * rinv, nz = (hz - sph.z) * rinv;
+    nx = (hx - sph.x) * rinv;
+    ny = (hy - sph.y) * rinv;
+    nz = (hz - sph.z) * rinv;
     if (!((r.dx * nx + r.dy * ny) + r.dz * nz < 0.0f)) {
         nx = -nx;
         ny = -ny;
         nz = -nz;
     }
+}
+
+// oren_nayar::scatter (material.cu:5-43) at hit point h with hit normal n: writes the continuation
+// ray into r and returns coeff (A + B cos(phi_i - phi_o) sin(alpha) tan(beta)) and q = cos / pdf; the
+// record is att_c * q with att_c = (albedo_c * coeff) * (1 / pi).
+template <int OPT>
+__device__ __forceinline__ void or_scatter_core(float hx, float hy, float hz, float nx, float ny, float nz, ray3& r,
+                                                rng6& s, float A, float B, float& coeff, float& q) {
     // onb (onb.h:7-12)
     float wx = nx, wy = ny, wz = nz;
     normalize3<OPT>(wx, wy, wz);
@@ -396,9 +408,6 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
         pdf = 1.0f / IQ_PI;
     }
     const float cosw = iq_fmaxf(0.0f, (nx * dx + ny * dy) + nz * dz);
-    const float sigma2 = 1.0f * 1.0f;
-    const float A = 1.0f - 0.5f * sigma2 / (sigma2 + 0.33f);
-    const float B = 0.45f * sigma2 / (sigma2 + 0.09f);
     const float phi_o = iq_atan2f(woy, wox);
     const float phi_i = iq_atan2f(dy, dx);
     const float cto = iq_fmaxf(0.0f, (wox * nx + woy * ny) + woz * nz);
@@ -407,8 +416,7 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     const float theta_i = cti > 1.0f ? 0.0f : iq_acosf(cti);
     const float alpha = iq_fmaxf(theta_i, theta_o);
     const float beta = iq_fminf(theta_i, theta_o);
-    const float coeff = A + B * iq_cosf(phi_i - phi_o) * iq_sinf(alpha) * iq_tanf(beta);
-    const float att = (0.5f * coeff) * (1.0f / IQ_PI);           // m_albedo * coeff / pi
+    coeff = A + B * iq_cosf(phi_i - phi_o) * iq_sinf(alpha) * iq_tanf(beta);
     r.ox = hx + nx * 0.0001f;                                    // hr.p + 0.0001f * hr.n
     r.oy = hy + ny * 0.0001f;
     r.oz = hz + nz * 0.0001f;
@@ -417,7 +425,61 @@ __device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, r
     r.dz = dz;
     // pdf is NaN, 1/pi or in [1e-5, 1/pi] and cosw = max(0, dot) >= pi * 1e-5 when the pdf was not
     // replaced (|n|^2 otherwise): inside the exact range of iq_div_pre
-    return att * ((OPT & kOptFastDiv) ? iq_div_pre(cosw, pdf, iq_rcp(pdf)) : cosw / pdf);
+    q = (OPT & kOptFastDiv) ? iq_div_pre(cosw, pdf, iq_rcp(pdf)) : cosw / pdf;
+}
+
+// The reference's sphere material oren_nayar(albedo .5, sigma 1) at the closest sphere hit
+// (path_tracer.cu:248, 292): continuation ray into r, returns the record's scalar att * cos / pdf.
+template <int OPT>
+__device__ __forceinline__ float oren_nayar_scatter(const float4 sph, float t, ray3& r, rng6& s) {
+    float hx, hy, hz, nx, ny, nz;
+    sphere_hit<OPT>(sph, t, r, hx, hy, hz, nx, ny, nz);
+    const float sigma2 = 1.0f * 1.0f;
+    const float A = 1.0f - 0.5f * sigma2 / (sigma2 + 0.33f);
+    const float B = 0.45f * sigma2 / (sigma2 + 0.09f);
+    float coeff, q;
+    or_scatter_core<OPT>(hx, hy, hz, nx, ny, nz, r, s, A, B, coeff, q);
+    const float att = (0.5f * coeff) * (1.0f / IQ_PI);           // m_albedo * coeff / pi
+    return att * q;
+}
+
+// Triangle hit record (shape.cu:62-103) for triangle k hit at t: Möller–Trumbore again for u, v (the
+// same operation sequence as test_triangle, so the same bits), the hit point, the interpolated
+// vertex normal normalized3((1-u-v) n0 + u n1 + v n2), flipped unless dir . (e1 x e2) < 0.
+template <int OPT>
+__device__ __forceinline__ void triangle_hit(const float4* __restrict__ tris, const float4* __restrict__ shade,
+                                             uint32_t k, float t, const ray3& r, float& hx, float& hy, float& hz,
+                                             float& nx, float& ny, float& nz) {
+    const float4 a = tris[(size_t)k * kTriFloat4], b = tris[(size_t)k * kTriFloat4 + 1],
+                 c = tris[(size_t)k * kTriFloat4 + 2];
+    const float e1x = a.w, e1y = b.x, e1z = b.y;
+    const float e2x = b.z, e2y = b.w, e2z = c.x;
+    const float px = r.dy * e2z - r.dz * e2y;
+    const float py = r.dz * e2x - r.dx * e2z;
+    const float pz = r.dx * e2y - r.dy * e2x;
+    const float det = (e1x * px + e1y * py) + e1z * pz;
+    const float inv = rcp_scene<OPT>(det);
+    const float tx = r.ox - a.x, ty = r.oy - a.y, tz = r.oz - a.z;
+    const float u = ((tx * px + ty * py) + tz * pz) * inv;
+    const float qx = ty * e1z - tz * e1y;
+    const float qy = tz * e1x - tx * e1z;
+    const float qz = tx * e1y - ty * e1x;
+    const float v = ((r.dx * qx + r.dy * qy) + r.dz * qz) * inv;
+    hx = r.ox + t * r.dx;
+    hy = r.oy + t * r.dy;
+    hz = r.oz + t * r.dz;
+    const float4 s0 = shade[(size_t)k * kTriShadeFloat4], s1 = shade[(size_t)k * kTriShadeFloat4 + 1],
+                 s2 = shade[(size_t)k * kTriShadeFloat4 + 2];
+    const float w0 = (1.0f - u) - v;
+    nx = (s0.x * w0 + s1.x * u) + s2.x * v;
+    ny = (s0.y * w0 + s1.y * u) + s2.y * v;
+    nz = (s0.z * w0 + s1.z * u) + s2.z * v;
+    normalize3<OPT>(nx, ny, nz);
+    if (!((r.dx * s0.w + r.dy * s1.w) + r.dz * s2.w < 0.0f)) {   // front_face: dir . (e1 x e2) < 0
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+    }
 }
 
 __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
@@ -764,7 +826,62 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
         bool term = false;
         float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
         wave_rays += (uint64_t)__popcll(__ballot(active));
-        if (active) {
+        if (active && (OPT & kOptMaterials)) {
+            // ---- material table (§8f.3): the hit primitive's material decides the scatter
+            if (kind != kHitNone) {
+                const uint32_t mi = kind == kHitTri ? p.tri_mat[hidx] : p.sph_mat[hidx];
+                const float4_storage m0 = p.mats[2 * mi], m1 = p.mats[2 * mi + 1];
+                if (__float_as_uint(m0.w) == IQPT_MAT_EMISSIVE) {
+                    term = true;                 // emissive::scatter: strength * albedo, cos = pdf = 1
+                    Lx = m1.x * m0.x;
+                    Ly = m1.x * m0.y;
+                    Lz = m1.x * m0.z;
+                } else {
+                    float hx, hy, hz, nx, ny, nz;
+                    if (kind == kHitSphere) {
+                        float4 sphr;
+                        if (!STREAM && kPair) {
+                            const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) *
+                                                                                          kSphPairFloat4) +
+                                             (hidx & 1u);
+                            sphr = make_float4(q[0], q[2], q[4], q[6]);
+                        } else {
+                            sphr = g_sph_plain[hidx];
+                        }
+                        sphere_hit<OPT>(sphr, closest, ray, hx, hy, hz, nx, ny, nz);
+                    } else {
+                        triangle_hit<OPT>(reinterpret_cast<const float4*>(p.tris),
+                                          reinterpret_cast<const float4*>(p.tri_shade), hidx, closest, ray, hx, hy,
+                                          hz, nx, ny, nz);
+                    }
+                    float coeff, q;
+                    or_scatter_core<OPT>(hx, hy, hz, nx, ny, nz, ray, st, m1.y, m1.z, coeff, q);
+                    // m_albedo * coeff / pi, times cos / pdf (path_tracer.cu:321-324)
+                    const float sx = ((m0.x * coeff) * (1.0f / IQ_PI)) * q;
+                    const float sy = ((m0.y * coeff) * (1.0f / IQ_PI)) * q;
+                    const float sz = ((m0.z * coeff) * (1.0f / IQ_PI)) * q;
+                    if (depth + 1 >= p.max_depth) {
+                        term = true;             // the last record is this scatter (biased, :252)
+                        Lx = sx;
+                        Ly = sy;
+                        Lz = sz;
+                    } else {
+                        const uint32_t b = (uint32_t)depth * 3u * kRenderBlock + threadIdx.x;
+                        lds_stk[b] = sx;
+                        lds_stk[b + kRenderBlock] = sy;
+                        lds_stk[b + 2u * kRenderBlock] = sz;
+                        ++depth;
+                    }
+                }
+            } else {
+                term = true;                     // sky gradient, :308-313
+                const float a = (ray.dy + 1.0f) * 0.5f;
+                const float one_a = 1.0f - a;
+                Lx = one_a + a * 0.5f;
+                Ly = one_a + a * 0.7f;
+                Lz = one_a + a * 1.0f;
+            }
+        } else if (active) {
             if (kind == kHitSphere) {
                 if (OPT & kOptStats) ++s_scatter_lanes;
                 float4 sphr;
@@ -815,10 +932,17 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
             float cx = Lx, cy = Ly, cz = Lz;
             // most paths end on their first ray (depth 0: no records)
             for (int i = depth - 1; i >= 0; --i) {
-                const float r = lds_stk[(uint32_t)i * kRenderBlock + threadIdx.x];
-                cx = cx * r;
-                cy = cy * r;
-                cz = cz * r;
+                if (OPT & kOptMaterials) {
+                    const uint32_t b = (uint32_t)i * 3u * kRenderBlock + threadIdx.x;
+                    cx = cx * lds_stk[b];
+                    cy = cy * lds_stk[b + kRenderBlock];
+                    cz = cz * lds_stk[b + 2u * kRenderBlock];
+                } else {
+                    const float r = lds_stk[(uint32_t)i * kRenderBlock + threadIdx.x];
+                    cx = cx * r;
+                    cy = cy * r;
+                    cz = cz * r;
+                }
             }
             // clamp (:345-347), path_color = 0 + color (:341,348), running mean (:356-358)
             cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
@@ -1058,6 +1182,13 @@ const variant kVariants[] = {
     // packets outside the kOptFastDiv range (iqpt_upload_packet)
     IQPT_V(8, false, kOptDefault & ~kOptFastDiv), IQPT_V(8, true, kOptDefault & ~kOptFastDiv),
     IQPT_V(16, false, kOptDefault & ~kOptFastDiv), IQPT_V(16, true, kOptDefault & ~kOptFastDiv),
+    // packets with a material table
+    IQPT_V(8, false, kOptDefault | kOptMaterials), IQPT_V(8, true, kOptDefault | kOptMaterials),
+    IQPT_V(16, false, kOptDefault | kOptMaterials), IQPT_V(16, true, kOptDefault | kOptMaterials),
+    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptMaterials),
+    IQPT_V(8, true, (kOptDefault & ~kOptFastDiv) | kOptMaterials),
+    IQPT_V(16, false, (kOptDefault & ~kOptFastDiv) | kOptMaterials),
+    IQPT_V(16, true, (kOptDefault & ~kOptFastDiv) | kOptMaterials),
 #if defined(IQPT_AB_VARIANTS)
     IQPT_V(8, false, 0),
     IQPT_V(8, true, 0),

@@ -92,6 +92,10 @@ struct iqpt_ctx {
     float4_storage* d_sph = nullptr;
     float4_storage* d_sph_pairs = nullptr;
     uint32_t ntri = 0, nsph = 0;
+    // material table (§8f.3), null without one
+    uint32_t* d_tri_mat = nullptr;
+    uint32_t* d_sph_mat = nullptr;
+    float4_storage* d_mats = nullptr;
     bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
     // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
     uint32_t* d_cull = nullptr;
@@ -114,7 +118,11 @@ int use_device(const iqpt_ctx* c) {
 void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, float* far_rw);
 
 void free_scene(iqpt_ctx* c) {
-    for (float4_storage** b : {&c->d_tris, &c->d_tri_pairs, &c->d_tri_shade, &c->d_sph, &c->d_sph_pairs}) {
+    for (float4_storage** b : {&c->d_tris, &c->d_tri_pairs, &c->d_tri_shade, &c->d_sph, &c->d_sph_pairs, &c->d_mats}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    for (uint32_t** b : {&c->d_tri_mat, &c->d_sph_mat}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
@@ -391,6 +399,20 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         total += m.num_indices / 3;
     }
     if (total > 0xffffffffull / 4) return iqpt::fail(IQPT_ERR_INVALID_ARG, "too many triangles");
+    // material table (iqpt.h): indices in range, known types
+    if (pk->materials) {
+        if ((ntdc && !pk->tri_dc_material) || (nsdc && !pk->sphere_dc_material))
+            return iqpt::fail(IQPT_ERR_INVALID_ARG, "material table without per-drawcall indices");
+        for (uint32_t i = 0; i < ntdc; ++i)
+            if (pk->tri_dc_material[i] >= pk->num_materials)
+                return iqpt::fail(IQPT_ERR_INVALID_ARG, "tri drawcall " + std::to_string(i) + ": material out of range");
+        for (uint32_t i = 0; i < nsdc; ++i)
+            if (pk->sphere_dc_material[i] >= pk->num_materials)
+                return iqpt::fail(IQPT_ERR_INVALID_ARG, "sphere drawcall " + std::to_string(i) + ": material out of range");
+        for (uint32_t k = 0; k < pk->num_materials; ++k)
+            if (pk->materials[k].type != IQPT_MAT_EMISSIVE && pk->materials[k].type != IQPT_MAT_OREN_NAYAR)
+                return iqpt::fail(IQPT_ERR_INVALID_ARG, "material " + std::to_string(k) + ": unknown type");
+    }
     tris.reserve(total * iqpt::kTriFloat4);
     shade.reserve(total * 3);
     for (uint32_t i = 0; i < ntdc; ++i) {
@@ -424,6 +446,33 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
     for (uint32_t i = 0; i < nsdc; ++i) {
         const iqpt_sphere_drawcall& s = pk->sphere_dcs[i];
         sph.push_back({s.center[0], s.center[1], s.center[2], s.radius});
+    }
+    // material records: (albedo.rgb, type bits), (strength | sigma, A, B, 0) with the Oren-Nayar
+    // constants of material.cu:22-24 evaluated here by the same IEEE operations (sigma clamped to
+    // [0, 1] as the oren_nayar constructor does, material.h:25-29)
+    std::vector<float4_storage> mats;
+    std::vector<uint32_t> tri_mat, sph_mat;
+    if (pk->materials) {
+        for (uint32_t k = 0; k < pk->num_materials; ++k) {
+            const iqpt_material& m = pk->materials[k];
+            float tbits;
+            std::memcpy(&tbits, &m.type, 4);
+            mats.push_back({m.albedo[0], m.albedo[1], m.albedo[2], tbits});
+            if (m.type == IQPT_MAT_EMISSIVE) {
+                mats.push_back({m.param, 0.0f, 0.0f, 0.0f});
+            } else {
+                const float sigma = m.param < 0.0f ? 0.0f : (m.param > 1.0f ? 1.0f : m.param);
+                const float sigma2 = sigma * sigma;
+                const float A = 1.0f - 0.5f * sigma2 / (sigma2 + 0.33f);
+                const float B = 0.45f * sigma2 / (sigma2 + 0.09f);
+                mats.push_back({sigma, A, B, 0.0f});
+            }
+        }
+        for (uint32_t i = 0; i < ntdc; ++i) {
+            const iqpt_tri_mesh& m = pk->tri_meshes[pk->tri_mesh_dcs[i].mesh_id];
+            tri_mat.insert(tri_mat.end(), m.num_indices / 3, pk->tri_dc_material[i]);
+        }
+        sph_mat.assign(pk->sphere_dc_material, pk->sphere_dc_material + nsdc);
     }
     // kOptFastDiv (iq_fastdiv.h): iq_rcp is exact for |x| in [2^-126, 2^126) and for 0, inf, NaN.
     // Möller–Trumbore determinants are |e1 . (dir x e2)| <= |e1| |e2| (|dir| = 1) < 2^126 when every
@@ -467,9 +516,17 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         IQPT_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(float4_storage), hipMemcpyHostToDevice));
         return IQPT_OK;
     };
+    auto upload_u32 = [&](const std::vector<uint32_t>& v, uint32_t** dst) -> int {
+        if (v.empty()) return IQPT_OK;
+        if (hipMalloc(dst, v.size() * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "material index allocation");
+        IQPT_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        return IQPT_OK;
+    };
     if ((st = upload(tris, &c->d_tris)) || (st = upload(tri_pairs, &c->d_tri_pairs)) ||
         (st = upload(shade, &c->d_tri_shade)) || (st = upload(sph, &c->d_sph)) ||
-        (st = upload(sph_pairs, &c->d_sph_pairs))) {
+        (st = upload(sph_pairs, &c->d_sph_pairs)) || (st = upload(mats, &c->d_mats)) ||
+        (st = upload_u32(tri_mat, &c->d_tri_mat)) || (st = upload_u32(sph_mat, &c->d_sph_mat))) {
         free_scene(c);
         return st;
     }
@@ -517,6 +574,11 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     int opt = c->opt;
     if (!c->fast_rcp_ok || c->width > (1u << 24) || c->height > (1u << 24)) opt &= ~iqpt::kOptFastDiv;
     if (!(opt & iqpt::kOptPair)) opt &= ~iqpt::kOptCull;       // masks are per primitive pair
+    if (c->d_mats) opt |= iqpt::kOptMaterials;                  // the packet carries a material table
+    p.tri_mat = c->d_tri_mat;
+    p.sph_mat = c->d_sph_mat;
+    p.mats = c->d_mats;
+    p.tri_shade = c->d_tri_shade;
     p.rcp_width = 1.0f / (float)c->width;
     p.rcp_height = 1.0f / (float)c->height;
     const bool pair = (opt & iqpt::kOptPair) != 0;
@@ -538,7 +600,8 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     const uint32_t lds = p.tri_batch * tri_rec + p.sph_batch * sph_rec +
                          (p.acc_tab ? ((spp + 1u) & ~1u) * 8u : 0u) +
                          ((opt & iqpt::kOptCull) ? iqpt::kRenderBlock * 16u : 0u) +
-                         (uint32_t)std::max(c->max_depth, 1) * iqpt::kRenderBlock * 4u;
+                         (uint32_t)std::max(c->max_depth, 1) * iqpt::kRenderBlock * 4u *
+                             ((opt & iqpt::kOptMaterials) ? 3u : 1u);
     if ((opt & iqpt::kOptCull) && (c->ntri + c->nsph) > 0) {
         if (!c->cull_valid && (st = build_cull(c)) != IQPT_OK) return st;
         p.cull = c->d_cull;

@@ -48,10 +48,22 @@ class SphereDrawcall(C.Structure):
     _fields_ = [("center", C.c_float * 4), ("radius", C.c_float)]
 
 
+class Material(C.Structure):
+    """iqpt_material (include/iqpt.h): IQPT_MAT_EMISSIVE (param = strength) or IQPT_MAT_OREN_NAYAR
+    (param = roughness sigma)."""
+    _fields_ = [("type", C.c_uint32), ("albedo", C.c_float * 4), ("param", C.c_float)]
+
+
+MAT_EMISSIVE = 0
+MAT_OREN_NAYAR = 1
+
+
 class PacketDesc(C.Structure):
     _fields_ = [("num_drawcalls", C.c_uint32 * 2), ("num_tri_meshes", C.c_uint32),
                 ("tri_meshes", C.POINTER(TriMesh)), ("tri_mesh_dcs", C.POINTER(TriMeshDrawcall)),
-                ("sphere_dcs", C.POINTER(SphereDrawcall))]
+                ("sphere_dcs", C.POINTER(SphereDrawcall)),
+                ("materials", C.POINTER(Material)), ("num_materials", C.c_uint32),
+                ("tri_dc_material", C.POINTER(C.c_uint32)), ("sphere_dc_material", C.POINTER(C.c_uint32))]
 
 
 class Camera(C.Structure):
@@ -103,6 +115,8 @@ SIGNATURES = [
     ("iqpt_scene_add_model", C.c_int, [_P, C.c_char_p, C.c_char_p, _FP, _FP, _FP]),
     ("iqpt_scene_num_meshes", C.c_int, [_P, C.POINTER(C.c_uint32)]),
     ("iqpt_scene_add_preset", C.c_int, [_P, C.c_char_p]),
+    ("iqpt_scene_add_material", C.c_int, [_P, C.POINTER(Material), C.POINTER(C.c_uint32)]),
+    ("iqpt_scene_set_model_material", C.c_int, [_P, C.c_char_p, C.c_uint32]),
     ("iqpt_scene_build_packet", C.c_int, [_P, C.POINTER(PacketDesc)]),
 ]
 

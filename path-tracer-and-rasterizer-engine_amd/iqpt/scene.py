@@ -72,6 +72,22 @@ class Scene:
     def add_preset(self, preset: str):
         check(self._lib.iqpt_scene_add_preset(self._h, preset.encode()), "add_preset")
 
+    def add_material(self, kind: int, albedo, param: float) -> int:
+        """Material table entry (iqpt.h): kind MAT_EMISSIVE (param = strength) or MAT_OREN_NAYAR
+        (param = roughness sigma). Returns its index."""
+        m = _lib.Material()
+        m.type = kind
+        a = list(albedo) + [0.0] * (4 - len(albedo))
+        for k in range(4):
+            m.albedo[k] = a[k]
+        m.param = param
+        idx = C.c_uint32()
+        check(self._lib.iqpt_scene_add_material(self._h, C.byref(m), C.byref(idx)), "add_material")
+        return idx.value
+
+    def set_model_material(self, model: str, material: int):
+        check(self._lib.iqpt_scene_set_model_material(self._h, model.encode(), material), "set_model_material")
+
     def num_meshes(self) -> int:
         n = C.c_uint32()
         check(self._lib.iqpt_scene_num_meshes(self._h, C.byref(n)), "num_meshes")
