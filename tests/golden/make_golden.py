@@ -25,6 +25,7 @@ CASES = {
     "mesh10k_crop": ("mesh10k", 1920, 1080, [2], 8, (944, 976, 400, 2, 12)),
     "mixed_crop": ("mixed", 3840, 2160, [1], 8, (1908, 1932, 1150, 1, 8)),
     "app_full": ("app_default", 96, 54, [4], 5, None),
+    "cornell_lit_crop": ("cornell_lit", 1920, 1080, [4], 8, (928, 992, 600, 1, 16)),   # §8f.3 material table
 }
 
 
@@ -41,7 +42,10 @@ def render(preset, w, h, launches, depth, crop):
 
 
 def main():
+    only = set(sys.argv[1:])
     for name, (preset, w, h, launches, depth, crop) in CASES.items():
+        if only and name not in only:
+            continue
         fr = render(preset, w, h, launches, depth, crop)
         np.savez_compressed(
             HERE / f"{name}.npz", lin=fr.lin, bgra=fr.bgra, rays=fr.rays.astype(np.uint16),
