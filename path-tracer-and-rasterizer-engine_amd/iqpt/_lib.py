@@ -123,6 +123,9 @@ SIGNATURES = [
 _lib = None
 
 
+ABI_VERSION = 2      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
+
+
 def load() -> C.CDLL:
     """Load libiqpt.so from the package directory (raises if it is absent: no fallback)."""
     global _lib
@@ -136,6 +139,9 @@ def load() -> C.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    if lib.iqpt_abi_version() != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {lib.iqpt_abi_version()}, the bindings expect {ABI_VERSION}: "
+                          "rebuild with __graft_entry__.build()")
     _lib = lib
     return lib
 
