@@ -1,0 +1,205 @@
+// iq_bvh.hpp — exact BVH for secondary rays, host side: error bounds + builder.
+//
+// The closest hit must be the one the reference's brute-force loop finds (path_tracer.cu:257-295):
+// over triangles, the accepted hit with the smallest computed t, the LAST one in packet order among
+// equal t (t_max < t rejects, t == closest is accepted). That is order-free — (min t, max index) —
+// so a BVH can visit triangles in any order, provided it never skips a triangle whose own
+// Möller–Trumbore test (shape.cu:62-103, in binary32 round-to-nearest as the kernel evaluates it)
+// would accept the ray with t <= closest. Skipping is decided with boxes, so the boxes must contain
+// every point where the float test can accept — not just the triangle:
+//
+//   With u = 2^-24, gamma_n = n u / (1 - n u), |d_i| <= M_d, |e1_i| <= M1, |e2_i| <= M2, |s_i| <= S
+//   (s = o - v0) and the computed determinant |det^| >= 1e-6 (smaller ones are rejected), forward
+//   error analysis of the kernel's operation sequence gives (P = 2 M_d M2, Q = 2 S M1):
+//     |det^ - det|        <= E_det = 3 M1 [gamma_3 (P + dP) + dP],          dP = gamma_2 P
+//     |N_u^ - s.p|        <= E_u   = 3 S (1+u) [gamma_3 (P + dP) + u (P + dP) + dP]
+//     |N_v^ - d.q|        <= E_v   = 3 M_d [gamma_3 (Q + dQ) + dQ],          dQ = (gamma_2 + 2u) Q
+//     |N_t^ - e2.q|       <= E_t   = 3 M2 [gamma_3 (Q + dQ) + dQ]
+//   and with R = E_det / 1e-6 < 1, the exact barycentrics of an accepted hit satisfy
+//     |u^ - u| <= Du = (E_u / 1e-6 + R + 2 gamma_2) / (1 - R)     (|u^| <= 1), likewise Dv,
+//     |t^ - t| <= (E_t / 1e-6 + R |t| + 2 gamma_2 |t^|) / (1 - R).
+//   The exact line point o + t d = v0 + u e1 + v e2 (det != 0: |det^ - det| < 1e-6 <= |det^|) has
+//   u >= -Du, v >= -Dv, u + v <= 1 + Du + Dv + 4u; moving it into the triangle shifts u by at most
+//   3 Du + 2 Dv + 4u and v by at most 2 Du + 3 Dv + 4u, so it lies in the triangle's box grown by
+//   delta = 3 (Du + Dv + 4u) (M1 + M2) per axis, at a parameter within Dt of the accepted t^.
+//   Every term is linear in S = max_i |o_i - v0_i| (the ray origin's distance to the triangle):
+//   delta = gA + gB S and |t^ - t| <= tA S + tB |t|. A node stores its triangles' tight vertex box
+//   and the maxima of (gA, gB, tA, tB) over them; traversal bounds S for the node from the ray
+//   origin and the tight box, grows the box by gA + gB S (rounded up) and widens the ray segment
+//   by tA S + tB closest. The bound therefore tightens near the ray origin, where secondary rays
+//   find their hits, instead of being priced at the scene's diameter. Rays with |d_i| > M_d or a
+//   non-finite origin test every triangle.
+//
+// Triangles whose R exceeds 1/4 (large triangles: the 1e-6 determinant threshold is tiny against
+// |e1| |e2|, so grazing hits are poorly conditioned) are not put in the BVH; they stay on an
+// "always test" list. Every bound is multiplied by a safety factor of 2 and box corners are rounded
+// outward. tests/test_bvh.py checks the bound against the oracle on adversarial rays (grazing
+// directions near the determinant threshold, hits on edges and vertices, origins near and far).
+#pragma once
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+namespace iqbvh {
+
+constexpr double kU = 5.9604644775390625e-8;   // 2^-24
+constexpr double kDetMin = 1e-6;               // |det| threshold of the reject test (as float 0.000001f)
+constexpr double kSafety = 2.0;
+
+inline double gamma_n(int n) { return n * kU / (1.0 - n * kU); }
+
+struct tri_coeffs {
+    bool eligible;        // R <= 1/4: may go into the BVH
+    double gA, gB;        // per-axis growth of the triangle's box: gA + gB S
+    double tA, tB;        // |t^ - t| <= tA S + tB |t|   (t <= closest during traversal)
+};
+
+// e1, e2: the kernel's world-space edges; Md: bound on |d_i| (normalized directions: 1 + a few ulp).
+inline tri_coeffs triangle_coeffs(const float e1[3], const float e2[3], double Md) {
+    const double M1 = std::max({std::fabs((double)e1[0]), std::fabs((double)e1[1]), std::fabs((double)e1[2])});
+    const double M2 = std::max({std::fabs((double)e2[0]), std::fabs((double)e2[1]), std::fabs((double)e2[2])});
+    const double g2 = gamma_n(2), g3 = gamma_n(3);
+    const double P = 2.0 * Md * M2, dP = g2 * P;
+    const double Q1 = 2.0 * M1, dQ1 = (g2 + 2.0 * kU) * Q1;               // Q = S Q1
+    const double E_det = 3.0 * M1 * (g3 * (P + dP) + dP);
+    const double E_u1 = 3.0 * (1.0 + kU) * (g3 * (P + dP) + kU * (P + dP) + dP);   // E_u = S E_u1
+    const double E_v1 = 3.0 * Md * (g3 * (Q1 + dQ1) + dQ1);                         // E_v = S E_v1
+    const double E_t1 = 3.0 * M2 * (g3 * (Q1 + dQ1) + dQ1);                         // E_t = S E_t1
+    const double R = kSafety * E_det / kDetMin;
+    tri_coeffs c;
+    c.eligible = std::isfinite(R) && R <= 0.25 && std::isfinite(M1) && std::isfinite(M2);
+    if (!c.eligible) {
+        c.gA = c.gB = c.tA = c.tB = INFINITY;
+        return c;
+    }
+    // Du = du0 + du1 S, Dv = dv0 + dv1 S; delta = 3 (Du + Dv + 4u) (M1 + M2)
+    const double d0 = kSafety * (R + 2.0 * g2) / (1.0 - R);
+    const double du1 = kSafety * (E_u1 / kDetMin) / (1.0 - R), dv1 = kSafety * (E_v1 / kDetMin) / (1.0 - R);
+    c.gA = 3.0 * (2.0 * d0 + 4.0 * kU) * (M1 + M2);
+    c.gB = 3.0 * (du1 + dv1) * (M1 + M2);
+    c.tA = kSafety * (E_t1 / kDetMin) / (1.0 - R);
+    c.tB = kSafety * (R + 4.0 * g2) / (1.0 - R);
+    return c;
+}
+
+// Node of the stackless (threaded) BVH, DFS preorder: a box and the index of the next node after the
+// subtree (`skip`); leaves hold [first, first + count) of the leaf-ordered triangle pairs.
+struct node {
+    float bmin[3];          // tight box of the subtree's vertices (rounded outward)
+    uint32_t skip;
+    float bmax[3];
+    uint32_t first_count;   // leaf: first pair << 8 | pair count (count 1..255); inner: 0
+    float gA, gB, tA, tB;   // maxima of the subtree's triangle coefficients (rounded up)
+};
+static_assert(sizeof(node) == 48, "node is three float4");
+
+struct build_input {
+    std::vector<float> lo, hi;       // 3 per triangle: tight vertex box, rounded outward
+    std::vector<float> centroid;     // 3 per triangle
+    std::vector<float> coeff;        // 4 per triangle: gA, gB, tA, tB rounded up
+    std::vector<uint32_t> tris;      // triangle indices in the BVH (packet order)
+};
+
+struct build_output {
+    std::vector<node> nodes;
+    std::vector<uint32_t> order;     // BVH triangles in leaf order (packet indices), pairs padded by ~0u
+};
+
+inline float round_down(double v) {
+    float f = (float)v;
+    if ((double)f > v) f = std::nextafter(f, -INFINITY);
+    return f;
+}
+inline float round_up(double v) {
+    float f = (float)v;
+    if ((double)f < v) f = std::nextafter(f, INFINITY);
+    return f;
+}
+
+// Median split on the longest centroid axis, leaves of <= kLeafTris triangles (kept even by padding).
+constexpr uint32_t kLeafTris = 4;
+
+inline void build(build_input& in, build_output& out) {
+    out.nodes.clear();
+    out.order.clear();
+    if (in.tris.empty()) return;
+    std::vector<uint32_t> idx(in.tris.size());
+    for (uint32_t i = 0; i < idx.size(); ++i) idx[i] = i;
+    // DFS preorder with an explicit stack; skip pointers patched when a subtree closes
+    struct frame {
+        uint32_t begin, end, node, stage;
+    };
+    std::vector<frame> st;
+    auto make = [&](uint32_t b, uint32_t e) {
+        node n;
+        n.bmin[0] = n.bmin[1] = n.bmin[2] = INFINITY;
+        n.bmax[0] = n.bmax[1] = n.bmax[2] = -INFINITY;
+        float co[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        for (uint32_t i = b; i < e; ++i) {
+            const uint32_t t = idx[i];
+            for (int a = 0; a < 3; ++a) {
+                n.bmin[a] = std::min(n.bmin[a], in.lo[3 * t + a]);
+                n.bmax[a] = std::max(n.bmax[a], in.hi[3 * t + a]);
+            }
+            for (int q = 0; q < 4; ++q) co[q] = std::max(co[q], in.coeff[4 * t + q]);
+        }
+        n.gA = co[0];
+        n.gB = co[1];
+        n.tA = co[2];
+        n.tB = co[3];
+        n.skip = 0;
+        n.first_count = 0;
+        out.nodes.push_back(n);
+        return (uint32_t)out.nodes.size() - 1;
+    };
+    st.push_back({0, (uint32_t)idx.size(), make(0, (uint32_t)idx.size()), 0});
+    while (!st.empty()) {
+        frame& f = st.back();
+        const uint32_t count = f.end - f.begin;
+        if (count <= kLeafTris) {
+            const uint32_t first_pair = (uint32_t)out.order.size() / 2;
+            for (uint32_t i = f.begin; i < f.end; ++i) out.order.push_back(in.tris[idx[i]]);
+            if (out.order.size() & 1u) out.order.push_back(~0u);
+            const uint32_t pairs = (uint32_t)out.order.size() / 2 - first_pair;
+            out.nodes[f.node].first_count = (first_pair << 8) | pairs;
+            out.nodes[f.node].skip = (uint32_t)out.nodes.size();
+            st.pop_back();
+            continue;
+        }
+        if (f.stage == 0) {
+            // split on the longest axis of the centroid bounds, at the median
+            float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (uint32_t i = f.begin; i < f.end; ++i)
+                for (int a = 0; a < 3; ++a) {
+                    cmin[a] = std::min(cmin[a], in.centroid[3 * idx[i] + a]);
+                    cmax[a] = std::max(cmax[a], in.centroid[3 * idx[i] + a]);
+                }
+            int ax = 0;
+            for (int a = 1; a < 3; ++a)
+                if (cmax[a] - cmin[a] > cmax[ax] - cmin[ax]) ax = a;
+            const uint32_t mid = f.begin + count / 2;
+            std::nth_element(idx.begin() + f.begin, idx.begin() + mid, idx.begin() + f.end,
+                             [&](uint32_t a, uint32_t b) {
+                                 const float ca = in.centroid[3 * a + ax], cb = in.centroid[3 * b + ax];
+                                 return ca < cb || (ca == cb && a < b);
+                             });
+            f.stage = 1;
+            const uint32_t b = f.begin;
+            const uint32_t n = make(b, mid);
+            st.push_back({b, mid, n, 0});
+        } else if (f.stage == 1) {
+            f.stage = 2;
+            const uint32_t mid = f.begin + count / 2, e = f.end;
+            const uint32_t n = make(mid, e);
+            st.push_back({mid, e, n, 0});
+        } else {
+            out.nodes[f.node].skip = (uint32_t)out.nodes.size();
+            st.pop_back();
+        }
+    }
+}
+
+}  // namespace iqbvh

@@ -86,6 +86,17 @@ struct kparams {
     const uint32_t* sph_mat;
     const float4_storage* mats;
     const float4_storage* tri_shade;
+    // exact BVH for secondary rays (iq_bvh.hpp; streamed scenes): nodes (3 x float4: tight box min +
+    // skip, box max + leaf first pair << 8 | count, error coefficients gA gB tA tB), leaf triangle
+    // pairs (kTriPairFloat4 each) with their packet indices (uint2; ~0u pads), triangles outside the
+    // BVH (tested by every ray); the bound holds for |d_i| <= md and a finite origin; gulp covers the
+    // rounding of a grown box side
+    const float4_storage* bvh_nodes;
+    const float4_storage* bvh_pairs;
+    const uint32_t* bvh_pidx;
+    const uint32_t* bvh_always;
+    uint32_t bvh_nnodes, bvh_nalways;
+    float bvh_md, bvh_gulp;
 };
 
 // Binning launch (iqpt_bin_kernel): the camera and pixel set of the context, the world-space scene.
@@ -136,7 +147,10 @@ constexpr int kOptStats = 1 << 7;      // wave-level counters (diagnostic builds
 constexpr int kOptFastDiv = 1 << 8;    // short exact reciprocal / division forms (iq_fastdiv.h)
 constexpr int kOptCull = 1 << 9;       // camera rays test only the pairs of their tile's mask (pair layout)
 constexpr int kOptMaterials = 1 << 10; // per-primitive material table (RGB scatter records)
-constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull;
+constexpr int kOptBvh = 1 << 11;       // secondary rays traverse the exact BVH (streamed scenes; inert
+                                       // when the packet has none)
+constexpr int kOptDefault =
+    kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull | kOptBvh;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.

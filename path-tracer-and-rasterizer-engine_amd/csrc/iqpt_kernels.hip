@@ -583,6 +583,119 @@ __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntr
     }
 }
 
+// Order-free closest-triangle update: the brute-force loop keeps the hit with the smallest t and,
+// among equal t, the one with the largest packet index (t == closest is accepted, path_tracer.cu:
+// 257-275); a BVH visits triangles in another order, so the tie is decided by index explicitly.
+__device__ __forceinline__ void take_triangle(float t, uint32_t k, float& closest, int& kind, uint32_t& idx) {
+    if (t < closest || (t == closest && (kind == kHitNone || k > idx))) {
+        closest = t;
+        kind = kHitTri;
+        idx = k;
+    }
+}
+
+// Möller–Trumbore for a leaf pair with explicit packet indices ka, kb (kb = ~0u: padding); the same
+// per-element operation sequence as test_triangle_pair, so accepted hits carry the same bits.
+template <int OPT>
+__device__ __forceinline__ void test_triangle_pair_ix(const float4 q0, const float4 q1, const float4 q2,
+                                                      const float4 q3, const float4 q4, const ray3 r, float& closest,
+                                                      int& kind, uint32_t& idx, uint32_t ka, uint32_t kb) {
+    const f2 v0x = {q0.x, q0.y}, v0y = {q0.z, q0.w}, v0z = {q1.x, q1.y};
+    const f2 e1x = {q1.z, q1.w}, e1y = {q2.x, q2.y}, e1z = {q2.z, q2.w};
+    const f2 e2x = {q3.x, q3.y}, e2y = {q3.z, q3.w}, e2z = {q4.x, q4.y};
+    const f2 px = r.dy * e2z - r.dz * e2y;
+    const f2 py = r.dz * e2x - r.dx * e2z;
+    const f2 pz = r.dx * e2y - r.dy * e2x;
+    const f2 det = (e1x * px + e1y * py) + e1z * pz;
+    bool a0 = !(iq_fabsf(det.x) < 0.000001f);
+    bool a1 = kb != ~0u && !(iq_fabsf(det.y) < 0.000001f);
+    if (!(a0 || a1)) return;
+    const f2 inv = {rcp_scene<OPT>(det.x), rcp_scene<OPT>(det.y)};
+    const f2 tx = r.ox - v0x, ty = r.oy - v0y, tz = r.oz - v0z;
+    const f2 u = ((tx * px + ty * py) + tz * pz) * inv;
+    a0 = a0 && !(u.x < 0.0f || u.x > 1.0f);
+    a1 = a1 && !(u.y < 0.0f || u.y > 1.0f);
+    if (!(a0 || a1)) return;
+    const f2 qx = ty * e1z - tz * e1y;
+    const f2 qy = tz * e1x - tx * e1z;
+    const f2 qz = tx * e1y - ty * e1x;
+    const f2 v = ((r.dx * qx + r.dy * qy) + r.dz * qz) * inv;
+    const f2 uv = u + v;
+    a0 = a0 && !(v.x < 0.0f || uv.x > 1.0f);
+    a1 = a1 && !(v.y < 0.0f || uv.y > 1.0f);
+    if (!(a0 || a1)) return;
+    const f2 t = ((e2x * qx + e2y * qy) + e2z * qz) * inv;
+    if (a0 && !(t.x < kTMin)) take_triangle(t.x, ka, closest, kind, idx);
+    if (a1 && !(t.y < kTMin)) take_triangle(t.y, kb, closest, kind, idx);
+}
+
+// True if ray r may use the BVH: the error bound of iq_bvh.hpp assumed its origin inside the grown
+// scene box and |d_i| <= md (NaN fails every comparison and falls back to the full loop).
+__device__ __forceinline__ bool bvh_ray_ok(const kparams& p, const ray3& r) {
+    // finite origin (NaN fails every comparison), normalized direction
+    return iq_fabsf(r.ox) <= 1e18f && iq_fabsf(r.oy) <= 1e18f && iq_fabsf(r.oz) <= 1e18f &&
+           iq_fabsf(r.dx) <= p.bvh_md && iq_fabsf(r.dy) <= p.bvh_md && iq_fabsf(r.dz) <= p.bvh_md;
+}
+
+// Closest triangle for one ray through the exact BVH (iq_bvh.hpp): the stackless DFS visits a node
+// when the segment t in [t_min - dt, closest + dt] meets its box grown by gA + gB S, where S bounds
+// the origin's distance to the node's vertices and dt = tA S + tB closest (each rounded up by a
+// factor 1 + 2^-20, the box side by gulp more); the slab test is widened by 8 ulp, more than its own
+// rounding. Leaves are tested with the reference's own Möller–Trumbore; the triangles left out of
+// the BVH are tested afterwards.
+template <int OPT>
+__device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, float& closest, int& kind, uint32_t& idx) {
+    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh_nodes);
+    const float4* __restrict__ pairs = reinterpret_cast<const float4*>(p.bvh_pairs);
+    const float ix = 1.0f / r.dx, iy = 1.0f / r.dy, iz = 1.0f / r.dz;
+    const float slack = 8.0f * 0x1p-24f, up = 1.0f + 0x1p-20f;
+    uint32_t i = 0;
+    while (i < p.bvh_nnodes) {
+        const float4 lo = nodes[3 * (size_t)i], hi = nodes[3 * (size_t)i + 1], co = nodes[3 * (size_t)i + 2];
+        const float sx = fmaxf(iq_fabsf(r.ox - lo.x), iq_fabsf(r.ox - hi.x));
+        const float sy = fmaxf(iq_fabsf(r.oy - lo.y), iq_fabsf(r.oy - hi.y));
+        const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
+        const float S = fmaxf(fmaxf(sx, sy), sz) * up;
+        const float g = (co.x + co.y * S) * up + p.bvh_gulp;
+        // per axis [t0, t1] of the slab; a NaN (0 * inf: origin on a slab plane of an axis-parallel
+        // ray) widens that axis to everything
+        float t0x = ((lo.x - g) - r.ox) * ix, t1x = ((hi.x + g) - r.ox) * ix;
+        float t0y = ((lo.y - g) - r.oy) * iy, t1y = ((hi.y + g) - r.oy) * iy;
+        float t0z = ((lo.z - g) - r.oz) * iz, t1z = ((hi.z + g) - r.oz) * iz;
+        float ax0 = fminf(t0x, t1x), ax1 = fmaxf(t0x, t1x);
+        float ay0 = fminf(t0y, t1y), ay1 = fmaxf(t0y, t1y);
+        float az0 = fminf(t0z, t1z), az1 = fmaxf(t0z, t1z);
+        if (t0x != t0x || t1x != t1x) { ax0 = -INFINITY; ax1 = INFINITY; }
+        if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
+        if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
+        // computed slab bounds are within 3 ulp (relative) of the exact ones: widen by 8 ulp
+        const float dt = (co.z * S + co.w * closest) * up;
+        float enter = fmaxf(fmaxf(ax0, ay0), az0), exit = fminf(fminf(ax1, ay1), az1);
+        enter = enter - iq_fabsf(enter) * slack;
+        exit = exit + iq_fabsf(exit) * slack;
+        const bool hit = enter <= exit && enter <= closest + dt && exit >= kTMin - dt;
+        const uint32_t skip = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
+        if (hit && fc != 0u) {
+            const uint32_t first = fc >> 8, cnt = fc & 0xffu;
+            for (uint32_t k = 0; k < cnt; ++k) {
+                const float4* q = pairs + (size_t)(first + k) * kTriPairFloat4;
+                const uint32_t ka = p.bvh_pidx[2 * (first + k)], kb = p.bvh_pidx[2 * (first + k) + 1];
+                test_triangle_pair_ix<OPT>(q[0], q[1], q[2], q[3], q[4], r, closest, kind, idx, ka, kb);
+            }
+        }
+        i = (hit && fc == 0u) ? i + 1 : skip;
+    }
+    const float4* __restrict__ tris = reinterpret_cast<const float4*>(p.tris);
+    for (uint32_t a = 0; a < p.bvh_nalways; ++a) {
+        const uint32_t k = p.bvh_always[a];
+        float c2 = closest;
+        int kd = kHitNone;
+        uint32_t id = 0;
+        test_triangle<OPT>(tris[3 * (size_t)k], tris[3 * (size_t)k + 1], tris[3 * (size_t)k + 2], r, c2, kd, id, k);
+        if (kd == kHitTri) take_triangle(c2, k, closest, kind, idx);
+    }
+}
+
 // The running-mean table occupies spp float2 of dynamic LDS when the launch builds it.
 __device__ __forceinline__ bool use_tab_lds(const kparams& p) { return p.acc_tab != 0u; }
 
@@ -614,6 +727,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
     uint4* lds_cm = reinterpret_cast<uint4*>(lds_tab + (use_tab_lds(p) ? ((p.spp + 1u) & ~1u) : 0u));
     const bool use_tab = (OPT & kOptAccTable) && p.acc_tab;
     constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
+    constexpr bool kBvh = STREAM && (OPT & kOptBvh) && (OPT & kOptPair);
 
     if (!STREAM) {
         for (uint32_t i = threadIdx.x; i < tri_recs * kTriRec; i += kRenderBlock) lds_tri[i] = g_tri[i];
@@ -728,11 +842,21 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
         const uint32_t* lane_mask =
             (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;   // null: 0
         if (STREAM) {
+            // Streamed scene. Per lane and mask word: a camera ray contributes its tile's mask (kOptCull),
+            // a secondary ray that takes the BVH (kOptBvh) contributes nothing to the triangle batches,
+            // any other ray every pair; the wave ORs the words, the block skips a batch nobody needs.
+            constexpr bool kWords = kCull || kBvh;
+            const bool bvh_lane = kBvh && p.bvh_nodes != nullptr && active && depth != 0 && bvh_ray_ok(p, ray);
+            const uint32_t* tile_mask =
+                (kCull && p.cull != nullptr && active && depth == 0)
+                    ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
+            const bool tri_all = active && tile_mask == nullptr && !bvh_lane;
+            const bool sph_all = active && tile_mask == nullptr;
             for (uint32_t base = 0; base < tri_recs; base += p.tri_batch) {
                 const uint32_t n = min(p.tri_batch, tri_recs - base);
-                uint32_t wm[kCull ? 8 : 1];
+                uint32_t wm[kWords ? 8 : 1];
                 bool any = true;
-                if (kCull) {
+                if (kWords) {
                     // the batch's mask words (a batch is at most 256 pairs, a multiple of 32: <= 8 aligned words)
                     any = false;
 #pragma unroll
@@ -740,7 +864,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                         const uint32_t w = base / 32u + (uint32_t)i;
                         wm[i] = 0u;
                         if ((uint32_t)i * 32u < n)
-                            wm[i] = cull ? wave_or(lane_mask ? lane_mask[w] : 0u) : ~0u;
+                            wm[i] = wave_or(tri_all ? ~0u : (tile_mask ? tile_mask[w] : 0u));
                         any = any || wm[i] != 0u;
                     }
                     // the barrier also orders this batch's LDS writes after the previous batch's reads
@@ -751,10 +875,10 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                 for (uint32_t i = threadIdx.x; i < n * kTriRec; i += kRenderBlock)
                     lds_tri[i] = g_tri[(size_t)base * kTriRec + i];
                 __syncthreads();
-                if (active) {
+                if (active && !bvh_lane) {
                     const uint32_t first = base * kTriPer;
                     const uint32_t cnt = min(n * kTriPer, p.ntri - first);
-                    if (kCull) {
+                    if (kWords) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) {
                             uint32_t m = wm[i];
@@ -772,18 +896,20 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                     }
                 }
             }
+            // secondary rays: triangles through the exact BVH (iq_bvh.hpp), before the spheres
+            if (bvh_lane) bvh_closest<OPT>(p, ray, closest, kind, hidx);
             for (uint32_t base = 0; base < sph_recs; base += p.sph_batch) {
                 const uint32_t n = min(p.sph_batch, sph_recs - base);
-                uint32_t wm[kCull ? 8 : 1];
+                uint32_t wm[kWords ? 8 : 1];
                 bool any = true;
-                if (kCull) {
+                if (kWords) {
                     any = false;
 #pragma unroll
                     for (int i = 0; i < 8; ++i) {
                         const uint32_t w = p.cull_wt + base / 32u + (uint32_t)i;
                         wm[i] = 0u;
                         if ((uint32_t)i * 32u < n)
-                            wm[i] = cull ? wave_or(lane_mask ? lane_mask[w] : 0u) : ~0u;
+                            wm[i] = wave_or(sph_all ? ~0u : (tile_mask ? tile_mask[w] : 0u));
                         any = any || wm[i] != 0u;
                     }
                     if (!__syncthreads_or(any ? 1 : 0)) continue;
@@ -796,7 +922,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                 if (active) {
                     const uint32_t first = base * kSphPer;
                     const uint32_t cnt = min(n * kSphPer, p.nsph - first);
-                    if (kCull) {
+                    if (kWords) {
 #pragma unroll
                         for (int i = 0; i < 8; ++i) {
                             uint32_t m = wm[i];
@@ -1176,19 +1302,15 @@ struct variant {
 };
 #define IQPT_V(M, S, O) {M, S, O, launch_t<M, S, O>, occ_t<M, S, O>}
 const variant kVariants[] = {
-    // MAXD 16 (max_depth 9-16) differs only in the LDS stack size the runtime reserves
-    IQPT_V(8, false, kOptDefault), IQPT_V(8, true, kOptDefault),
-    IQPT_V(16, false, kOptDefault), IQPT_V(16, true, kOptDefault),
-    // packets outside the kOptFastDiv range (iqpt_upload_packet)
-    IQPT_V(8, false, kOptDefault & ~kOptFastDiv), IQPT_V(8, true, kOptDefault & ~kOptFastDiv),
-    IQPT_V(16, false, kOptDefault & ~kOptFastDiv), IQPT_V(16, true, kOptDefault & ~kOptFastDiv),
-    // packets with a material table
-    IQPT_V(8, false, kOptDefault | kOptMaterials), IQPT_V(8, true, kOptDefault | kOptMaterials),
-    IQPT_V(16, false, kOptDefault | kOptMaterials), IQPT_V(16, true, kOptDefault | kOptMaterials),
-    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptMaterials),
-    IQPT_V(8, true, (kOptDefault & ~kOptFastDiv) | kOptMaterials),
-    IQPT_V(16, false, (kOptDefault & ~kOptFastDiv) | kOptMaterials),
-    IQPT_V(16, true, (kOptDefault & ~kOptFastDiv) | kOptMaterials),
+    // MAXD 16 (max_depth 9-16) differs only in the LDS stack size the runtime reserves. Streamed
+    // scenes run without the 5-wave bound (the BVH traversal needs the registers; 4 waves/SIMD).
+#define IQPT_PROD(O) IQPT_V(8, false, O), IQPT_V(16, false, O), IQPT_V(8, true, (O) & ~kOptLB5), \
+                     IQPT_V(16, true, (O) & ~kOptLB5)
+    IQPT_PROD(kOptDefault),
+    IQPT_PROD(kOptDefault & ~kOptFastDiv),                  // packets outside the kOptFastDiv range
+    IQPT_PROD(kOptDefault | kOptMaterials),                 // packets with a material table
+    IQPT_PROD((kOptDefault & ~kOptFastDiv) | kOptMaterials),
+#undef IQPT_PROD
 #if defined(IQPT_AB_VARIANTS)
     IQPT_V(8, false, 0),
     IQPT_V(8, true, 0),
@@ -1207,6 +1329,8 @@ const variant kVariants[] = {
     IQPT_V(8, false, kOptDefault & ~kOptCull),
     IQPT_V(8, true, kOptDefault & ~kOptCull),
     IQPT_V(8, false, kOptDefault & ~kOptCull & ~kOptFastDiv),
+    IQPT_V(8, true, kOptDefault & ~kOptBvh),
+    IQPT_V(8, true, (kOptDefault | kOptMaterials) & ~kOptBvh),
 #endif
 };
 #undef IQPT_V

@@ -15,6 +15,7 @@
 #include <utility>
 #include <vector>
 
+#include "iq_bvh.hpp"
 #include "iq_host_math.hpp"
 #include "iq_interval.h"
 #include "iq_xorwow.h"
@@ -96,6 +97,13 @@ struct iqpt_ctx {
     uint32_t* d_tri_mat = nullptr;
     uint32_t* d_sph_mat = nullptr;
     float4_storage* d_mats = nullptr;
+    // exact BVH for secondary rays (iq_bvh.hpp), null when the packet has few triangles
+    float4_storage* d_bvh_nodes = nullptr;
+    float4_storage* d_bvh_pairs = nullptr;
+    uint32_t* d_bvh_pidx = nullptr;
+    uint32_t* d_bvh_always = nullptr;
+    uint32_t bvh_nnodes = 0, bvh_nalways = 0;
+    float bvh_md = 0.0f, bvh_gulp = 0.0f;
     bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
     // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
     uint32_t* d_cull = nullptr;
@@ -118,11 +126,13 @@ int use_device(const iqpt_ctx* c) {
 void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, float* far_rw);
 
 void free_scene(iqpt_ctx* c) {
-    for (float4_storage** b : {&c->d_tris, &c->d_tri_pairs, &c->d_tri_shade, &c->d_sph, &c->d_sph_pairs, &c->d_mats}) {
+    for (float4_storage** b : {&c->d_tris, &c->d_tri_pairs, &c->d_tri_shade, &c->d_sph, &c->d_sph_pairs, &c->d_mats,
+                               &c->d_bvh_nodes, &c->d_bvh_pairs}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
-    for (uint32_t** b : {&c->d_tri_mat, &c->d_sph_mat}) {
+    c->bvh_nnodes = c->bvh_nalways = 0;
+    for (uint32_t** b : {&c->d_tri_mat, &c->d_sph_mat, &c->d_bvh_pidx, &c->d_bvh_always}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
@@ -212,6 +222,104 @@ void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, f
         *near_rw = 1.0f / P[15];
         *far_rw = 1.0f / wf;
     }
+}
+
+// Exact BVH for secondary rays (iq_bvh.hpp) over the world-space triangles `tris` (kTriFloat4 each)
+// and the spheres (for the scene box). Fills the host arrays the upload copies to the device.
+struct bvh_host {
+    std::vector<float4_storage> nodes, pairs;
+    std::vector<uint32_t> pidx, always;
+    float md, gulp;
+};
+constexpr uint32_t kBvhMinTriangles = 256;
+
+bool build_bvh(const std::vector<float4_storage>& tris, const std::vector<float4_storage>& sph, bvh_host& out) {
+    const size_t ntri = tris.size() / iqpt::kTriFloat4;
+    if (ntri < kBvhMinTriangles) return false;
+    // scene box (exact corners of every triangle in double, spheres' centre +- radius)
+    double blo[3] = {INFINITY, INFINITY, INFINITY}, bhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    std::vector<double> corners(ntri * 9);
+    for (size_t k = 0; k < ntri; ++k) {
+        const float4_storage* t = &tris[k * iqpt::kTriFloat4];
+        const double v0[3] = {t[0].x, t[0].y, t[0].z};
+        const double e1[3] = {t[0].w, t[1].x, t[1].y}, e2[3] = {t[1].z, t[1].w, t[2].x};
+        for (int a = 0; a < 3; ++a) {
+            const double c3[3] = {v0[a], v0[a] + e1[a], v0[a] + e2[a]};
+            for (int q = 0; q < 3; ++q) {
+                corners[k * 9 + 3 * q + a] = c3[q];
+                blo[a] = std::min(blo[a], c3[q]);
+                bhi[a] = std::max(bhi[a], c3[q]);
+            }
+        }
+    }
+    for (const float4_storage& s4 : sph) {
+        const double c[3] = {s4.x, s4.y, s4.z}, r = std::fabs((double)s4.w);
+        for (int a = 0; a < 3; ++a) {
+            blo[a] = std::min(blo[a], c[a] - r);
+            bhi[a] = std::max(bhi[a], c[a] + r);
+        }
+    }
+    double ext = 0.0, maxabs = 0.0;
+    for (int a = 0; a < 3; ++a) {
+        ext = std::max(ext, bhi[a] - blo[a]);
+        maxabs = std::max({maxabs, std::fabs(blo[a]), std::fabs(bhi[a])});
+    }
+    if (!std::isfinite(ext) || maxabs > 1e9) return false;
+    // rays may use the BVH with |d_i| <= md and a finite origin (the bound holds for any origin:
+    // it grows with the origin's distance S to the node, iq_bvh.hpp)
+    const double Md = 1.001;
+    out.md = 1.001f;
+    // a box side lo - g rounds to nearest: |error| <= 2^-24 (maxabs + g); the kernel adds gulp and
+    // scales g by 1 + 2^-20, which covers it
+    out.gulp = iqbvh::round_up(maxabs * 0x1p-22);
+    iqbvh::build_input in;
+    for (size_t k = 0; k < ntri; ++k) {
+        const float4_storage* t = &tris[k * iqpt::kTriFloat4];
+        const float e1[3] = {t[0].w, t[1].x, t[1].y}, e2[3] = {t[1].z, t[1].w, t[2].x};
+        const iqbvh::tri_coeffs b = iqbvh::triangle_coeffs(e1, e2, Md);
+        if (!b.eligible) {
+            out.always.push_back((uint32_t)k);
+            continue;
+        }
+        for (int a = 0; a < 3; ++a) {
+            const double lo = std::min({corners[k * 9 + a], corners[k * 9 + 3 + a], corners[k * 9 + 6 + a]});
+            const double hi = std::max({corners[k * 9 + a], corners[k * 9 + 3 + a], corners[k * 9 + 6 + a]});
+            in.lo.push_back(iqbvh::round_down(lo));
+            in.hi.push_back(iqbvh::round_up(hi));
+            in.centroid.push_back((float)((lo + hi) * 0.5));
+        }
+        const double co[4] = {b.gA, b.gB, b.tA, b.tB};
+        for (double v : co) in.coeff.push_back(iqbvh::round_up(v));
+        in.tris.push_back((uint32_t)k);
+    }
+    iqbvh::build_output bo;
+    iqbvh::build(in, bo);
+    for (const iqbvh::node& n : bo.nodes) {
+        float4_storage lo, hi;
+        lo.x = n.bmin[0];
+        lo.y = n.bmin[1];
+        lo.z = n.bmin[2];
+        std::memcpy(&lo.w, &n.skip, 4);
+        hi.x = n.bmax[0];
+        hi.y = n.bmax[1];
+        hi.z = n.bmax[2];
+        std::memcpy(&hi.w, &n.first_count, 4);
+        out.nodes.push_back(lo);
+        out.nodes.push_back(hi);
+        out.nodes.push_back(float4_storage{n.gA, n.gB, n.tA, n.tB});
+    }
+    // leaf pairs in the kernel's pair layout (iqpt_internal.hpp), padding elements zero
+    const size_t npairs = bo.order.size() / 2;
+    out.pairs.assign(npairs * iqpt::kTriPairFloat4, float4_storage{0.0f, 0.0f, 0.0f, 0.0f});
+    out.pidx = bo.order;
+    for (size_t q = 0; q < bo.order.size(); ++q) {
+        if (bo.order[q] == ~0u) continue;
+        const float4_storage* t = &tris[(size_t)bo.order[q] * iqpt::kTriFloat4];
+        const float f[9] = {t[0].x, t[0].y, t[0].z, t[0].w, t[1].x, t[1].y, t[1].z, t[1].w, t[2].x};
+        float* dst = &out.pairs[(q / 2) * iqpt::kTriPairFloat4].x;
+        for (int comp = 0; comp < 9; ++comp) dst[2 * comp + (q & 1)] = f[comp];
+    }
+    return true;
 }
 
 // Pixel-state planes between device tile-major storage and host compact row-major order
@@ -516,6 +624,8 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         IQPT_HIP(hipMemcpy(*dst, v.data(), v.size() * sizeof(float4_storage), hipMemcpyHostToDevice));
         return IQPT_OK;
     };
+    bvh_host bvh;
+    const bool have_bvh = build_bvh(tris, sph, bvh);
     auto upload_u32 = [&](const std::vector<uint32_t>& v, uint32_t** dst) -> int {
         if (v.empty()) return IQPT_OK;
         if (hipMalloc(dst, v.size() * sizeof(uint32_t)) != hipSuccess)
@@ -526,9 +636,17 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
     if ((st = upload(tris, &c->d_tris)) || (st = upload(tri_pairs, &c->d_tri_pairs)) ||
         (st = upload(shade, &c->d_tri_shade)) || (st = upload(sph, &c->d_sph)) ||
         (st = upload(sph_pairs, &c->d_sph_pairs)) || (st = upload(mats, &c->d_mats)) ||
-        (st = upload_u32(tri_mat, &c->d_tri_mat)) || (st = upload_u32(sph_mat, &c->d_sph_mat))) {
+        (st = upload_u32(tri_mat, &c->d_tri_mat)) || (st = upload_u32(sph_mat, &c->d_sph_mat)) ||
+        (have_bvh && ((st = upload(bvh.nodes, &c->d_bvh_nodes)) || (st = upload(bvh.pairs, &c->d_bvh_pairs)) ||
+                      (st = upload_u32(bvh.pidx, &c->d_bvh_pidx)) || (st = upload_u32(bvh.always, &c->d_bvh_always))))) {
         free_scene(c);
         return st;
+    }
+    if (have_bvh) {
+        c->bvh_nnodes = (uint32_t)(bvh.nodes.size() / 3);
+        c->bvh_nalways = (uint32_t)bvh.always.size();
+        c->bvh_md = bvh.md;
+        c->bvh_gulp = bvh.gulp;
     }
     c->ntri = (uint32_t)total;
     c->nsph = nsdc;
@@ -577,6 +695,16 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     if (c->d_mats) opt |= iqpt::kOptMaterials;                  // the packet carries a material table
     p.tri_mat = c->d_tri_mat;
     p.sph_mat = c->d_sph_mat;
+    if (c->d_bvh_nodes && c->bvh_nnodes) {
+        p.bvh_nodes = c->d_bvh_nodes;
+        p.bvh_pairs = c->d_bvh_pairs;
+        p.bvh_pidx = c->d_bvh_pidx;
+        p.bvh_always = c->d_bvh_always;
+        p.bvh_nnodes = c->bvh_nnodes;
+        p.bvh_nalways = c->bvh_nalways;
+        p.bvh_md = c->bvh_md;
+        p.bvh_gulp = c->bvh_gulp;
+    }
     p.mats = c->d_mats;
     p.tri_shade = c->d_tri_shade;
     p.rcp_width = 1.0f / (float)c->width;
@@ -588,6 +716,10 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     const uint32_t sph_recs = pair ? p.nsph_pairs : p.nsph;
     const uint64_t resident = (uint64_t)tri_recs * tri_rec + (uint64_t)sph_recs * sph_rec;
     const bool stream_batches = resident > iqpt::kLdsResidentBytes;
+    // production streamed variants are built without the 5-wave bound (registers for the BVH)
+    if (stream_batches && !iqpt::render_variant_exists(c->max_depth, true, opt) &&
+        iqpt::render_variant_exists(c->max_depth, true, opt & ~iqpt::kOptLB5))
+        opt &= ~iqpt::kOptLB5;
     if (stream_batches) {
         p.tri_batch = pair ? iqpt::kTriBatch / 2 : iqpt::kTriBatch;   // records
         p.sph_batch = pair ? iqpt::kSphBatch / 2 : iqpt::kSphBatch;
@@ -887,6 +1019,26 @@ int iqpt_debug_cull_tile(const iqpt_camera* cam, uint32_t xa, uint32_t xb, uint3
         sph_culled[k] = b.ok && iqiv::sphere_culled(b, sp, sp[3]) ? 1 : 0;
     }
     return b.ok ? 1 : 0;
+}
+
+/* Internal (tests/test_gpu_bvh.py): the BVH of the uploaded packet — node count and the number of
+ * triangles left on the always-tested list (both 0 without a BVH). */
+int iqpt_debug_bvh_info(iqpt_ctx* c, uint32_t* nnodes, uint32_t* nalways) {
+    if (!c || !nnodes || !nalways) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *nnodes = c->d_bvh_nodes ? c->bvh_nnodes : 0u;
+    *nalways = c->d_bvh_nodes ? c->bvh_nalways : 0u;
+    return IQPT_OK;
+}
+
+/* Internal (tests/test_bvh.py): the error bound of iq_bvh.hpp for one triangle's edges, evaluated
+ * at S = max_i |o_i - v0_i|. out: box growth, dt_a, dt_b (|t^ - t| <= dt_a + dt_b |t|). Returns 1 if the triangle is BVH-eligible, 0 if not. */
+int iqpt_debug_bvh_bound(const float* e1, const float* e2, double S, double Md, double* out3) {
+    if (!e1 || !e2 || !out3) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    const iqbvh::tri_coeffs b = iqbvh::triangle_coeffs(e1, e2, Md);
+    out3[0] = b.gA + b.gB * S;
+    out3[1] = b.tA * S;
+    out3[2] = b.tB;
+    return b.eligible ? 1 : 0;
 }
 
 /* Internal (tests/test_gpu_libm.py): evaluate the device build of the shared math on n inputs on

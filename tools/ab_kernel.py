@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 from iqpt import _build, _lib  # noqa: E402
 
 OPT = {"cam": 1, "acc": 2, "pair": 4, "sincos": 32, "stats": 128}
-DEFAULT = 1 | 2 | 4 | 8 | 32 | 256 | 512
+DEFAULT = 1 | 2 | 4 | 8 | 32 | 256 | 512 | 2048
 
 
 def main():
@@ -61,7 +61,8 @@ def main():
     pk = sc.build_packet()
     cam = iqpt.make_camera(cfg.width, cfg.height)
     variants = {"default": DEFAULT, "none": 0, "-cull": DEFAULT & ~512, "-fastdiv": DEFAULT & ~256,
-                "-pair": DEFAULT & ~4, "-sincos": DEFAULT & ~32}
+                "-pair": DEFAULT & ~4, "-sincos": DEFAULT & ~32,
+                "-bvh": DEFAULT & ~2048}
     if args.variants:
         variants = {kv.split("=")[0]: int(kv.split("=")[1], 0) for kv in args.variants.split(",")}
     ps = None
