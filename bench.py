@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="c2")
+    ap.add_argument("--spp", type=int, default=0,
+                    help="samples per pixel per step (default: the config's; a progressive pass of C5's 1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--verify-rows", type=int, default=16)
@@ -87,7 +89,7 @@ def cpu_baseline(cfg, pk, cam, seconds: float) -> dict:
                       f"(max_depth {cfg.max_depth}) in {dt:.1f} s, {rays} rays"}
 
 
-def verify_vs_oracle(cfg, pk, cam, lin_rank, rank, world, nrows, seed=1984) -> dict:
+def verify_vs_oracle(cfg, pk, cam, lin_rank, rank, world, nrows, seed=1984, spp=None) -> dict:
     """After the first 64-spp frame: compare a band of this rank's rows with the oracle. `rank` and
     `world` describe the row partition (world 1 = the rank owns the whole frame)."""
     sys.path.insert(0, str(REPO / "oracle"))
@@ -97,7 +99,7 @@ def verify_vs_oracle(cfg, pk, cam, lin_rank, rank, world, nrows, seed=1984) -> d
     k0 = (first - rank) // world
     ps = iqpt.pixel_set(cfg.width, cfg.height, 0, cfg.width, first, world, nrows)
     fr = oracle.OracleFrame(cfg.width, cfg.height, pixels=ps, seed=seed, max_depth=cfg.max_depth)
-    fr.render(pk, cam, cfg.spp)
+    fr.render(pk, cam, spp or cfg.spp)
     mine = lin_rank.reshape(-1, cfg.width, 4)[k0:k0 + nrows].reshape(-1, 4)
     a = mine[:, :3].astype(np.float64)
     b = fr.lin[:, :3].astype(np.float64)
@@ -129,6 +131,7 @@ def main():
             dist.barrier()
 
     cfg = CONFIGS[args.config]
+    spp_step = args.spp or cfg.spp
     scene = Scene()
     scene.add_preset(cfg.preset)
     pk = scene.build_packet()
@@ -160,7 +163,7 @@ def main():
 
     def step():
         nonlocal frame
-        pt.render(cfg.spp)
+        pt.render(spp_step)
         if world > 1 and not weak:
             fetch_accum()
             dist.gather(accum, gather_list, dst=0)
@@ -174,7 +177,7 @@ def main():
         if i == 0 and args.verify_rows > 0:
             lin, _ = pt.read()
             verify = verify_vs_oracle(cfg, pk, cam, lin, part_rank, part_world, min(args.verify_rows, ps.nrows),
-                                      seed=seed)
+                                      seed=seed, spp=spp_step)
     torch.cuda.synchronize()
     barrier()
     rays0 = pt.rays()
@@ -232,7 +235,7 @@ def main():
                     traffic = pmc.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        samples = cfg.width * cfg.height * cfg.spp * args.steps
+        samples = cfg.width * cfg.height * spp_step * args.steps
         out = {
             "metric": "Mrays/sec at 1920x1080 8-bounce; per-pixel RMSE vs reference",
             "value": round(mrays, 3),
@@ -248,7 +251,7 @@ def main():
             "data": ("synthetic (procedural Cornell-box scene of SURVEY.md §8d, seed 1984"
                      + (", rank r: seed 1984+r)" if weak and world > 1 else ")")),
             "config": {"workload": f"{cfg.name}:{cfg.preset}", "width": cfg.width, "height": cfg.height,
-                       "spp_per_step": cfg.spp, "max_depth": cfg.max_depth, "triangles": stats["triangles"],
+                       "spp_per_step": spp_step, "max_depth": cfg.max_depth, "triangles": stats["triangles"],
                        "spheres": stats["spheres"],
                        "partition": (f"full frame per rank x{world} (seed 1984+rank)" if weak
                                      else f"cyclic rows x{world}"),
@@ -271,7 +274,9 @@ def main():
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "flops_per_ray": f_ray,
                 "note": "algorithmic FLOPs F_ray = 52 T + 19 S (SURVEY.md §8d) x rays per launch / HIP-event "
-                        "kernel time; FP32 vector peak (no MFMA: nothing here is a dense contraction)",
+                        "kernel time; FP32 vector peak (no MFMA: nothing here is a dense contraction)"
+                        + ("; frac > 1: the reference's brute-force tests per ray, most of which the tile masks "
+                           "and the BVH skip (DESIGN.md §5)" if achieved_tflops > FP32_PEAK_TFLOPS else ""),
             },
         }
         if world == 1 and not args.no_cpu_baseline:

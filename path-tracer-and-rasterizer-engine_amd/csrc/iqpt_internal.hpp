@@ -149,6 +149,7 @@ constexpr int kOptCull = 1 << 9;       // camera rays test only the pairs of the
 constexpr int kOptMaterials = 1 << 10; // per-primitive material table (RGB scatter records)
 constexpr int kOptBvh = 1 << 11;       // secondary rays traverse the exact BVH (streamed scenes; inert
                                        // when the packet has none)
+constexpr int kOptBvhPrimary = 1 << 12; // camera rays take the BVH too (instead of the tile masks)
 constexpr int kOptDefault =
     kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull | kOptBvh;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)

@@ -728,6 +728,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
     const bool use_tab = (OPT & kOptAccTable) && p.acc_tab;
     constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
     constexpr bool kBvh = STREAM && (OPT & kOptBvh) && (OPT & kOptPair);
+    constexpr bool kBvhPrimary = kBvh && (OPT & kOptBvhPrimary);
 
     if (!STREAM) {
         for (uint32_t i = threadIdx.x; i < tri_recs * kTriRec; i += kRenderBlock) lds_tri[i] = g_tri[i];
@@ -846,13 +847,17 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
             // a secondary ray that takes the BVH (kOptBvh) contributes nothing to the triangle batches,
             // any other ray every pair; the wave ORs the words, the block skips a batch nobody needs.
             constexpr bool kWords = kCull || kBvh;
-            const bool bvh_lane = kBvh && p.bvh_nodes != nullptr && active && depth != 0 && bvh_ray_ok(p, ray);
+            const bool bvh_lane = kBvh && p.bvh_nodes != nullptr && active && (depth != 0 || kBvhPrimary) &&
+                                  bvh_ray_ok(p, ray);
             const uint32_t* tile_mask =
                 (kCull && p.cull != nullptr && active && depth == 0)
                     ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
+            const uint32_t* tri_mask = bvh_lane ? nullptr : tile_mask;
             const bool tri_all = active && tile_mask == nullptr && !bvh_lane;
             const bool sph_all = active && tile_mask == nullptr;
-            for (uint32_t base = 0; base < tri_recs; base += p.tri_batch) {
+            // the whole block skips the triangle batches when every ray takes the BVH
+            const bool tri_block = !kWords || __syncthreads_or((tri_all || tri_mask != nullptr) ? 1 : 0);
+            for (uint32_t base = 0; tri_block && base < tri_recs; base += p.tri_batch) {
                 const uint32_t n = min(p.tri_batch, tri_recs - base);
                 uint32_t wm[kWords ? 8 : 1];
                 bool any = true;
@@ -864,7 +869,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                         const uint32_t w = base / 32u + (uint32_t)i;
                         wm[i] = 0u;
                         if ((uint32_t)i * 32u < n)
-                            wm[i] = wave_or(tri_all ? ~0u : (tile_mask ? tile_mask[w] : 0u));
+                            wm[i] = wave_or(tri_all ? ~0u : (tri_mask ? tri_mask[w] : 0u));
                         any = any || wm[i] != 0u;
                     }
                     // the barrier also orders this batch's LDS writes after the previous batch's reads
@@ -1304,8 +1309,11 @@ struct variant {
 const variant kVariants[] = {
     // MAXD 16 (max_depth 9-16) differs only in the LDS stack size the runtime reserves. Streamed
     // scenes run without the 5-wave bound (the BVH traversal needs the registers; 4 waves/SIMD).
+    // Streamed scenes also get the kOptBvhPrimary form (camera rays through the BVH), chosen per
+    // packet by timing (iqpt_runtime.cpp).
 #define IQPT_PROD(O) IQPT_V(8, false, O), IQPT_V(16, false, O), IQPT_V(8, true, (O) & ~kOptLB5), \
-                     IQPT_V(16, true, (O) & ~kOptLB5)
+                     IQPT_V(16, true, (O) & ~kOptLB5), IQPT_V(8, true, ((O) | kOptBvhPrimary) & ~kOptLB5), \
+                     IQPT_V(16, true, ((O) | kOptBvhPrimary) & ~kOptLB5)
     IQPT_PROD(kOptDefault),
     IQPT_PROD(kOptDefault & ~kOptFastDiv),                  // packets outside the kOptFastDiv range
     IQPT_PROD(kOptDefault | kOptMaterials),                 // packets with a material table

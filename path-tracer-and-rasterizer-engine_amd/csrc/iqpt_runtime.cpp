@@ -114,6 +114,14 @@ struct iqpt_ctx {
     // timing
     std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
     std::vector<hipEvent_t> event_pool;
+    // camera rays of a streamed scene with a BVH: tile masks or the BVH (kOptBvhPrimary), whichever
+    // the first two launches after a packet upload time faster per sample (results are identical);
+    // tools/ab_kernel.py fixes the option set instead (opt_fixed)
+    bool opt_fixed = false;
+    int tune_stage = 0;          // 0: next launch times masks, 1: times the BVH, 2: decide, 3: decided
+    bool tune_primary = false;
+    hipEvent_t tune_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    double tune_work[2] = {0.0, 0.0};
 };
 
 namespace {
@@ -138,6 +146,8 @@ void free_scene(iqpt_ctx* c) {
     }
     c->ntri = c->nsph = 0;
     c->cull_valid = false;
+    c->tune_stage = 0;
+    c->tune_primary = false;
 }
 
 // (Re)build the kOptCull tile masks of the current camera and packet on the context's stream.
@@ -471,6 +481,8 @@ int iqpt_destroy(iqpt_ctx* c) {
         (void)hipEventDestroy(pr.second);
     }
     for (hipEvent_t ev : c->event_pool) (void)hipEventDestroy(ev);
+    for (hipEvent_t ev : c->tune_ev)
+        if (ev) (void)hipEventDestroy(ev);
     if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return IQPT_OK;
@@ -750,6 +762,32 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     p.rays = c->d_rays;
     p.queue = c->d_queue;
     p.stats = c->d_stats;
+    // kOptBvhPrimary: decided by timing (see iqpt_ctx::tune_stage)
+    int tune_slot = -1;
+    if (!c->opt_fixed && stream_batches && p.bvh_nodes && p.cull && (opt & iqpt::kOptBvh) &&
+        iqpt::render_variant_exists(c->max_depth, true, opt | iqpt::kOptBvhPrimary)) {
+        if (c->tune_stage == 2) {
+            float ms_a = 0.0f, ms_b = 0.0f;
+            if (hipEventSynchronize(c->tune_ev[3]) == hipSuccess &&
+                hipEventElapsedTime(&ms_a, c->tune_ev[0], c->tune_ev[1]) == hipSuccess &&
+                hipEventElapsedTime(&ms_b, c->tune_ev[2], c->tune_ev[3]) == hipSuccess)
+                c->tune_primary = (double)ms_b * c->tune_work[0] < (double)ms_a * c->tune_work[1];
+            c->tune_stage = 3;
+        }
+        if (c->tune_stage < 2) {
+            tune_slot = c->tune_stage;
+            for (int k = 0; k < 2; ++k) {
+                hipEvent_t& ev = c->tune_ev[2 * tune_slot + k];
+                if (!ev && hipEventCreate(&ev) != hipSuccess) ev = nullptr;
+                if (!ev) tune_slot = -1;
+            }
+            if (tune_slot == 0) {   // load both code objects before either is timed
+                int o2 = 0;
+                (void)iqpt::render_occupancy(c->max_depth, true, opt | iqpt::kOptBvhPrimary, lds, &o2);
+            }
+        }
+        if ((tune_slot == 1) || (tune_slot < 0 && c->tune_primary)) opt |= iqpt::kOptBvhPrimary;
+    }
     int occ = 0;
     if (iqpt::render_occupancy(c->max_depth, stream_batches, opt, lds, &occ) != 0 || occ < 1) occ = 1;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
@@ -757,10 +795,16 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     IQPT_HIP(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), c->stream));
     hipEvent_t e0 = take_event(c), e1 = take_event(c);
     if (e0) (void)hipEventRecord(e0, c->stream);
+    if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
     int le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
+    if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1) (void)hipEventRecord(e1, c->stream);
     if (e0 && e1) c->timed.emplace_back(e0, e1);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "render kernel launch");
+    if (tune_slot >= 0) {
+        c->tune_work[tune_slot] = (double)spp * (double)c->npix;
+        c->tune_stage = tune_slot + 1;
+    }
     c->frame += spp;
     return IQPT_OK;
 }
@@ -989,6 +1033,7 @@ int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
         IQPT_HIP(hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
     }
     c->opt = opt;
+    c->opt_fixed = true;
     return IQPT_OK;
 }
 

@@ -24,15 +24,16 @@ def bvh_info(pt):
     return n.value, a.value
 
 
-def run_both(scene, w, h, spp, depth, pixels=None, seed=1984, cam=None):
+def run_both(scene, w, h, spp, depth, pixels=None, seed=1984, cam=None, launches=None):
     pk = scene.build_packet()
     cam = cam or make_camera(w, h)
     pt = PathTracer(w, h, pixels=pixels, seed=seed, max_depth=depth)
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, pixels=pixels, seed=seed, max_depth=depth)
-    pt.render(spp)
-    fr.render(pk, cam, spp)
+    for s in (launches or [spp]):
+        pt.render(s)
+        fr.render(pk, cam, s)
     lin, bgra = pt.read()
     c = compare(lin, fr.lin)
     assert c["bitexact"] == c["npix"], c
@@ -121,3 +122,13 @@ def test_presets_with_materials(require_gpu, preset, w, h, crop):
     sc.set_model_material("lamp", sc.add_material(MAT_EMISSIVE, (1.0, 0.9, 0.8, 1.0), 10.0))
     pt, _ = run_both(sc, w, h, 2, 8, pixels=pixel_set(w, h, *crop))
     assert bvh_info(pt)[0] > 0
+
+
+def test_camera_ray_path_switch_between_launches(require_gpu):
+    """The first two launches of a streamed scene with a BVH time the tile-mask and the BVH camera-ray
+    kernels, later launches use the faster: every launch continues the same frame sequence."""
+    sc = Scene()
+    sc.add_preset("mixed")
+    w, h = 3840, 2160
+    pt, _ = run_both(sc, w, h, 0, 8, pixels=pixel_set(w, h, 1800, 2000, 1000, 13, 8), launches=[1, 2, 1, 1])
+    assert pt.frames() == 5
