@@ -492,12 +492,22 @@ __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
 // `tab` is false when the launch has more samples than the table holds (rc is then not set).
 // kOptFastDiv: for c in [2^-90, 1) (c is clamped to [0, 1] or NaN) and n < 2^32 the quotient is
 // normal and Markstein's correction of c * rc, rc = RN(1/n) from the table, is exact (iq_fastdiv.h).
+// Branch-free under kOptFastDiv: Markstein's form also gives the exact quotient for c = 1 (RN(1/n)
+// = rc) and c = 0 (+0, as 0 / n), so only 0 < c < 2^-90 (a quotient that could be subnormal) takes
+// the generic division.
 template <int OPT>
 __device__ __forceinline__ float mean_term(float c, float nf, float rc, bool tab) {
+    if (tab && (OPT & kOptFastDiv)) {
+        float q = iq_div_pre(c, nf, rc);
+        if (c > 0.0f && c < 0x1p-90f) {
+            asm volatile("" ::: "memory");   // keep the rare IEEE expansion behind a branch (no if-conversion)
+            q = c / nf;
+        }
+        return q;
+    }
     if (tab) {
         if (c == 1.0f) return rc;
         if (c == 0.0f) return 0.0f;
-        if ((OPT & kOptFastDiv) && c >= 0x1p-90f) return iq_div_pre(c, nf, rc);
     }
     return c / nf;
 }
@@ -724,7 +734,9 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
     float4* lds_sph = lds + (size_t)p.tri_batch * kTriRec;
     float2* lds_tab = reinterpret_cast<float2*>(lds_sph + (size_t)p.sph_batch * kSphRec);
     // kOptCull: one (mask word 0 of triangles, of spheres, tile, -) slot per thread, 16-B aligned
-    uint4* lds_cm = reinterpret_cast<uint4*>(lds_tab + (use_tab_lds(p) ? ((p.spp + 1u) & ~1u) : 0u));
+    // kOptAccTable: (1/n, (n-1)/n) per sample of the launch, then (float)n (padded to 16 B)
+    float* lds_tab_n = reinterpret_cast<float*>(lds_tab + (use_tab_lds(p) ? ((p.spp + 1u) & ~1u) : 0u));
+    uint4* lds_cm = reinterpret_cast<uint4*>(lds_tab_n + (use_tab_lds(p) ? ((p.spp + 3u) & ~3u) : 0u));
     const bool use_tab = (OPT & kOptAccTable) && p.acc_tab;
     constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
     constexpr bool kBvh = STREAM && (OPT & kOptBvh) && (OPT & kOptPair);
@@ -739,6 +751,7 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
         for (uint32_t s = threadIdx.x; s < p.spp; s += kRenderBlock) {
             const uint64_t n = p.frame0 + s + 1;
             lds_tab[s] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
+            lds_tab_n[s] = (float)n;
         }
     }
     __syncthreads();
@@ -1082,16 +1095,17 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
             cx = 0.0f + cx;
             cy = 0.0f + cy;
             cz = 0.0f + cz;
-            const uint64_t n = p.frame0 + done + 1;
-            // (float)n of the 64-bit frame counter; when every frame of the launch fits 32 bits the
-            // 32-bit conversion is the same correctly rounded value (one v_cvt_f32_u32)
-            const float nf = p.frames32 ? (float)(uint32_t)n : (float)n;
-            float keep, rc = 0.0f;
+            float keep, nf, rc = 0.0f;
             if (use_tab) {
                 const float2 tv = lds_tab[done];
                 rc = tv.x;
                 keep = tv.y;
+                nf = lds_tab_n[done];
             } else {
+                const uint64_t n = p.frame0 + done + 1;
+                // (float)n of the 64-bit frame counter; when every frame of the launch fits 32 bits
+                // the 32-bit conversion is the same correctly rounded value (one v_cvt_f32_u32)
+                nf = p.frames32 ? (float)(uint32_t)n : (float)n;
                 keep = (p.frames32 ? (float)(uint32_t)(n - 1) : (float)(n - 1)) / nf;
             }
             acc.x = mean_term<OPT>(cx, nf, rc, use_tab) + acc.x * keep;

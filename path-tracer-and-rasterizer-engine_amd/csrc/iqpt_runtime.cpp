@@ -742,7 +742,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     // scene batch + running-mean table (padded to 16 B) + (kOptCull) one uint4 slot per thread +
     // the scatter-record stack (max_depth - 1 records per thread; one float each)
     const uint32_t lds = p.tri_batch * tri_rec + p.sph_batch * sph_rec +
-                         (p.acc_tab ? ((spp + 1u) & ~1u) * 8u : 0u) +
+                         (p.acc_tab ? ((spp + 1u) & ~1u) * 8u + ((spp + 3u) & ~3u) * 4u : 0u) +
                          ((opt & iqpt::kOptCull) ? iqpt::kRenderBlock * 16u : 0u) +
                          (uint32_t)std::max(c->max_depth, 1) * iqpt::kRenderBlock * 4u *
                              ((opt & iqpt::kOptMaterials) ? 3u : 1u);
