@@ -101,11 +101,6 @@ __device__ __forceinline__ float sqrt_any(float x) {
     return iq_sqrtf(x);
 }
 
-// dot4(v, column c of M) of iqvec::transformed (vector.h:371-383); M row-major m[r][c].
-__device__ __forceinline__ float dot_col(float x, float y, float z, float w, const float* M, int c) {
-    return ((x * M[c] + y * M[4 + c]) + z * M[8 + c]) + w * M[12 + c];
-}
-
 // normalized3 (vector.h:239-244) in place.
 template <int OPT>
 __device__ __forceinline__ void normalize3(float& x, float& y, float& z) {
@@ -144,21 +139,27 @@ __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_
     const float ys = (float)y + jy;
     const float y_ndc = 1.0f - ((OPT & kOptFastDiv) ? iq_div_pre(ys, (float)p.height, p.rcp_height)
                                                     : ys / (float)p.height) * 2.0f;
+    // rows of the inverse projection P and inverse view V (row-major m[r][c], camera.h:30-31)
     const float* P = p.inv_proj;
     const float* Vw = p.inv_view;
-    float nx = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 0);
-    float ny = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 1);
-    float nz = dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 2);
-    float fx = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 0);
-    float fy = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 1);
-    float fz = dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 2);
+    const float4 P0 = make_float4(P[0], P[1], P[2], P[3]), P1 = make_float4(P[4], P[5], P[6], P[7]);
+    const float4 P2 = make_float4(P[8], P[9], P[10], P[11]), P3 = make_float4(P[12], P[13], P[14], P[15]);
+    const float4 V0 = make_float4(Vw[0], Vw[1], Vw[2], Vw[3]), V1 = make_float4(Vw[4], Vw[5], Vw[6], Vw[7]);
+    const float4 V2 = make_float4(Vw[8], Vw[9], Vw[10], Vw[11]), V3 = make_float4(Vw[12], Vw[13], Vw[14], Vw[15]);
+    // dot4(v, column c) of iqvec::transformed (vector.h:371-383), columns spelled out
+    float nx = ((x_ndc * P0.x + y_ndc * P1.x) + 0.0f * P2.x) + 1.0f * P3.x;
+    float ny = ((x_ndc * P0.y + y_ndc * P1.y) + 0.0f * P2.y) + 1.0f * P3.y;
+    float nz = ((x_ndc * P0.z + y_ndc * P1.z) + 0.0f * P2.z) + 1.0f * P3.z;
+    float fx = ((x_ndc * P0.x + y_ndc * P1.x) + 1.0f * P2.x) + 1.0f * P3.x;
+    float fy = ((x_ndc * P0.y + y_ndc * P1.y) + 1.0f * P2.y) + 1.0f * P3.y;
+    float fz = ((x_ndc * P0.z + y_ndc * P1.z) + 1.0f * P2.z) + 1.0f * P3.z;
     float ninv, finv;
     if ((OPT & kOptCamConst) && p.cam_const) {
         ninv = p.cam_near_rw;
         finv = p.cam_far_rw;
     } else {
-        ninv = rcp_any<OPT>(dot_col(x_ndc, y_ndc, 0.0f, 1.0f, P, 3));
-        finv = rcp_any<OPT>(dot_col(x_ndc, y_ndc, 1.0f, 1.0f, P, 3));
+        ninv = rcp_any<OPT>(((x_ndc * P0.w + y_ndc * P1.w) + 0.0f * P2.w) + 1.0f * P3.w);
+        finv = rcp_any<OPT>(((x_ndc * P0.w + y_ndc * P1.w) + 1.0f * P2.w) + 1.0f * P3.w);
     }
     nx = nx * ninv;
     ny = ny * ninv;
@@ -167,12 +168,12 @@ __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_
     fy = fy * finv;
     fz = fz * finv;
     // to world space: usage POINT forces w = 1 (vector.h:374)
-    const float wnx = dot_col(nx, ny, nz, 1.0f, Vw, 0);
-    const float wny = dot_col(nx, ny, nz, 1.0f, Vw, 1);
-    const float wnz = dot_col(nx, ny, nz, 1.0f, Vw, 2);
-    const float wfx = dot_col(fx, fy, fz, 1.0f, Vw, 0);
-    const float wfy = dot_col(fx, fy, fz, 1.0f, Vw, 1);
-    const float wfz = dot_col(fx, fy, fz, 1.0f, Vw, 2);
+    const float wnx = ((nx * V0.x + ny * V1.x) + nz * V2.x) + 1.0f * V3.x;
+    const float wny = ((nx * V0.y + ny * V1.y) + nz * V2.y) + 1.0f * V3.y;
+    const float wnz = ((nx * V0.z + ny * V1.z) + nz * V2.z) + 1.0f * V3.z;
+    const float wfx = ((fx * V0.x + fy * V1.x) + fz * V2.x) + 1.0f * V3.x;
+    const float wfy = ((fx * V0.y + fy * V1.y) + fz * V2.y) + 1.0f * V3.y;
+    const float wfz = ((fx * V0.z + fy * V1.z) + fz * V2.z) + 1.0f * V3.z;
     float dx = wfx - wnx, dy = wfy - wny, dz = wfz - wnz;
     normalize3<OPT>(dx, dy, dz);
     r.ox = wnx;
