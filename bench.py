@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--verify-rows", type=int, default=16)
     ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r01_pmc_traffic.json"))
+    ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r01_c2_pmc_mix_v3.json"),
+                    help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo = rehearsal)")
     ap.add_argument("--one-device", action="store_true",
@@ -235,6 +237,15 @@ def main():
                     traffic = pmc.get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
+        valu_busy = None
+        mix_path = Path(args.pmc_mix_json)
+        if mix_path.exists():
+            try:
+                mix = json.loads(mix_path.read_text())
+                if mix.get("config") == cfg.name and world == 1:
+                    valu_busy = mix.get("valu_busy_frac")
+            except Exception:
+                valu_busy = None
         samples = cfg.width * cfg.height * spp_step * args.steps
         out = {
             "metric": "Mrays/sec at 1920x1080 8-bounce; per-pixel RMSE vs reference",
@@ -273,8 +284,12 @@ def main():
                 "kernel": iqpt.kernel_name(),
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "flops_per_ray": f_ray,
+                "valu_busy_frac": valu_busy,
                 "note": "algorithmic FLOPs F_ray = 52 T + 19 S (SURVEY.md §8d) x rays per launch / HIP-event "
-                        "kernel time; FP32 vector peak (no MFMA: nothing here is a dense contraction)"
+                        "kernel time; FP32 vector peak (no MFMA: nothing here is a dense contraction). "
+                        "valu_busy_frac: share of SIMD time with a VALU instruction in flight (PMC "
+                        "SQ_ACTIVE_INST_VALU, profiles/): the kernel is VALU-issue bound; the FLOP fraction is "
+                        "low because MT/RNG/compare instructions are not FMA-dense"
                         + ("; frac > 1: the reference's brute-force tests per ray, most of which the tile masks "
                            "and the BVH skip (DESIGN.md §5)" if achieved_tflops > FP32_PEAK_TFLOPS else ""),
             },
