@@ -55,6 +55,7 @@ struct kparams {
     float cam_near_rw, cam_far_rw;   // 1 / w_near, 1 / w_far when cam_const
     float rcp_width, rcp_height;     // RN(1 / W), RN(1 / H) (kOptFastDiv camera divisions)
     uint32_t acc_tab;                // build the per-launch (1/n, (n-1)/n) table in LDS
+    uint32_t diag;                   // kOptDiag ablation bits (A/B builds): 1 camera ray, 2 intersection, 4 mean
     uint32_t frames32;               // frame0 + spp < 2^32: 32-bit frame-counter conversions
     const float4_storage* tris;      // ntri * kTriFloat4 (single layout)
     const float4_storage* tri_pairs; // ntri_pairs * kTriPairFloat4 (pair layout)
@@ -150,6 +151,7 @@ constexpr int kOptMaterials = 1 << 10; // per-primitive material table (RGB scat
 constexpr int kOptBvh = 1 << 11;       // secondary rays traverse the exact BVH (streamed scenes; inert
                                        // when the packet has none)
 constexpr int kOptBvhPrimary = 1 << 12; // camera rays take the BVH too (instead of the tile masks)
+constexpr int kOptDiag = 1 << 13;      // A/B builds only: timing ablations selected by kparams::diag (NOT exact)
 constexpr int kOptDefault =
     kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull | kOptBvh;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)

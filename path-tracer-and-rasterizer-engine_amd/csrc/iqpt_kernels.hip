@@ -566,10 +566,11 @@ template <int OPT>
 __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntri, const float4* sph, uint32_t nsph,
                                                  const uint32_t* lane_mask, uint32_t cm_t, uint32_t cm_s, bool all,
                                                  bool active, const ray3 ray, float& closest, int& kind,
-                                                 uint32_t& hidx, uint32_t wt) {
+                                                 uint32_t& hidx, uint32_t wt, unsigned long long* st = nullptr) {
     const uint32_t tp = (ntri + 1) / 2, sp = (nsph + 1) / 2;
     for (uint32_t w = 0; w * 32u < tp; ++w) {
         uint32_t m = all ? ~0u : wave_or(lane_mask ? (w == 0 ? cm_t : lane_mask[w]) : 0u);
+        if ((OPT & kOptStats) && st) st[0] += (unsigned long long)__builtin_popcount(w * 32u + 32u <= tp ? m : (m & ((1u << (tp - w * 32u)) - 1u)));
         while (m) {
             const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
@@ -582,6 +583,7 @@ __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntr
     }
     for (uint32_t w = 0; w * 32u < sp; ++w) {
         uint32_t m = all ? ~0u : wave_or(lane_mask ? (w == 0 ? cm_s : lane_mask[wt + w]) : 0u);
+        if ((OPT & kOptStats) && st) st[1] += (unsigned long long)__builtin_popcount(w * 32u + 32u <= sp ? m : (m & ((1u << (sp - w * 32u)) - 1u)));
         while (m) {
             const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
             m &= m - 1u;
@@ -778,9 +780,30 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
     // ---- stats (kOptStats): wave-level counters
     unsigned long long s_iter = 0, s_ready = 0, s_scatter_exec = 0, s_scatter_lanes = 0, s_term_exec = 0,
                        s_term_lanes = 0;
+    unsigned long long s_tests[2] = {0, 0};   // wave-level triangle / sphere pair tests (culled resident path)
+    unsigned long long s_full = 0;            // iterations forced to the full loop (a secondary ray in the wave)
 
     // ---- wave-uniform chunk state: the current tile [chunk_next, chunk_end) of tile-major storage
     uint32_t chunk_tile = 0;
+    // pixel complete: BGRA8 (:360-365), accumulator and RNG state back to HBM
+    auto store_pixel = [&]() {
+        const uint32_t r8 = to_u8(255.0f * iq_sqrtf(acc.x));
+        const uint32_t g8 = to_u8(255.0f * iq_sqrtf(acc.y));
+        const uint32_t b8 = to_u8(255.0f * iq_sqrtf(acc.z));
+        const uint32_t pix = tile_store_index(px - p.x0, (py - p.y0) / p.ystep, p.ncols, p.nrows);
+        p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+        float* o = reinterpret_cast<float*>(p.lin + pix);          // w is never written
+        o[0] = acc.x;
+        o[1] = acc.y;
+        o[2] = acc.z;
+        p.rng[pix] = st.v0;
+        p.rng[(size_t)p.npix + pix] = st.v1;
+        p.rng[2 * (size_t)p.npix + pix] = st.v2;
+        p.rng[3 * (size_t)p.npix + pix] = st.v3;
+        p.rng[4 * (size_t)p.npix + pix] = st.v4;
+        p.rng[5 * (size_t)p.npix + pix] = st.d;
+        done = 0;
+    };
     auto refill = [&]() {
         uint64_t need = __ballot(!active);
         while (need != 0ull && !exhausted) {
@@ -959,10 +982,18 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                     }
                 }
             }
+        } else if ((OPT & kOptDiag) && (p.diag & 2u)) {
+            // diagnostic: no intersection; every ray hits triangle 0 at t = 1
+            if (active) {
+                closest = 1.0f;
+                kind = kHitTri;
+                hidx = 0;
+            }
         } else if (kCull && p.cull != nullptr) {
             const uint4 cm = lds_cm[threadIdx.x];
             intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray,
-                                  closest, kind, hidx, p.cull_wt);
+                                  closest, kind, hidx, p.cull_wt, (OPT & kOptStats) ? s_tests : nullptr);
+            if (OPT & kOptStats) s_full += cull ? 0ull : 1ull;
         } else if (active) {
             intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
         }
@@ -1109,29 +1140,22 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
                 nf = p.frames32 ? (float)(uint32_t)n : (float)n;
                 keep = (p.frames32 ? (float)(uint32_t)(n - 1) : (float)(n - 1)) / nf;
             }
-            acc.x = mean_term<OPT>(cx, nf, rc, use_tab) + acc.x * keep;
-            acc.y = mean_term<OPT>(cy, nf, rc, use_tab) + acc.y * keep;
-            acc.z = mean_term<OPT>(cz, nf, rc, use_tab) + acc.z * keep;
+            if ((OPT & kOptDiag) && (p.diag & 4u)) {
+                acc.x += cx;                     // diagnostic: no running-mean arithmetic
+            } else {
+                acc.x = mean_term<OPT>(cx, nf, rc, use_tab) + acc.x * keep;
+                acc.y = mean_term<OPT>(cy, nf, rc, use_tab) + acc.y * keep;
+                acc.z = mean_term<OPT>(cz, nf, rc, use_tab) + acc.z * keep;
+            }
             ++done;
             depth = 0;
             if (done == p.spp) {
-                // pixel complete: BGRA8 (:360-365), accumulator and RNG state back to HBM
-                const uint32_t r8 = to_u8(255.0f * iq_sqrtf(acc.x));
-                const uint32_t g8 = to_u8(255.0f * iq_sqrtf(acc.y));
-                const uint32_t b8 = to_u8(255.0f * iq_sqrtf(acc.z));
-                const uint32_t pix = tile_store_index(px - p.x0, (py - p.y0) / p.ystep, p.ncols, p.nrows);
-                p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
-                float* o = reinterpret_cast<float*>(p.lin + pix);          // w is never written
-                o[0] = acc.x;
-                o[1] = acc.y;
-                o[2] = acc.z;
-                p.rng[pix] = st.v0;
-                p.rng[(size_t)p.npix + pix] = st.v1;
-                p.rng[2 * (size_t)p.npix + pix] = st.v2;
-                p.rng[3 * (size_t)p.npix + pix] = st.v3;
-                p.rng[4 * (size_t)p.npix + pix] = st.v4;
-                p.rng[5 * (size_t)p.npix + pix] = st.d;
+                store_pixel();
                 active = false;
+            } else if ((OPT & kOptDiag) && (p.diag & 1u)) {
+                // diagnostic (timing ablation, not the reference): keep the RNG draws, reuse the ray
+                ray.dx += 1e-7f * (float)xorwow_next(st);
+                ray.dy += 1e-7f * (float)xorwow_next(st);
             } else {
                 camera_ray<OPT>(p, px, py, st, ray);
             }
@@ -1154,6 +1178,9 @@ __global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_
             atomicAdd(p.stats + 5, s_term_exec);
             atomicAdd(p.stats + 6, s_term_lanes);
             atomicAdd(p.stats + 7, 1ull);
+            atomicAdd(p.stats + 8, s_tests[0]);
+            atomicAdd(p.stats + 9, s_tests[1]);
+            atomicAdd(p.stats + 10, s_full);
         }
     }
 }
@@ -1353,6 +1380,7 @@ const variant kVariants[] = {
     IQPT_V(8, true, kOptDefault & ~kOptCull),
     IQPT_V(8, false, kOptDefault & ~kOptCull & ~kOptFastDiv),
     IQPT_V(8, true, kOptDefault & ~kOptBvh),
+    IQPT_V(8, false, kOptDefault | kOptDiag),
     IQPT_V(8, true, (kOptDefault | kOptMaterials) & ~kOptBvh),
 #endif
 };

@@ -118,6 +118,7 @@ struct iqpt_ctx {
     // the first two launches after a packet upload time faster per sample (results are identical);
     // tools/ab_kernel.py fixes the option set instead (opt_fixed)
     bool opt_fixed = false;
+    uint32_t diag = 0;           // kOptDiag ablation bits (tools/ab_kernel.py)
     int tune_stage = 0;          // 0: next launch times masks, 1: times the BVH, 2: decide, 3: decided
     bool tune_primary = false;
     hipEvent_t tune_ev[4] = {nullptr, nullptr, nullptr, nullptr};
@@ -690,6 +691,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     std::memcpy(p.inv_view, c->cam.inv_view, sizeof p.inv_view);
     cam_constants(c->cam, &p.cam_const, &p.cam_near_rw, &p.cam_far_rw);
     p.acc_tab = spp <= iqpt::kAccTableMax ? 1u : 0u;
+    p.diag = c->diag;
     p.frames32 = (c->frame + (uint64_t)spp) < (1ull << 32) ? 1u : 0u;
     p.tris = c->d_tris;
     p.tri_pairs = c->d_tri_pairs;
@@ -1019,6 +1021,13 @@ int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
     return IQPT_OK;
 }
 
+/* Internal (tools/ab_kernel.py): kOptDiag timing ablations (A/B builds; results are not the reference's). */
+int iqpt_debug_set_diag(iqpt_ctx* c, uint32_t bits) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->diag = bits;
+    return IQPT_OK;
+}
+
 /* Internal (tools/ab_kernel.py): select the kernel option mask of a context and read the
  * diagnostic counters of kOptStats variants. Not part of include/iqpt.h. */
 int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
@@ -1028,9 +1037,9 @@ int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
     int st = use_device(c);
     if (st) return st;
     if ((opt & iqpt::kOptStats) && !c->d_stats) {
-        if (hipMalloc(&c->d_stats, 8 * sizeof(unsigned long long)) != hipSuccess)
+        if (hipMalloc(&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess)
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "stats");
-        IQPT_HIP(hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
+        IQPT_HIP(hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));
     }
     c->opt = opt;
     c->opt_fixed = true;
@@ -1111,17 +1120,18 @@ int iqpt_debug_libm(int fn, const float* a, const float* b, float* out, uint64_t
     return st;
 }
 
-int iqpt_debug_read_stats(iqpt_ctx* c, unsigned long long* out8) {
+int iqpt_debug_read_stats(iqpt_ctx* c, unsigned long long* out16) {
+    unsigned long long* out8 = out16;   // 16 counters (tools/ab_kernel.py)
     if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     int st = use_device(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     if (!c->d_stats) {
-        std::memset(out8, 0, 8 * sizeof(unsigned long long));
+        std::memset(out8, 0, 16 * sizeof(unsigned long long));
         return IQPT_OK;
     }
-    IQPT_HIP(hipMemcpy(out8, c->d_stats, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    IQPT_HIP(hipMemset(c->d_stats, 0, 8 * sizeof(unsigned long long)));
+    IQPT_HIP(hipMemcpy(out8, c->d_stats, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    IQPT_HIP(hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));
     return IQPT_OK;
 }
 

@@ -41,6 +41,7 @@ def main():
     lib = _lib.load()
     lib.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
     lib.iqpt_debug_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    lib.iqpt_debug_set_diag.argtypes = [C.c_void_p, C.c_uint32]
     import iqpt
     from iqpt.scene import CONFIGS
     cfg = CONFIGS[args.config]
@@ -63,8 +64,16 @@ def main():
     variants = {"default": DEFAULT, "none": 0, "-cull": DEFAULT & ~512, "-fastdiv": DEFAULT & ~256,
                 "-pair": DEFAULT & ~4, "-sincos": DEFAULT & ~32,
                 "-bvh": DEFAULT & ~2048}
+    diag = {}
     if args.variants:
-        variants = {kv.split("=")[0]: int(kv.split("=")[1], 0) for kv in args.variants.split(",")}
+        # name=optmask or name=optmask#d (d: kOptDiag timing-ablation bits, iqpt_debug_set_diag)
+        variants = {}
+        for kv in args.variants.split(","):
+            name, val = kv.split("=")
+            if "#" in val:
+                val, dbits = val.split("#")
+                diag[name] = int(dbits)
+            variants[name] = int(val, 0)
     ps = None
     if args.crop:
         x0, x1, y0, ys, nr = (int(v) for v in args.crop.split(","))
@@ -85,6 +94,8 @@ def main():
     for name, opt in list(variants.items()):
         pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
         st = lib.iqpt_debug_set_kernel_options(pt.handle, opt)
+        if st == 0 and name in diag:
+            st = lib.iqpt_debug_set_diag(pt.handle, diag[name])
         if st != 0:
             print(f"skip {name}: {lib.iqpt_last_error().decode()}", file=sys.stderr)
             pt.close()
@@ -130,13 +141,16 @@ def main():
             print("stats variant unavailable:", e, file=sys.stderr)
             spp = 0
     if spp:
-        s = (C.c_ulonglong * 8)()
+        s = (C.c_ulonglong * 16)()
         lib.iqpt_debug_read_stats(pt.handle, s)
-        it, ready, active, sc_ex, sc_l, t_ex, t_l, waves = list(s)
+        it, ready, active, sc_ex, sc_l, t_ex, t_l, waves = list(s)[:8]
+        tri_tests, sph_tests, full_iters = list(s)[8:11]
         stats = {"opt": stats_opt, "waves": waves, "iterations": it, "ready_lane_frac": ready / max(1, it * 64),
                  "active_lane_frac": active / max(1, it * 64), "scatter_exec_per_iter": sc_ex / max(1, it),
                  "scatter_lanes_per_exec": sc_l / max(1, sc_ex), "term_exec_per_iter": t_ex / max(1, it),
-                 "term_lanes_per_exec": t_l / max(1, t_ex), "rays": pt.rays()}
+                 "term_lanes_per_exec": t_l / max(1, t_ex), "rays": pt.rays(),
+                 "tri_pair_tests_per_iter": tri_tests / max(1, it), "sph_pair_tests_per_iter": sph_tests / max(1, it),
+                 "full_loop_iter_frac": full_iters / max(1, it)}
     out = {"config": cfg.name, "spp": spp, "rounds": args.rounds, "variants": res, "stats_default": stats}
     print(json.dumps(out, indent=1))
     if args.out:
