@@ -53,8 +53,10 @@ inline double gamma_n(int n) { return n * kU / (1.0 - n * kU); }
 
 struct tri_coeffs {
     bool eligible;        // R <= 1/4: may go into the BVH
-    double gA, gB;        // per-axis growth of the triangle's box: gA + gB S
+    double gA, gB;        // per-axis growth of the triangle's box: gA + gB S (= gR + gC + gB S)
+    double gR, gC;        // the parts of gA that scale with 1/D (normal cones) and that do not
     double tA, tB;        // |t^ - t| <= tA S + tB |t|   (t <= closest during traversal)
+    double edet;          // safety x E_det: |det^ - det| (normal cones, below)
 };
 
 // e1, e2: the kernel's world-space edges; Md: bound on |d_i| (normalized directions: 1 + a few ulp).
@@ -72,17 +74,46 @@ inline tri_coeffs triangle_coeffs(const float e1[3], const float e2[3], double M
     tri_coeffs c;
     c.eligible = std::isfinite(R) && R <= 0.25 && std::isfinite(M1) && std::isfinite(M2);
     if (!c.eligible) {
-        c.gA = c.gB = c.tA = c.tB = INFINITY;
+        c.gA = c.gB = c.gR = c.gC = c.tA = c.tB = INFINITY;
         return c;
     }
     // Du = du0 + du1 S, Dv = dv0 + dv1 S; delta = 3 (Du + Dv + 4u) (M1 + M2)
     const double d0 = kSafety * (R + 2.0 * g2) / (1.0 - R);
     const double du1 = kSafety * (E_u1 / kDetMin) / (1.0 - R), dv1 = kSafety * (E_v1 / kDetMin) / (1.0 - R);
     c.gA = 3.0 * (2.0 * d0 + 4.0 * kU) * (M1 + M2);
+    c.gR = 3.0 * (2.0 * kSafety * R / (1.0 - R)) * (M1 + M2);
+    c.gC = 3.0 * (4.0 * kSafety * g2 / (1.0 - R) + 4.0 * kU) * (M1 + M2);
     c.gB = 3.0 * (du1 + dv1) * (M1 + M2);
     c.tA = kSafety * (E_t1 / kDetMin) / (1.0 - R);
     c.tB = kSafety * (R + 4.0 * g2) / (1.0 - R);
+    c.edet = kSafety * E_det;
     return c;
+}
+
+// Normal cones (tightening for non-grazing rays). Every bound above divides an error by the smallest
+// determinant an accepted hit can have, priced at the reject threshold 1e-6. For a given ray a larger
+// lower bound D is often known: det = e1 . (d x e2) = -d . n with n = e1 x e2, so if the normals of a
+// node's triangles lie (as lines) within angle beta of an axis a and |n| >= Nmin, then
+// |det^| >= Nmin |d| cos(theta + beta) - E_det with theta = angle(d, a) (when theta + beta < 90 deg).
+// With lambda = 1e-6 / max(1e-6, D) <= 1 the bounds become
+//   growth <= lambda (gR + gB S) + gC,   |t^ - t| <= lambda tA S + tB |t|
+// (R, Du, Dv and the t error scale with 1/D; gC and tB hold the D-independent remainders — gC is a
+// few ulp of the triangle size and is applied as one scene-wide maximum).
+// Triangles that no ray can accept (|n| sqrt(3) Md + E_det < 1e-6) do not constrain a cone.
+struct tri_normal {
+    double n[3];          // e1 x e2 (exact in double up to one rounding per component)
+    double len;           // |n|
+    bool hittable;
+};
+
+inline tri_normal triangle_normal(const float e1[3], const float e2[3], double Md, double edet) {
+    tri_normal t;
+    t.n[0] = (double)e1[1] * e2[2] - (double)e1[2] * e2[1];
+    t.n[1] = (double)e1[2] * e2[0] - (double)e1[0] * e2[2];
+    t.n[2] = (double)e1[0] * e2[1] - (double)e1[1] * e2[0];
+    t.len = std::sqrt(t.n[0] * t.n[0] + t.n[1] * t.n[1] + t.n[2] * t.n[2]);
+    t.hittable = t.len * std::sqrt(3.0) * Md + edet >= kDetMin;
+    return t;
 }
 
 // Node of the stackless (threaded) BVH, DFS preorder: a box and the index of the next node after the
@@ -92,14 +123,22 @@ struct node {
     uint32_t skip;
     float bmax[3];
     uint32_t first_count;   // leaf: first pair << 8 | pair count (count 1..255); inner: 0
-    float gA, gB, tA, tB;   // maxima of the subtree's triangle coefficients (rounded up)
+    float gR, gB, tA, tB;   // maxima of the subtree's triangle coefficients (rounded up)
+    float axis[3];          // normal cone of the hittable triangles (float axis, |axis| ~ 1)
+    float cos_beta;         // rounded down; 0 = no useful cone
+    float sin_beta;         // rounded up
+    float nmin;             // min |e1 x e2| over hittable triangles, rounded down
+    float edet;             // max safety x E_det, rounded up
+    float pad;
 };
-static_assert(sizeof(node) == 48, "node is three float4");
+static_assert(sizeof(node) == 80, "node is five float4");
 
 struct build_input {
     std::vector<float> lo, hi;       // 3 per triangle: tight vertex box, rounded outward
     std::vector<float> centroid;     // 3 per triangle
-    std::vector<float> coeff;        // 4 per triangle: gA, gB, tA, tB rounded up
+    std::vector<float> coeff;        // 4 per triangle: gR, gB, tA, tB rounded up
+    std::vector<tri_normal> normal;  // per triangle
+    std::vector<double> edet;        // per triangle
     std::vector<uint32_t> tris;      // triangle indices in the BVH (packet order)
 };
 
@@ -146,10 +185,55 @@ inline void build(build_input& in, build_output& out) {
             }
             for (int q = 0; q < 4; ++q) co[q] = std::max(co[q], in.coeff[4 * t + q]);
         }
-        n.gA = co[0];
+        n.gR = co[0];
         n.gB = co[1];
         n.tA = co[2];
         n.tB = co[3];
+        // normal cone (as lines) of the hittable triangles
+        n.axis[0] = 1.0f;
+        n.axis[1] = n.axis[2] = 0.0f;
+        n.cos_beta = 0.0f;
+        n.sin_beta = 1.0f;
+        n.nmin = 0.0f;
+        n.edet = 0.0f;
+        n.pad = 0.0f;
+        double sum[3] = {0.0, 0.0, 0.0}, ref[3] = {0.0, 0.0, 0.0}, nmin = INFINITY, edet = 0.0;
+        bool have_ref = false;
+        for (uint32_t i = b; i < e; ++i) {
+            const uint32_t t = idx[i];
+            edet = std::max(edet, in.edet[t]);
+            const tri_normal& tn = in.normal[t];
+            if (!tn.hittable) continue;
+            nmin = std::min(nmin, tn.len);
+            const double u[3] = {tn.n[0] / tn.len, tn.n[1] / tn.len, tn.n[2] / tn.len};
+            if (!have_ref) {
+                for (int a = 0; a < 3; ++a) ref[a] = u[a];
+                have_ref = true;
+            }
+            const double sg = (u[0] * ref[0] + u[1] * ref[1] + u[2] * ref[2]) < 0.0 ? -1.0 : 1.0;
+            for (int a = 0; a < 3; ++a) sum[a] += sg * u[a];
+        }
+        const double sl = std::sqrt(sum[0] * sum[0] + sum[1] * sum[1] + sum[2] * sum[2]);
+        if (have_ref && sl > 1e-3 && std::isfinite(nmin)) {
+            float af[3];
+            for (int a = 0; a < 3; ++a) af[a] = (float)(sum[a] / sl);
+            const double al = std::sqrt((double)af[0] * af[0] + (double)af[1] * af[1] + (double)af[2] * af[2]);
+            double cmin = 1.0;
+            for (uint32_t i = b; i < e; ++i) {
+                const tri_normal& tn = in.normal[idx[i]];
+                if (!tn.hittable) continue;
+                const double c = std::fabs(tn.n[0] * af[0] + tn.n[1] * af[1] + tn.n[2] * af[2]) / (tn.len * al);
+                cmin = std::min(cmin, c);
+            }
+            cmin = std::min(1.0, cmin * (1.0 - 1e-12)) - 1e-12;
+            if (cmin > 0.0) {
+                for (int a = 0; a < 3; ++a) n.axis[a] = af[a];
+                n.cos_beta = round_down(cmin);
+                n.sin_beta = round_up(std::min(1.0, std::sqrt(std::max(0.0, 1.0 - cmin * cmin)) * (1.0 + 1e-12) + 1e-12));
+                n.nmin = round_down(nmin * (1.0 - 1e-12));
+            }
+        }
+        n.edet = round_up(edet);
         n.skip = 0;
         n.first_count = 0;
         out.nodes.push_back(n);

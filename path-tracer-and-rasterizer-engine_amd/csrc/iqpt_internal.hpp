@@ -32,6 +32,7 @@ struct alignas(16) float4_storage {
 //  * spheres: (center.xyz, radius) float4, and sphere pairs 2 x float4 = 32 B:
 //      (cx_a, cx_b, cy_a, cy_b), (cz_a, cz_b, r_a, r_b).
 constexpr int kTriFloat4 = 3;
+constexpr int kBvhNodeFloat4 = 5;
 constexpr int kTriPairFloat4 = 5;
 constexpr int kSphPairFloat4 = 2;
 // Shading record per triangle (only read for the closest hit): world normals n0, n1, n2 and the
@@ -87,8 +88,9 @@ struct kparams {
     const uint32_t* sph_mat;
     const float4_storage* mats;
     const float4_storage* tri_shade;
-    // exact BVH for secondary rays (iq_bvh.hpp; streamed scenes): nodes (3 x float4: tight box min +
-    // skip, box max + leaf first pair << 8 | count, error coefficients gA gB tA tB), leaf triangle
+    // exact BVH for secondary rays (iq_bvh.hpp; streamed scenes): nodes (kBvhNodeFloat4 x float4:
+    // tight box min + skip, box max + leaf first pair << 8 | count, error coefficients gA gB tA tB,
+    // normal-cone axis + cos beta, (sin beta, Nmin, E_det, -)), leaf triangle
     // pairs (kTriPairFloat4 each) with their packet indices (uint2; ~0u pads), triangles outside the
     // BVH (tested by every ray); the bound holds for |d_i| <= md and a finite origin; gulp covers the
     // rounding of a grown box side

@@ -661,15 +661,33 @@ __device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, floa
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh_nodes);
     const float4* __restrict__ pairs = reinterpret_cast<const float4*>(p.bvh_pairs);
     const float ix = 1.0f / r.dx, iy = 1.0f / r.dy, iz = 1.0f / r.dz;
-    const float slack = 8.0f * 0x1p-24f, up = 1.0f + 0x1p-20f;
+    const float slack = 8.0f * 0x1p-24f, up = 1.0f + 0x1p-20f, up16 = 1.0f + 0x1p-16f;
+    // |d|^2 and |d|, rounded up (normal cones)
+    const float dd = ((r.dx * r.dx + r.dy * r.dy) + r.dz * r.dz) * up16;
+    const float dl = __builtin_sqrtf(dd) * up16;
     uint32_t i = 0;
     while (i < p.bvh_nnodes) {
-        const float4 lo = nodes[3 * (size_t)i], hi = nodes[3 * (size_t)i + 1], co = nodes[3 * (size_t)i + 2];
+        const float4* nd = nodes + (size_t)kBvhNodeFloat4 * i;
+        const float4 lo = nd[0], hi = nd[1], co = nd[2], cone = nd[3], cone2 = nd[4];
         const float sx = fmaxf(iq_fabsf(r.ox - lo.x), iq_fabsf(r.ox - hi.x));
         const float sy = fmaxf(iq_fabsf(r.oy - lo.y), iq_fabsf(r.oy - hi.y));
         const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
         const float S = fmaxf(fmaxf(sx, sy), sz) * up;
-        const float g = (co.x + co.y * S) * up + p.bvh_gulp;
+        // lambda = 1e-6 / D, D a lower bound of |det^| over the node's triangles for this ray
+        // (iq_bvh.hpp normal cones): |d| cos(theta + beta) from the cone, every step rounded toward
+        // a smaller D; an unusable cone (cos beta = 0) or a grazing ray leaves lambda = 1
+        float lambda = 1.0f;
+        if (cone.w > 0.0f) {
+            const float c = iq_fabsf((r.dx * cone.x + r.dy * cone.y) + r.dz * cone.z);
+            const float c_lo = fmaxf(0.0f, c * (1.0f - 0x1p-16f) - 0x1p-20f * dl);
+            // |d| sin(theta) <= sqrt(dd - c_lo^2); the subtraction's rounding (<= 2u dd) is covered by
+            // adding 2^-20 dd before the root
+            const float s_hi = __builtin_sqrtf(fmaxf(0.0f, dd - c_lo * c_lo) + 0x1p-20f * dd) * up16;
+            const float cos_lo = (c_lo * cone.w) * (1.0f - 0x1p-16f) - (s_hi * cone2.x) * up16;
+            const float D = (cos_lo * cone2.y) * (1.0f - 0x1p-16f) - cone2.z * up16;
+            if (D > 1e-6f) lambda = fminf(1.0f, (1e-6f * __builtin_amdgcn_rcpf(D)) * up16);
+        }
+        const float g = (lambda * (co.x + co.y * S)) * up + p.bvh_gulp;   // gulp includes gC
         // per axis [t0, t1] of the slab; a NaN (0 * inf: origin on a slab plane of an axis-parallel
         // ray) widens that axis to everything
         float t0x = ((lo.x - g) - r.ox) * ix, t1x = ((hi.x + g) - r.ox) * ix;
@@ -682,7 +700,7 @@ __device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, floa
         if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
         if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
         // computed slab bounds are within 3 ulp (relative) of the exact ones: widen by 8 ulp
-        const float dt = (co.z * S + co.w * closest) * up;
+        const float dt = ((lambda * co.z) * S + co.w * closest) * up;
         float enter = fmaxf(fmaxf(ax0, ay0), az0), exit = fminf(fminf(ax1, ay1), az1);
         enter = enter - iq_fabsf(enter) * slack;
         exit = exit + iq_fabsf(exit) * slack;
@@ -715,13 +733,14 @@ __device__ __forceinline__ bool use_tab_lds(const kparams& p) { return p.acc_tab
 // ------------------------------------------------------------------------------------------------
 // The megakernel. MAXD bounds max_depth (variant selection; the scatter stack lives in LDS); STREAM selects LDS batch streaming
 // (scene larger than the resident budget) with workgroup-uniform iteration; OPT is the kOpt* mask.
-template <int OPT>
+template <int OPT, bool STREAM>
 constexpr int min_waves_per_simd() {
-    return (OPT & kOptLB6) ? 6 : ((OPT & kOptLB5) ? 5 : 1);
+    // streamed variants (BVH traversal) are held to 4 waves/SIMD (<= 128 VGPRs)
+    return (OPT & kOptLB6) ? 6 : ((OPT & kOptLB5) ? 5 : (STREAM ? 4 : 1));
 }
 
 template <int MAXD, bool STREAM, int OPT>
-__global__ __launch_bounds__(kRenderBlock, min_waves_per_simd<OPT>()) void iqpt_render_kernel(const kparams p) {
+__global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) void iqpt_render_kernel(const kparams p) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     constexpr bool kPair = (OPT & kOptPair) != 0;
     constexpr int kTriRec = kPair ? kTriPairFloat4 : kTriFloat4;   // float4 per LDS record

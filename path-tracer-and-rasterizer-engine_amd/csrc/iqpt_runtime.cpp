@@ -282,7 +282,7 @@ bool build_bvh(const std::vector<float4_storage>& tris, const std::vector<float4
     out.md = 1.001f;
     // a box side lo - g rounds to nearest: |error| <= 2^-24 (maxabs + g); the kernel adds gulp and
     // scales g by 1 + 2^-20, which covers it
-    out.gulp = iqbvh::round_up(maxabs * 0x1p-22);
+    double gc_max = 0.0;
     iqbvh::build_input in;
     for (size_t k = 0; k < ntri; ++k) {
         const float4_storage* t = &tris[k * iqpt::kTriFloat4];
@@ -299,10 +299,15 @@ bool build_bvh(const std::vector<float4_storage>& tris, const std::vector<float4
             in.hi.push_back(iqbvh::round_up(hi));
             in.centroid.push_back((float)((lo + hi) * 0.5));
         }
-        const double co[4] = {b.gA, b.gB, b.tA, b.tB};
+        const double co[4] = {b.gR, b.gB, b.tA, b.tB};
+        gc_max = std::max(gc_max, b.gC);
         for (double v : co) in.coeff.push_back(iqbvh::round_up(v));
+        in.normal.push_back(iqbvh::triangle_normal(e1, e2, Md, b.edet));
+        in.edet.push_back(b.edet);
         in.tris.push_back((uint32_t)k);
     }
+    // the D-independent part of the growth (gC) is applied as one scene-wide maximum
+    out.gulp = iqbvh::round_up(maxabs * 0x1p-22 + gc_max);
     iqbvh::build_output bo;
     iqbvh::build(in, bo);
     for (const iqbvh::node& n : bo.nodes) {
@@ -317,7 +322,9 @@ bool build_bvh(const std::vector<float4_storage>& tris, const std::vector<float4
         std::memcpy(&hi.w, &n.first_count, 4);
         out.nodes.push_back(lo);
         out.nodes.push_back(hi);
-        out.nodes.push_back(float4_storage{n.gA, n.gB, n.tA, n.tB});
+        out.nodes.push_back(float4_storage{n.gR, n.gB, n.tA, n.tB});
+        out.nodes.push_back(float4_storage{n.axis[0], n.axis[1], n.axis[2], n.cos_beta});
+        out.nodes.push_back(float4_storage{n.sin_beta, n.nmin, n.edet, 0.0f});
     }
     // leaf pairs in the kernel's pair layout (iqpt_internal.hpp), padding elements zero
     const size_t npairs = bo.order.size() / 2;
@@ -656,7 +663,7 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         return st;
     }
     if (have_bvh) {
-        c->bvh_nnodes = (uint32_t)(bvh.nodes.size() / 3);
+        c->bvh_nnodes = (uint32_t)(bvh.nodes.size() / iqpt::kBvhNodeFloat4);
         c->bvh_nalways = (uint32_t)bvh.always.size();
         c->bvh_md = bvh.md;
         c->bvh_gulp = bvh.gulp;
@@ -1085,13 +1092,17 @@ int iqpt_debug_bvh_info(iqpt_ctx* c, uint32_t* nnodes, uint32_t* nalways) {
 }
 
 /* Internal (tests/test_bvh.py): the error bound of iq_bvh.hpp for one triangle's edges, evaluated
- * at S = max_i |o_i - v0_i|. out: box growth, dt_a, dt_b (|t^ - t| <= dt_a + dt_b |t|). Returns 1 if the triangle is BVH-eligible, 0 if not. */
-int iqpt_debug_bvh_bound(const float* e1, const float* e2, double S, double Md, double* out3) {
-    if (!e1 || !e2 || !out3) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+ * at S = max_i |o_i - v0_i| and a lower bound D of the accepted determinant (D <= 1e-6: the reject
+ * threshold). out: box growth, dt_a, dt_b (|t^ - t| <= dt_a + dt_b |t|), safety x E_det. Returns 1 if
+ * the triangle is BVH-eligible, 0 if not. */
+int iqpt_debug_bvh_bound(const float* e1, const float* e2, double S, double Md, double D, double* out4) {
+    if (!e1 || !e2 || !out4) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     const iqbvh::tri_coeffs b = iqbvh::triangle_coeffs(e1, e2, Md);
-    out3[0] = b.gA + b.gB * S;
-    out3[1] = b.tA * S;
-    out3[2] = b.tB;
+    const double lambda = D > iqbvh::kDetMin ? iqbvh::kDetMin / D : 1.0;
+    out4[0] = lambda * (b.gR + b.gB * S) + b.gC;
+    out4[1] = lambda * b.tA * S;
+    out4[2] = b.tB;
+    out4[3] = b.edet;
     return b.eligible ? 1 : 0;
 }
 

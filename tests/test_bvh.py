@@ -24,15 +24,21 @@ T_MIN = np.float32(0.000001)
 FLT_MAX = np.float32(3.4028235e38)
 
 
-def bound(e1, e2, S, Md=1.001):
+def bound(e1, e2, S, Md=1.001, D=0.0):
+    """(eligible, [growth, dt_a, dt_b]) of iq_bvh.hpp at distance S and determinant lower bound D."""
+    ok, out = bound4(e1, e2, S, Md, D)
+    return ok, out[:3]
+
+
+def bound4(e1, e2, S, Md=1.001, D=0.0):
     lib = _lib.load()
     f = lib.iqpt_debug_bvh_bound
-    f.argtypes = [FP, FP, C.c_double, C.c_double, DP]
+    f.argtypes = [FP, FP, C.c_double, C.c_double, C.c_double, DP]
     f.restype = C.c_int
     e1 = np.ascontiguousarray(e1, np.float32)
     e2 = np.ascontiguousarray(e2, np.float32)
-    out = np.zeros(3)
-    ok = f(e1.ctypes.data_as(FP), e2.ctypes.data_as(FP), S, Md, out.ctypes.data_as(DP))
+    out = np.zeros(4)
+    ok = f(e1.ctypes.data_as(FP), e2.ctypes.data_as(FP), S, Md, D, out.ctypes.data_as(DP))
     return ok == 1, out
 
 
@@ -102,12 +108,20 @@ def test_accepted_hits_lie_inside_the_grown_box(seed):
         e2o = ((v0 + e2).astype(np.float32) - v0).astype(np.float32)
         ok2, (delta, dta, dtb) = bound(e1o, e2o, S)
         assert ok2
+        # the normal-cone form: the same bound priced at this ray's own determinant lower bound
+        n = np.cross(e1o.astype(np.float64), e2o.astype(np.float64))
+        _, (_, _, _, edet) = bound4(e1o, e2o, S)
+        D = abs(float(np.dot(d.astype(np.float64), n))) - edet
+        _, (delta_c, dta_c, dtb_c) = bound(e1o, e2o, S, D=D)
         te, ue, ve = exact_solution(v0, e1o, e2o, o, d)
         P = o.astype(np.float64) + te * d.astype(np.float64)
         corners = np.stack([v0, v0 + e1o.astype(np.float64), v0 + e2o.astype(np.float64)])
         lo, hi = corners.min(axis=0) - delta, corners.max(axis=0) + delta
         assert np.all(P >= lo) and np.all(P <= hi), (P, lo, hi, delta, ue, ve)
         assert abs(that - te) <= dta + dtb * abs(that), (that, te, dta, dtb)
+        lo, hi = corners.min(axis=0) - delta_c, corners.max(axis=0) + delta_c
+        assert np.all(P >= lo) and np.all(P <= hi), (P, lo, hi, delta_c, D)
+        assert abs(that - te) <= dta_c + dtb_c * abs(that), (that, te, dta_c, dtb_c, D)
         checked += 1
         det = abs(np.dot(e1o.astype(np.float64), np.cross(d.astype(np.float64), e2o.astype(np.float64))))
         grazing += det < 1e-5
@@ -122,3 +136,6 @@ def test_large_triangles_are_kept_out_of_the_bvh():
     assert ok and d1 < 0.02             # C5's small mesh triangles, seen from 1 unit away
     _, (d2, a2, b2) = bound(e1, e2, 2.0)
     assert d2 > d1 and a2 == pytest.approx(2 * a1) and b2 == b1     # linear in S
+    # a ray meeting the triangle at 60 deg from its plane: |det| ~ 1.3e-4, the bound shrinks ~100x
+    _, (d3, a3, _) = bound(e1, e2, 1.0, D=1.3e-4)
+    assert d3 < d1 / 50 and a3 < a1 / 50
