@@ -650,70 +650,103 @@ __device__ __forceinline__ bool bvh_ray_ok(const kparams& p, const ray3& r) {
            iq_fabsf(r.dx) <= p.bvh_md && iq_fabsf(r.dy) <= p.bvh_md && iq_fabsf(r.dz) <= p.bvh_md;
 }
 
-// Closest triangle for one ray through the exact BVH (iq_bvh.hpp): the stackless DFS visits a node
-// when the segment t in [t_min - dt, closest + dt] meets its box grown by gA + gB S, where S bounds
-// the origin's distance to the node's vertices and dt = tA S + tB closest (each rounded up by a
-// factor 1 + 2^-20, the box side by gulp more); the slab test is widened by 8 ulp, more than its own
-// rounding. Leaves are tested with the reference's own Möller–Trumbore; the triangles left out of
-// the BVH are tested afterwards.
+// Per-ray constants of the BVH node test.
+struct bvh_ray {
+    float ix, iy, iz;    // 1 / d (IEEE)
+    float dd, dl;        // |d|^2 and |d|, rounded up (normal cones)
+};
+
+__device__ __forceinline__ bvh_ray bvh_ray_setup(const ray3 r) {
+    const float up16 = 1.0f + 0x1p-16f;
+    bvh_ray b;
+    b.ix = 1.0f / r.dx;
+    b.iy = 1.0f / r.dy;
+    b.iz = 1.0f / r.dz;
+    b.dd = ((r.dx * r.dx + r.dy * r.dy) + r.dz * r.dz) * up16;
+    b.dl = __builtin_sqrtf(b.dd) * up16;
+    return b;
+}
+
+// Box test of node i (iq_bvh.hpp): the segment t in [t_min - dt, closest + dt] against the node's box
+// grown by lambda (gR + gB S) + gC, where S bounds the origin's distance to the node's vertices,
+// lambda = 1e-6 / D comes from the node's normal cone and dt = lambda tA S + tB closest (each rounded
+// up by 1 + 2^-20, the box side by gulp more); the slab test is widened by 8 ulp, more than its own
+// rounding. Returns the widened entry parameter and the closest-independent part of dt.
+__device__ __forceinline__ bool bvh_node_test(const kparams& p, const float4* __restrict__ nodes, uint32_t i,
+                                              const ray3 r, const bvh_ray br, float closest, float& enter_out,
+                                              float& dtc_out) {
+    const float slack = 8.0f * 0x1p-24f, up = 1.0f + 0x1p-20f, up16 = 1.0f + 0x1p-16f;
+    const float4* nd = nodes + (size_t)kBvhNodeFloat4 * i;
+    const float4 lo = nd[0], hi = nd[1], co = nd[2], cone = nd[3], cone2 = nd[4];
+    const float sx = fmaxf(iq_fabsf(r.ox - lo.x), iq_fabsf(r.ox - hi.x));
+    const float sy = fmaxf(iq_fabsf(r.oy - lo.y), iq_fabsf(r.oy - hi.y));
+    const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
+    const float S = fmaxf(fmaxf(sx, sy), sz) * up;
+    // lambda = 1e-6 / D, D a lower bound of |det^| over the node's triangles for this ray
+    // (iq_bvh.hpp normal cones): |d| cos(theta + beta) from the cone, every step rounded toward
+    // a smaller D; an unusable cone (cos beta = 0) or a grazing ray leaves lambda = 1
+    float lambda = 1.0f;
+    if (cone.w > 0.0f) {
+        const float c = iq_fabsf((r.dx * cone.x + r.dy * cone.y) + r.dz * cone.z);
+        const float c_lo = fmaxf(0.0f, c * (1.0f - 0x1p-16f) - 0x1p-20f * br.dl);
+        // |d| sin(theta) <= sqrt(dd - c_lo^2); the subtraction's rounding (<= 2u dd) is covered by
+        // adding 2^-20 dd before the root
+        const float s_hi = __builtin_sqrtf(fmaxf(0.0f, br.dd - c_lo * c_lo) + 0x1p-20f * br.dd) * up16;
+        const float cos_lo = (c_lo * cone.w) * (1.0f - 0x1p-16f) - (s_hi * cone2.x) * up16;
+        const float D = (cos_lo * cone2.y) * (1.0f - 0x1p-16f) - cone2.z * up16;
+        if (D > 1e-6f) lambda = fminf(1.0f, (1e-6f * __builtin_amdgcn_rcpf(D)) * up16);
+    }
+    const float g = (lambda * (co.x + co.y * S)) * up + p.bvh_gulp;   // gulp includes gC
+    // per axis [t0, t1] of the slab; a NaN (0 * inf: origin on a slab plane of an axis-parallel
+    // ray) widens that axis to everything
+    float t0x = ((lo.x - g) - r.ox) * br.ix, t1x = ((hi.x + g) - r.ox) * br.ix;
+    float t0y = ((lo.y - g) - r.oy) * br.iy, t1y = ((hi.y + g) - r.oy) * br.iy;
+    float t0z = ((lo.z - g) - r.oz) * br.iz, t1z = ((hi.z + g) - r.oz) * br.iz;
+    float ax0 = fminf(t0x, t1x), ax1 = fmaxf(t0x, t1x);
+    float ay0 = fminf(t0y, t1y), ay1 = fmaxf(t0y, t1y);
+    float az0 = fminf(t0z, t1z), az1 = fmaxf(t0z, t1z);
+    if (t0x != t0x || t1x != t1x) { ax0 = -INFINITY; ax1 = INFINITY; }
+    if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
+    if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
+    // computed slab bounds are within 3 ulp (relative) of the exact ones: widen by 8 ulp
+    const float dtc = ((lambda * co.z) * S) * up;
+    const float dt = (dtc + co.w * closest) * up;
+    float enter = fmaxf(fmaxf(ax0, ay0), az0), exit = fminf(fminf(ax1, ay1), az1);
+    enter = enter - iq_fabsf(enter) * slack;
+    exit = exit + iq_fabsf(exit) * slack;
+    enter_out = enter;
+    dtc_out = dtc;
+    return enter <= exit && enter <= closest + dt && exit >= kTMin - dt;
+}
+
+template <int OPT>
+__device__ __forceinline__ void bvh_leaf(const kparams& p, uint32_t fc, const ray3 r, float& closest, int& kind,
+                                         uint32_t& idx) {
+    const float4* __restrict__ pairs = reinterpret_cast<const float4*>(p.bvh_pairs);
+    const uint32_t first = fc >> 8, cnt = fc & 0xffu;
+    for (uint32_t k = 0; k < cnt; ++k) {
+        const float4* q = pairs + (size_t)(first + k) * kTriPairFloat4;
+        const uint32_t ka = p.bvh_pidx[2 * (first + k)], kb = p.bvh_pidx[2 * (first + k) + 1];
+        test_triangle_pair_ix<OPT>(q[0], q[1], q[2], q[3], q[4], r, closest, kind, idx, ka, kb);
+    }
+}
+
+// Closest triangle for one ray through the exact BVH (iq_bvh.hpp): a stackless DFS in the tree's
+// fixed order (skip pointers), leaves tested with the reference's own Möller–Trumbore and the
+// triangles left out of the BVH afterwards; the result is the brute-force loop's (min t, max index)
+// whatever the visiting order. (A near-child-first traversal with a per-lane LDS stack was measured
+// slower on C4/C5 — profiles/ab/r01_ab38_c*_order.json — and is not kept.)
 template <int OPT>
 __device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, float& closest, int& kind, uint32_t& idx) {
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh_nodes);
-    const float4* __restrict__ pairs = reinterpret_cast<const float4*>(p.bvh_pairs);
-    const float ix = 1.0f / r.dx, iy = 1.0f / r.dy, iz = 1.0f / r.dz;
-    const float slack = 8.0f * 0x1p-24f, up = 1.0f + 0x1p-20f, up16 = 1.0f + 0x1p-16f;
-    // |d|^2 and |d|, rounded up (normal cones)
-    const float dd = ((r.dx * r.dx + r.dy * r.dy) + r.dz * r.dz) * up16;
-    const float dl = __builtin_sqrtf(dd) * up16;
+    const bvh_ray br = bvh_ray_setup(r);
     uint32_t i = 0;
     while (i < p.bvh_nnodes) {
-        const float4* nd = nodes + (size_t)kBvhNodeFloat4 * i;
-        const float4 lo = nd[0], hi = nd[1], co = nd[2], cone = nd[3], cone2 = nd[4];
-        const float sx = fmaxf(iq_fabsf(r.ox - lo.x), iq_fabsf(r.ox - hi.x));
-        const float sy = fmaxf(iq_fabsf(r.oy - lo.y), iq_fabsf(r.oy - hi.y));
-        const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
-        const float S = fmaxf(fmaxf(sx, sy), sz) * up;
-        // lambda = 1e-6 / D, D a lower bound of |det^| over the node's triangles for this ray
-        // (iq_bvh.hpp normal cones): |d| cos(theta + beta) from the cone, every step rounded toward
-        // a smaller D; an unusable cone (cos beta = 0) or a grazing ray leaves lambda = 1
-        float lambda = 1.0f;
-        if (cone.w > 0.0f) {
-            const float c = iq_fabsf((r.dx * cone.x + r.dy * cone.y) + r.dz * cone.z);
-            const float c_lo = fmaxf(0.0f, c * (1.0f - 0x1p-16f) - 0x1p-20f * dl);
-            // |d| sin(theta) <= sqrt(dd - c_lo^2); the subtraction's rounding (<= 2u dd) is covered by
-            // adding 2^-20 dd before the root
-            const float s_hi = __builtin_sqrtf(fmaxf(0.0f, dd - c_lo * c_lo) + 0x1p-20f * dd) * up16;
-            const float cos_lo = (c_lo * cone.w) * (1.0f - 0x1p-16f) - (s_hi * cone2.x) * up16;
-            const float D = (cos_lo * cone2.y) * (1.0f - 0x1p-16f) - cone2.z * up16;
-            if (D > 1e-6f) lambda = fminf(1.0f, (1e-6f * __builtin_amdgcn_rcpf(D)) * up16);
-        }
-        const float g = (lambda * (co.x + co.y * S)) * up + p.bvh_gulp;   // gulp includes gC
-        // per axis [t0, t1] of the slab; a NaN (0 * inf: origin on a slab plane of an axis-parallel
-        // ray) widens that axis to everything
-        float t0x = ((lo.x - g) - r.ox) * ix, t1x = ((hi.x + g) - r.ox) * ix;
-        float t0y = ((lo.y - g) - r.oy) * iy, t1y = ((hi.y + g) - r.oy) * iy;
-        float t0z = ((lo.z - g) - r.oz) * iz, t1z = ((hi.z + g) - r.oz) * iz;
-        float ax0 = fminf(t0x, t1x), ax1 = fmaxf(t0x, t1x);
-        float ay0 = fminf(t0y, t1y), ay1 = fmaxf(t0y, t1y);
-        float az0 = fminf(t0z, t1z), az1 = fmaxf(t0z, t1z);
-        if (t0x != t0x || t1x != t1x) { ax0 = -INFINITY; ax1 = INFINITY; }
-        if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
-        if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
-        // computed slab bounds are within 3 ulp (relative) of the exact ones: widen by 8 ulp
-        const float dt = ((lambda * co.z) * S + co.w * closest) * up;
-        float enter = fmaxf(fmaxf(ax0, ay0), az0), exit = fminf(fminf(ax1, ay1), az1);
-        enter = enter - iq_fabsf(enter) * slack;
-        exit = exit + iq_fabsf(exit) * slack;
-        const bool hit = enter <= exit && enter <= closest + dt && exit >= kTMin - dt;
+        float enter, dtc;
+        const bool hit = bvh_node_test(p, nodes, i, r, br, closest, enter, dtc);
+        const float4 lo = nodes[(size_t)kBvhNodeFloat4 * i], hi = nodes[(size_t)kBvhNodeFloat4 * i + 1];
         const uint32_t skip = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
-        if (hit && fc != 0u) {
-            const uint32_t first = fc >> 8, cnt = fc & 0xffu;
-            for (uint32_t k = 0; k < cnt; ++k) {
-                const float4* q = pairs + (size_t)(first + k) * kTriPairFloat4;
-                const uint32_t ka = p.bvh_pidx[2 * (first + k)], kb = p.bvh_pidx[2 * (first + k) + 1];
-                test_triangle_pair_ix<OPT>(q[0], q[1], q[2], q[3], q[4], r, closest, kind, idx, ka, kb);
-            }
-        }
+        if (hit && fc != 0u) bvh_leaf<OPT>(p, fc, r, closest, kind, idx);
         i = (hit && fc == 0u) ? i + 1 : skip;
     }
     const float4* __restrict__ tris = reinterpret_cast<const float4*>(p.tris);
