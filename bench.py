@@ -246,7 +246,8 @@ def main():
                     valu_busy = mix.get("valu_busy_frac")
             except Exception:
                 valu_busy = None
-        samples = cfg.width * cfg.height * spp_step * args.steps
+        # weak: every rank renders the whole frame; strong: the ranks share one frame
+        samples = cfg.width * cfg.height * spp_step * args.steps * (world if weak else 1)
         out = {
             "metric": "Mrays/sec at 1920x1080 8-bounce; per-pixel RMSE vs reference",
             "value": round(mrays, 3),
