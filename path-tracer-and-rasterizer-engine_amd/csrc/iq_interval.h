@@ -85,6 +85,7 @@ struct camera_in {
 
 struct bundle {
     ivl o[3], d[3];
+    ivl len;          // |far - near| before normalization (normalize3's len)
     bool ok;
 };
 
@@ -140,6 +141,7 @@ IQ_HD inline bundle camera_bundle(const camera_in& c, uint32_t xa, uint32_t xb, 
     const ivl len2 = add(add(sq(d[0]), sq(d[1])), sq(d[2]));
     const ivl len = sqrt_(len2);
     if (!(len.lo > 0.0f) || !finite(len)) return b;
+    b.len = len;
     const ivl inv = rcp(len);
     for (int k = 0; k < 3; ++k) {
         b.d[k] = mul(d[k], inv);

@@ -55,6 +55,10 @@ struct kparams {
     uint32_t cam_const;              // inverse projection has constant w (see camera_ray)
     float cam_near_rw, cam_far_rw;   // 1 / w_near, 1 / w_far when cam_const
     float rcp_width, rcp_height;     // RN(1 / W), RN(1 / H) (kOptFastDiv camera divisions)
+    // kOptCamAxis (camera_ray_axis): P[0], P[5], P[12], P[13], 1/w_near, 1/w_far, V[0], V[12], V[5],
+    // V[6], V[13], V[14], then the launch constants z_n V[9], z_n V[10], z_f V[9], z_f V[10]
+    // (z_n, z_f: unprojected z of the near / far point divided by its w)
+    float cam_ax[16];
     uint32_t acc_tab;                // build the per-launch (1/n, (n-1)/n) table in LDS
     uint32_t diag;                   // kOptDiag ablation bits (A/B builds): 1 camera ray, 2 intersection, 4 mean
     uint32_t frames32;               // frame0 + spp < 2^32: 32-bit frame-counter conversions
@@ -154,6 +158,8 @@ constexpr int kOptBvh = 1 << 11;       // secondary rays traverse the exact BVH 
                                        // when the packet has none)
 constexpr int kOptBvhPrimary = 1 << 12; // camera rays take the BVH too (instead of the tile masks)
 constexpr int kOptDiag = 1 << 13;      // A/B builds only: timing ablations selected by kparams::diag (NOT exact)
+constexpr int kOptCamAxis = 1 << 14;   // short camera transform for pitch-only cameras (kparams::cam_ax; the runtime
+                                       // checks the zero pattern and the frame-wide normalization bounds)
 constexpr int kOptDefault =
     kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull | kOptBvh;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
@@ -172,6 +178,9 @@ int launch_bin(void* stream, const kbin& b);
 // Per-tile cost estimate from the masks: set triangle-pair bits + 8 x set sphere-pair bits.
 int launch_tile_cost(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
                      uint32_t* cost);
+// Device probe of the camera transforms (iqpt_debug_camera_rays): general and kOptCamAxis forms.
+int launch_camera_probe(void* stream, const kparams& p, const float* ndc, float* gen, float* axis, uint32_t n,
+                        bool do_axis);
 // Device probe of the shared math (iqpt_debug_libm).
 int launch_libm(void* stream, int fn, const float* a, const float* b, float* out, uint32_t n);
 // grid_blocks = persistent grid size; lds_bytes dynamic LDS; stream = hipStream_t; opt = kOpt* mask.

@@ -128,17 +128,7 @@ struct ray3 {
 // w_far = ((x*0 + y*0) + m23) + m33 = fl(m23 + m33) for every finite x, y, so 1/w are launch
 // constants computed by the same IEEE division on the host (p.cam_near_rw / p.cam_far_rw).
 template <int OPT>
-__device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_t y, rng6& s, ray3& r) {
-    const float jx = rand_real(s, -0.5f, 0.5f);
-    // (x + jx) / W: under kOptFastDiv Markstein's correction of (x + jx) * RN(1/W) (RN(1/W) from the
-    // host); exact here since x + jx is 0 or in [2^-32, 2^24] and W in [1, 2^24] (iq_fastdiv.h)
-    const float xs = (float)x + jx;
-    const float x_ndc = ((OPT & kOptFastDiv) ? iq_div_pre(xs, (float)p.width, p.rcp_width)
-                                             : xs / (float)p.width) * 2.0f - 1.0f;
-    const float jy = rand_real(s, -0.5f, 0.5f);
-    const float ys = (float)y + jy;
-    const float y_ndc = 1.0f - ((OPT & kOptFastDiv) ? iq_div_pre(ys, (float)p.height, p.rcp_height)
-                                                    : ys / (float)p.height) * 2.0f;
+__device__ __forceinline__ void camera_ndc(const kparams& p, float x_ndc, float y_ndc, ray3& r) {
     // rows of the inverse projection P and inverse view V (row-major m[r][c], camera.h:30-31)
     const float* P = p.inv_proj;
     const float* Vw = p.inv_view;
@@ -182,6 +172,55 @@ __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_
     r.dx = dx;
     r.dy = dy;
     r.dz = dz;
+}
+
+// kOptCamAxis: the same transform for a pitch-only camera. The runtime enables it when P[1] = P[2] =
+// P[4] = P[6] = P[8] = P[9] = 0 (standard perspective inverse, kOptCamConst's w row) and V[1] = V[2] =
+// V[4] = V[8] = 0 (no yaw, no roll), every entry finite, and none of P[12], P[13], P[14], V[12], V[13],
+// V[14] is -0. Every term of camera_ndc left out here is (finite) * (+-0), so each dot product of
+// camera_ndc equals the kept terms' sum s, or both are zeros of possibly opposite sign; the last
+// addend of every chain is kept (P[12], P[13], V[12], V[13], V[14]; the z chains are launch
+// constants ending in P[14]), and c + z = c for c != 0, +0 + z = +0 for a zero z, so both chains
+// end on the same bits. The z terms are computed on the host with the same float operations
+// (cam_axis_constants). The runtime also proves with the interval bundle of iq_interval.h over the
+// whole frame that normalize3's zero branch is never taken and |far - near| < 2^100, so 1/len is
+// iq_rcp's exact case.
+template <int OPT>
+__device__ __forceinline__ void camera_ray_axis(const kparams& p, float x_ndc, float y_ndc, ray3& r) {
+    const float* k = p.cam_ax;
+    const f2 nf_rw = {k[4], k[5]};                  // 1 / w_near, 1 / w_far
+    const f2 xw = (x_ndc * k[0] + k[2]) * nf_rw;    // (((x P[0] + y P[4]) + z P[8]) + P[12]) / w
+    const f2 yw = (y_ndc * k[1] + k[3]) * nf_rw;    // (((x P[1] + y P[5]) + z P[9]) + P[13]) / w
+    const f2 kzy = {k[12], k[14]}, kzz = {k[13], k[15]};
+    const f2 wx = xw * k[6] + k[7];                 // ((x V[0] + y V[4]) + z V[8]) + V[12]
+    const f2 wy = (yw * k[8] + kzy) + k[10];        // ((x V[1] + y V[5]) + z V[9]) + V[13]
+    const f2 wz = (yw * k[9] + kzz) + k[11];        // ((x V[2] + y V[6]) + z V[10]) + V[14]
+    float dx = wx.y - wx.x, dy = wy.y - wy.x, dz = wz.y - wz.x;
+    // normalize3 without the zero branch; len in [1e-5, 2^100): iq_rcp is exact (kOptFastDiv)
+    const float len = sqrt_n<OPT>((dx * dx + dy * dy) + dz * dz);
+    const float inv = (OPT & kOptFastDiv) ? iq_rcp(len) : 1.0f / len;
+    r.ox = wx.x;
+    r.oy = wy.x;
+    r.oz = wz.x;
+    r.dx = dx * inv;
+    r.dy = dy * inv;
+    r.dz = dz * inv;
+}
+
+template <int OPT>
+__device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_t y, rng6& s, ray3& r) {
+    const float jx = rand_real(s, -0.5f, 0.5f);
+    // (x + jx) / W: under kOptFastDiv Markstein's correction of (x + jx) * RN(1/W) (RN(1/W) from the
+    // host); exact here since x + jx is 0 or in [2^-32, 2^24] and W in [1, 2^24] (iq_fastdiv.h)
+    const float xs = (float)x + jx;
+    const float x_ndc = ((OPT & kOptFastDiv) ? iq_div_pre(xs, (float)p.width, p.rcp_width)
+                                             : xs / (float)p.width) * 2.0f - 1.0f;
+    const float jy = rand_real(s, -0.5f, 0.5f);
+    const float ys = (float)y + jy;
+    const float y_ndc = 1.0f - ((OPT & kOptFastDiv) ? iq_div_pre(ys, (float)p.height, p.rcp_height)
+                                                    : ys / (float)p.height) * 2.0f;
+    if (OPT & kOptCamAxis) camera_ray_axis<OPT>(p, x_ndc, y_ndc, r);
+    else camera_ndc<OPT>(p, x_ndc, y_ndc, r);
 }
 
 // CUDA float -> uint8_t: NaN -> 0, saturating, truncating (path_tracer.cu:361-363).
@@ -1265,6 +1304,24 @@ __global__ __launch_bounds__(256) void iqpt_libm_kernel(int fn, const float* a, 
     out[i] = r;
 }
 
+// Camera probe (tests/test_gpu_camera.py): the general transform and kOptCamAxis's short one for n
+// given (x_ndc, y_ndc), ray components written as 6 floats each (bits compared by the test).
+__global__ __launch_bounds__(256) void iqpt_camera_probe_kernel(const kparams p, const float* ndc, float* gen,
+                                                                float* axis, uint32_t n, int do_axis) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    constexpr int kOpt = kOptDefault;
+    ray3 r;
+    camera_ndc<kOpt>(p, ndc[2 * i], ndc[2 * i + 1], r);
+    const float g[6] = {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz};
+    for (int k = 0; k < 6; ++k) gen[6 * (size_t)i + k] = g[k];
+    if (do_axis) {
+        camera_ray_axis<kOpt | kOptCamAxis>(p, ndc[2 * i], ndc[2 * i + 1], r);
+        const float a[6] = {r.ox, r.oy, r.oz, r.dx, r.dy, r.dz};
+        for (int k = 0; k < 6; ++k) axis[6 * (size_t)i + k] = a[k];
+    }
+}
+
 // kOptCull tile masks: one thread per (tile, mask word), 32 primitive pairs per word. A pair's bit
 // is cleared only if iq_interval.h proves that the reference's tests reject both of its primitives
 // for every camera ray of the tile (every pixel, every jitter).
@@ -1409,6 +1466,10 @@ const variant kVariants[] = {
                      IQPT_V(16, true, (O) & ~kOptLB5), IQPT_V(8, true, ((O) | kOptBvhPrimary) & ~kOptLB5), \
                      IQPT_V(16, true, ((O) | kOptBvhPrimary) & ~kOptLB5)
     IQPT_PROD(kOptDefault),
+    // pitch-only cameras (kOptCamAxis), resident scenes
+    IQPT_V(8, false, kOptDefault | kOptCamAxis), IQPT_V(16, false, kOptDefault | kOptCamAxis),
+    IQPT_V(8, false, kOptDefault | kOptMaterials | kOptCamAxis),
+    IQPT_V(16, false, kOptDefault | kOptMaterials | kOptCamAxis),
     IQPT_PROD(kOptDefault & ~kOptFastDiv),                  // packets outside the kOptFastDiv range
     IQPT_PROD(kOptDefault | kOptMaterials),                 // packets with a material table
     IQPT_PROD((kOptDefault & ~kOptFastDiv) | kOptMaterials),
@@ -1469,6 +1530,14 @@ int launch_relayout(void* stream, const uint32_t* src, uint32_t* dst, uint32_t n
 int launch_libm(void* stream, int fn, const float* a, const float* b, float* out, uint32_t n) {
     if (n == 0) return 0;
     hipLaunchKernelGGL(iqpt_libm_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, fn, a, b, out, n);
+    return (int)hipGetLastError();
+}
+
+int launch_camera_probe(void* stream, const kparams& p, const float* ndc, float* gen, float* axis, uint32_t n,
+                        bool do_axis) {
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(iqpt_camera_probe_kernel, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, p, ndc,
+                       gen, axis, n, do_axis ? 1 : 0);
     return (int)hipGetLastError();
 }
 

@@ -122,6 +122,7 @@ struct iqpt_ctx {
     int tune_stage = 0;          // 0: next launch times masks, 1: times the BVH, 2: decide, 3: decided
     bool tune_primary = false;
     hipEvent_t tune_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    int last_opt = -1;           // option set of the last render launch (iqpt_debug_last_options)
     double tune_work[2] = {0.0, 0.0};
 };
 
@@ -233,6 +234,52 @@ void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, f
         *near_rw = 1.0f / P[15];
         *far_rw = 1.0f / wf;
     }
+}
+
+// kOptCamAxis (camera_ray_axis in iqpt_kernels.hip): the zero pattern of a pitch-only camera under a
+// standard perspective inverse, no -0 among the chains' last addends, every entry finite,
+// kOptCamConst's constant w, and — from the interval bundle of every camera ray of the frame
+// (iq_interval.h) — normalize3's zero branch never taken and |far - near| < 2^100. Fills the 16
+// launch constants; false when the camera does not qualify.
+bool cam_axis_constants(const iqpt_camera& cam, float* k) {
+    const float* P = cam.inv_proj;
+    const float* V = cam.inv_view;
+    for (int i = 0; i < 16; ++i)
+        if (!std::isfinite(P[i]) || !std::isfinite(V[i])) return false;
+    uint32_t cc = 0;
+    float nrw = 0.0f, frw = 0.0f;
+    cam_constants(cam, &cc, &nrw, &frw);
+    if (!cc || !std::isfinite(nrw) || !std::isfinite(frw)) return false;
+    for (int i : {1, 2, 4, 6, 8, 9})
+        if (P[i] != 0.0f) return false;
+    for (int i : {1, 2, 4, 8})
+        if (V[i] != 0.0f) return false;
+    for (float last : {P[12], P[13], P[14], V[12], V[13], V[14]})
+        if (last == 0.0f && std::signbit(last)) return false;
+    if (cam.width == 0 || cam.height == 0) return false;
+    iqiv::camera_in ci;
+    ci.width = cam.width;
+    ci.height = cam.height;
+    ci.rcp_width = 0.0f;
+    ci.rcp_height = 0.0f;
+    ci.inv_proj = P;
+    ci.inv_view = V;
+    ci.cam_const = 1;
+    ci.near_rw = nrw;
+    ci.far_rw = frw;
+    const iqiv::bundle b = iqiv::camera_bundle(ci, 0, cam.width - 1, 0, cam.height - 1);
+    if (!b.ok || !(b.len.hi < 0x1p100f)) return false;
+    // unprojected z of the near / far point (camera_ndc's chain; its zero terms only change the
+    // sign of a zero inner sum, which the last addend P[14] (not -0) absorbs), divided by w
+    const float zn = (((0.0f + 0.0f) + 0.0f * P[10]) + P[14]) * nrw;
+    const float zf = (((0.0f + 0.0f) + 1.0f * P[10]) + P[14]) * frw;
+    const float vals[16] = {P[0], P[5], P[12], P[13], nrw, frw, V[0], V[12], V[5], V[6], V[13], V[14],
+                            zn * V[9], zn * V[10], zf * V[9], zf * V[10]};
+    for (int i = 0; i < 16; ++i) {
+        if (!std::isfinite(vals[i])) return false;
+        k[i] = vals[i];
+    }
+    return true;
 }
 
 // Exact BVH for secondary rays (iq_bvh.hpp) over the world-space triangles `tris` (kTriFloat4 each)
@@ -730,6 +777,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     p.tri_shade = c->d_tri_shade;
     p.rcp_width = 1.0f / (float)c->width;
     p.rcp_height = 1.0f / (float)c->height;
+    const bool cam_axis = (opt & iqpt::kOptCamConst) && cam_axis_constants(c->cam, p.cam_ax);
     const bool pair = (opt & iqpt::kOptPair) != 0;
     const uint32_t tri_rec = pair ? iqpt::kTriPairFloat4 * 16 : iqpt::kTriFloat4 * 16;   // bytes per LDS record
     const uint32_t sph_rec = pair ? iqpt::kSphPairFloat4 * 16 : 16;
@@ -741,6 +789,11 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     if (stream_batches && !iqpt::render_variant_exists(c->max_depth, true, opt) &&
         iqpt::render_variant_exists(c->max_depth, true, opt & ~iqpt::kOptLB5))
         opt &= ~iqpt::kOptLB5;
+    // kOptCamAxis: the short camera transform where the camera qualifies and the variant is built
+    // (resident scenes); a fixed option set (tools/ab_kernel.py) keeps the bit only if it qualifies
+    if (!cam_axis) opt &= ~iqpt::kOptCamAxis;
+    else if (!c->opt_fixed && iqpt::render_variant_exists(c->max_depth, stream_batches, opt | iqpt::kOptCamAxis))
+        opt |= iqpt::kOptCamAxis;
     if (stream_batches) {
         p.tri_batch = pair ? iqpt::kTriBatch / 2 : iqpt::kTriBatch;   // records
         p.sph_batch = pair ? iqpt::kSphBatch / 2 : iqpt::kSphBatch;
@@ -810,6 +863,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     if (e1) (void)hipEventRecord(e1, c->stream);
     if (e0 && e1) c->timed.emplace_back(e0, e1);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "render kernel launch");
+    c->last_opt = opt;
     if (tune_slot >= 0) {
         c->tune_work[tune_slot] = (double)spp * (double)c->npix;
         c->tune_stage = tune_slot + 1;
@@ -1129,6 +1183,55 @@ int iqpt_debug_libm(int fn, const float* a, const float* b, float* out, uint64_t
     (void)hipFree(db);
     (void)hipFree(dout);
     return st;
+}
+
+/* Internal (tests/test_camera_axis.py): 1 if the camera qualifies for the short pitch-only transform
+ * (kOptCamAxis), its 16 launch constants in k16; 0 otherwise. Host only. */
+int iqpt_debug_cam_axis(const iqpt_camera* cam, float* k16) {
+    if (!cam || !k16) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    std::memset(k16, 0, 16 * sizeof(float));
+    return cam_axis_constants(*cam, k16) ? 1 : 0;
+}
+
+/* Internal (tests/test_gpu_camera.py): the general camera transform and, if the camera qualifies,
+ * the kOptCamAxis one, on the GPU for n (x_ndc, y_ndc) pairs; 6 floats (origin, direction) per ray
+ * into gen / axis. Returns 1 if the axis form ran, 0 if not (synchronous). */
+int iqpt_debug_camera_rays(const iqpt_camera* cam, const float* ndc, uint64_t n, float* gen, float* axis) {
+    if (!cam || !ndc || !gen || !axis) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (n > (1ull << 24)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "n too large");
+    iqpt::kparams p;
+    std::memset(&p, 0, sizeof p);
+    p.width = cam->width;
+    p.height = cam->height;
+    std::memcpy(p.inv_proj, cam->inv_proj, sizeof p.inv_proj);
+    std::memcpy(p.inv_view, cam->inv_view, sizeof p.inv_view);
+    cam_constants(*cam, &p.cam_const, &p.cam_near_rw, &p.cam_far_rw);
+    const bool ax = cam_axis_constants(*cam, p.cam_ax);
+    if (n == 0) return ax ? 1 : 0;
+    float *dn = nullptr, *dg = nullptr, *da = nullptr;
+    int st = IQPT_OK;
+    if (hipMalloc(&dn, n * 2 * sizeof(float)) != hipSuccess || hipMalloc(&dg, n * 6 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&da, n * 6 * sizeof(float)) != hipSuccess) {
+        st = iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "camera probe buffers");
+    } else {
+        hipError_t e = hipMemcpy(dn, ndc, n * 2 * sizeof(float), hipMemcpyHostToDevice);
+        if (e == hipSuccess) e = hipMemset(da, 0, n * 6 * sizeof(float));
+        if (e == hipSuccess) e = (hipError_t)iqpt::launch_camera_probe(nullptr, p, dn, dg, da, (uint32_t)n, ax);
+        if (e == hipSuccess) e = hipMemcpy(gen, dg, n * 6 * sizeof(float), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) e = hipMemcpy(axis, da, n * 6 * sizeof(float), hipMemcpyDeviceToHost);
+        if (e != hipSuccess) st = iqpt::hip_fail(e, "camera probe");
+    }
+    (void)hipFree(dn);
+    (void)hipFree(dg);
+    (void)hipFree(da);
+    return st ? st : (ax ? 1 : 0);
+}
+
+/* Internal (tests): the kernel option set of the context's last render launch (-1 before any). */
+int iqpt_debug_last_options(iqpt_ctx* c, int* opt) {
+    if (!c || !opt) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *opt = c->last_opt;
+    return IQPT_OK;
 }
 
 int iqpt_debug_read_stats(iqpt_ctx* c, unsigned long long* out16) {
