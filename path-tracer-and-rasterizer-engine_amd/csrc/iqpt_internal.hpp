@@ -56,12 +56,13 @@ struct kparams {
     float cam_near_rw, cam_far_rw;   // 1 / w_near, 1 / w_far when cam_const
     float rcp_width, rcp_height;     // RN(1 / W), RN(1 / H) (kOptFastDiv camera divisions)
     // kOptCamAxis (camera_ray_axis): P[0], P[5], P[12], P[13], 1/w_near, 1/w_far, V[0], V[12], V[5],
-    // V[6], V[13], V[14], then the launch constants z_n V[9], z_n V[10], z_f V[9], z_f V[10]
+    // V[6], V[13], V[14], then the launch constants z_n V[9], z_f V[9], z_n V[10], z_f V[10]
     // (z_n, z_f: unprojected z of the near / far point divided by its w)
     float cam_ax[16];
     uint32_t acc_tab;                // build the per-launch (1/n, (n-1)/n) table in LDS
     uint32_t diag;                   // kOptDiag ablation bits (A/B builds): 1 camera ray, 2 intersection, 4 mean
     uint32_t frames32;               // frame0 + spp < 2^32: 32-bit frame-counter conversions
+    float mean_tiny;                 // kOptFastDiv running mean: c below this takes the IEEE division
     const float4_storage* tris;      // ntri * kTriFloat4 (single layout)
     const float4_storage* tri_pairs; // ntri_pairs * kTriPairFloat4 (pair layout)
     uint32_t ntri, ntri_pairs;
@@ -158,10 +159,13 @@ constexpr int kOptBvh = 1 << 11;       // secondary rays traverse the exact BVH 
                                        // when the packet has none)
 constexpr int kOptBvhPrimary = 1 << 12; // camera rays take the BVH too (instead of the tile masks)
 constexpr int kOptDiag = 1 << 13;      // A/B builds only: timing ablations selected by kparams::diag (NOT exact)
+constexpr int kOptExp = 1 << 15;       // A/B builds only: an alternative formulation under test (exact)
 constexpr int kOptCamAxis = 1 << 14;   // short camera transform for pitch-only cameras (kparams::cam_ax; the runtime
                                        // checks the zero pattern and the frame-wide normalization bounds)
 constexpr int kOptDefault =
     kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull | kOptBvh;
+constexpr uint32_t kStatsHeader = 16;        // kOptStats: 16 counters, then per-wave (start, end, iterations)
+constexpr uint32_t kStatsWaveSlots = 65536;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.

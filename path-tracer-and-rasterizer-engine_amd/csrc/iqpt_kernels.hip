@@ -188,13 +188,23 @@ __device__ __forceinline__ void camera_ndc(const kparams& p, float x_ndc, float 
 template <int OPT>
 __device__ __forceinline__ void camera_ray_axis(const kparams& p, float x_ndc, float y_ndc, ray3& r) {
     const float* k = p.cam_ax;
-    const f2 nf_rw = {k[4], k[5]};                  // 1 / w_near, 1 / w_far
-    const f2 xw = (x_ndc * k[0] + k[2]) * nf_rw;    // (((x P[0] + y P[4]) + z P[8]) + P[12]) / w
-    const f2 yw = (y_ndc * k[1] + k[3]) * nf_rw;    // (((x P[1] + y P[5]) + z P[9]) + P[13]) / w
-    const f2 kzy = {k[12], k[14]}, kzz = {k[13], k[15]};
-    const f2 wx = xw * k[6] + k[7];                 // ((x V[0] + y V[4]) + z V[8]) + V[12]
-    const f2 wy = (yw * k[8] + kzy) + k[10];        // ((x V[1] + y V[5]) + z V[9]) + V[13]
-    const f2 wz = (yw * k[9] + kzz) + k[11];        // ((x V[2] + y V[6]) + z V[10]) + V[14]
+    f2 wx, wy, wz;                                  // (near, far) world-space points
+    if (OPT & kOptExp) {
+        // scalar form (A/B)
+        const float xp = x_ndc * k[0] + k[2], yp = y_ndc * k[1] + k[3];
+        const float xn = xp * k[4], xf = xp * k[5], yn = yp * k[4], yf = yp * k[5];
+        wx = (f2){xn * k[6] + k[7], xf * k[6] + k[7]};
+        wy = (f2){(yn * k[8] + k[12]) + k[10], (yf * k[8] + k[13]) + k[10]};
+        wz = (f2){(yn * k[9] + k[14]) + k[11], (yf * k[9] + k[15]) + k[11]};
+    } else {
+        const f2 nf_rw = {k[4], k[5]};              // 1 / w_near, 1 / w_far
+        const f2 xw = (x_ndc * k[0] + k[2]) * nf_rw;   // (((x P[0] + y P[4]) + z P[8]) + P[12]) / w
+        const f2 yw = (y_ndc * k[1] + k[3]) * nf_rw;   // (((x P[1] + y P[5]) + z P[9]) + P[13]) / w
+        const f2 kzy = {k[12], k[13]}, kzz = {k[14], k[15]};
+        wx = xw * k[6] + k[7];                      // ((x V[0] + y V[4]) + z V[8]) + V[12]
+        wy = (yw * k[8] + kzy) + k[10];             // ((x V[1] + y V[5]) + z V[9]) + V[13]
+        wz = (yw * k[9] + kzz) + k[11];             // ((x V[2] + y V[6]) + z V[10]) + V[14]
+    }
     float dx = wx.y - wx.x, dy = wy.y - wy.x, dz = wz.y - wz.x;
     // normalize3 without the zero branch; len in [1e-5, 2^100): iq_rcp is exact (kOptFastDiv)
     const float len = sqrt_n<OPT>((dx * dx + dy * dy) + dz * dz);
@@ -526,30 +536,49 @@ __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-// c / n of the running mean (path_tracer.cu:356-358). kOptAccTable: 1/n is read from a per-launch
-// table built with the same IEEE division (so c = 1 gives the identical bits) and 0/n = +0 (c is
-// never -0 here: path_color = 0 + color).
-// `tab` is false when the launch has more samples than the table holds (rc is then not set).
-// kOptFastDiv: for c in [2^-90, 1) (c is clamped to [0, 1] or NaN) and n < 2^32 the quotient is
-// normal and Markstein's correction of c * rc, rc = RN(1/n) from the table, is exact (iq_fastdiv.h).
-// Branch-free under kOptFastDiv: Markstein's form also gives the exact quotient for c = 1 (RN(1/n)
-// = rc) and c = 0 (+0, as 0 / n), so only 0 < c < 2^-90 (a quotient that could be subnormal) takes
-// the generic division.
+// c / n of the running mean (path_tracer.cu:356-358) without the table (variants without
+// kOptAccTable): the IEEE division.
+// With kOptAccTable (every production variant; the runtime keeps launches within the table) the
+// three channels are done together in mean_terms below.
 template <int OPT>
-__device__ __forceinline__ float mean_term(float c, float nf, float rc, bool tab) {
-    if (tab && (OPT & kOptFastDiv)) {
-        float q = iq_div_pre(c, nf, rc);
-        if (c > 0.0f && c < 0x1p-90f) {
-            asm volatile("" ::: "memory");   // keep the rare IEEE expansion behind a branch (no if-conversion)
-            q = c / nf;
-        }
-        return q;
-    }
-    if (tab) {
-        if (c == 1.0f) return rc;
-        if (c == 0.0f) return 0.0f;
-    }
+__device__ __forceinline__ float mean_term(float c, float nf) {
     return c / nf;
+}
+
+// (cx, cy, cz) / n for the clamped colour (each channel in [0, 1] or NaN, never -0: path_color =
+// 0 + color) with rc = RN(1/n) from the per-launch table. kOptFastDiv: Markstein's correction
+// q + (c - n q) rc, q = c rc, is the IEEE quotient while the quotient is normal and the operands are
+// within [2^-100, 2^100] (n < 2^64 is); c = 0 gives +0 (as 0 / n) and NaN stays NaN, so no fixup
+// is needed in this domain. Channels 0 < c < p.mean_tiny (a quotient that could be subnormal, or c
+// below 2^-99) take the IEEE division: one test for all three ((bits - 1) as unsigned maps +0 and
+// NaN above the threshold's bits). Without kOptFastDiv: c = 1 gives rc, c = 0 gives +0, else the
+// IEEE division.
+template <int OPT>
+__device__ __forceinline__ void mean_terms(float cx, float cy, float cz, float nf, float rc, float tiny,
+                                           float& qx, float& qy, float& qz) {
+    if (OPT & kOptFastDiv) {
+        const f2 c2 = {cx, cy};
+        const f2 q0 = c2 * rc;
+        const f2 r = __builtin_elementwise_fma(-(f2){nf, nf}, q0, c2);
+        const f2 q1 = __builtin_elementwise_fma(r, (f2){rc, rc}, q0);
+        const float z0 = cz * rc;
+        const float zr = __builtin_fmaf(-nf, z0, cz);
+        qx = q1.x;
+        qy = q1.y;
+        qz = __builtin_fmaf(zr, rc, z0);
+        const uint32_t lim = __float_as_uint(tiny) - 1u;
+        const uint32_t m = min(min(__float_as_uint(cx) - 1u, __float_as_uint(cy) - 1u), __float_as_uint(cz) - 1u);
+        if (__builtin_expect(m < lim, 0)) {
+            asm volatile("" ::: "memory");   // keep the rare IEEE expansion behind a branch (no if-conversion)
+            qx = cx / nf;
+            qy = cy / nf;
+            qz = cz / nf;
+        }
+        return;
+    }
+    qx = cx == 1.0f ? rc : (cx == 0.0f ? 0.0f : cx / nf);
+    qy = cy == 1.0f ? rc : (cy == 0.0f ? 0.0f : cy / nf);
+    qz = cz == 1.0f ? rc : (cz == 0.0f ? 0.0f : cz / nf);
 }
 
 // Closest hit over the primitives in [tri0, tri1) / [sph0, sph1) of the given base arrays (LDS),
@@ -600,15 +629,21 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {
 // secondary ray. Skipped pairs are rejected by the reference's own tests for every camera ray of
 // the tile, and the remaining pairs are visited in index order, so results are unchanged. Called by
 // all lanes of the wave (wave_or); only active lanes test.
-// Word 0 of each mask comes from the lane's registers (cm_t, cm_s: loaded with the pixel).
+// Word 0 of each mask comes from the lane's registers (cm_t, cm_s: loaded with the pixel). When
+// every active lane is in the same tile (uni_mask = that tile's words; the caller has made the first
+// lane an active one) the OR is that tile's mask itself: word 0 read from the first lane, the others
+// with uniform loads, no DPP.
 template <int OPT>
 __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntri, const float4* sph, uint32_t nsph,
                                                  const uint32_t* lane_mask, uint32_t cm_t, uint32_t cm_s, bool all,
                                                  bool active, const ray3 ray, float& closest, int& kind,
-                                                 uint32_t& hidx, uint32_t wt, unsigned long long* st = nullptr) {
+                                                 uint32_t& hidx, uint32_t wt, const uint32_t* uni_mask,
+                                                 unsigned long long* st = nullptr) {
     const uint32_t tp = (ntri + 1) / 2, sp = (nsph + 1) / 2;
     for (uint32_t w = 0; w * 32u < tp; ++w) {
-        uint32_t m = all ? ~0u : wave_or(lane_mask ? (w == 0 ? cm_t : lane_mask[w]) : 0u);
+        uint32_t m = all ? ~0u
+                         : (uni_mask ? (w == 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)cm_t) : uni_mask[w])
+                                     : wave_or(lane_mask ? (w == 0 ? cm_t : lane_mask[w]) : 0u));
         if ((OPT & kOptStats) && st) st[0] += (unsigned long long)__builtin_popcount(w * 32u + 32u <= tp ? m : (m & ((1u << (tp - w * 32u)) - 1u)));
         while (m) {
             const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
@@ -621,7 +656,9 @@ __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntr
         }
     }
     for (uint32_t w = 0; w * 32u < sp; ++w) {
-        uint32_t m = all ? ~0u : wave_or(lane_mask ? (w == 0 ? cm_s : lane_mask[wt + w]) : 0u);
+        uint32_t m = all ? ~0u
+                         : (uni_mask ? (w == 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)cm_s) : uni_mask[wt + w])
+                                     : wave_or(lane_mask ? (w == 0 ? cm_s : lane_mask[wt + w]) : 0u));
         if ((OPT & kOptStats) && st) st[1] += (unsigned long long)__builtin_popcount(w * 32u + 32u <= sp ? m : (m & ((1u << (sp - w * 32u)) - 1u)));
         while (m) {
             const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
@@ -831,7 +868,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // kOptAccTable: (1/n, (n-1)/n) per sample of the launch, then (float)n (padded to 16 B)
     float* lds_tab_n = reinterpret_cast<float*>(lds_tab + (use_tab_lds(p) ? ((p.spp + 1u) & ~1u) : 0u));
     uint4* lds_cm = reinterpret_cast<uint4*>(lds_tab_n + (use_tab_lds(p) ? ((p.spp + 3u) & ~3u) : 0u));
-    const bool use_tab = (OPT & kOptAccTable) && p.acc_tab;
+    constexpr bool use_tab = (OPT & kOptAccTable) != 0;   // the runtime keeps every launch within the table
     constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
     constexpr bool kBvh = STREAM && (OPT & kOptBvh) && (OPT & kOptPair);
     constexpr bool kBvhPrimary = kBvh && (OPT & kOptBvhPrimary);
@@ -948,6 +985,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
         }
     };
 
+    const uint64_t t_start = (OPT & kOptStats) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (p.spp > 0) refill();
 
     while (true) {
@@ -1081,9 +1119,21 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 hidx = 0;
             }
         } else if (kCull && p.cull != nullptr) {
-            const uint4 cm = lds_cm[threadIdx.x];
+            uint4 cm = lds_cm[threadIdx.x];
+            // one tile for every active lane (the usual case: a tile's lanes start together and, on
+            // tiles whose camera rays all end on their first hit, finish together): its own mask
+            const uint64_t act = __ballot(active);
+            const uint32_t first = act ? (uint32_t)__builtin_ctzll(act) : 0u;
+            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
+            const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
+            if (uni) {
+                // word 0 is read from the first lane: give every lane the first active lane's words
+                cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
+                cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
+            }
+            const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
             intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray,
-                                  closest, kind, hidx, p.cull_wt, (OPT & kOptStats) ? s_tests : nullptr);
+                                  closest, kind, hidx, p.cull_wt, uni_mask, (OPT & kOptStats) ? s_tests : nullptr);
             if (OPT & kOptStats) s_full += cull ? 0ull : 1ull;
         } else if (active) {
             intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
@@ -1233,10 +1283,16 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             }
             if ((OPT & kOptDiag) && (p.diag & 4u)) {
                 acc.x += cx;                     // diagnostic: no running-mean arithmetic
+            } else if (use_tab) {
+                float qx, qy, qz;
+                mean_terms<OPT>(cx, cy, cz, nf, rc, p.mean_tiny, qx, qy, qz);
+                acc.x = qx + acc.x * keep;
+                acc.y = qy + acc.y * keep;
+                acc.z = qz + acc.z * keep;
             } else {
-                acc.x = mean_term<OPT>(cx, nf, rc, use_tab) + acc.x * keep;
-                acc.y = mean_term<OPT>(cy, nf, rc, use_tab) + acc.y * keep;
-                acc.z = mean_term<OPT>(cz, nf, rc, use_tab) + acc.z * keep;
+                acc.x = mean_term<OPT>(cx, nf) + acc.x * keep;
+                acc.y = mean_term<OPT>(cy, nf) + acc.y * keep;
+                acc.z = mean_term<OPT>(cz, nf) + acc.z * keep;
             }
             ++done;
             depth = 0;
@@ -1272,6 +1328,13 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             atomicAdd(p.stats + 8, s_tests[0]);
             atomicAdd(p.stats + 9, s_tests[1]);
             atomicAdd(p.stats + 10, s_full);
+            // wave timeline (s_memrealtime, 100 MHz): start, end, iterations per wave
+            const uint64_t slot = atomicAdd(p.stats + 11, 1ull);
+            if (slot < kStatsWaveSlots) {
+                p.stats[kStatsHeader + 3 * slot] = t_start;
+                p.stats[kStatsHeader + 3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
+                p.stats[kStatsHeader + 3 * slot + 2] = s_iter;
+            }
         }
     }
 }
@@ -1494,6 +1557,7 @@ const variant kVariants[] = {
     IQPT_V(8, false, kOptDefault & ~kOptCull & ~kOptFastDiv),
     IQPT_V(8, true, kOptDefault & ~kOptBvh),
     IQPT_V(8, false, kOptDefault | kOptDiag),
+    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptExp),
     IQPT_V(8, true, (kOptDefault | kOptMaterials) & ~kOptBvh),
 #endif
 };

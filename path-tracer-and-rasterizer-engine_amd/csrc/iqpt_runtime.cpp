@@ -274,7 +274,7 @@ bool cam_axis_constants(const iqpt_camera& cam, float* k) {
     const float zn = (((0.0f + 0.0f) + 0.0f * P[10]) + P[14]) * nrw;
     const float zf = (((0.0f + 0.0f) + 1.0f * P[10]) + P[14]) * frw;
     const float vals[16] = {P[0], P[5], P[12], P[13], nrw, frw, V[0], V[12], V[5], V[6], V[13], V[14],
-                            zn * V[9], zn * V[10], zf * V[9], zf * V[10]};
+                            zn * V[9], zf * V[9], zn * V[10], zf * V[10]};
     for (int i = 0; i < 16; ++i) {
         if (!std::isfinite(vals[i])) return false;
         k[i] = vals[i];
@@ -722,12 +722,29 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
     return IQPT_OK;
 }
 
+namespace {
+int render_launch(iqpt_ctx* c, uint32_t spp);
+}
+
 int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     if (!c->have_camera || !c->have_packet) return iqpt::fail(IQPT_ERR_NOT_READY, "camera and packet must be set");
     if (spp == 0) return IQPT_OK;
     int st = use_device(c);
     if (st) return st;
+    // launches of at most kAccTableMax samples, so the running-mean table always covers the launch
+    // (a pixel's samples are sequential either way: same bits as one launch)
+    while (spp > 0) {
+        const uint32_t n = std::min(spp, iqpt::kAccTableMax);
+        if ((st = render_launch(c, n)) != IQPT_OK) return st;
+        spp -= n;
+    }
+    return IQPT_OK;
+}
+
+namespace {
+int render_launch(iqpt_ctx* c, uint32_t spp) {
+    int st = IQPT_OK;
     iqpt::kparams p;
     std::memset(&p, 0, sizeof p);
     p.width = c->width;
@@ -747,6 +764,13 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     p.acc_tab = spp <= iqpt::kAccTableMax ? 1u : 0u;
     p.diag = c->diag;
     p.frames32 = (c->frame + (uint64_t)spp) < (1ull << 32) ? 1u : 0u;
+    // running mean under kOptFastDiv: c / n by Markstein's correction is exact while the quotient is
+    // normal, c >= 2^-125 n; with n <= frame0 + spp the threshold 2^-124 (frame0 + spp) (rounded up,
+    // at least 2^-100 for the operand range) routes the rest to the IEEE division (mean_terms)
+    {
+        const double nmax = (double)(c->frame + (uint64_t)spp);
+        p.mean_tiny = (float)std::max(std::ldexp(nmax, -124) * 2.0, std::ldexp(1.0, -99));
+    }
     p.tris = c->d_tris;
     p.tri_pairs = c->d_tri_pairs;
     p.ntri = c->ntri;
@@ -789,11 +813,10 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     if (stream_batches && !iqpt::render_variant_exists(c->max_depth, true, opt) &&
         iqpt::render_variant_exists(c->max_depth, true, opt & ~iqpt::kOptLB5))
         opt &= ~iqpt::kOptLB5;
-    // kOptCamAxis: the short camera transform where the camera qualifies and the variant is built
-    // (resident scenes); a fixed option set (tools/ab_kernel.py) keeps the bit only if it qualifies
+    // kOptCamAxis (opt-in through iqpt_debug_set_kernel_options): the short camera transform, kept
+    // only where the camera qualifies. Not selected by default: 10 % fewer VALU instructions per
+    // wave-iteration on C2 but no shorter launch
     if (!cam_axis) opt &= ~iqpt::kOptCamAxis;
-    else if (!c->opt_fixed && iqpt::render_variant_exists(c->max_depth, stream_batches, opt | iqpt::kOptCamAxis))
-        opt |= iqpt::kOptCamAxis;
     if (stream_batches) {
         p.tri_batch = pair ? iqpt::kTriBatch / 2 : iqpt::kTriBatch;   // records
         p.sph_batch = pair ? iqpt::kSphBatch / 2 : iqpt::kSphBatch;
@@ -871,6 +894,7 @@ int iqpt_render(iqpt_ctx* c, uint32_t spp) {
     c->frame += spp;
     return IQPT_OK;
 }
+}  // namespace
 
 int iqpt_sync(iqpt_ctx* c) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
@@ -1098,9 +1122,10 @@ int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
     int st = use_device(c);
     if (st) return st;
     if ((opt & iqpt::kOptStats) && !c->d_stats) {
-        if (hipMalloc(&c->d_stats, 16 * sizeof(unsigned long long)) != hipSuccess)
+        const size_t words = iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots;
+        if (hipMalloc(&c->d_stats, words * sizeof(unsigned long long)) != hipSuccess)
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "stats");
-        IQPT_HIP(hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));
+        IQPT_HIP(hipMemset(c->d_stats, 0, words * sizeof(unsigned long long)));
     }
     c->opt = opt;
     c->opt_fixed = true;
@@ -1227,10 +1252,38 @@ int iqpt_debug_camera_rays(const iqpt_camera* cam, const float* ndc, uint64_t n,
     return st ? st : (ax ? 1 : 0);
 }
 
+/* Internal (tests/test_gpu_materials.py): set the frame counter (frames accumulated so far), e.g.
+ * beyond 2^32 to exercise the running mean's large-n forms. */
+int iqpt_debug_set_frame(iqpt_ctx* c, uint64_t frame) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->frame = frame;
+    return IQPT_OK;
+}
+
 /* Internal (tests): the kernel option set of the context's last render launch (-1 before any). */
 int iqpt_debug_last_options(iqpt_ctx* c, int* opt) {
     if (!c || !opt) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     *opt = c->last_opt;
+    return IQPT_OK;
+}
+
+/* Internal (tools/ab_kernel.py): the per-wave timeline of the last kOptStats launch: up to `cap`
+ * (start, end, iterations) triples (s_memrealtime ticks, 100 MHz); *n = waves recorded. Call before
+ * iqpt_debug_read_stats (which clears the buffer). */
+int iqpt_debug_read_wave_times(iqpt_ctx* c, unsigned long long* out, uint32_t cap, uint32_t* n) {
+    if (!c || !out || !n) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *n = 0;
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    if (!c->d_stats) return IQPT_OK;
+    unsigned long long cnt = 0;
+    IQPT_HIP(hipMemcpy(&cnt, c->d_stats + 11, sizeof cnt, hipMemcpyDeviceToHost));
+    const uint32_t m = (uint32_t)std::min<unsigned long long>({cnt, (unsigned long long)cap,
+                                                               (unsigned long long)iqpt::kStatsWaveSlots});
+    if (m) IQPT_HIP(hipMemcpy(out, c->d_stats + iqpt::kStatsHeader, 3 * (size_t)m * sizeof(unsigned long long),
+                              hipMemcpyDeviceToHost));
+    *n = m;
     return IQPT_OK;
 }
 
@@ -1245,7 +1298,7 @@ int iqpt_debug_read_stats(iqpt_ctx* c, unsigned long long* out16) {
         return IQPT_OK;
     }
     IQPT_HIP(hipMemcpy(out8, c->d_stats, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    IQPT_HIP(hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));
+    IQPT_HIP(hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));   // counters and the wave slot index
     return IQPT_OK;
 }
 

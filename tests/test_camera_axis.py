@@ -54,8 +54,8 @@ def short(k, x, y):
         xw = [(x * k[0] + k[2]) * k[4], (x * k[0] + k[2]) * k[5]]
         yw = [(y * k[1] + k[3]) * k[4], (y * k[1] + k[3]) * k[5]]
         wx = [xw[i] * k[6] + k[7] for i in range(2)]
-        wy = [(yw[0] * k[8] + k[12]) + k[10], (yw[1] * k[8] + k[14]) + k[10]]
-        wz = [(yw[0] * k[9] + k[13]) + k[11], (yw[1] * k[9] + k[15]) + k[11]]
+        wy = [(yw[0] * k[8] + k[12]) + k[10], (yw[1] * k[8] + k[13]) + k[10]]
+        wz = [(yw[0] * k[9] + k[14]) + k[11], (yw[1] * k[9] + k[15]) + k[11]]
         d = [wx[1] - wx[0], wy[1] - wy[0], wz[1] - wz[0]]
         ln = np.sqrt((d[0] * d[0] + d[1] * d[1]) + d[2] * d[2])
         inv = f32(1) / ln

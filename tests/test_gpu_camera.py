@@ -1,6 +1,7 @@
-"""kOptCamAxis on the GPU: the device builds of camera_ndc and camera_ray_axis give the same bits
-(zero signs included) on random and adversarial NDC inputs, renders with pitch-only cameras select
-the short transform and match the oracle bit for bit, and other cameras keep the general one."""
+"""kOptCamAxis on the GPU (an opt-in variant): the device builds of camera_ndc and camera_ray_axis give
+the same bits (zero signs included) on random and adversarial NDC inputs, renders with pitch-only
+cameras run the short transform and match the oracle bit for bit, other cameras keep the general
+one, and the default selection does not use it."""
 import ctypes as C
 
 import numpy as np
@@ -62,11 +63,20 @@ def test_device_camera_transforms_bit_identical(require_gpu, which):
     assert np.array_equal(gen.view(np.uint32), host.view(np.uint32))
 
 
-def render_both(cam, w, h, spp, depth=8, preset="cornell"):
+K_OPT_DEFAULT = 2863
+K_OPT_MATERIALS = 1 << 10
+
+
+def render_both(cam, w, h, spp, depth=8, preset="cornell", axis=True):
     sc = Scene()
     sc.add_preset(preset)
     pk = sc.build_packet()
     pt = PathTracer(w, h, max_depth=depth)
+    if axis:   # opt-in variant (the runtime drops the bit when the camera does not qualify)
+        lb = _lib.load()
+        lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
+        opt = K_OPT_DEFAULT | K_OPT_CAM_AXIS | (K_OPT_MATERIALS if preset == "cornell_lit" else 0)
+        _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, opt), "iqpt_debug_set_kernel_options")
     pt.set_camera(cam)
     pt.upload_packet(pk)
     pt.render(spp)
@@ -89,7 +99,7 @@ def test_pitch_camera_renders_match_oracle(require_gpu, pitch, pos):
     assert opt & K_OPT_CAM_AXIS
 
 
-def test_lit_scene_with_material_table_uses_short_camera(require_gpu):
+def test_lit_scene_with_material_table_short_camera(require_gpu):
     opt = render_both(make_camera(96, 64), 96, 64, 3, preset="cornell_lit")
     assert opt & K_OPT_CAM_AXIS
 
@@ -97,4 +107,9 @@ def test_lit_scene_with_material_table_uses_short_camera(require_gpu):
 def test_yawed_camera_keeps_general_transform(require_gpu):
     cam = make_camera(96, 64, position=(0.3, 0.5, -3.0, 0.0), forward=(-0.2, -0.5, 3.0, 0.0))
     opt = render_both(cam, 96, 64, 4)
+    assert not opt & K_OPT_CAM_AXIS
+
+
+def test_default_selection_keeps_general_transform(require_gpu):
+    opt = render_both(make_camera(96, 64), 96, 64, 2, axis=False)
     assert not opt & K_OPT_CAM_AXIS

@@ -84,3 +84,41 @@ def test_streamed_scene_with_materials(require_gpu):
     sc.set_model_material("ball", sc.add_material(MAT_OREN_NAYAR, (0.9, 0.9, 0.9, 0.0), 0.4))
     sc.set_model_material("light", sc.add_material(MAT_EMISSIVE, (1.0, 1.0, 1.0, 1.0), 8.0))
     run_both(sc, 96, 64, [2], 5, pixels=pixel_set(96, 64, 16, 80, 8, 1, 40))
+
+
+@pytest.mark.parametrize("frame0", [0, 2 ** 33, 2 ** 40])
+def test_tiny_colours_and_large_frame_counters(require_gpu, frame0):
+    """The running mean's short division (Markstein with RN(1/n) from the table) is exact only while
+    c / n is normal: colours near 2^-90 after 2^33 or 2^40 frames give subnormal quotients and must
+    take the IEEE division (kparams::mean_tiny), colours near 2^-100 and exact zeros too."""
+    import ctypes as C
+    from iqpt import _lib
+    sc = Scene()
+    sc.add_mesh_quad("quad")
+    sc.add_mesh_uv_sphere("sphere")
+    sc.add_model("wall", "quad", 3.0, 0.0, (0.0, 0.5, 1.0))
+    sc.add_model("floor", "quad", 3.0, (1.5707963267948966, 0, 0), (0.0, -0.5, 0.0))
+    sc.add_model("ball", "sphere", 0.35, 0.0, (0.0, 0.1, 0.3))
+    sc.set_model_material("wall", sc.add_material(MAT_EMISSIVE, (2.0 ** -88, 2.0 ** -92, 0.25, 1.0), 1.0))
+    sc.set_model_material("floor", sc.add_material(MAT_EMISSIVE, (2.0 ** -100, 0.0, 2.0 ** -80, 1.0), 1.0))
+    sc.set_model_material("ball", sc.add_material(MAT_OREN_NAYAR, (0.5, 0.5, 0.5, 0.0), 0.5))
+    pk = sc.build_packet()
+    w, h = 64, 48
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, max_depth=4)
+    lib = _lib.load()
+    lib.iqpt_debug_set_frame.argtypes = [C.c_void_p, C.c_uint64]
+    _lib.check(lib.iqpt_debug_set_frame(pt._h, frame0), "iqpt_debug_set_frame")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, max_depth=4)
+    fr.frame = frame0
+    for s in (3, 2):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    c = compare(lin, fr.lin)
+    assert c["bitexact"] == c["npix"], c
+    assert np.array_equal(bgra, fr.bgra)
+    if frame0:
+        assert np.any((lin[:, :3] > 0) & (lin[:, :3] < 2.0 ** -126))   # subnormal means were produced

@@ -115,8 +115,11 @@ def main():
         exact[name] = bool(np.array_equal(lin.view(np.uint32), ref[0].view(np.uint32))
                            and np.array_equal(bgra, ref[1]) and pt.rays() == ref[2])
     times = {n: [] for n in ctxs}
-    for _ in range(args.rounds):
-        for name, pt in ctxs.items():
+    names = list(ctxs)
+    for r in range(args.rounds):
+        # alternate the order every round (position effects: clocks, caches)
+        for name in (names if r % 2 == 0 else names[::-1]):
+            pt = ctxs[name]
             pt.sync()
             pt.kernel_time()
             pt.render(spp)
@@ -127,7 +130,8 @@ def main():
     for name in ctxs:
         med = statistics.median(times[name])
         res[name] = {"median_ms": round(med, 4), "min_ms": round(min(times[name]), 4),
-                     "vs_default": round(med / base, 4), "bitexact": exact[name]}
+                     "vs_default": round(med / base, 4), "bitexact": exact[name],
+                     "times_ms": [round(t, 4) for t in times[name]]}
     # stats variant (counters; slower, diagnostic only)
     stats = None
     pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
@@ -140,7 +144,24 @@ def main():
         except iqpt.IqptError as e:
             print("stats variant unavailable:", e, file=sys.stderr)
             spp = 0
+    timeline = None
     if spp:
+        cap = 65536
+        wt = (C.c_ulonglong * (3 * cap))()
+        nw = C.c_uint32(0)
+        lib.iqpt_debug_read_wave_times.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32,
+                                                   C.POINTER(C.c_uint32)]
+        if lib.iqpt_debug_read_wave_times(pt.handle, wt, cap, C.byref(nw)) == 0 and nw.value:
+            a = np.array(wt[:3 * nw.value], dtype=np.float64).reshape(-1, 3)
+            t0 = a[:, 0].min()
+            start_us, end_us = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0     # 100 MHz ticks
+            kern = end_us.max()
+            timeline = {"waves": int(nw.value), "kernel_us": round(kern, 1),
+                        "start_us_max": round(start_us.max(), 1),
+                        "end_us_pct": {str(q): round(float(np.percentile(end_us, q)), 1)
+                                       for q in (0, 1, 5, 10, 25, 50, 75, 90, 95, 99, 100)},
+                        "mean_lifetime_frac": round(float((end_us - start_us).mean() / kern), 4),
+                        "iters_pct": {str(q): int(np.percentile(a[:, 2], q)) for q in (0, 50, 100)}}
         s = (C.c_ulonglong * 16)()
         lib.iqpt_debug_read_stats(pt.handle, s)
         it, ready, active, sc_ex, sc_l, t_ex, t_l, waves = list(s)[:8]
@@ -151,7 +172,8 @@ def main():
                  "term_lanes_per_exec": t_l / max(1, t_ex), "rays": pt.rays(),
                  "tri_pair_tests_per_iter": tri_tests / max(1, it), "sph_pair_tests_per_iter": sph_tests / max(1, it),
                  "full_loop_iter_frac": full_iters / max(1, it)}
-    out = {"config": cfg.name, "spp": spp, "rounds": args.rounds, "variants": res, "stats_default": stats}
+    out = {"config": cfg.name, "spp": spp, "rounds": args.rounds, "variants": res, "stats_default": stats,
+           "wave_timeline": timeline}
     print(json.dumps(out, indent=1))
     if args.out:
         Path(args.out).write_text(json.dumps(out, indent=1))
