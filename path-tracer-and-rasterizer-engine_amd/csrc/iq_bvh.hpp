@@ -286,4 +286,139 @@ inline void build(build_input& in, build_output& out) {
     }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Sphere BVH (secondary rays in scenes with many spheres).
+//
+// The reference folds the spheres in packet order after the triangles (path_tracer.cu:283-295,
+// shape.cu:13-46): for each sphere, delta = halfb^2 - cc < 0 rejects; t = halfb - sqrt(delta) is
+// rejected if closest < t; if t < t_min the far root halfb + sqrt(delta) is taken WITHOUT the t_max
+// test (rejected only below t_min). So a sphere is one of
+//   * inert:   delta^ < 0 or t_far^ < t_min — never changes the state;
+//   * normal:  t_near^ >= t_min — "closest = min(closest, t_near^)", the later sphere on ties;
+//   * inside:  t_near^ < t_min <= t_far^ (the origin is inside or within ~1e-6 of it) — since
+//              closest >= t_min always holds, it sets closest = t_far^ unconditionally.
+// The fold is therefore order-free up to its LAST inside sphere j*: with none, the result is the
+// smallest t_near^ over normal spheres (largest index among equal t, a sphere beating a triangle
+// at equal t); with one, it is t_far^(j*) lowered by normal spheres of index > j* (same rule). A
+// traversal may visit spheres in any order if it never skips a non-inert sphere.
+//
+// Bound. With u = 2^-24, w = c - o (exact) and its computed oc (|oc_i - w_i| <= u |w_i|), |d| within
+// a few ulp of 1 (normalized, |d_i| <= 1.001), the kernel's delta^ differs from the exact
+// Delta(oc) = (d.oc)^2 - |oc|^2 + r^2 by at most 13.2 u |oc|^2 + 3 u r^2 (first order, forward error
+// of the operation sequence of shape.cu:16-25), and Delta(oc) = r^2 - |oc x d|^2 + |oc|^2 (|d|^2 - 1).
+// So delta^ >= 0 implies that the ray line passes within rho <= sqrt(r^2 + K) + 2 u S of the
+// centre, K = 12 u r^2 + 43 u S^2 (S >= |w|; the 2 u S covers oc's rounding). Each term is doubled
+// (safety 2), and sqrt(r^2 + K) - r = K / (sqrt(r^2 + K) + r) is evaluated without cancellation:
+//   growth(S) = K / (sqrt(r_min^2 + K) + r_min) + 4 u S + 8 u r_max,  K = 24 u r_max^2 + 86 u S^2
+// is an upper bound over a node's spheres (decreasing in r_min). The sphere then lies in its box
+// grown by growth(S). The computed roots are within 10 u S of the grown sphere's (the root error is
+// in |halfb^ - d.w| <= 4 u S and the square root of the already bounded delta), so a non-inert
+// sphere has t_far^ >= t_min and hence meets the half-line s >= t_min - 20 u S, and its t_near^ is
+// at least the grown box's entry minus 20 u S: a node whose entry exceeds the running closest by
+// more than that holds neither a better normal sphere nor an inside one (inside spheres have
+// t_near^ < t_min <= closest). Scenes with |c_i| or r above 2^60 get no sphere BVH (the bound
+// assumes no overflow; ray origins are bounded by bvh_ray_ok), and spheres much larger than the
+// median stay on an "always" list tested by every ray (their boxes would cover every node).
+struct sph_node {
+    float bmin[3];          // box of the subtree's spheres, centre -/+ radius (rounded outward)
+    uint32_t skip;
+    float bmax[3];
+    uint32_t first_count;   // leaf: first sphere slot << 8 | count (1..255); inner: 0
+    float rmin, rmax;       // radii of the subtree (rmin rounded down, rmax up)
+    float pad0, pad1;
+};
+static_assert(sizeof(sph_node) == 48, "sphere node is three float4");
+
+// growth(S) of the bound above in double (tests/test_sphere_bvh.py; the kernel evaluates the same
+// expression in float with upward rounding)
+inline double sphere_growth(double rmin, double rmax, double S) {
+    const double K = 24.0 * kU * rmax * rmax + 86.0 * kU * S * S;
+    return K / (std::sqrt(rmin * rmin + K) + rmin) + 4.0 * kU * S + 8.0 * kU * rmax;
+}
+
+constexpr uint32_t kLeafSpheres = 4;
+
+// centres/radii: float per sphere (c.xyz, r) in packet order; bvh: indices (packet order) of the
+// spheres put in the BVH. Median split on the longest centre axis. Fills the nodes (DFS preorder with
+// skip pointers) and the leaf order (packet indices).
+inline void build_spheres(const std::vector<float>& sph4, const std::vector<uint32_t>& ids,
+                          std::vector<sph_node>& nodes, std::vector<uint32_t>& order) {
+    nodes.clear();
+    order.clear();
+    if (ids.empty()) return;
+    std::vector<uint32_t> idx(ids);
+    struct frame {
+        uint32_t begin, end, node, stage;
+    };
+    std::vector<frame> st;
+    auto make = [&](uint32_t b, uint32_t e) {
+        sph_node n;
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        double rmin = INFINITY, rmax = 0.0;
+        for (uint32_t i = b; i < e; ++i) {
+            const float* s4 = &sph4[4 * (size_t)idx[i]];
+            const double r = std::fabs((double)s4[3]);
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], (double)s4[a] - r);
+                hi[a] = std::max(hi[a], (double)s4[a] + r);
+            }
+            rmin = std::min(rmin, r);
+            rmax = std::max(rmax, r);
+        }
+        for (int a = 0; a < 3; ++a) {
+            n.bmin[a] = round_down(lo[a]);
+            n.bmax[a] = round_up(hi[a]);
+        }
+        n.rmin = round_down(rmin);
+        n.rmax = round_up(rmax);
+        n.pad0 = n.pad1 = 0.0f;
+        n.skip = 0;
+        n.first_count = 0;
+        nodes.push_back(n);
+        return (uint32_t)nodes.size() - 1;
+    };
+    st.push_back({0, (uint32_t)idx.size(), make(0, (uint32_t)idx.size()), 0});
+    while (!st.empty()) {
+        frame& f = st.back();
+        const uint32_t count = f.end - f.begin;
+        if (count <= kLeafSpheres) {
+            const uint32_t first = (uint32_t)order.size();
+            for (uint32_t i = f.begin; i < f.end; ++i) order.push_back(idx[i]);
+            nodes[f.node].first_count = (first << 8) | count;
+            nodes[f.node].skip = (uint32_t)nodes.size();
+            st.pop_back();
+            continue;
+        }
+        if (f.stage == 0) {
+            float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (uint32_t i = f.begin; i < f.end; ++i)
+                for (int a = 0; a < 3; ++a) {
+                    cmin[a] = std::min(cmin[a], sph4[4 * (size_t)idx[i] + a]);
+                    cmax[a] = std::max(cmax[a], sph4[4 * (size_t)idx[i] + a]);
+                }
+            int ax = 0;
+            for (int a = 1; a < 3; ++a)
+                if (cmax[a] - cmin[a] > cmax[ax] - cmin[ax]) ax = a;
+            const uint32_t mid = f.begin + count / 2;
+            std::nth_element(idx.begin() + f.begin, idx.begin() + mid, idx.begin() + f.end,
+                             [&](uint32_t a, uint32_t b) {
+                                 const float ca = sph4[4 * (size_t)a + ax], cb = sph4[4 * (size_t)b + ax];
+                                 return ca < cb || (ca == cb && a < b);
+                             });
+            f.stage = 1;
+            const uint32_t b = f.begin;
+            const uint32_t n = make(b, mid);
+            st.push_back({b, mid, n, 0});
+        } else if (f.stage == 1) {
+            f.stage = 2;
+            const uint32_t mid = f.begin + count / 2, e = f.end;
+            const uint32_t n = make(mid, e);
+            st.push_back({mid, e, n, 0});
+        } else {
+            nodes[f.node].skip = (uint32_t)nodes.size();
+            st.pop_back();
+        }
+    }
+}
+
 }  // namespace iqbvh

@@ -105,7 +105,17 @@ struct kparams {
     const uint32_t* bvh_always;
     uint32_t bvh_nnodes, bvh_nalways;
     float bvh_md, bvh_gulp;
+    // exact sphere BVH (iq_bvh.hpp, streamed scenes with many spheres): nodes (kSphNodeFloat4 x float4:
+    // box min + skip, box max + leaf first << 8 | count, (r_min, r_max, -, -)), leaf spheres (centre,
+    // radius) with their packet indices, spheres outside the BVH (tested by every ray)
+    const float4_storage* sbvh_nodes;
+    const float4_storage* sbvh_sph;
+    const uint32_t* sbvh_idx;
+    const uint32_t* sbvh_always;
+    uint32_t sbvh_nnodes, sbvh_nalways;
+    float sbvh_gulp;
 };
+constexpr int kSphNodeFloat4 = 3;
 
 // Binning launch (iqpt_bin_kernel): the camera and pixel set of the context, the world-space scene.
 struct kbin {

@@ -836,6 +836,133 @@ __device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, floa
     }
 }
 
+// ---- exact sphere BVH (iq_bvh.hpp: the fold's inert / normal / inside spheres and the bound) ----
+// Order-free state of the sphere fold over the spheres seen so far: the best normal sphere (smallest
+// t_near, largest index on ties) among indices >= min_idx, and the last (largest-index) inside sphere.
+struct sph_fold {
+    float bt;         // best normal t_near (kTMax sentinel with bi = ~0u: none)
+    uint32_t bi;
+    float tin;        // t_far of the inside sphere iin
+    uint32_t iin;     // ~0u: none
+};
+
+// One sphere k with the reference's test (shape.cu:13-46, the operation sequence of test_sphere).
+template <int OPT>
+__device__ __forceinline__ void sph_visit(const float4 s, uint32_t k, const ray3 r, uint32_t min_idx, sph_fold& f,
+                                          float& bound) {
+    const float ocx = s.x - r.ox, ocy = s.y - r.oy, ocz = s.z - r.oz;
+    const float halfb = (r.dx * ocx + r.dy * ocy) + r.dz * ocz;
+    const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.w * s.w;
+    const float delta = halfb * halfb - cc;
+    if (delta < 0.0f) return;                                   // inert
+    const float sd = sqrt_any<OPT>(delta);
+    const float tn = halfb - sd;
+    if (tn < kTMin) {
+        const float tf = halfb + sd;
+        if (tf < kTMin) return;                                 // inert
+        if (f.iin == ~0u || k > f.iin) {                        // inside: the last one decides
+            f.iin = k;
+            f.tin = tf;
+        }
+        return;
+    }
+    if (k < min_idx) return;
+    if (tn < f.bt || (tn == f.bt && (f.bi == ~0u || k > f.bi))) {
+        f.bt = tn;
+        f.bi = k;
+        bound = fminf(bound, tn);
+    }
+}
+
+// Stackless traversal of the sphere BVH (skip pointers) plus the always-tested spheres, folding
+// into f; nodes whose grown box the ray cannot meet before `bound` (+ slack) are skipped.
+template <int OPT>
+__device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const bvh_ray br, float eps,
+                                          uint32_t min_idx, float bound, sph_fold& f) {
+    const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.sbvh_nodes);
+    const float4* __restrict__ leaf = reinterpret_cast<const float4*>(p.sbvh_sph);
+    const float u = 0x1p-24f, up = 1.0f + 0x1p-16f, slack = 8.0f * 0x1p-24f;
+    uint32_t i = 0;
+    while (i < p.sbvh_nnodes) {
+        const float4* nd = nodes + (size_t)kSphNodeFloat4 * i;
+        const float4 lo = nd[0], hi = nd[1], rr = nd[2];
+        const uint32_t skip = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
+        // S >= |c - o| for every centre of the node (box corners), rounded up
+        const float sx = fmaxf(iq_fabsf(r.ox - lo.x), iq_fabsf(r.ox - hi.x));
+        const float sy = fmaxf(iq_fabsf(r.oy - lo.y), iq_fabsf(r.oy - hi.y));
+        const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
+        const float S2 = ((sx * sx + sy * sy) + sz * sz) * up;
+        const float S = __builtin_sqrtf(S2) * up;
+        // growth(S) of iq_bvh.hpp with the ray's |d|^2 deviation eps folded in (rounded up)
+        const float K = ((24.0f * u) * (rr.y * rr.y) + (86.0f * u + 2.01f * eps) * S2) * (1.0f + 0x1p-8f) +
+                        (2.01f * eps) * (rr.y * rr.y);
+        const float g = (K * __builtin_amdgcn_rcpf(__builtin_sqrtf(rr.x * rr.x + K) + rr.x) * (1.0f + 0x1p-12f) +
+                         (4.0f * u) * S + (8.0f * u) * rr.y) * up + p.sbvh_gulp;
+        const float dts = ((20.0f * u + 4.0f * eps) * S) * up + 1e-30f;
+        float t0x = ((lo.x - g) - r.ox) * br.ix, t1x = ((hi.x + g) - r.ox) * br.ix;
+        float t0y = ((lo.y - g) - r.oy) * br.iy, t1y = ((hi.y + g) - r.oy) * br.iy;
+        float t0z = ((lo.z - g) - r.oz) * br.iz, t1z = ((hi.z + g) - r.oz) * br.iz;
+        float ax0 = fminf(t0x, t1x), ax1 = fmaxf(t0x, t1x);
+        float ay0 = fminf(t0y, t1y), ay1 = fmaxf(t0y, t1y);
+        float az0 = fminf(t0z, t1z), az1 = fmaxf(t0z, t1z);
+        if (t0x != t0x || t1x != t1x) { ax0 = -INFINITY; ax1 = INFINITY; }
+        if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
+        if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
+        float enter = fmaxf(fmaxf(ax0, ay0), az0), exit = fminf(fminf(ax1, ay1), az1);
+        enter = enter - iq_fabsf(enter) * slack;
+        exit = exit + iq_fabsf(exit) * slack;
+        const bool hit = enter <= exit && exit >= kTMin - dts && enter <= bound + dts;
+        if (hit && fc != 0u) {
+            const uint32_t first = fc >> 8, cnt = fc & 0xffu;
+            for (uint32_t k = 0; k < cnt; ++k)
+                sph_visit<OPT>(leaf[first + k], p.sbvh_idx[first + k], r, min_idx, f, bound);
+        }
+        i = (hit && fc == 0u) ? i + 1 : skip;
+    }
+    const float4* __restrict__ sph = reinterpret_cast<const float4*>(p.spheres);
+    for (uint32_t a = 0; a < p.sbvh_nalways; ++a) {
+        const uint32_t k = p.sbvh_always[a];
+        sph_visit<OPT>(sph[k], k, r, min_idx, f, bound);
+    }
+}
+
+// The spheres' part of the closest hit (after the triangles) through the sphere BVH: the reference's
+// in-order fold (path_tracer.cu:283-295) from its order-free form (iq_bvh.hpp). A ray whose |d|^2 is
+// not within 2^-10 of 1 folds over every sphere in packet order instead.
+template <int OPT>
+__device__ __forceinline__ void sbvh_closest(const kparams& p, const ray3 r, float& closest, int& kind,
+                                             uint32_t& idx) {
+    const bvh_ray br = bvh_ray_setup(r);
+    const float dd = (r.dx * r.dx + r.dy * r.dy) + r.dz * r.dz;
+    const float eps = iq_fabsf(dd - 1.0f) + 8.0f * 0x1p-24f;
+    if (!(eps <= 0x1p-10f)) {
+        const float4* __restrict__ sph = reinterpret_cast<const float4*>(p.spheres);
+        for (uint32_t k = 0; k < p.nsph; ++k) test_sphere<OPT>(sph[k], r, closest, kind, idx, k);
+        return;
+    }
+    sph_fold f = {kTMax, ~0u, 0.0f, ~0u};
+    sbvh_pass<OPT>(p, r, br, eps, 0u, closest, f);
+    if (f.iin == ~0u) {
+        // no inside sphere: min(closest, best normal), the sphere on ties
+        if (f.bi != ~0u && !(closest < f.bt)) {
+            closest = f.bt;
+            kind = kHitSphere;
+            idx = f.bi;
+        }
+        return;
+    }
+    // the last inside sphere sets closest = its far root; normal spheres after it lower it
+    closest = f.tin;
+    kind = kHitSphere;
+    idx = f.iin;
+    sph_fold g = {kTMax, ~0u, 0.0f, ~0u};
+    sbvh_pass<OPT>(p, r, br, eps, f.iin + 1u, closest, g);
+    if (g.bi != ~0u && !(closest < g.bt)) {
+        closest = g.bt;
+        idx = g.bi;
+    }
+}
+
 // The running-mean table occupies spp float2 of dynamic LDS when the launch builds it.
 __device__ __forceinline__ bool use_tab_lds(const kparams& p) { return p.acc_tab != 0u; }
 
@@ -910,6 +1037,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                        s_term_lanes = 0;
     unsigned long long s_tests[2] = {0, 0};   // wave-level triangle / sphere pair tests (culled resident path)
     unsigned long long s_full = 0;            // iterations forced to the full loop (a secondary ray in the wave)
+    unsigned long long s_refill = 0, s_refill_lanes = 0;   // refills that started pixels, pixels started
 
     // ---- wave-uniform chunk state: the current tile [chunk_next, chunk_end) of tile-major storage
     uint32_t chunk_tile = 0;
@@ -979,6 +1107,11 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 }
                 active = true;
             }
+            if (OPT & kOptStats) {
+                const uint32_t got = min((uint32_t)__popcll(need), avail);
+                s_refill += got ? 1ull : 0ull;
+                s_refill_lanes += got;
+            }
             const uint32_t cnt = (uint32_t)__popcll(need);
             chunk_next += cnt < avail ? cnt : avail;
             need = __ballot(!active);
@@ -1013,14 +1146,22 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             // a secondary ray that takes the BVH (kOptBvh) contributes nothing to the triangle batches,
             // any other ray every pair; the wave ORs the words, the block skips a batch nobody needs.
             constexpr bool kWords = kCull || kBvh;
-            const bool bvh_lane = kBvh && p.bvh_nodes != nullptr && active && (depth != 0 || kBvhPrimary) &&
-                                  bvh_ray_ok(p, ray);
+            const bool bvh_ray = kBvh && active && (depth != 0 || kBvhPrimary) &&
+                                 (p.bvh_nodes != nullptr || p.sbvh_nodes != nullptr) && bvh_ray_ok(p, ray);
+            const bool bvh_lane = bvh_ray && p.bvh_nodes != nullptr;
             const uint32_t* tile_mask =
                 (kCull && p.cull != nullptr && active && depth == 0)
                     ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
             const uint32_t* tri_mask = bvh_lane ? nullptr : tile_mask;
             const bool tri_all = active && tile_mask == nullptr && !bvh_lane;
-            const bool sph_all = active && tile_mask == nullptr;
+            // the spheres through the sphere BVH (same rays as the triangle BVH) instead of the batches
+            const bool sbvh_lane = bvh_ray && p.sbvh_nodes != nullptr;
+            // kOptDiag timing ablations (A/B builds, not exact): 8 = secondary rays skip the spheres,
+            // 16 = secondary rays skip the triangle BVH
+            const bool diag_nosph = (OPT & kOptDiag) && (p.diag & 8u) && depth != 0;
+            const bool diag_nobvh = (OPT & kOptDiag) && (p.diag & 16u) && depth != 0;
+            const bool sph_all = active && tile_mask == nullptr && !diag_nosph && !sbvh_lane;
+            const uint32_t* sph_mask = sbvh_lane ? nullptr : tile_mask;
             // the whole block skips the triangle batches when every ray takes the BVH
             const bool tri_block = !kWords || __syncthreads_or((tri_all || tri_mask != nullptr) ? 1 : 0);
             for (uint32_t base = 0; tri_block && base < tri_recs; base += p.tri_batch) {
@@ -1068,7 +1209,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 }
             }
             // secondary rays: triangles through the exact BVH (iq_bvh.hpp), before the spheres
-            if (bvh_lane) bvh_closest<OPT>(p, ray, closest, kind, hidx);
+            if (bvh_lane && !diag_nobvh) bvh_closest<OPT>(p, ray, closest, kind, hidx);
             for (uint32_t base = 0; base < sph_recs; base += p.sph_batch) {
                 const uint32_t n = min(p.sph_batch, sph_recs - base);
                 uint32_t wm[kWords ? 8 : 1];
@@ -1080,7 +1221,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         const uint32_t w = p.cull_wt + base / 32u + (uint32_t)i;
                         wm[i] = 0u;
                         if ((uint32_t)i * 32u < n)
-                            wm[i] = wave_or(sph_all ? ~0u : (tile_mask ? tile_mask[w] : 0u));
+                            wm[i] = wave_or(sph_all ? ~0u : (sph_mask ? sph_mask[w] : 0u));
                         any = any || wm[i] != 0u;
                     }
                     if (!__syncthreads_or(any ? 1 : 0)) continue;
@@ -1090,7 +1231,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 for (uint32_t i = threadIdx.x; i < n * kSphRec; i += kRenderBlock)
                     lds_sph[i] = g_sph[(size_t)base * kSphRec + i];
                 __syncthreads();
-                if (active) {
+                if (active && !diag_nosph && !sbvh_lane) {
                     const uint32_t first = base * kSphPer;
                     const uint32_t cnt = min(n * kSphPer, p.nsph - first);
                     if (kWords) {
@@ -1111,6 +1252,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     }
                 }
             }
+            if (sbvh_lane && !diag_nosph) sbvh_closest<OPT>(p, ray, closest, kind, hidx);
         } else if ((OPT & kOptDiag) && (p.diag & 2u)) {
             // diagnostic: no intersection; every ray hits triangle 0 at t = 1
             if (active) {
@@ -1328,6 +1470,8 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             atomicAdd(p.stats + 8, s_tests[0]);
             atomicAdd(p.stats + 9, s_tests[1]);
             atomicAdd(p.stats + 10, s_full);
+            atomicAdd(p.stats + 12, s_refill);
+            atomicAdd(p.stats + 13, s_refill_lanes);
             // wave timeline (s_memrealtime, 100 MHz): start, end, iterations per wave
             const uint64_t slot = atomicAdd(p.stats + 11, 1ull);
             if (slot < kStatsWaveSlots) {
@@ -1557,6 +1701,7 @@ const variant kVariants[] = {
     IQPT_V(8, false, kOptDefault & ~kOptCull & ~kOptFastDiv),
     IQPT_V(8, true, kOptDefault & ~kOptBvh),
     IQPT_V(8, false, kOptDefault | kOptDiag),
+    IQPT_V(8, true, ((kOptDefault | kOptBvhPrimary | kOptDiag) & ~kOptLB5)),
     IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptExp),
     IQPT_V(8, true, (kOptDefault | kOptMaterials) & ~kOptBvh),
 #endif

@@ -104,6 +104,13 @@ struct iqpt_ctx {
     uint32_t* d_bvh_always = nullptr;
     uint32_t bvh_nnodes = 0, bvh_nalways = 0;
     float bvh_md = 0.0f, bvh_gulp = 0.0f;
+    // exact sphere BVH (iq_bvh.hpp), null when the packet has few spheres
+    float4_storage* d_sbvh_nodes = nullptr;
+    float4_storage* d_sbvh_sph = nullptr;
+    uint32_t* d_sbvh_idx = nullptr;
+    uint32_t* d_sbvh_always = nullptr;
+    uint32_t sbvh_nnodes = 0, sbvh_nalways = 0;
+    float sbvh_gulp = 0.0f;
     bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
     // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
     uint32_t* d_cull = nullptr;
@@ -137,12 +144,14 @@ void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, f
 
 void free_scene(iqpt_ctx* c) {
     for (float4_storage** b : {&c->d_tris, &c->d_tri_pairs, &c->d_tri_shade, &c->d_sph, &c->d_sph_pairs, &c->d_mats,
-                               &c->d_bvh_nodes, &c->d_bvh_pairs}) {
+                               &c->d_bvh_nodes, &c->d_bvh_pairs, &c->d_sbvh_nodes, &c->d_sbvh_sph}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
     c->bvh_nnodes = c->bvh_nalways = 0;
-    for (uint32_t** b : {&c->d_tri_mat, &c->d_sph_mat, &c->d_bvh_pidx, &c->d_bvh_always}) {
+    c->sbvh_nnodes = c->sbvh_nalways = 0;
+    for (uint32_t** b : {&c->d_tri_mat, &c->d_sph_mat, &c->d_bvh_pidx, &c->d_bvh_always, &c->d_sbvh_idx,
+                         &c->d_sbvh_always}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
@@ -384,6 +393,62 @@ bool build_bvh(const std::vector<float4_storage>& tris, const std::vector<float4
         float* dst = &out.pairs[(q / 2) * iqpt::kTriPairFloat4].x;
         for (int comp = 0; comp < 9; ++comp) dst[2 * comp + (q & 1)] = f[comp];
     }
+    return true;
+}
+
+// Exact sphere BVH (iq_bvh.hpp) over the world-space spheres (center.xyz, radius): spheres much larger
+// than the median stay on the always-tested list. None for few spheres or coordinates beyond 2^60.
+struct sbvh_host {
+    std::vector<float4_storage> nodes, sph;
+    std::vector<uint32_t> idx, always;
+    float gulp;
+};
+constexpr uint32_t kSbvhMinSpheres = 64;
+
+bool build_sbvh(const std::vector<float4_storage>& sph, sbvh_host& out) {
+    const size_t n = sph.size();
+    if (n < kSbvhMinSpheres) return false;
+    std::vector<float> s4(4 * n), radii(n);
+    double maxabs = 0.0;
+    for (size_t k = 0; k < n; ++k) {
+        const float v[4] = {sph[k].x, sph[k].y, sph[k].z, sph[k].w};
+        for (int a = 0; a < 4; ++a) {
+            if (!std::isfinite(v[a]) || std::fabs(v[a]) > 0x1p60f) return false;
+            s4[4 * k + a] = v[a];
+        }
+        radii[k] = std::fabs(v[3]);
+        for (int a = 0; a < 3; ++a) maxabs = std::max(maxabs, std::fabs((double)v[a]) + std::fabs((double)v[3]));
+    }
+    std::vector<float> sorted(radii);
+    std::nth_element(sorted.begin(), sorted.begin() + n / 2, sorted.end());
+    const double big = 8.0 * (double)sorted[n / 2];
+    std::vector<uint32_t> ids;
+    for (size_t k = 0; k < n; ++k) {
+        if ((double)radii[k] > big) out.always.push_back((uint32_t)k);
+        else ids.push_back((uint32_t)k);
+    }
+    std::vector<iqbvh::sph_node> nodes;
+    std::vector<uint32_t> order;
+    iqbvh::build_spheres(s4, ids, nodes, order);
+    for (const iqbvh::sph_node& nd : nodes) {
+        float4_storage lo, hi;
+        lo.x = nd.bmin[0];
+        lo.y = nd.bmin[1];
+        lo.z = nd.bmin[2];
+        std::memcpy(&lo.w, &nd.skip, 4);
+        hi.x = nd.bmax[0];
+        hi.y = nd.bmax[1];
+        hi.z = nd.bmax[2];
+        std::memcpy(&hi.w, &nd.first_count, 4);
+        out.nodes.push_back(lo);
+        out.nodes.push_back(hi);
+        out.nodes.push_back(float4_storage{nd.rmin, nd.rmax, 0.0f, 0.0f});
+    }
+    for (uint32_t k : order) out.sph.push_back(sph[k]);
+    out.idx = order;
+    // a grown box side lo - g rounds to nearest: |error| <= 2^-24 (maxabs + g), covered by gulp and
+    // the kernel's (1 + 2^-16) on g
+    out.gulp = iqbvh::round_up(maxabs * 0x1p-22);
     return true;
 }
 
@@ -693,6 +758,8 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
     };
     bvh_host bvh;
     const bool have_bvh = build_bvh(tris, sph, bvh);
+    sbvh_host sbvh;
+    const bool have_sbvh = build_sbvh(sph, sbvh);
     auto upload_u32 = [&](const std::vector<uint32_t>& v, uint32_t** dst) -> int {
         if (v.empty()) return IQPT_OK;
         if (hipMalloc(dst, v.size() * sizeof(uint32_t)) != hipSuccess)
@@ -705,9 +772,17 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         (st = upload(sph_pairs, &c->d_sph_pairs)) || (st = upload(mats, &c->d_mats)) ||
         (st = upload_u32(tri_mat, &c->d_tri_mat)) || (st = upload_u32(sph_mat, &c->d_sph_mat)) ||
         (have_bvh && ((st = upload(bvh.nodes, &c->d_bvh_nodes)) || (st = upload(bvh.pairs, &c->d_bvh_pairs)) ||
-                      (st = upload_u32(bvh.pidx, &c->d_bvh_pidx)) || (st = upload_u32(bvh.always, &c->d_bvh_always))))) {
+                      (st = upload_u32(bvh.pidx, &c->d_bvh_pidx)) || (st = upload_u32(bvh.always, &c->d_bvh_always)))) ||
+        (have_sbvh && ((st = upload(sbvh.nodes, &c->d_sbvh_nodes)) || (st = upload(sbvh.sph, &c->d_sbvh_sph)) ||
+                       (st = upload_u32(sbvh.idx, &c->d_sbvh_idx)) ||
+                       (st = upload_u32(sbvh.always, &c->d_sbvh_always))))) {
         free_scene(c);
         return st;
+    }
+    if (have_sbvh) {
+        c->sbvh_nnodes = (uint32_t)(sbvh.nodes.size() / iqpt::kSphNodeFloat4);
+        c->sbvh_nalways = (uint32_t)sbvh.always.size();
+        c->sbvh_gulp = sbvh.gulp;
     }
     if (have_bvh) {
         c->bvh_nnodes = (uint32_t)(bvh.nodes.size() / iqpt::kBvhNodeFloat4);
@@ -796,6 +871,16 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         p.bvh_nalways = c->bvh_nalways;
         p.bvh_md = c->bvh_md;
         p.bvh_gulp = c->bvh_gulp;
+    }
+    if (c->d_sbvh_nodes && c->sbvh_nnodes) {
+        p.sbvh_nodes = c->d_sbvh_nodes;
+        p.sbvh_sph = c->d_sbvh_sph;
+        p.sbvh_idx = c->d_sbvh_idx;
+        p.sbvh_always = c->d_sbvh_always;
+        p.sbvh_nnodes = c->sbvh_nnodes;
+        p.sbvh_nalways = c->sbvh_nalways;
+        p.sbvh_gulp = c->sbvh_gulp;
+        p.bvh_md = 1.001f;          // bvh_ray_ok: |d_i| bound shared with the triangle BVH
     }
     p.mats = c->d_mats;
     p.tri_shade = c->d_tri_shade;
@@ -1169,6 +1254,19 @@ int iqpt_debug_bvh_info(iqpt_ctx* c, uint32_t* nnodes, uint32_t* nalways) {
     *nalways = c->d_bvh_nodes ? c->bvh_nalways : 0u;
     return IQPT_OK;
 }
+
+/* Internal (tests/test_gpu_sphere_bvh.py): the sphere BVH of the uploaded packet — node count and the
+ * number of spheres on the always-tested list (both 0 without one). */
+int iqpt_debug_sbvh_info(iqpt_ctx* c, uint32_t* nnodes, uint32_t* nalways) {
+    if (!c || !nnodes || !nalways) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *nnodes = c->d_sbvh_nodes ? c->sbvh_nnodes : 0u;
+    *nalways = c->d_sbvh_nodes ? c->sbvh_nalways : 0u;
+    return IQPT_OK;
+}
+
+/* Internal (tests/test_sphere_bvh.py): the sphere bound of iq_bvh.hpp, growth(S) for radii r_min,
+ * r_max at origin distance S. */
+double iqpt_debug_sphere_growth(double rmin, double rmax, double S) { return iqbvh::sphere_growth(rmin, rmax, S); }
 
 /* Internal (tests/test_bvh.py): the error bound of iq_bvh.hpp for one triangle's edges, evaluated
  * at S = max_i |o_i - v0_i| and a lower bound D of the accepted determinant (D <= 1e-6: the reject
