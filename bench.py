@@ -43,6 +43,7 @@ from iqpt import dist as iqdist  # noqa: E402
 from iqpt.scene import CONFIGS, Scene, make_camera, packet_stats  # noqa: E402
 
 FP32_PEAK_TFLOPS = 157.3        # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
+HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E peak, MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec
 
 
@@ -57,8 +58,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--verify-rows", type=int, default=16)
-    ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r01_pmc_traffic.json"))
-    ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r01_c2_pmc_mix_v3.json"),
+    ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r01_pmc_traffic_v2.json"))
+    ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r01_c2_pmc_mix_v4.json"),
                     help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy)")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo = rehearsal)")
@@ -238,12 +239,14 @@ def main():
             except Exception:
                 traffic = None
         valu_busy = None
+        wave_split = None
         mix_path = Path(args.pmc_mix_json)
         if mix_path.exists():
             try:
                 mix = json.loads(mix_path.read_text())
                 if mix.get("config") == cfg.name and world == 1:
                     valu_busy = mix.get("valu_busy_frac")
+                    wave_split = mix.get("wave_time_split")
             except Exception:
                 valu_busy = None
         # weak: every rank renders the whole frame; strong: the ranks share one frame
@@ -286,11 +289,18 @@ def main():
                 "kernel_avg_ms": round(kern_avg_ms, 4),
                 "flops_per_ray": f_ray,
                 "valu_busy_frac": valu_busy,
+                "wave_time_split": wave_split,
+                "hbm": ({"achieved": round(traffic / (kern_avg_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": round(traffic / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
+                        if traffic and kern_avg_ms > 0 else None),
                 "note": "algorithmic FLOPs F_ray = 52 T + 19 S (SURVEY.md §8d) x rays per launch / HIP-event "
                         "kernel time; FP32 vector peak (no MFMA: nothing here is a dense contraction). "
                         "valu_busy_frac: share of SIMD time with a VALU instruction in flight (PMC "
-                        "SQ_ACTIVE_INST_VALU, profiles/): the kernel is VALU-issue bound; the FLOP fraction is "
-                        "low because MT/RNG/compare instructions are not FMA-dense"
+                        "SQ_ACTIVE_INST_VALU); wave_time_split: issuing / ready but behind other waves / parked "
+                        "on s_waitcnt (LDS and memory latency), profiles/. The VALU pipe is ~0.9 busy but the "
+                        "launch is not set by VALU issue alone (DESIGN.md §3.1); the FLOP fraction is low "
+                        "because MT/RNG/compare instructions are not FMA-dense. hbm: PMC bytes per launch "
+                        "(traffic) over the kernel time against 8 TB/s"
                         + ("; frac > 1: the reference's brute-force tests per ray, most of which the tile masks "
                            "and the BVH skip (DESIGN.md §5)" if achieved_tflops > FP32_PEAK_TFLOPS else ""),
             },

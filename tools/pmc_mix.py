@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Instruction mix and wave-time breakdown of the render kernel from rocprofv3 PMC passes.
+
+Pass A: SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32
+Pass B: SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE
+(each in its own run with --kernel-trace only). SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count
+quad-cycles; WAIT_ANY (parked on s_waitcnt / barrier) + WAIT_INST_ANY (ready, not issued) +
+ACTIVE_INST_ANY ~= WAVE_CYCLES (MI355X_MICROARCH.md, rocprofv3 PMC slots). GRBM_GUI_ACTIVE is summed
+over the 8 XCDs: kernel cycles = GRBM_GUI_ACTIVE / 8. valu_busy_frac = VALU-active cycles per SIMD
+over the kernel's cycles (1024 SIMDs).
+
+usage: pmc_mix.py <passA.csv> <passB.csv> <config> <wave_iterations_per_launch> <out.json> [label]
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+SIMDS = 256 * 4
+
+
+def last_dispatch(path):
+    agg = defaultdict(lambda: defaultdict(float))
+    dur = {}
+    with open(path) as f:
+        for r in csv.DictReader(f):
+            if "iqpt_render_kernel" not in r.get("Kernel_Name", ""):
+                continue
+            agg[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+            dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    if not agg:
+        raise SystemExit(f"no iqpt_render_kernel rows in {path}")
+    d = sorted(agg, key=int)[-1]
+    return dict(agg[d]), dur[d]
+
+
+def main():
+    a_csv, b_csv, config, iters, out = sys.argv[1:6]
+    label = sys.argv[6] if len(sys.argv) > 6 else ""
+    iters = float(iters)
+    a, _ = last_dispatch(a_csv)
+    b, dur = last_dispatch(b_csv)
+    kcycles = b["GRBM_GUI_ACTIVE"] / 8.0
+    wave = b["SQ_WAVE_CYCLES"]
+    res = {
+        "config": config,
+        "kernel": label or "iqpt_render_kernel",
+        "wave_iterations_per_launch": iters,
+        "counters": {**a, **b},
+        "per_iteration": {k: round(v / iters, 2) for k, v in a.items() if k.startswith("SQ_INSTS")},
+        "kernel_ms_profiled": round(dur * 1e3, 4),
+        "clock_ghz": round(kcycles / dur / 1e9, 3),
+        "valu_busy_frac": round(b["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / kcycles, 3),
+        "wave_time_split": {"issuing": round(b["SQ_ACTIVE_INST_ANY"] / wave, 3),
+                            "ready_not_issued": round(b["SQ_WAIT_INST_ANY"] / wave, 3),
+                            "parked_on_waitcnt": round(b["SQ_WAIT_ANY"] / wave, 3)},
+        "mean_waves_per_simd": round(wave * 4 / SIMDS / kcycles, 2),
+    }
+    with open(out, "w") as fh:
+        json.dump(res, fh, indent=1)
+    print(json.dumps(res))
+
+
+if __name__ == "__main__":
+    main()
