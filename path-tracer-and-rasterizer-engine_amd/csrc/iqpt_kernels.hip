@@ -1162,6 +1162,32 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             const bool diag_nobvh = (OPT & kOptDiag) && (p.diag & 16u) && depth != 0;
             const bool sph_all = active && tile_mask == nullptr && !diag_nosph && !sbvh_lane;
             const uint32_t* sph_mask = sbvh_lane ? nullptr : tile_mask;
+            // One tile for every lane that contributes mask words (and no lane that needs every pair): the
+            // wave's OR is that tile's mask, read with uniform loads instead of a DPP OR per word
+            // (camera-ray waves, the usual case); no contributing lane at all: every word is 0.
+            const uint32_t* uni_tri = nullptr;
+            const uint32_t* uni_sph = nullptr;
+            bool tri_none = false, sph_none = false;
+            if (kCull && p.cull != nullptr) {
+                const uint32_t tile = lds_cm[threadIdx.x].z;
+                const uint64_t mt = __ballot(tri_mask != nullptr), ms = __ballot(sph_mask != nullptr);
+                if (__ballot(tri_all) == 0ull) {
+                    if (mt == 0ull) {
+                        tri_none = true;
+                    } else {
+                        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(mt));
+                        if (__ballot(tri_mask != nullptr && tile != t0) == 0ull) uni_tri = p.cull + (size_t)t0 * p.cull_stride;
+                    }
+                }
+                if (__ballot(sph_all) == 0ull) {
+                    if (ms == 0ull) {
+                        sph_none = true;
+                    } else {
+                        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(ms));
+                        if (__ballot(sph_mask != nullptr && tile != t0) == 0ull) uni_sph = p.cull + (size_t)t0 * p.cull_stride;
+                    }
+                }
+            }
             // the whole block skips the triangle batches when every ray takes the BVH
             const bool tri_block = !kWords || __syncthreads_or((tri_all || tri_mask != nullptr) ? 1 : 0);
             for (uint32_t base = 0; tri_block && base < tri_recs; base += p.tri_batch) {
@@ -1176,7 +1202,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         const uint32_t w = base / 32u + (uint32_t)i;
                         wm[i] = 0u;
                         if ((uint32_t)i * 32u < n)
-                            wm[i] = wave_or(tri_all ? ~0u : (tri_mask ? tri_mask[w] : 0u));
+                            wm[i] = tri_none ? 0u
+                                             : (uni_tri ? uni_tri[w]
+                                                        : wave_or(tri_all ? ~0u : (tri_mask ? tri_mask[w] : 0u)));
                         any = any || wm[i] != 0u;
                     }
                     // the barrier also orders this batch's LDS writes after the previous batch's reads
@@ -1187,7 +1215,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 for (uint32_t i = threadIdx.x; i < n * kTriRec; i += kRenderBlock)
                     lds_tri[i] = g_tri[(size_t)base * kTriRec + i];
                 __syncthreads();
-                if (active && !bvh_lane) {
+                if (active && !bvh_lane && !((OPT & kOptDiag) && (p.diag & 32u))) {   // diag 32: no pair tests
                     const uint32_t first = base * kTriPer;
                     const uint32_t cnt = min(n * kTriPer, p.ntri - first);
                     if (kWords) {
@@ -1221,7 +1249,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         const uint32_t w = p.cull_wt + base / 32u + (uint32_t)i;
                         wm[i] = 0u;
                         if ((uint32_t)i * 32u < n)
-                            wm[i] = wave_or(sph_all ? ~0u : (sph_mask ? sph_mask[w] : 0u));
+                            wm[i] = sph_none ? 0u
+                                             : (uni_sph ? uni_sph[w]
+                                                        : wave_or(sph_all ? ~0u : (sph_mask ? sph_mask[w] : 0u)));
                         any = any || wm[i] != 0u;
                     }
                     if (!__syncthreads_or(any ? 1 : 0)) continue;
@@ -1702,6 +1732,7 @@ const variant kVariants[] = {
     IQPT_V(8, true, kOptDefault & ~kOptBvh),
     IQPT_V(8, false, kOptDefault | kOptDiag),
     IQPT_V(8, true, ((kOptDefault | kOptBvhPrimary | kOptDiag) & ~kOptLB5)),
+    IQPT_V(8, true, ((kOptDefault | kOptDiag) & ~kOptLB5)),
     IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptExp),
     IQPT_V(8, true, (kOptDefault | kOptMaterials) & ~kOptBvh),
 #endif
