@@ -86,6 +86,11 @@ struct kparams {
     // masks, most expensive tiles first (longest-processing-time order: a shorter launch tail)
     const uint32_t* tile_order;
     uint32_t ntx, ntiles;            // tiles of the owned set (kCullTile x kCullTile)
+    // candidate lists of the masks (streamed scenes): ascending pair indices of tile t's set bits at
+    // list[off_tri[t] .. off_tri[t + 1]) and list[off_sph[t] .. off_sph[t + 1]); null = none
+    const uint32_t* list;
+    const uint32_t* list_off_tri;
+    const uint32_t* list_off_sph;
     // kOptMaterials (packet material table): material index per triangle / sphere, the material
     // records (2 x float4 each: (albedo.rgb, type bits), (strength | sigma, A, B, 0)) and the
     // triangle shading records (kTriShadeFloat4 per triangle)
@@ -189,9 +194,11 @@ int launch_relayout(void* stream, const uint32_t* src, uint32_t* dst, uint32_t n
                     uint32_t words, uint32_t planes, bool to_compact);
 // Tile masks for kOptCull (one thread per tile word).
 int launch_bin(void* stream, const kbin& b);
-// Per-tile cost estimate from the masks: set triangle-pair bits + 8 x set sphere-pair bits.
-int launch_tile_cost(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
-                     uint32_t* cost);
+// Per-tile candidate counts from the masks (triangle pairs, sphere pairs), and the candidate lists.
+int launch_tile_count(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
+                      uint32_t* cnt_tri, uint32_t* cnt_sph);
+int launch_tile_list(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
+                     const uint32_t* off_tri, const uint32_t* off_sph, uint32_t* list);
 // Device probe of the camera transforms (iqpt_debug_camera_rays): general and kOptCamAxis forms.
 int launch_camera_probe(void* stream, const kparams& p, const float* ndc, float* gen, float* axis, uint32_t n,
                         bool do_axis);

@@ -1168,6 +1168,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             const uint32_t* uni_tri = nullptr;
             const uint32_t* uni_sph = nullptr;
             bool tri_none = false, sph_none = false;
+            uint32_t tt = 0, ts = 0;                      // the uniform tiles
             if (kCull && p.cull != nullptr) {
                 const uint32_t tile = lds_cm[threadIdx.x].z;
                 const uint64_t mt = __ballot(tri_mask != nullptr), ms = __ballot(sph_mask != nullptr);
@@ -1175,21 +1176,40 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     if (mt == 0ull) {
                         tri_none = true;
                     } else {
-                        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(mt));
-                        if (__ballot(tri_mask != nullptr && tile != t0) == 0ull) uni_tri = p.cull + (size_t)t0 * p.cull_stride;
+                        tt = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(mt));
+                        if (__ballot(tri_mask != nullptr && tile != tt) == 0ull) uni_tri = p.cull + (size_t)tt * p.cull_stride;
                     }
                 }
                 if (__ballot(sph_all) == 0ull) {
                     if (ms == 0ull) {
                         sph_none = true;
                     } else {
-                        const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(ms));
-                        if (__ballot(sph_mask != nullptr && tile != t0) == 0ull) uni_sph = p.cull + (size_t)t0 * p.cull_stride;
+                        ts = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(ms));
+                        if (__ballot(sph_mask != nullptr && tile != ts) == 0ull) uni_sph = p.cull + (size_t)ts * p.cull_stride;
                     }
                 }
             }
-            // the whole block skips the triangle batches when every ray takes the BVH
-            const bool tri_block = !kWords || __syncthreads_or((tri_all || tri_mask != nullptr) ? 1 : 0);
+            // A uniform-tile wave takes its tile's candidate pairs from the candidate list (ascending
+            // pair indices: the order of the masked batch loop, so the same closest hit), reading each
+            // pair straight from global memory with wave-uniform loads, and needs none of the batches.
+            const bool list_tri = uni_tri != nullptr && p.list != nullptr;
+            const bool list_sph = uni_sph != nullptr && p.list != nullptr;
+            if (list_tri) {
+                const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
+                const uint32_t a = p.list_off_tri[tt], b = p.list_off_tri[tt + 1];
+                for (uint32_t e = a; e < b; ++e) {
+                    const uint32_t j = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[e]);
+                    if (tri_mask != nullptr) {
+                        const float4* q = gp + (size_t)j * kTriPairFloat4;
+                        test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
+                                                2 * j + 1 < p.ntri);
+                    }
+                }
+                tri_none = true;                          // nothing left for the batches from this wave
+            }
+            // the whole block skips the triangle batches when every ray takes the BVH or a list
+            const bool tri_block =
+                !kWords || __syncthreads_or((tri_all || (tri_mask != nullptr && !list_tri)) ? 1 : 0);
             for (uint32_t base = 0; tri_block && base < tri_recs; base += p.tri_batch) {
                 const uint32_t n = min(p.tri_batch, tri_recs - base);
                 uint32_t wm[kWords ? 8 : 1];
@@ -1215,7 +1235,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 for (uint32_t i = threadIdx.x; i < n * kTriRec; i += kRenderBlock)
                     lds_tri[i] = g_tri[(size_t)base * kTriRec + i];
                 __syncthreads();
-                if (active && !bvh_lane && !((OPT & kOptDiag) && (p.diag & 32u))) {   // diag 32: no pair tests
+                if (active && !bvh_lane && !list_tri && !((OPT & kOptDiag) && (p.diag & 32u))) {   // diag 32: no pair tests
                     const uint32_t first = base * kTriPer;
                     const uint32_t cnt = min(n * kTriPer, p.ntri - first);
                     if (kWords) {
@@ -1238,6 +1258,18 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             }
             // secondary rays: triangles through the exact BVH (iq_bvh.hpp), before the spheres
             if (bvh_lane && !diag_nobvh) bvh_closest<OPT>(p, ray, closest, kind, hidx);
+            if (list_sph) {
+                const float4* __restrict__ gs = reinterpret_cast<const float4*>(p.sph_pairs);
+                const uint32_t a = p.list_off_sph[ts], b = p.list_off_sph[ts + 1];
+                for (uint32_t e = a; e < b; ++e) {
+                    const uint32_t j = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[e]);
+                    if (sph_mask != nullptr) {
+                        const float4* q = gs + (size_t)j * kSphPairFloat4;
+                        test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, 2 * j, 2 * j + 1 < p.nsph);
+                    }
+                }
+                sph_none = true;
+            }
             for (uint32_t base = 0; base < sph_recs; base += p.sph_batch) {
                 const uint32_t n = min(p.sph_batch, sph_recs - base);
                 uint32_t wm[kWords ? 8 : 1];
@@ -1261,7 +1293,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 for (uint32_t i = threadIdx.x; i < n * kSphRec; i += kRenderBlock)
                     lds_sph[i] = g_sph[(size_t)base * kSphRec + i];
                 __syncthreads();
-                if (active && !diag_nosph && !sbvh_lane) {
+                if (active && !diag_nosph && !sbvh_lane && !list_sph) {
                     const uint32_t first = base * kSphPer;
                     const uint32_t cnt = min(n * kSphPer, p.nsph - first);
                     if (kWords) {
@@ -1617,16 +1649,36 @@ __global__ __launch_bounds__(256) void iqpt_bin_kernel(const kbin b) {
     b.cull[gid] = bits;
 }
 
-// Cost estimate per tile for the queue order: candidate triangle pairs + 8 x candidate sphere pairs
-// (a camera ray that can hit a sphere starts an Oren-Nayar path: more rays and the scatter shading).
-__global__ __launch_bounds__(256) void iqpt_tile_cost_kernel(const uint32_t* cull, uint32_t ntiles, uint32_t wt,
-                                                             uint32_t stride, uint32_t* cost) {
+// Per tile: candidate triangle pairs and sphere pairs of its masks (the queue-order cost and the
+// sizes of the candidate lists).
+__global__ __launch_bounds__(256) void iqpt_tile_count_kernel(const uint32_t* cull, uint32_t ntiles, uint32_t wt,
+                                                              uint32_t stride, uint32_t* cnt_tri, uint32_t* cnt_sph) {
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     if (t >= ntiles) return;
     const uint32_t* m = cull + (size_t)t * stride;
-    uint32_t c = 0;
-    for (uint32_t w = 0; w < stride; ++w) c += (uint32_t)__popc(m[w]) * (w < wt ? 1u : 8u);
-    cost[t] = c;
+    uint32_t a = 0, b = 0;
+    for (uint32_t w = 0; w < stride; ++w) {
+        if (w < wt) a += (uint32_t)__popc(m[w]);
+        else b += (uint32_t)__popc(m[w]);
+    }
+    cnt_tri[t] = a;
+    cnt_sph[t] = b;
+}
+
+// Candidate lists: the set bits of each tile's masks as ascending pair indices, triangle pairs at
+// off_tri[t], sphere pairs at off_sph[t] (exclusive prefix sums of the counts).
+__global__ __launch_bounds__(256) void iqpt_tile_list_kernel(const uint32_t* cull, uint32_t ntiles, uint32_t wt,
+                                                             uint32_t stride, const uint32_t* off_tri,
+                                                             const uint32_t* off_sph, uint32_t* list) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= ntiles) return;
+    const uint32_t* m = cull + (size_t)t * stride;
+    uint32_t o = off_tri[t];
+    for (uint32_t w = 0; w < wt; ++w)
+        for (uint32_t b = m[w]; b; b &= b - 1u) list[o++] = w * 32u + (uint32_t)__builtin_ctz(b);
+    o = off_sph[t];
+    for (uint32_t w = wt; w < stride; ++w)
+        for (uint32_t b = m[w]; b; b &= b - 1u) list[o++] = (w - wt) * 32u + (uint32_t)__builtin_ctz(b);
 }
 
 // Compact row-major <-> tile-major reorder of pixel-state planes (one thread per 32-bit word).
@@ -1789,11 +1841,19 @@ int launch_bin(void* stream, const kbin& b) {
     return (int)hipGetLastError();
 }
 
-int launch_tile_cost(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
-                     uint32_t* cost) {
+int launch_tile_count(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
+                      uint32_t* cnt_tri, uint32_t* cnt_sph) {
     if (ntiles == 0) return 0;
-    hipLaunchKernelGGL(iqpt_tile_cost_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, cull,
-                       ntiles, wt, stride, cost);
+    hipLaunchKernelGGL(iqpt_tile_count_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, cull,
+                       ntiles, wt, stride, cnt_tri, cnt_sph);
+    return (int)hipGetLastError();
+}
+
+int launch_tile_list(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
+                     const uint32_t* off_tri, const uint32_t* off_sph, uint32_t* list) {
+    if (ntiles == 0) return 0;
+    hipLaunchKernelGGL(iqpt_tile_list_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, cull,
+                       ntiles, wt, stride, off_tri, off_sph, list);
     return (int)hipGetLastError();
 }
 

@@ -115,6 +115,8 @@ struct iqpt_ctx {
     // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
     uint32_t* d_cull = nullptr;
     uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
+    uint32_t* d_list = nullptr;         // candidate lists of the masks, then their offsets (tri, sph)
+    uint64_t list_total = 0;
     size_t cull_cap = 0;       // words allocated
     bool cull_valid = false;
     uint32_t cull_ntx = 0, cull_nty = 0, cull_wt = 0, cull_stride = 0;
@@ -162,6 +164,8 @@ void free_scene(iqpt_ctx* c) {
 }
 
 // (Re)build the kOptCull tile masks of the current camera and packet on the context's stream.
+constexpr uint64_t kListBudget = 1ull << 26;   // candidate-list entries (256 MB)
+
 int build_cull(iqpt_ctx* c) {
     const uint32_t ntp = (c->ntri + 1) / 2, nsp = (c->nsph + 1) / 2;
     c->cull_ntx = (c->ncols + iqpt::kCullTile - 1) / iqpt::kCullTile;
@@ -208,17 +212,59 @@ int build_cull(iqpt_ctx* c) {
     const int le = iqpt::launch_bin(c->stream, b);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "cull binning kernel");
     // queue order over tiles (a queue chunk is one tile): most expensive first, so the pixels that set
-    // the end of the launch are cheap ones
+    // the end of the launch are cheap ones. Cost = candidate triangle pairs + 8 x candidate sphere pairs
+    // (a camera ray that can hit a sphere starts an Oren-Nayar path: more rays and the scatter shading).
     const uint32_t ntiles = c->cull_ntx * c->cull_nty;
-    uint32_t* d_cost = nullptr;
-    IQPT_HIP(hipMalloc(&d_cost, (size_t)ntiles * sizeof(uint32_t)));
-    std::vector<uint32_t> cost(ntiles);
-    const int lc = iqpt::launch_tile_cost(c->stream, c->d_cull, ntiles, c->cull_wt, c->cull_stride, d_cost);
-    hipError_t e = lc ? (hipError_t)lc : hipMemcpyAsync(cost.data(), d_cost, (size_t)ntiles * sizeof(uint32_t),
+    uint32_t* d_cnt = nullptr;
+    IQPT_HIP(hipMalloc(&d_cnt, 2 * (size_t)ntiles * sizeof(uint32_t)));
+    std::vector<uint32_t> cnt(2 * (size_t)ntiles);
+    const int lc = iqpt::launch_tile_count(c->stream, c->d_cull, ntiles, c->cull_wt, c->cull_stride, d_cnt,
+                                           d_cnt + ntiles);
+    hipError_t e = lc ? (hipError_t)lc : hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof(uint32_t),
                                                         hipMemcpyDeviceToHost, c->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    (void)hipFree(d_cost);
-    if (e != hipSuccess) return iqpt::hip_fail(e, "tile cost");
+    if (e != hipSuccess) {
+        (void)hipFree(d_cnt);
+        return iqpt::hip_fail(e, "tile counts");
+    }
+    std::vector<uint32_t> cost(ntiles);
+    for (uint32_t t = 0; t < ntiles; ++t) cost[t] = cnt[t] + 8u * cnt[ntiles + t];
+    // candidate lists for the streamed kernel (pairs of a tile without scanning its mask words): only
+    // worth building where the masks are long; skipped when they would exceed the list budget
+    if (c->d_list) (void)hipFree(c->d_list);
+    c->d_list = nullptr;
+    const bool want_lists = c->cull_stride > 8;
+    uint64_t total = 0;
+    std::vector<uint32_t> off(2 * ((size_t)ntiles + 1));
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        off[t] = (uint32_t)std::min<uint64_t>(total, 0xffffffffull);
+        total += cnt[t];
+    }
+    off[ntiles] = (uint32_t)std::min<uint64_t>(total, 0xffffffffull);
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        off[ntiles + 1 + t] = (uint32_t)std::min<uint64_t>(total, 0xffffffffull);
+        total += cnt[ntiles + t];
+    }
+    off[2 * (size_t)ntiles + 1] = (uint32_t)std::min<uint64_t>(total, 0xffffffffull);
+    if (want_lists && total > 0 && total <= kListBudget) {
+        uint32_t* d_off = nullptr;
+        bool ok = hipMalloc(&c->d_list, (total + off.size()) * sizeof(uint32_t)) == hipSuccess;
+        if (ok) {
+            d_off = c->d_list + total;
+            ok = hipMemcpyAsync(d_off, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                c->stream) == hipSuccess &&
+                 iqpt::launch_tile_list(c->stream, c->d_cull, ntiles, c->cull_wt, c->cull_stride, d_off,
+                                        d_off + ntiles + 1, c->d_list) == 0 &&
+                 hipStreamSynchronize(c->stream) == hipSuccess;
+        }
+        if (!ok) {
+            if (c->d_list) (void)hipFree(c->d_list);
+            c->d_list = nullptr;
+        } else {
+            c->list_total = total;
+        }
+    }
+    (void)hipFree(d_cnt);
     std::vector<uint32_t> order(ntiles);
     for (uint32_t t = 0; t < ntiles; ++t) order[t] = t;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
@@ -596,6 +642,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
     if (c->d_tile_order) (void)hipFree(c->d_tile_order);
+    if (c->d_list) (void)hipFree(c->d_list);
     for (auto& pr : c->timed) {
         (void)hipEventDestroy(pr.first);
         (void)hipEventDestroy(pr.second);
@@ -923,6 +970,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         p.cull_ntx = c->cull_ntx;
         p.cull_wt = c->cull_wt;
         p.cull_stride = c->cull_stride;
+        if (c->d_list) {
+            p.list = c->d_list;
+            p.list_off_tri = c->d_list + c->list_total;
+            p.list_off_sph = p.list_off_tri + (c->cull_ntx * c->cull_nty + 1);
+        }
     }
     p.ntx = (c->ncols + iqpt::kCullTile - 1) / iqpt::kCullTile;
     p.ntiles = p.ntx * ((c->set.nrows + iqpt::kCullTile - 1) / iqpt::kCullTile);
