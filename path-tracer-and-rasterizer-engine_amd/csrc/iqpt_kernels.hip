@@ -1197,13 +1197,22 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             if (list_tri) {
                 const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
                 const uint32_t a = p.list_off_tri[tt], b = p.list_off_tri[tt + 1];
+                // software-pipelined: the next pair's records are loaded while this one is tested (C4 -1.7 %)
+                uint32_t j = a < b ? (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[a]) : 0u;
+                float4 q0, q1, q2, q3, q4;
+                if (a < b) {
+                    const float4* q = gp + (size_t)j * kTriPairFloat4;
+                    q0 = q[0]; q1 = q[1]; q2 = q[2]; q3 = q[3]; q4 = q[4];
+                }
                 for (uint32_t e = a; e < b; ++e) {
-                    const uint32_t j = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[e]);
-                    if (tri_mask != nullptr) {
-                        const float4* q = gp + (size_t)j * kTriPairFloat4;
-                        test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
+                    const uint32_t jn = e + 1 < b ? (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[e + 1]) : j;
+                    const float4* qn = gp + (size_t)jn * kTriPairFloat4;
+                    const float4 n0 = qn[0], n1 = qn[1], n2 = qn[2], n3 = qn[3], n4 = qn[4];
+                    if (tri_mask != nullptr)
+                        test_triangle_pair<OPT>(q0, q1, q2, q3, q4, ray, closest, kind, hidx, 2 * j,
                                                 2 * j + 1 < p.ntri);
-                    }
+                    j = jn;
+                    q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4;
                 }
                 tri_none = true;                          // nothing left for the batches from this wave
             }
