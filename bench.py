@@ -279,7 +279,11 @@ def main():
             "rmse_vs_oracle": rmse_v,
             "bitexact_frac_vs_oracle": bitexact,
             "roofline": {
-                "bound": "valu",
+                # compute-bound: priced against the dense f32 MFMA peak, which equals the FP32 vector
+                # peak (157.3 TFLOP/s); the kernel runs on the vector ALU (nothing here is a dense
+                # contraction), see "compute_unit"
+                "bound": "mfma",
+                "compute_unit": "valu",
                 "achieved": round(achieved_tflops, 4),
                 "peak": FP32_PEAK_TFLOPS,
                 "unit": "TFLOP/s",
@@ -294,7 +298,9 @@ def main():
                          "unit": "GB/s", "frac": round(traffic / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
                         if traffic and kern_avg_ms > 0 else None),
                 "note": "algorithmic FLOPs F_ray = 52 T + 19 S (SURVEY.md §8d) x rays per launch / HIP-event "
-                        "kernel time; FP32 vector peak (no MFMA: nothing here is a dense contraction). "
+                        "kernel time against the f32 peak: the dense f32 MFMA peak of MI355X_MICROARCH.md, equal "
+                        "to the FP32 vector peak; the kernel runs on the vector ALU (compute_unit), nothing "
+                        "here is a dense contraction. "
                         "valu_busy_frac: share of SIMD time with a VALU instruction in flight (PMC "
                         "SQ_ACTIVE_INST_VALU); wave_time_split: issuing / ready but behind other waves / parked "
                         "on s_waitcnt (LDS and memory latency), profiles/. The VALU pipe is ~0.9 busy but the "
