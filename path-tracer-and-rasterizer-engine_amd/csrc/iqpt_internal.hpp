@@ -179,7 +179,7 @@ constexpr int kOptCamAxis = 1 << 14;   // short camera transform for pitch-only 
                                        // checks the zero pattern and the frame-wide normalization bounds)
 constexpr int kOptDefault =
     kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull | kOptBvh;
-constexpr uint32_t kStatsHeader = 16;        // kOptStats: 16 counters, then per-wave (start, end, iterations)
+constexpr uint32_t kStatsHeader = 24;        // kOptStats: 24 counters, then per-wave (start, end, iterations)
 constexpr uint32_t kStatsWaveSlots = 65536;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 

@@ -813,7 +813,8 @@ __device__ __forceinline__ void bvh_leaf(const kparams& p, uint32_t fc, const ra
 // whatever the visiting order. (A near-child-first traversal with a per-lane LDS stack was measured
 // slower on C4/C5 — profiles/ab/r01_ab38_c*_order.json — and is not kept.)
 template <int OPT>
-__device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, float& closest, int& kind, uint32_t& idx) {
+__device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, float& closest, int& kind, uint32_t& idx,
+                                            uint32_t* cnt = nullptr) {
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.bvh_nodes);
     const bvh_ray br = bvh_ray_setup(r);
     uint32_t i = 0;
@@ -822,6 +823,10 @@ __device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, floa
         const bool hit = bvh_node_test(p, nodes, i, r, br, closest, enter, dtc);
         const float4 lo = nodes[(size_t)kBvhNodeFloat4 * i], hi = nodes[(size_t)kBvhNodeFloat4 * i + 1];
         const uint32_t skip = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
+        if ((OPT & kOptStats) && cnt) {
+            cnt[0] += 1u;
+            if (hit && fc != 0u) cnt[1] += fc & 0xffu;
+        }
         if (hit && fc != 0u) bvh_leaf<OPT>(p, fc, r, closest, kind, idx);
         i = (hit && fc == 0u) ? i + 1 : skip;
     }
@@ -878,7 +883,7 @@ __device__ __forceinline__ void sph_visit(const float4 s, uint32_t k, const ray3
 // into f; nodes whose grown box the ray cannot meet before `bound` (+ slack) are skipped.
 template <int OPT>
 __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const bvh_ray br, float eps,
-                                          uint32_t min_idx, float bound, sph_fold& f) {
+                                          uint32_t min_idx, float bound, sph_fold& f, uint32_t* cnt = nullptr) {
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.sbvh_nodes);
     const float4* __restrict__ leaf = reinterpret_cast<const float4*>(p.sbvh_sph);
     const float u = 0x1p-24f, up = 1.0f + 0x1p-16f, slack = 8.0f * 0x1p-24f;
@@ -912,9 +917,11 @@ __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const 
         enter = enter - iq_fabsf(enter) * slack;
         exit = exit + iq_fabsf(exit) * slack;
         const bool hit = enter <= exit && exit >= kTMin - dts && enter <= bound + dts;
+        if ((OPT & kOptStats) && cnt) cnt[0] += 1u;
         if (hit && fc != 0u) {
-            const uint32_t first = fc >> 8, cnt = fc & 0xffu;
-            for (uint32_t k = 0; k < cnt; ++k)
+            const uint32_t first = fc >> 8, nl = fc & 0xffu;
+            if ((OPT & kOptStats) && cnt) cnt[1] += nl;
+            for (uint32_t k = 0; k < nl; ++k)
                 sph_visit<OPT>(leaf[first + k], p.sbvh_idx[first + k], r, min_idx, f, bound);
         }
         i = (hit && fc == 0u) ? i + 1 : skip;
@@ -931,7 +938,7 @@ __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const 
 // not within 2^-10 of 1 folds over every sphere in packet order instead.
 template <int OPT>
 __device__ __forceinline__ void sbvh_closest(const kparams& p, const ray3 r, float& closest, int& kind,
-                                             uint32_t& idx) {
+                                             uint32_t& idx, uint32_t* cnt = nullptr) {
     const bvh_ray br = bvh_ray_setup(r);
     const float dd = (r.dx * r.dx + r.dy * r.dy) + r.dz * r.dz;
     const float eps = iq_fabsf(dd - 1.0f) + 8.0f * 0x1p-24f;
@@ -941,7 +948,7 @@ __device__ __forceinline__ void sbvh_closest(const kparams& p, const ray3 r, flo
         return;
     }
     sph_fold f = {kTMax, ~0u, 0.0f, ~0u};
-    sbvh_pass<OPT>(p, r, br, eps, 0u, closest, f);
+    sbvh_pass<OPT>(p, r, br, eps, 0u, closest, f, cnt);
     if (f.iin == ~0u) {
         // no inside sphere: min(closest, best normal), the sphere on ties
         if (f.bi != ~0u && !(closest < f.bt)) {
@@ -1038,6 +1045,8 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     unsigned long long s_tests[2] = {0, 0};   // wave-level triangle / sphere pair tests (culled resident path)
     unsigned long long s_full = 0;            // iterations forced to the full loop (a secondary ray in the wave)
     unsigned long long s_refill = 0, s_refill_lanes = 0;   // refills that started pixels, pixels started
+    // per lane (kOptStats): BVH rays, nodes visited, leaf pairs / spheres tested — triangle and sphere BVH
+    uint32_t c_tri[2] = {0u, 0u}, c_sph[2] = {0u, 0u}, c_tri_rays = 0u, c_sph_rays = 0u;
 
     // ---- wave-uniform chunk state: the current tile [chunk_next, chunk_end) of tile-major storage
     uint32_t chunk_tile = 0;
@@ -1121,8 +1130,11 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     const uint64_t t_start = (OPT & kOptStats) ? __builtin_amdgcn_s_memrealtime() : 0ull;
     if (p.spp > 0) refill();
 
+    // kOptBvhPrimary: every ray goes through the BVHs, no LDS batches, so no workgroup barriers: the
+    // waves iterate independently, as in the resident kernel
+    constexpr bool kBatches = STREAM && !kBvhPrimary;
     while (true) {
-        if (STREAM) {
+        if (kBatches) {
             if (!__syncthreads_or(active ? 1 : 0)) break;
         } else {
             if (!__any(active)) break;
@@ -1141,7 +1153,35 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
         const bool cull = kCull && p.cull != nullptr && !__any(active && depth != 0);
         const uint32_t* lane_mask =
             (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;   // null: 0
-        if (STREAM) {
+        if (kBvhPrimary) {
+            // Triangles through the exact BVH, spheres through the exact sphere BVH (each falls back to
+            // the brute-force fold from global memory where its BVH is absent or the ray is outside
+            // the bounds' assumptions, bvh_ray_ok); triangles first, as in path_tracer.cu:257-295.
+            if (active) {
+                const bool ok = bvh_ray_ok(p, ray);
+                if (ok && p.bvh_nodes != nullptr) {
+                    if (OPT & kOptStats) ++c_tri_rays;
+                    bvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_tri : nullptr);
+                } else {
+                    const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
+                    for (uint32_t j = 0; j < p.ntri_pairs; ++j) {
+                        const float4* q = gp + (size_t)j * kTriPairFloat4;
+                        test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
+                                                2 * j + 1 < p.ntri);
+                    }
+                }
+                if (ok && p.sbvh_nodes != nullptr) {
+                    if (OPT & kOptStats) ++c_sph_rays;
+                    sbvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_sph : nullptr);
+                } else {
+                    const float4* __restrict__ gs = reinterpret_cast<const float4*>(p.sph_pairs);
+                    for (uint32_t j = 0; j < p.nsph_pairs; ++j) {
+                        const float4* q = gs + (size_t)j * kSphPairFloat4;
+                        test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, 2 * j, 2 * j + 1 < p.nsph);
+                    }
+                }
+            }
+        } else if (STREAM) {
             // Streamed scene. Per lane and mask word: a camera ray contributes its tile's mask (kOptCull),
             // a secondary ray that takes the BVH (kOptBvh) contributes nothing to the triangle batches,
             // any other ray every pair; the wave ORs the words, the block skips a batch nobody needs.
@@ -1266,7 +1306,10 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 }
             }
             // secondary rays: triangles through the exact BVH (iq_bvh.hpp), before the spheres
-            if (bvh_lane && !diag_nobvh) bvh_closest<OPT>(p, ray, closest, kind, hidx);
+            if (bvh_lane && !diag_nobvh) {
+                if (OPT & kOptStats) ++c_tri_rays;
+                bvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_tri : nullptr);
+            }
             if (list_sph) {
                 const float4* __restrict__ gs = reinterpret_cast<const float4*>(p.sph_pairs);
                 const uint32_t a = p.list_off_sph[ts], b = p.list_off_sph[ts + 1];
@@ -1323,7 +1366,10 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     }
                 }
             }
-            if (sbvh_lane && !diag_nosph) sbvh_closest<OPT>(p, ray, closest, kind, hidx);
+            if (sbvh_lane && !diag_nosph) {
+                if (OPT & kOptStats) ++c_sph_rays;
+                sbvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_sph : nullptr);
+            }
         } else if ((OPT & kOptDiag) && (p.diag & 2u)) {
             // diagnostic: no intersection; every ray hits triangle 0 at t = 1
             if (active) {
@@ -1543,6 +1589,19 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             atomicAdd(p.stats + 10, s_full);
             atomicAdd(p.stats + 12, s_refill);
             atomicAdd(p.stats + 13, s_refill_lanes);
+        }
+        {
+            // BVH work, summed over the wave's lanes
+            unsigned long long v[6] = {c_tri_rays, c_tri[0], c_tri[1], c_sph_rays, c_sph[0], c_sph[1]};
+#pragma unroll
+            for (int k = 0; k < 6; ++k) {
+#pragma unroll
+                for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
+            }
+            if (lane == 0 && p.stats) {
+#pragma unroll
+                for (int k = 0; k < 6; ++k) atomicAdd(p.stats + 14 + k, v[k]);
+            }
             // wave timeline (s_memrealtime, 100 MHz): start, end, iterations per wave
             const uint64_t slot = atomicAdd(p.stats + 11, 1ull);
             if (slot < kStatsWaveSlots) {
@@ -1786,6 +1845,7 @@ const variant kVariants[] = {
     IQPT_V(8, true, kOptDefault | kOptLB5),
     IQPT_V(8, false, kOptDefault | kOptStats),
     IQPT_V(8, true, kOptDefault | kOptStats),
+    IQPT_V(8, true, ((kOptDefault | kOptStats | kOptBvhPrimary) & ~kOptLB5)),
     IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptStats),
     IQPT_V(8, false, kOptDefault & ~kOptCull),
     IQPT_V(8, true, kOptDefault & ~kOptCull),

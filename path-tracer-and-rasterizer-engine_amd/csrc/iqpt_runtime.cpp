@@ -1438,17 +1438,17 @@ int iqpt_debug_read_wave_times(iqpt_ctx* c, unsigned long long* out, uint32_t ca
 }
 
 int iqpt_debug_read_stats(iqpt_ctx* c, unsigned long long* out16) {
-    unsigned long long* out8 = out16;   // 16 counters (tools/ab_kernel.py)
+    unsigned long long* out8 = out16;   // kStatsHeader (24) counters (tools/ab_kernel.py)
     if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     int st = use_device(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     if (!c->d_stats) {
-        std::memset(out8, 0, 16 * sizeof(unsigned long long));
+        std::memset(out8, 0, iqpt::kStatsHeader * sizeof(unsigned long long));
         return IQPT_OK;
     }
-    IQPT_HIP(hipMemcpy(out8, c->d_stats, 16 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    IQPT_HIP(hipMemset(c->d_stats, 0, 16 * sizeof(unsigned long long)));   // counters and the wave slot index
+    IQPT_HIP(hipMemcpy(out8, c->d_stats, iqpt::kStatsHeader * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    IQPT_HIP(hipMemset(c->d_stats, 0, iqpt::kStatsHeader * sizeof(unsigned long long)));   // counters, wave slot index
     return IQPT_OK;
 }
 

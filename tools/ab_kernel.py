@@ -162,18 +162,23 @@ def main():
                                        for q in (0, 1, 5, 10, 25, 50, 75, 90, 95, 99, 100)},
                         "mean_lifetime_frac": round(float((end_us - start_us).mean() / kern), 4),
                         "iters_pct": {str(q): int(np.percentile(a[:, 2], q)) for q in (0, 50, 100)}}
-        s = (C.c_ulonglong * 16)()
+        s = (C.c_ulonglong * 24)()
         lib.iqpt_debug_read_stats(pt.handle, s)
         it, ready, active, sc_ex, sc_l, t_ex, t_l, waves = list(s)[:8]
         tri_tests, sph_tests, full_iters = list(s)[8:11]
         refills, refill_lanes = list(s)[12:14]
+        tri_rays, tri_nodes, tri_pairs, sph_rays, sph_nodes, sph_tests = list(s)[14:20]
         stats = {"opt": stats_opt, "waves": waves, "iterations": it, "ready_lane_frac": ready / max(1, it * 64),
                  "active_lane_frac": active / max(1, it * 64), "scatter_exec_per_iter": sc_ex / max(1, it),
                  "scatter_lanes_per_exec": sc_l / max(1, sc_ex), "term_exec_per_iter": t_ex / max(1, it),
                  "term_lanes_per_exec": t_l / max(1, t_ex), "rays": pt.rays(),
                  "tri_pair_tests_per_iter": tri_tests / max(1, it), "sph_pair_tests_per_iter": sph_tests / max(1, it),
                  "full_loop_iter_frac": full_iters / max(1, it),
-                 "refills_per_iter": refills / max(1, it), "pixels_per_refill": refill_lanes / max(1, refills)}
+                 "refills_per_iter": refills / max(1, it), "pixels_per_refill": refill_lanes / max(1, refills),
+                 "tri_bvh": {"rays": tri_rays, "nodes_per_ray": tri_nodes / max(1, tri_rays),
+                             "leaf_pairs_per_ray": tri_pairs / max(1, tri_rays)},
+                 "sph_bvh": {"rays": sph_rays, "nodes_per_ray": sph_nodes / max(1, sph_rays),
+                             "spheres_per_ray": sph_tests / max(1, sph_rays)}}
     out = {"config": cfg.name, "spp": spp, "rounds": args.rounds, "variants": res, "stats_default": stats,
            "wave_timeline": timeline}
     print(json.dumps(out, indent=1))
