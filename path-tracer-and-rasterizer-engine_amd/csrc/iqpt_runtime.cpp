@@ -984,10 +984,14 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     p.rays = c->d_rays;
     p.queue = c->d_queue;
     p.stats = c->d_stats;
-    // kOptBvhPrimary: decided by timing (see iqpt_ctx::tune_stage)
+    // kOptBvhPrimary: decided by timing (see iqpt_ctx::tune_stage); its batch-free variants keep the
+    // 5-wave bound the batched streamed variants drop
+    const int prim_opt = (opt | iqpt::kOptBvhPrimary) |
+                         (iqpt::render_variant_exists(c->max_depth, true, opt | iqpt::kOptBvhPrimary | iqpt::kOptLB5)
+                              ? iqpt::kOptLB5 : 0);
     int tune_slot = -1;
     if (!c->opt_fixed && stream_batches && p.bvh_nodes && p.cull && (opt & iqpt::kOptBvh) &&
-        iqpt::render_variant_exists(c->max_depth, true, opt | iqpt::kOptBvhPrimary)) {
+        iqpt::render_variant_exists(c->max_depth, true, prim_opt)) {
         if (c->tune_stage == 2) {
             float ms_a = 0.0f, ms_b = 0.0f;
             if (hipEventSynchronize(c->tune_ev[3]) == hipSuccess &&
@@ -1005,10 +1009,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             }
             if (tune_slot == 0) {   // load both code objects before either is timed
                 int o2 = 0;
-                (void)iqpt::render_occupancy(c->max_depth, true, opt | iqpt::kOptBvhPrimary, lds, &o2);
+                (void)iqpt::render_occupancy(c->max_depth, true, prim_opt, lds, &o2);
             }
         }
-        if ((tune_slot == 1) || (tune_slot < 0 && c->tune_primary)) opt |= iqpt::kOptBvhPrimary;
+        if ((tune_slot == 1) || (tune_slot < 0 && c->tune_primary)) opt = prim_opt;
     }
     int occ = 0;
     if (iqpt::render_occupancy(c->max_depth, stream_batches, opt, lds, &occ) != 0 || occ < 1) occ = 1;
