@@ -62,17 +62,19 @@ def _headers() -> list[Path]:
     return sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("*.hpp")) + sorted(INCLUDE.glob("*.h"))
 
 
-def build_lib(force: bool = False, ab: bool = False) -> Path:
-    """Compile the HIP kernels + runtime into libiqpt.so (gfx950); ab=True adds the A/B variants."""
-    target = AB_LIB_PATH if ab else LIB_PATH
+def build_lib(force: bool = False, ab: bool = False, flags: tuple[str, ...] = (),
+              target: Path | None = None) -> Path:
+    """Compile the HIP kernels + runtime into libiqpt.so (gfx950); ab=True adds the A/B variants.
+    ``flags``/``target``: extra compiler flags into another library (compiler-option A/B runs)."""
+    target = target or (AB_LIB_PATH if ab else LIB_PATH)
     srcs = [CSRC / s for s in LIB_SOURCES]
     if not force and _newer(target, srcs + _headers() + [Path(__file__)]):
         return target
-    bdir = BUILD_DIR / ("ab" if ab else "prod")
+    bdir = BUILD_DIR / (target.stem if flags else ("ab" if ab else "prod"))
     bdir.mkdir(parents=True, exist_ok=True)
     objs = []
     cmds = []
-    extra = ["-DIQPT_AB_VARIANTS"] if ab else []
+    extra = (["-DIQPT_AB_VARIANTS"] if ab else []) + list(flags)
     for s in srcs:
         o = bdir / (s.name + ".o")
         cmds.append([HIPCC, *HIP_FLAGS, *extra, "-x", "hip", "-c", str(s), "-o", str(o)])

@@ -35,8 +35,9 @@ def main():
     ap.add_argument("--crop", default="", help="x0,x1,y0,ystep,nrows pixel set")
     ap.add_argument("--variants", default="", help="comma list of name=optmask")
     ap.add_argument("--scene", default="", help="empty | walls (cornell without spheres) | preset name")
+    ap.add_argument("--lib", default="", help="load this prebuilt A/B library (compiler-option runs)")
     args = ap.parse_args()
-    lib_path = _build.build_lib(ab=True)
+    lib_path = Path(args.lib) if args.lib else _build.build_lib(ab=True)
     _lib.LIB_PATH = lib_path                    # load the A/B build instead of the production one
     lib = _lib.load()
     lib.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
