@@ -41,6 +41,7 @@
 #include <cfloat>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <vector>
 
 namespace iqbvh {
@@ -131,7 +132,7 @@ struct node {
     float edet;             // max safety x E_det, rounded up
     float pad;
 };
-static_assert(sizeof(node) == 80, "node is five float4");
+static_assert(sizeof(node) == 80, "host-side node (the device node is 64 bytes, iqpt_runtime.cpp)");
 
 struct build_input {
     std::vector<float> lo, hi;       // 3 per triangle: tight vertex box, rounded outward
@@ -156,6 +157,12 @@ inline float round_up(double v) {
     float f = (float)v;
     if ((double)f < v) f = std::nextafter(f, INFINITY);
     return f;
+}
+// bf16 bits (the high half of a float) rounded up, for v >= 0
+inline uint32_t bf16_up_bits(float v) {
+    uint32_t u;
+    std::memcpy(&u, &v, 4);
+    return (u & 0xffffu) ? (u >> 16) + 1u : (u >> 16);
 }
 
 // Median split on the longest centroid axis, leaves of <= kLeafTris triangles (kept even by padding).

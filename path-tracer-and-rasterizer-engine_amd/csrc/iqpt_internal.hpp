@@ -32,7 +32,7 @@ struct alignas(16) float4_storage {
 //  * spheres: (center.xyz, radius) float4, and sphere pairs 2 x float4 = 32 B:
 //      (cx_a, cx_b, cy_a, cy_b), (cz_a, cz_b, r_a, r_b).
 constexpr int kTriFloat4 = 3;
-constexpr int kBvhNodeFloat4 = 5;
+constexpr int kBvhNodeFloat4 = 4;     // 64 bytes: one cache line per node visit
 constexpr int kTriPairFloat4 = 5;
 constexpr int kSphPairFloat4 = 2;
 // Shading record per triangle (only read for the closest hit): world normals n0, n1, n2 and the
@@ -99,14 +99,13 @@ struct kparams {
     const float4_storage* mats;
     const float4_storage* tri_shade;
     // exact BVH for secondary rays (iq_bvh.hpp; streamed scenes): nodes (kBvhNodeFloat4 x float4:
-    // tight box min + skip, box max + leaf first pair << 8 | count, error coefficients gA gB tA tB,
-    // normal-cone axis + cos beta, (sin beta, Nmin, E_det, -)), leaf triangle
-    // pairs (kTriPairFloat4 each) with their packet indices (uint2; ~0u pads), triangles outside the
+    // (tight box min, link: skip pointer or 1 << 31 | leaf first pair << 8 | count), (box max, tA | tB
+    // bf16 rounded up), (normal-cone axis, E_det), (gR, gB, Nmin cos beta, Nmin sin beta)), leaf triangle
+    // pairs (kTriPairFloat4 each; the packet indices in the last float4's z, w, ~0u pads), triangles outside the
     // BVH (tested by every ray); the bound holds for |d_i| <= md and a finite origin; gulp covers the
     // rounding of a grown box side
     const float4_storage* bvh_nodes;
     const float4_storage* bvh_pairs;
-    const uint32_t* bvh_pidx;
     const uint32_t* bvh_always;
     uint32_t bvh_nnodes, bvh_nalways;
     float bvh_md, bvh_gulp;

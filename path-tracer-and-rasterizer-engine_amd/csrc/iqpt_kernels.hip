@@ -753,23 +753,24 @@ __device__ __forceinline__ bool bvh_node_test(const kparams& p, const float4* __
                                               float& dtc_out) {
     const float slack = 8.0f * 0x1p-24f, up = 1.0f + 0x1p-20f, up16 = 1.0f + 0x1p-16f;
     const float4* nd = nodes + (size_t)kBvhNodeFloat4 * i;
-    const float4 lo = nd[0], hi = nd[1], co = nd[2], cone = nd[3], cone2 = nd[4];
+    const float4 lo = nd[0], hi = nd[1], ax = nd[2], co = nd[3];
     const float sx = fmaxf(iq_fabsf(r.ox - lo.x), iq_fabsf(r.ox - hi.x));
     const float sy = fmaxf(iq_fabsf(r.oy - lo.y), iq_fabsf(r.oy - hi.y));
     const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
     const float S = fmaxf(fmaxf(sx, sy), sz) * up;
     // lambda = 1e-6 / D, D a lower bound of |det^| over the node's triangles for this ray
-    // (iq_bvh.hpp normal cones): |d| cos(theta + beta) from the cone, every step rounded toward
-    // a smaller D; an unusable cone (cos beta = 0) or a grazing ray leaves lambda = 1
+    // (iq_bvh.hpp normal cones): Nmin |d| cos(theta + beta) = |d| cos(theta) A - |d| sin(theta) B with
+    // A = Nmin cos(beta), B = Nmin sin(beta), every step rounded toward a smaller D; an unusable cone
+    // (A = 0) or a grazing ray leaves lambda = 1
     float lambda = 1.0f;
-    if (cone.w > 0.0f) {
-        const float c = iq_fabsf((r.dx * cone.x + r.dy * cone.y) + r.dz * cone.z);
+    if (co.z > 0.0f) {
+        const float c = iq_fabsf((r.dx * ax.x + r.dy * ax.y) + r.dz * ax.z);
         const float c_lo = fmaxf(0.0f, c * (1.0f - 0x1p-16f) - 0x1p-20f * br.dl);
         // |d| sin(theta) <= sqrt(dd - c_lo^2); the subtraction's rounding (<= 2u dd) is covered by
         // adding 2^-20 dd before the root
         const float s_hi = __builtin_sqrtf(fmaxf(0.0f, br.dd - c_lo * c_lo) + 0x1p-20f * br.dd) * up16;
-        const float cos_lo = (c_lo * cone.w) * (1.0f - 0x1p-16f) - (s_hi * cone2.x) * up16;
-        const float D = (cos_lo * cone2.y) * (1.0f - 0x1p-16f) - cone2.z * up16;
+        const float nc = ((c_lo * co.z) * (1.0f - 0x1p-16f) - (s_hi * co.w) * up16) * (1.0f - 0x1p-16f);
+        const float D = nc - ax.w * up16;
         if (D > 1e-6f) lambda = fminf(1.0f, (1e-6f * __builtin_amdgcn_rcpf(D)) * up16);
     }
     const float g = (lambda * (co.x + co.y * S)) * up + p.bvh_gulp;   // gulp includes gC
@@ -785,8 +786,10 @@ __device__ __forceinline__ bool bvh_node_test(const kparams& p, const float4* __
     if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
     if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
     // computed slab bounds are within 3 ulp (relative) of the exact ones: widen by 8 ulp
-    const float dtc = ((lambda * co.z) * S) * up;
-    const float dt = (dtc + co.w * closest) * up;
+    const uint32_t tab = __float_as_uint(hi.w);                        // tA | tB, bf16 rounded up
+    const float tA = __uint_as_float(tab & 0xffff0000u), tB = __uint_as_float(tab << 16);
+    const float dtc = ((lambda * tA) * S) * up;
+    const float dt = (dtc + tB * closest) * up;
     float enter = fmaxf(fmaxf(ax0, ay0), az0), exit = fminf(fminf(ax1, ay1), az1);
     enter = enter - iq_fabsf(enter) * slack;
     exit = exit + iq_fabsf(exit) * slack;
@@ -802,8 +805,9 @@ __device__ __forceinline__ void bvh_leaf(const kparams& p, uint32_t fc, const ra
     const uint32_t first = fc >> 8, cnt = fc & 0xffu;
     for (uint32_t k = 0; k < cnt; ++k) {
         const float4* q = pairs + (size_t)(first + k) * kTriPairFloat4;
-        const uint32_t ka = p.bvh_pidx[2 * (first + k)], kb = p.bvh_pidx[2 * (first + k) + 1];
-        test_triangle_pair_ix<OPT>(q[0], q[1], q[2], q[3], q[4], r, closest, kind, idx, ka, kb);
+        const float4 q4 = q[4];                                   // (e2z_a, e2z_b, index a, index b)
+        test_triangle_pair_ix<OPT>(q[0], q[1], q[2], q[3], q4, r, closest, kind, idx, __float_as_uint(q4.z),
+                                   __float_as_uint(q4.w));
     }
 }
 
@@ -821,14 +825,15 @@ __device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, floa
     while (i < p.bvh_nnodes) {
         float enter, dtc;
         const bool hit = bvh_node_test(p, nodes, i, r, br, closest, enter, dtc);
-        const float4 lo = nodes[(size_t)kBvhNodeFloat4 * i], hi = nodes[(size_t)kBvhNodeFloat4 * i + 1];
-        const uint32_t skip = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
+        // link: skip pointer (inner node) or 1 << 31 | first pair << 8 | count (leaf, followed by i + 1)
+        const uint32_t link = __float_as_uint(nodes[(size_t)kBvhNodeFloat4 * i].w);
+        const bool leaf = (link >> 31) != 0u;
         if ((OPT & kOptStats) && cnt) {
             cnt[0] += 1u;
-            if (hit && fc != 0u) cnt[1] += fc & 0xffu;
+            if (hit && leaf) cnt[1] += link & 0xffu;
         }
-        if (hit && fc != 0u) bvh_leaf<OPT>(p, fc, r, closest, kind, idx);
-        i = (hit && fc == 0u) ? i + 1 : skip;
+        if (hit && leaf) bvh_leaf<OPT>(p, link & 0x7fffffffu, r, closest, kind, idx);
+        i = (hit || leaf) ? i + 1 : link;
     }
     const float4* __restrict__ tris = reinterpret_cast<const float4*>(p.tris);
     for (uint32_t a = 0; a < p.bvh_nalways; ++a) {

@@ -100,7 +100,6 @@ struct iqpt_ctx {
     // exact BVH for secondary rays (iq_bvh.hpp), null when the packet has few triangles
     float4_storage* d_bvh_nodes = nullptr;
     float4_storage* d_bvh_pairs = nullptr;
-    uint32_t* d_bvh_pidx = nullptr;
     uint32_t* d_bvh_always = nullptr;
     uint32_t bvh_nnodes = 0, bvh_nalways = 0;
     float bvh_md = 0.0f, bvh_gulp = 0.0f;
@@ -152,7 +151,7 @@ void free_scene(iqpt_ctx* c) {
     }
     c->bvh_nnodes = c->bvh_nalways = 0;
     c->sbvh_nnodes = c->sbvh_nalways = 0;
-    for (uint32_t** b : {&c->d_tri_mat, &c->d_sph_mat, &c->d_bvh_pidx, &c->d_bvh_always, &c->d_sbvh_idx,
+    for (uint32_t** b : {&c->d_tri_mat, &c->d_sph_mat, &c->d_bvh_always, &c->d_sbvh_idx,
                          &c->d_sbvh_always}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
@@ -341,7 +340,7 @@ bool cam_axis_constants(const iqpt_camera& cam, float* k) {
 // and the spheres (for the scene box). Fills the host arrays the upload copies to the device.
 struct bvh_host {
     std::vector<float4_storage> nodes, pairs;
-    std::vector<uint32_t> pidx, always;
+    std::vector<uint32_t> always;
     float md, gulp;
 };
 constexpr uint32_t kBvhMinTriangles = 256;
@@ -412,27 +411,32 @@ bool build_bvh(const std::vector<float4_storage>& tris, const std::vector<float4
     out.gulp = iqbvh::round_up(maxabs * 0x1p-22 + gc_max);
     iqbvh::build_output bo;
     iqbvh::build(in, bo);
+    // the 64-byte device node (iqpt_internal.hpp kBvhNodeFloat4): a leaf's successor is always the next
+    // node, so one word holds the link — skip pointer (inner) or 1 << 31 | first pair << 8 | count (leaf);
+    // tA, tB as bf16 rounded up; the cone as A = Nmin cos(beta) (down) and B = Nmin sin(beta) (up), from
+    // which the kernel bounds Nmin |d| cos(theta + beta) = |d| cos(theta) A - |d| sin(theta) B
+    if (bo.order.size() / 2 >= (1u << 23)) return false;
     for (const iqbvh::node& n : bo.nodes) {
-        float4_storage lo, hi;
-        lo.x = n.bmin[0];
-        lo.y = n.bmin[1];
-        lo.z = n.bmin[2];
-        std::memcpy(&lo.w, &n.skip, 4);
-        hi.x = n.bmax[0];
-        hi.y = n.bmax[1];
-        hi.z = n.bmax[2];
-        std::memcpy(&hi.w, &n.first_count, 4);
-        out.nodes.push_back(lo);
-        out.nodes.push_back(hi);
-        out.nodes.push_back(float4_storage{n.gR, n.gB, n.tA, n.tB});
-        out.nodes.push_back(float4_storage{n.axis[0], n.axis[1], n.axis[2], n.cos_beta});
-        out.nodes.push_back(float4_storage{n.sin_beta, n.nmin, n.edet, 0.0f});
+        const uint32_t link = n.first_count ? (0x80000000u | n.first_count) : n.skip;
+        const uint32_t tab = (iqbvh::bf16_up_bits(n.tA) << 16) | iqbvh::bf16_up_bits(n.tB);
+        float4_storage w[4] = {{n.bmin[0], n.bmin[1], n.bmin[2], 0.0f},
+                               {n.bmax[0], n.bmax[1], n.bmax[2], 0.0f},
+                               {n.axis[0], n.axis[1], n.axis[2], n.edet},
+                               {n.gR, n.gB, 0.0f, 0.0f}};
+        std::memcpy(&w[0].w, &link, 4);
+        std::memcpy(&w[1].w, &tab, 4);
+        if (n.cos_beta > 0.0f && n.nmin > 0.0f) {
+            w[3].z = iqbvh::round_down((double)n.cos_beta * (double)n.nmin);
+            w[3].w = iqbvh::round_up((double)n.sin_beta * (double)n.nmin);
+        }
+        for (const float4_storage& v : w) out.nodes.push_back(v);
     }
-    // leaf pairs in the kernel's pair layout (iqpt_internal.hpp), padding elements zero
+    // leaf pairs in the kernel's pair layout (iqpt_internal.hpp), padding elements zero; the two
+    // packet indices ride in the record's spare last two words (no separate index load per pair)
     const size_t npairs = bo.order.size() / 2;
     out.pairs.assign(npairs * iqpt::kTriPairFloat4, float4_storage{0.0f, 0.0f, 0.0f, 0.0f});
-    out.pidx = bo.order;
     for (size_t q = 0; q < bo.order.size(); ++q) {
+        std::memcpy(&out.pairs[(q / 2) * iqpt::kTriPairFloat4 + 4].z + (q & 1), &bo.order[q], 4);
         if (bo.order[q] == ~0u) continue;
         const float4_storage* t = &tris[(size_t)bo.order[q] * iqpt::kTriFloat4];
         const float f[9] = {t[0].x, t[0].y, t[0].z, t[0].w, t[1].x, t[1].y, t[1].z, t[1].w, t[2].x};
@@ -819,7 +823,7 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         (st = upload(sph_pairs, &c->d_sph_pairs)) || (st = upload(mats, &c->d_mats)) ||
         (st = upload_u32(tri_mat, &c->d_tri_mat)) || (st = upload_u32(sph_mat, &c->d_sph_mat)) ||
         (have_bvh && ((st = upload(bvh.nodes, &c->d_bvh_nodes)) || (st = upload(bvh.pairs, &c->d_bvh_pairs)) ||
-                      (st = upload_u32(bvh.pidx, &c->d_bvh_pidx)) || (st = upload_u32(bvh.always, &c->d_bvh_always)))) ||
+                      (st = upload_u32(bvh.always, &c->d_bvh_always)))) ||
         (have_sbvh && ((st = upload(sbvh.nodes, &c->d_sbvh_nodes)) || (st = upload(sbvh.sph, &c->d_sbvh_sph)) ||
                        (st = upload_u32(sbvh.idx, &c->d_sbvh_idx)) ||
                        (st = upload_u32(sbvh.always, &c->d_sbvh_always))))) {
@@ -912,7 +916,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     if (c->d_bvh_nodes && c->bvh_nnodes) {
         p.bvh_nodes = c->d_bvh_nodes;
         p.bvh_pairs = c->d_bvh_pairs;
-        p.bvh_pidx = c->d_bvh_pidx;
         p.bvh_always = c->d_bvh_always;
         p.bvh_nnodes = c->bvh_nnodes;
         p.bvh_nalways = c->bvh_nalways;
