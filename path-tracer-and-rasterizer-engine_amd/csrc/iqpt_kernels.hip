@@ -892,6 +892,13 @@ __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const 
     const float4* __restrict__ nodes = reinterpret_cast<const float4*>(p.sbvh_nodes);
     const float4* __restrict__ leaf = reinterpret_cast<const float4*>(p.sbvh_sph);
     const float u = 0x1p-24f, up = 1.0f + 0x1p-16f, slack = 8.0f * 0x1p-24f;
+    // the always-tested spheres first (the large ones: their hits tighten the bound for the traversal;
+    // the fold is order-free)
+    const float4* __restrict__ sph = reinterpret_cast<const float4*>(p.spheres);
+    for (uint32_t a = 0; a < p.sbvh_nalways; ++a) {
+        const uint32_t k = p.sbvh_always[a];
+        sph_visit<OPT>(sph[k], k, r, min_idx, f, bound);
+    }
     uint32_t i = 0;
     while (i < p.sbvh_nnodes) {
         const float4* nd = nodes + (size_t)kSphNodeFloat4 * i;
@@ -931,11 +938,6 @@ __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const 
         }
         i = (hit && fc == 0u) ? i + 1 : skip;
     }
-    const float4* __restrict__ sph = reinterpret_cast<const float4*>(p.spheres);
-    for (uint32_t a = 0; a < p.sbvh_nalways; ++a) {
-        const uint32_t k = p.sbvh_always[a];
-        sph_visit<OPT>(sph[k], k, r, min_idx, f, bound);
-    }
 }
 
 // The spheres' part of the closest hit (after the triangles) through the sphere BVH: the reference's
@@ -972,6 +974,65 @@ __device__ __forceinline__ void sbvh_closest(const kparams& p, const ray3 r, flo
     if (g.bi != ~0u && !(closest < g.bt)) {
         closest = g.bt;
         idx = g.bi;
+    }
+}
+
+// Closest hit with the spheres first (the BVH-primary variants): the sphere fold's
+// order-free state over every sphere (iq_bvh.hpp), then — unless the origin is inside a sphere, whose
+// far root overrides any triangle (shape.cu:27-33 skips the t_max test) — the triangles with the best
+// sphere's t as their starting bound, so the triangle BVH prunes everything behind it. Same result as
+// triangles-then-spheres (path_tracer.cu:253-295): a triangle wins only with t below the sphere's (the
+// sphere takes equal t). Requires a sphere BVH, a finite origin and a ray within the sphere bound's
+// |d|^2 limit (sbvh_first_ok).
+__device__ __forceinline__ bool sbvh_first_ok(const kparams& p, const ray3 r) {
+    const float dd = (r.dx * r.dx + r.dy * r.dy) + r.dz * r.dz;
+    return p.sbvh_nodes != nullptr && iq_fabsf(r.ox) <= 1e18f && iq_fabsf(r.oy) <= 1e18f &&
+           iq_fabsf(r.oz) <= 1e18f && iq_fabsf(dd - 1.0f) + 8.0f * 0x1p-24f <= 0x1p-10f;
+}
+
+template <int OPT>
+__device__ __forceinline__ void closest_spheres_first(const kparams& p, const ray3 r, bool tri_bvh, float& closest,
+                                                      int& kind, uint32_t& idx, uint32_t* ctri = nullptr,
+                                                      uint32_t* csph = nullptr) {
+    const bvh_ray br = bvh_ray_setup(r);
+    const float dd = (r.dx * r.dx + r.dy * r.dy) + r.dz * r.dz;
+    const float eps = iq_fabsf(dd - 1.0f) + 8.0f * 0x1p-24f;
+    sph_fold f = {kTMax, ~0u, 0.0f, ~0u};
+    sbvh_pass<OPT>(p, r, br, eps, 0u, kTMax, f, csph);
+    if (f.iin != ~0u) {
+        // the last inside sphere sets closest = its far root; normal spheres after it lower it
+        closest = f.tin;
+        kind = kHitSphere;
+        idx = f.iin;
+        sph_fold g = {kTMax, ~0u, 0.0f, ~0u};
+        sbvh_pass<OPT>(p, r, br, eps, f.iin + 1u, closest, g);
+        if (g.bi != ~0u && !(closest < g.bt)) {
+            closest = g.bt;
+            idx = g.bi;
+        }
+        return;
+    }
+    const bool sph = f.bi != ~0u;
+    float c = sph ? f.bt : kTMax;
+    int kd = kHitNone;
+    uint32_t id = 0;
+    if (tri_bvh) {
+        bvh_closest<OPT>(p, r, c, kd, id, ctri);
+    } else {
+        const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
+        for (uint32_t j = 0; j < p.ntri_pairs; ++j) {
+            const float4* q = gp + (size_t)j * kTriPairFloat4;
+            test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], r, c, kd, id, 2 * j, 2 * j + 1 < p.ntri);
+        }
+    }
+    if (kd == kHitTri && !(sph && c == f.bt)) {
+        closest = c;
+        kind = kHitTri;
+        idx = id;
+    } else if (sph) {
+        closest = f.bt;
+        kind = kHitSphere;
+        idx = f.bi;
     }
 }
 
@@ -1161,8 +1222,17 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
         if (kBvhPrimary) {
             // Triangles through the exact BVH, spheres through the exact sphere BVH (each falls back to
             // the brute-force fold from global memory where its BVH is absent or the ray is outside
-            // the bounds' assumptions, bvh_ray_ok); triangles first, as in path_tracer.cu:257-295.
-            if (active) {
+            // the bounds' assumptions, bvh_ray_ok). With a sphere BVH the spheres go first and bound the
+            // triangle traversal (closest_spheres_first); otherwise triangles first, as in
+            // path_tracer.cu:257-295. Both give the reference's result.
+            if (active && sbvh_first_ok(p, ray)) {
+                if (OPT & kOptStats) {
+                    ++c_sph_rays;
+                    if (p.bvh_nodes != nullptr && bvh_ray_ok(p, ray)) ++c_tri_rays;
+                }
+                closest_spheres_first<OPT>(p, ray, p.bvh_nodes != nullptr && bvh_ray_ok(p, ray), closest, kind, hidx,
+                                           (OPT & kOptStats) ? c_tri : nullptr, (OPT & kOptStats) ? c_sph : nullptr);
+            } else if (active) {
                 const bool ok = bvh_ray_ok(p, ray);
                 if (ok && p.bvh_nodes != nullptr) {
                     if (OPT & kOptStats) ++c_tri_rays;

@@ -23,10 +23,17 @@ def sbvh_info(pt):
     return n.value, a.value
 
 
-def run_both(scene, w, h, launches, depth, camera=None, pixels=None):
+PRIM = 6959      # kOptDefault | kOptBvhPrimary (iqpt_internal.hpp), a production variant
+
+
+def run_both(scene, w, h, launches, depth, camera=None, pixels=None, opt=None):
     pk = scene.build_packet()
     cam = camera or make_camera(w, h)
     pt = PathTracer(w, h, max_depth=depth, pixels=pixels)
+    if opt is not None:
+        lb = _lib.load()
+        lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, opt), "iqpt_debug_set_kernel_options")
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, max_depth=depth, pixels=pixels)
@@ -57,16 +64,18 @@ def grid(sc, n, r=0.04, y=0.04, prefix="s"):
         sc.add_model(f"{prefix}{i:04d}", "sphere", r, 0.0, (-1.2 + 0.1 * (i % 25), y, -0.3 + 0.1 * (i // 25)))
 
 
-def test_grid_with_ground_on_always_list(require_gpu):
+@pytest.mark.parametrize("opt", [None, PRIM], ids=["auto", "prim"])
+def test_grid_with_ground_on_always_list(require_gpu, opt):
     sc = Scene()
     streamed_base(sc)
     grid(sc, 300)
     sc.add_model("ground", "sphere", 10.0, 0.0, (0.0, -10.0, 0.0))
-    nodes, always = run_both(sc, 96, 64, [2, 1], 8)
+    nodes, always = run_both(sc, 96, 64, [2, 1], 8, opt=opt)
     assert nodes > 0 and always == 1
 
 
-def test_origins_inside_spheres(require_gpu):
+@pytest.mark.parametrize("opt", [None, PRIM], ids=["auto", "prim"])
+def test_origins_inside_spheres(require_gpu, opt):
     """Camera inside a sphere of the BVH (every camera ray takes that sphere's far root), plus nested and
     overlapping spheres so that bounces also start inside spheres."""
     sc = Scene()
@@ -76,11 +85,12 @@ def test_origins_inside_spheres(require_gpu):
     sc.add_model("nest_a", "sphere", 0.35, 0.0, (0.0, 0.45, 0.4))
     sc.add_model("nest_b", "sphere", 0.2, 0.0, (0.05, 0.45, 0.4))          # inside nest_a
     sc.add_model("nest_c", "sphere", 0.25, 0.0, (0.3, 0.5, 0.4))           # overlaps nest_a
-    nodes, always = run_both(sc, 80, 60, [2], 8)
+    nodes, always = run_both(sc, 80, 60, [2], 8, opt=opt)
     assert nodes > 0 and always == 0
 
 
-def test_duplicate_spheres_tie_to_the_later_one(require_gpu):
+@pytest.mark.parametrize("opt", [None, PRIM], ids=["auto", "prim"])
+def test_duplicate_spheres_tie_to_the_later_one(require_gpu, opt):
     """Every sphere twice at the same place: each hit is an exact t tie and the later (second) sphere's
     material must be the one shaded — the duplicates are emissive with different colours."""
     sc = Scene()
@@ -97,7 +107,7 @@ def test_duplicate_spheres_tie_to_the_later_one(require_gpu):
     sc.add_model("floor", "sphere", 10.0, 0.0, (0.0, -10.0, 0.0))
     sc.set_model_material("floor", rough)
     sc.set_model_material("ball", rough)
-    nodes, always = run_both(sc, 96, 64, [3], 6)
+    nodes, always = run_both(sc, 96, 64, [3], 6, opt=opt)
     assert nodes > 0
 
 
