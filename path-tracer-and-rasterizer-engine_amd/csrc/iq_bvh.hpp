@@ -165,7 +165,100 @@ inline uint32_t bf16_up_bits(float v) {
     return (u & 0xffffu) ? (u >> 16) + 1u : (u >> 16);
 }
 
-// Median split on the longest centroid axis, leaves of <= kLeafTris triangles (kept even by padding).
+// Binned surface-area-heuristic split of idx[b, e) (16 bins per axis over the centroid bounds; cost =
+// area(left box) x left count + area(right box) x right count). Falls back to the median on the longest
+// centroid axis when the centroids do not spread. Any split is exact: node boxes are computed from
+// their members. cen(i) / lo(i) / hi(i) give primitive i's centroid and box (float[3]).
+template <class Cen, class Lo, class Hi>
+inline uint32_t sah_split(std::vector<uint32_t>& idx, uint32_t b, uint32_t e, Cen cen, Lo lo, Hi hi) {
+    constexpr int kBins = 16;
+    float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (uint32_t i = b; i < e; ++i)
+        for (int a = 0; a < 3; ++a) {
+            cmin[a] = std::min(cmin[a], cen(idx[i])[a]);
+            cmax[a] = std::max(cmax[a], cen(idx[i])[a]);
+        }
+    auto area = [](const double* l, const double* h) {
+        if (!(l[0] <= h[0])) return 0.0;
+        const double dx = h[0] - l[0], dy = h[1] - l[1], dz = h[2] - l[2];
+        return dx * dy + dy * dz + dz * dx;
+    };
+    auto bin_of = [&](uint32_t t, int ax) {
+        const double ext = (double)cmax[ax] - cmin[ax];
+        const int k = (int)(((double)cen(t)[ax] - cmin[ax]) / ext * kBins);
+        return std::min(kBins - 1, std::max(0, k));
+    };
+    double best = INFINITY;
+    int best_ax = -1, best_bin = 0;
+    for (int ax = 0; ax < 3; ++ax) {
+        if (!(cmax[ax] > cmin[ax])) continue;
+        uint32_t cnt[kBins] = {};
+        double bl[kBins][3], bh[kBins][3];
+        for (int k = 0; k < kBins; ++k)
+            for (int a = 0; a < 3; ++a) {
+                bl[k][a] = INFINITY;
+                bh[k][a] = -INFINITY;
+            }
+        for (uint32_t i = b; i < e; ++i) {
+            const uint32_t t = idx[i];
+            const int k = bin_of(t, ax);
+            ++cnt[k];
+            for (int a = 0; a < 3; ++a) {
+                bl[k][a] = std::min(bl[k][a], (double)lo(t)[a]);
+                bh[k][a] = std::max(bh[k][a], (double)hi(t)[a]);
+            }
+        }
+        double rarea[kBins];
+        uint32_t rcnt[kBins];
+        double l[3] = {INFINITY, INFINITY, INFINITY}, h[3] = {-INFINITY, -INFINITY, -INFINITY};
+        uint32_t n = 0;
+        for (int k = kBins - 1; k >= 1; --k) {
+            for (int a = 0; a < 3; ++a) {
+                l[a] = std::min(l[a], bl[k][a]);
+                h[a] = std::max(h[a], bh[k][a]);
+            }
+            n += cnt[k];
+            rarea[k] = area(l, h);
+            rcnt[k] = n;
+        }
+        for (int a = 0; a < 3; ++a) {
+            l[a] = INFINITY;
+            h[a] = -INFINITY;
+        }
+        n = 0;
+        for (int k = 1; k < kBins; ++k) {
+            for (int a = 0; a < 3; ++a) {
+                l[a] = std::min(l[a], bl[k - 1][a]);
+                h[a] = std::max(h[a], bh[k - 1][a]);
+            }
+            n += cnt[k - 1];
+            if (n == 0 || rcnt[k] == 0) continue;
+            const double c = area(l, h) * n + rarea[k] * rcnt[k];
+            if (c < best) {
+                best = c;
+                best_ax = ax;
+                best_bin = k;
+            }
+        }
+    }
+    if (best_ax >= 0) {
+        const auto it = std::stable_partition(idx.begin() + b, idx.begin() + e,
+                                              [&](uint32_t t) { return bin_of(t, best_ax) < best_bin; });
+        const uint32_t mid = (uint32_t)(it - idx.begin());
+        if (mid > b && mid < e) return mid;
+    }
+    int ax = 0;
+    for (int a = 1; a < 3; ++a)
+        if (cmax[a] - cmin[a] > cmax[ax] - cmin[ax]) ax = a;
+    const uint32_t mid = b + (e - b) / 2;
+    std::nth_element(idx.begin() + b, idx.begin() + mid, idx.begin() + e, [&](uint32_t x, uint32_t y) {
+        const float cx = cen(x)[ax], cy = cen(y)[ax];
+        return cx < cy || (cx == cy && x < y);
+    });
+    return mid;
+}
+
+// Binned-SAH splits (sah_split), leaves of <= kLeafTris triangles (kept even by padding).
 constexpr uint32_t kLeafTris = 4;
 
 inline void build(build_input& in, build_output& out) {
@@ -176,7 +269,7 @@ inline void build(build_input& in, build_output& out) {
     for (uint32_t i = 0; i < idx.size(); ++i) idx[i] = i;
     // DFS preorder with an explicit stack; skip pointers patched when a subtree closes
     struct frame {
-        uint32_t begin, end, node, stage;
+        uint32_t begin, end, node, stage, mid;
     };
     std::vector<frame> st;
     auto make = [&](uint32_t b, uint32_t e) {
@@ -246,7 +339,7 @@ inline void build(build_input& in, build_output& out) {
         out.nodes.push_back(n);
         return (uint32_t)out.nodes.size() - 1;
     };
-    st.push_back({0, (uint32_t)idx.size(), make(0, (uint32_t)idx.size()), 0});
+    st.push_back({0, (uint32_t)idx.size(), make(0, (uint32_t)idx.size()), 0, 0});
     while (!st.empty()) {
         frame& f = st.back();
         const uint32_t count = f.end - f.begin;
@@ -261,31 +354,19 @@ inline void build(build_input& in, build_output& out) {
             continue;
         }
         if (f.stage == 0) {
-            // split on the longest axis of the centroid bounds, at the median
-            float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
-            for (uint32_t i = f.begin; i < f.end; ++i)
-                for (int a = 0; a < 3; ++a) {
-                    cmin[a] = std::min(cmin[a], in.centroid[3 * idx[i] + a]);
-                    cmax[a] = std::max(cmax[a], in.centroid[3 * idx[i] + a]);
-                }
-            int ax = 0;
-            for (int a = 1; a < 3; ++a)
-                if (cmax[a] - cmin[a] > cmax[ax] - cmin[ax]) ax = a;
-            const uint32_t mid = f.begin + count / 2;
-            std::nth_element(idx.begin() + f.begin, idx.begin() + mid, idx.begin() + f.end,
-                             [&](uint32_t a, uint32_t b) {
-                                 const float ca = in.centroid[3 * a + ax], cb = in.centroid[3 * b + ax];
-                                 return ca < cb || (ca == cb && a < b);
-                             });
+            const uint32_t mid = sah_split(
+                idx, f.begin, f.end, [&](uint32_t t) { return &in.centroid[3 * t]; },
+                [&](uint32_t t) { return &in.lo[3 * t]; }, [&](uint32_t t) { return &in.hi[3 * t]; });
+            f.mid = mid;
             f.stage = 1;
             const uint32_t b = f.begin;
             const uint32_t n = make(b, mid);
-            st.push_back({b, mid, n, 0});
+            st.push_back({b, mid, n, 0, 0});
         } else if (f.stage == 1) {
             f.stage = 2;
-            const uint32_t mid = f.begin + count / 2, e = f.end;
+            const uint32_t mid = f.mid, e = f.end;
             const uint32_t n = make(mid, e);
-            st.push_back({mid, e, n, 0});
+            st.push_back({mid, e, n, 0, 0});
         } else {
             out.nodes[f.node].skip = (uint32_t)out.nodes.size();
             st.pop_back();
@@ -354,8 +435,15 @@ inline void build_spheres(const std::vector<float>& sph4, const std::vector<uint
     order.clear();
     if (ids.empty()) return;
     std::vector<uint32_t> idx(ids);
+    std::vector<float> slo(sph4.size() / 4 * 3), shi(sph4.size() / 4 * 3);   // sphere boxes (SAH)
+    for (size_t k = 0; k < sph4.size() / 4; ++k)
+        for (int a = 0; a < 3; ++a) {
+            const float r = std::fabs(sph4[4 * k + 3]);
+            slo[3 * k + a] = sph4[4 * k + a] - r;
+            shi[3 * k + a] = sph4[4 * k + a] + r;
+        }
     struct frame {
-        uint32_t begin, end, node, stage;
+        uint32_t begin, end, node, stage, mid;
     };
     std::vector<frame> st;
     auto make = [&](uint32_t b, uint32_t e) {
@@ -384,7 +472,7 @@ inline void build_spheres(const std::vector<float>& sph4, const std::vector<uint
         nodes.push_back(n);
         return (uint32_t)nodes.size() - 1;
     };
-    st.push_back({0, (uint32_t)idx.size(), make(0, (uint32_t)idx.size()), 0});
+    st.push_back({0, (uint32_t)idx.size(), make(0, (uint32_t)idx.size()), 0, 0});
     while (!st.empty()) {
         frame& f = st.back();
         const uint32_t count = f.end - f.begin;
@@ -397,30 +485,19 @@ inline void build_spheres(const std::vector<float>& sph4, const std::vector<uint
             continue;
         }
         if (f.stage == 0) {
-            float cmin[3] = {INFINITY, INFINITY, INFINITY}, cmax[3] = {-INFINITY, -INFINITY, -INFINITY};
-            for (uint32_t i = f.begin; i < f.end; ++i)
-                for (int a = 0; a < 3; ++a) {
-                    cmin[a] = std::min(cmin[a], sph4[4 * (size_t)idx[i] + a]);
-                    cmax[a] = std::max(cmax[a], sph4[4 * (size_t)idx[i] + a]);
-                }
-            int ax = 0;
-            for (int a = 1; a < 3; ++a)
-                if (cmax[a] - cmin[a] > cmax[ax] - cmin[ax]) ax = a;
-            const uint32_t mid = f.begin + count / 2;
-            std::nth_element(idx.begin() + f.begin, idx.begin() + mid, idx.begin() + f.end,
-                             [&](uint32_t a, uint32_t b) {
-                                 const float ca = sph4[4 * (size_t)a + ax], cb = sph4[4 * (size_t)b + ax];
-                                 return ca < cb || (ca == cb && a < b);
-                             });
+            const uint32_t mid = sah_split(
+                idx, f.begin, f.end, [&](uint32_t t) { return &sph4[4 * (size_t)t]; },
+                [&](uint32_t t) { return &slo[3 * (size_t)t]; }, [&](uint32_t t) { return &shi[3 * (size_t)t]; });
+            f.mid = mid;
             f.stage = 1;
             const uint32_t b = f.begin;
             const uint32_t n = make(b, mid);
-            st.push_back({b, mid, n, 0});
+            st.push_back({b, mid, n, 0, 0});
         } else if (f.stage == 1) {
             f.stage = 2;
-            const uint32_t mid = f.begin + count / 2, e = f.end;
+            const uint32_t mid = f.mid, e = f.end;
             const uint32_t n = make(mid, e);
-            st.push_back({mid, e, n, 0});
+            st.push_back({mid, e, n, 0, 0});
         } else {
             nodes[f.node].skip = (uint32_t)nodes.size();
             st.pop_back();
