@@ -259,7 +259,10 @@ inline uint32_t sah_split(std::vector<uint32_t>& idx, uint32_t b, uint32_t e, Ce
 }
 
 // Binned-SAH splits (sah_split), leaves of <= kLeafTris triangles (kept even by padding).
-constexpr uint32_t kLeafTris = 4;
+#ifndef IQPT_LEAF_TRIS
+#define IQPT_LEAF_TRIS 4
+#endif
+constexpr uint32_t kLeafTris = IQPT_LEAF_TRIS;
 
 inline void build(build_input& in, build_output& out) {
     out.nodes.clear();
@@ -424,7 +427,10 @@ inline double sphere_growth(double rmin, double rmax, double S) {
     return K / (std::sqrt(rmin * rmin + K) + rmin) + 4.0 * kU * S + 8.0 * kU * rmax;
 }
 
-constexpr uint32_t kLeafSpheres = 4;
+#ifndef IQPT_LEAF_SPHERES
+#define IQPT_LEAF_SPHERES 4
+#endif
+constexpr uint32_t kLeafSpheres = IQPT_LEAF_SPHERES;
 
 // centres/radii: float per sphere (c.xyz, r) in packet order; bvh: indices (packet order) of the
 // spheres put in the BVH. Median split on the longest centre axis. Fills the nodes (DFS preorder with
