@@ -4,29 +4,35 @@
 Metric: Mrays/s at 1920x1080, 8 bounces (C2: Cornell box, 5 quads + 2 spheres, 64 spp per frame),
 with the per-pixel RMSE vs the CPU oracle (reference semantics) reported beside it.
 
-One step = one 64-spp C2 frame per GPU rendered by the HIP megakernel (one launch per GPU, one
-process per GPU). Two multi-GPU modes:
+One step = one 64-spp C2 frame rendered by the HIP megakernel, one process per GPU.
 
-* --scaling weak (default): every rank renders the full 1080p frame with its own RNG
-  streams (seed 1984 + rank; rank 0 is the reference's own seed), so per-GPU work is fixed and the
-  job grows with N — N independent 64-spp estimates of the same view. No collective in the timed
-  region; after timing, the N accumulators are averaged onto rank 0 with one RCCL reduce (the
-  N x 64-spp image).
-* --scaling strong: the pixel rows of ONE frame are dealt cyclically over the ranks and the float4
-  accumulators are gathered to rank 0 over RCCL inside every step (bit-identical to the 1-GPU
-  frame).
+* N = 1: the whole frame on one GPU.
+* N > 1, --scaling strong (default; C3 of BASELINE.json): the pixel rows of ONE frame
+  are dealt cyclically over the ranks (row y -> rank y mod N; RNG streams are keyed by the global
+  pixel id, path_tracer.cu:36-46/336-339, so the assembled frame is bit-identical to the 1-GPU frame)
+  and every step ends with an RCCL gather over xGMI of the presented BGRA8 framebuffer to rank 0
+  (--gather frame; the reference reads this buffer back every frame, path_tracer.cu:385) or of the
+  float accumulators (--gather accum). After the timed steps the float accumulators are gathered
+  once and checked.
+* N > 1, --scaling weak (opt-in): every rank renders the full frame with its own RNG streams (seed
+  1984 + rank): N independent estimates, no collective in the timed region.
 
 value = closest-hit queries traced by all ranks in the K timed steps / the max over ranks of the
-timed wall time.
+barrier-bracketed wall time.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--no-cpu-baseline] [--config c2]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2] [--scaling strong|weak]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+Without torch.distributed.run, --gpus N > 1 starts its N rank processes itself (before anything
+touches the GPU) and returns rank 0's JSON line.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 from pathlib import Path
@@ -34,17 +40,8 @@ from pathlib import Path
 REPO = Path(__file__).resolve().parent
 sys.path.insert(0, str(REPO / "path-tracer-and-rasterizer-engine_amd"))
 
-import numpy as np  # noqa: E402
-import torch  # noqa: E402
-import torch.distributed as dist  # noqa: E402
-
-import iqpt  # noqa: E402
-from iqpt import dist as iqdist  # noqa: E402
-from iqpt.scene import CONFIGS, Scene, make_camera, packet_stats  # noqa: E402
-
-FP32_PEAK_TFLOPS = 157.3        # MI355X FP32 vector (= f32 MFMA) peak, MI355X_MICROARCH.md
+FP32_PEAK_TFLOPS = 157.3        # MI355X FP32 vector peak (MI355X_MICROARCH.md); the path runs on the VALU
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E peak, MI355X_MICROARCH.md
-HBM_PEAK_GBS = 8000.0           # MI355X HBM3E spec
 
 
 def parse():
@@ -56,27 +53,85 @@ def parse():
     ap.add_argument("--spp", type=int, default=0,
                     help="samples per pixel per step (default: the config's; a progressive pass of C5's 1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
+                    help="wall time of the CPU-baseline sample (BASELINE.md §3: >= 60 s)")
     ap.add_argument("--verify-rows", type=int, default=16)
     ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r01_pmc_traffic_v2.json"))
     ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r01_c2_pmc_mix_v4.json"),
                     help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy)")
+    ap.add_argument("--work-json", default="",
+                    help="executed-work counters of the config (tools/work_counters.py): prices C4/C5")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo = rehearsal)")
     ap.add_argument("--one-device", action="store_true",
                     help="all ranks on GPU 0 (multi-rank rehearsal on a 1-GPU box; use with --backend gloo)")
     ap.add_argument("--save-frame", default="", help="rank 0 writes the assembled float frame (.npy)")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: every rank renders the full frame with seed 1984+rank; strong: rows of one frame")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong (default): rows of one frame + gather; weak: every rank a full frame, seed 1984+rank")
+    ap.add_argument("--gather", default="frame", choices=["frame", "accum"],
+                    help="what the strong-scaling step gathers to rank 0: the BGRA8 frame or the float accumulators")
+    ap.add_argument("--split", default="auto", choices=["auto", "on", "off"],
+                    help="sample-parallel chains (iqpt_set_split, DESIGN.md §3.7)")
     return ap.parse_args()
 
 
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def spawn_ranks(args) -> int:
+    """--gpus N > 1 without a launcher: start N fresh rank processes (nothing here has touched the GPU)
+    with the torch.distributed environment, wait for all, return the worst exit code. A failing rank
+    ends the others (their exact PIDs), so no rank waits forever in a collective."""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(Path(__file__).resolve())] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def cpu_info() -> dict:
+    model = ""
+    try:
+        for line in Path("/proc/cpuinfo").read_text().splitlines():
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"cpu_model": model, "cpus_visible": os.cpu_count()}
+
+
+def baseline_threads() -> int:
+    """The CPU share of this GPU: OMP_NUM_THREADS where the harness sets it (16 per GPU on the MI355X
+    boxes), else every CPU this process may run on."""
+    env = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return env or len(os.sched_getaffinity(0))
+
+
 def cpu_baseline(cfg, pk, cam, seconds: float) -> dict:
-    """The oracle (reference restated as a host loop, OpenMP) on the same scene: full-frame 1-spp
-    passes until `seconds` of wall time (Mrays/s does not depend on spp)."""
+    """The oracle (the reference kernel restated as a host loop, OpenMP, same per-ray work) on the same
+    scene: full-frame 1-spp passes until `seconds` of wall time (Mrays/s does not depend on spp)."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # cpu_baseline leg only
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    threads = baseline_threads()
     fr = oracle.OracleFrame(cfg.width, cfg.height, max_depth=cfg.max_depth)
     rays = 0
     passes = 0
@@ -88,14 +143,17 @@ def cpu_baseline(cfg, pk, cam, seconds: float) -> dict:
         if dt >= seconds:
             break
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "per_core": rays / dt / 1e6 / threads, **cpu_info(),
             "sample": f"{passes} full {cfg.width}x{cfg.height} 1-spp passes of {cfg.preset} "
-                      f"(max_depth {cfg.max_depth}) in {dt:.1f} s, {rays} rays"}
+                      f"(max_depth {cfg.max_depth}) in {dt:.1f} s, {rays} rays, {threads} OpenMP threads"}
 
 
 def verify_vs_oracle(cfg, pk, cam, lin_rank, rank, world, nrows, seed=1984, spp=None) -> dict:
-    """After the first 64-spp frame: compare a band of this rank's rows with the oracle. `rank` and
-    `world` describe the row partition (world 1 = the rank owns the whole frame)."""
+    """After the first frame: compare a band of this rank's rows with the oracle. `rank` and `world`
+    describe the row partition (world 1 = the rank owns the whole frame)."""
+    import iqpt
     sys.path.insert(0, str(REPO / "oracle"))
+    import numpy as np
     import oracle
     y_band = int(cfg.height * 0.46)                     # through both spheres
     first = y_band + ((rank - y_band) % world)          # first row >= y_band owned by this rank
@@ -111,15 +169,82 @@ def verify_vs_oracle(cfg, pk, cam, lin_rank, rank, world, nrows, seed=1984, spp=
     return {"rmse": rmse, "bitexact_frac": float(same.mean()), "pixels": int(mine.shape[0])}
 
 
+def load_json(path: str, cfg_name: str):
+    p = Path(path) if path else None
+    if not p or not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+    except (OSError, ValueError):
+        return None
+    return d if d.get("config") == cfg_name else None
+
+
+def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name) -> dict:
+    """The dominant kernel against the FP32 vector (VALU) peak.
+
+    C1/C2/C3: algorithmic FLOPs F_ray = 52 T + 19 S per ray (the reference's brute-force
+    closest hit) x rays of one launch / the launch's HIP-event time. C4/C5: the BVH and the tile masks
+    skip almost all of the brute-force tests, so the work is priced from EXECUTED tests per ray
+    (tools/work_counters.py: node tests, leaf Möller–Trumbore tests, sphere tests, from the kOptStats
+    counters) when --work-json has them; the brute-force rate is kept as "reference_equivalent"."""
+    f_ray = cfg.flops_per_ray
+    t = kern_avg_ms * 1e-3
+    ref_tflops = f_ray * rays_per_launch / t / 1e12 if t > 0 else 0.0
+    traffic = None
+    pmc = load_json(args.pmc_json, cfg.name)
+    if pmc and world == 1:
+        traffic = pmc.get("hbm_bytes_per_launch")
+    mix = load_json(args.pmc_mix_json, cfg.name)
+    work = load_json(args.work_json, cfg.name)
+    out = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "kernel": kernel_name,
+           "kernel_avg_ms": round(kern_avg_ms, 4), "traffic": traffic,
+           "valu_busy_frac": (mix or {}).get("valu_busy_frac") if world == 1 else None,
+           "wave_time_split": (mix or {}).get("wave_time_split") if world == 1 else None}
+    if work and work.get("flops_per_ray"):
+        ex = work["flops_per_ray"] * rays_per_launch / t / 1e12 if t > 0 else 0.0
+        out.update(achieved=round(ex, 4), frac=round(ex / FP32_PEAK_TFLOPS, 5),
+                   flops_per_ray=work["flops_per_ray"], work_basis="executed tests per ray (" + args.work_json + ")",
+                   reference_equivalent={"achieved": round(ref_tflops, 2), "flops_per_ray": f_ray,
+                                         "frac": round(ref_tflops / FP32_PEAK_TFLOPS, 4)})
+    elif ref_tflops <= FP32_PEAK_TFLOPS:
+        out.update(achieved=round(ref_tflops, 4), frac=round(ref_tflops / FP32_PEAK_TFLOPS, 5),
+                   flops_per_ray=f_ray, work_basis="algorithmic F_ray = 52 T + 19 S (SURVEY.md §8d)")
+    else:
+        # the brute-force price exceeds the peak: the kernel skips that work, so it is no roofline
+        out.update(achieved=None, frac=None, flops_per_ray=None,
+                   work_basis="none: run tools/work_counters.py for the executed-work price",
+                   reference_equivalent={"achieved": round(ref_tflops, 2), "flops_per_ray": f_ray})
+    if traffic and t > 0:
+        out["hbm"] = {"achieved": round(traffic / t / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                      "frac": round(traffic / t / 1e9 / HBM_PEAK_GBPS, 5)}
+    out["note"] = ("achieved = FLOPs per launch / the launch's HIP-event time (kernel_avg_ms) against the FP32 "
+                   "vector peak; the path runs on the VALU, nothing is a dense contraction (no MFMA). traffic: "
+                   "PMC HBM bytes per launch (tools/pmc_traffic.py); valu_busy_frac / wave_time_split: PMC "
+                   "instruction-mix pass (tools/pmc_mix.py), profiles/.")
+    return out
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import iqpt
+    from iqpt import _lib
+    from iqpt import dist as iqdist
+    from iqpt.scene import CONFIGS, Scene, make_camera, packet_stats
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    # Rehearsal of the multi-rank path on a 1-GPU box: every rank on device 0 and the gather over
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # Rehearsal of the multi-rank path on a 1-GPU box: every rank on device 0 and the collectives over
     # gloo through host memory (RCCL refuses two ranks on one GPU). The driver's runs use nccl.
     device = 0 if args.one_device else local_rank
     torch.cuda.set_device(device)
@@ -128,6 +253,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", device))
         else:
             dist.init_process_group("gloo")
+    n_ranks_seen = dist.get_world_size() if world > 1 else 1
 
     def barrier():
         if world > 1:
@@ -145,33 +271,51 @@ def main():
     part_rank, part_world = (0, 1) if weak else (rank, world)
     seed = iqpt.DEFAULT_SEED + (rank if weak else 0)
     ps = iqdist.pixel_set_for_rank(cfg.width, cfg.height, part_rank, part_world)
+    setup = {}
+    t0 = time.perf_counter()
     pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, seed=seed, max_depth=cfg.max_depth, device=device)
+    setup["create_and_rng_init_ms"] = (time.perf_counter() - t0) * 1e3
+    pt.set_split({"auto": _lib.SPLIT_AUTO, "on": _lib.SPLIT_ON, "off": _lib.SPLIT_OFF}[args.split])
     pt.set_camera(cam)
+    t0 = time.perf_counter()
     pt.upload_packet(pk)
+    setup["upload_relayout_bvh_ms"] = (time.perf_counter() - t0) * 1e3
+    t0 = time.perf_counter()
+    pt.prepare()
+    setup["tile_masks_order_split_ms"] = (time.perf_counter() - t0) * 1e3
 
     on_gpu = args.backend == "nccl"
     tdev = "cuda" if on_gpu else "cpu"
     max_px = iqdist.max_rows(cfg.height, part_world) * cfg.width
-    accum = torch.zeros((max_px, 4), dtype=torch.float32, device=tdev) if world > 1 else None
-    gather_list = ([torch.empty_like(accum) for _ in range(world)]
-                   if (world > 1 and rank == 0 and not weak) else None)
-    frame = None
+    strong_multi = world > 1 and not weak
+    words = 4 if args.gather == "accum" else 1
+    dtype = torch.float32 if args.gather == "accum" else torch.int32
+    buf = torch.zeros((max_px, words), dtype=dtype, device=tdev) if strong_multi else None
+    gather_list = [torch.empty_like(buf) for _ in range(world)] if (strong_multi and rank == 0) else None
+    assembled = None
 
-    def fetch_accum():
+    def fetch(dst, what):
+        n = dst.numel() * 4
         if on_gpu:
-            pt.copy_accum_device(accum.data_ptr(), accum.numel() * 4)     # D2D, then RCCL
+            (pt.copy_accum_device if what == "accum" else pt.copy_frame_device)(dst.data_ptr(), n)
         else:
-            lin_host, _ = pt.read()
-            accum[: lin_host.shape[0]] = torch.from_numpy(lin_host)
+            lin_host, bgra_host = pt.read()
+            src = lin_host if what == "accum" else bgra_host.view(np.int32)
+            dst[: src.shape[0]] = torch.from_numpy(np.ascontiguousarray(src).reshape(src.shape[0], -1))
+
+    def deinterleave(parts, channels):
+        # rank r holds rows r, r + N, ...: [N, rows, W, c] -> [rows, N, W, c] -> the first H rows
+        st = torch.stack(parts).view(world, -1, cfg.width, channels)
+        return st.transpose(0, 1).reshape(-1, cfg.width, channels)[: cfg.height]
 
     def step():
-        nonlocal frame
+        nonlocal assembled
         pt.render(spp_step)
-        if world > 1 and not weak:
-            fetch_accum()
-            dist.gather(accum, gather_list, dst=0)
+        if strong_multi:
+            fetch(buf, args.gather)
+            dist.gather(buf, gather_list, dst=0)
             if rank == 0:
-                frame = iqdist.assemble(gather_list, cfg.width, cfg.height, world)
+                assembled = deinterleave(gather_list, words)
 
     # warmup (the first frame is also checked against the oracle)
     verify = None
@@ -197,29 +341,35 @@ def main():
     elapsed = t1 - t0
     rays = pt.rays() - rays0
     kern_ms, launches = pt.kernel_time()
-    if weak and world > 1:
-        # after timing: the N independent estimates averaged onto rank 0 (the N x spp image)
-        fetch_accum()
-        dist.reduce(accum, dst=0, op=dist.ReduceOp.SUM)
-        if rank == 0:
-            frame = accum / float(world)
 
-    vals = torch.tensor([elapsed, float(rays), kern_ms / max(1, launches), verify["rmse"] if verify else 0.0,
-                         verify["bitexact_frac"] if verify else 1.0], dtype=torch.float64,
-                        device="cuda" if on_gpu else "cpu")
+    # after timing: the float frame on rank 0 (strong: the gathered accumulators de-interleaved, bit-
+    # identical to one GPU's frame; weak: the N independent estimates averaged)
+    frame = None
     if world > 1:
-        t_max = vals[0:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        acc = torch.zeros((max_px, 4), dtype=torch.float32, device=tdev)
+        fetch(acc, "accum")
+        if weak:
+            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                frame = (acc / float(world))[: cfg.width * cfg.height]
+        else:
+            parts = [torch.empty_like(acc) for _ in range(world)] if rank == 0 else None
+            dist.gather(acc, parts, dst=0)
+            if rank == 0:
+                frame = deinterleave(parts, 4).reshape(-1, 4)
+
+    dev = "cuda" if on_gpu else "cpu"
+    vals = torch.tensor([elapsed, float(rays), kern_ms / max(1, launches), verify["rmse"] if verify else 0.0,
+                         verify["bitexact_frac"] if verify else 1.0], dtype=torch.float64, device=dev)
+    if world > 1:
+        mx = vals[[0, 2, 3]].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
         tot = vals[1:2].clone()
         dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        kmax = vals[2:3].clone()
-        dist.all_reduce(kmax, op=dist.ReduceOp.MAX)
-        rmse = vals[3:4].clone()
-        dist.all_reduce(rmse, op=dist.ReduceOp.MAX)
-        bx = vals[4:5].clone()
-        dist.all_reduce(bx, op=dist.ReduceOp.MIN)
-        elapsed, total_rays, kern_avg_ms = t_max.item(), tot.item(), kmax.item()
-        rmse_v, bitexact = rmse.item(), bx.item()
+        mn = vals[4:5].clone()
+        dist.all_reduce(mn, op=dist.ReduceOp.MIN)
+        elapsed, kern_avg_ms, rmse_v = mx.tolist()
+        total_rays, bitexact = tot.item(), mn.item()
     else:
         total_rays, kern_avg_ms = float(rays), kern_ms / max(1, launches)
         rmse_v, bitexact = (verify["rmse"], verify["bitexact_frac"]) if verify else (None, None)
@@ -227,30 +377,8 @@ def main():
     if rank == 0:
         mrays = total_rays / elapsed / 1e6
         rays_per_launch = float(rays) / max(1, args.steps)           # rank 0's kernel
-        f_ray = cfg.flops_per_ray
-        achieved_tflops = f_ray * rays_per_launch / (kern_avg_ms * 1e-3) / 1e12 if kern_avg_ms > 0 else 0.0
-        traffic = None
-        pmc_path = Path(args.pmc_json)
-        if pmc_path.exists():
-            try:
-                pmc = json.loads(pmc_path.read_text())
-                if pmc.get("config") == cfg.name and world == 1:
-                    traffic = pmc.get("hbm_bytes_per_launch")
-            except Exception:
-                traffic = None
-        valu_busy = None
-        wave_split = None
-        mix_path = Path(args.pmc_mix_json)
-        if mix_path.exists():
-            try:
-                mix = json.loads(mix_path.read_text())
-                if mix.get("config") == cfg.name and world == 1:
-                    valu_busy = mix.get("valu_busy_frac")
-                    wave_split = mix.get("wave_time_split")
-            except Exception:
-                valu_busy = None
-        # weak: every rank renders the whole frame; strong: the ranks share one frame
         samples = cfg.width * cfg.height * spp_step * args.steps * (world if weak else 1)
+        gathered = "BGRA8 frame" if args.gather == "frame" else "float4 accumulators"
         out = {
             "metric": "Mrays/sec at 1920x1080 8-bounce; per-pixel RMSE vs reference",
             "value": round(mrays, 3),
@@ -263,60 +391,33 @@ def main():
             "scaling": "weak" if weak else "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "data": ("synthetic (procedural Cornell-box scene of SURVEY.md §8d, seed 1984"
+            "data": ("synthetic (procedural scene of SURVEY.md §8d, seed 1984"
                      + (", rank r: seed 1984+r)" if weak and world > 1 else ")")),
-            "config": {"workload": f"{cfg.name}:{cfg.preset}", "width": cfg.width, "height": cfg.height,
+            "config": {"workload": f"{cfg.name}:{cfg.preset}" + ("" if world == 1 or weak else " (C3 row-tiled)"),
+                       "width": cfg.width, "height": cfg.height,
                        "spp_per_step": spp_step, "max_depth": cfg.max_depth, "triangles": stats["triangles"],
                        "spheres": stats["spheres"],
                        "partition": (f"full frame per rank x{world} (seed 1984+rank)" if weak
-                                     else f"cyclic rows x{world}"),
+                                     else (f"cyclic rows x{world}" if world > 1 else "full frame")),
                        "collective": ("none" if world == 1 else
                                       ("none in the timed region; one reduce of the accumulators after it"
-                                       if weak else "gather of float4 accumulators every step")
-                                      + (" (rccl)" if on_gpu else " (gloo via host, rehearsal)"))},
+                                       if weak else f"gather of the {gathered} to rank 0 every step")
+                                      + (" (rccl)" if on_gpu else " (gloo via host, rehearsal)")),
+                       "split": args.split},
+            "n_ranks_seen": n_ranks_seen,
             "msamples_per_s": round(samples / elapsed / 1e6, 3),
             "rays_per_sample": round(total_rays / samples, 5),
             "rmse_vs_oracle": rmse_v,
             "bitexact_frac_vs_oracle": bitexact,
-            "roofline": {
-                # compute-bound: priced against the dense f32 MFMA peak, which equals the FP32 vector
-                # peak (157.3 TFLOP/s); the kernel runs on the vector ALU (nothing here is a dense
-                # contraction), see "compute_unit"
-                "bound": "mfma",
-                "compute_unit": "valu",
-                "achieved": round(achieved_tflops, 4),
-                "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": round(achieved_tflops / FP32_PEAK_TFLOPS, 5),
-                "traffic": traffic,
-                "kernel": iqpt.kernel_name(),
-                "kernel_avg_ms": round(kern_avg_ms, 4),
-                "flops_per_ray": f_ray,
-                "valu_busy_frac": valu_busy,
-                "wave_time_split": wave_split,
-                "hbm": ({"achieved": round(traffic / (kern_avg_ms * 1e-3) / 1e9, 2), "peak": HBM_PEAK_GBPS,
-                         "unit": "GB/s", "frac": round(traffic / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 5)}
-                        if traffic and kern_avg_ms > 0 else None),
-                "note": "algorithmic FLOPs F_ray = 52 T + 19 S (SURVEY.md §8d) x rays per launch / HIP-event "
-                        "kernel time against the f32 peak: the dense f32 MFMA peak of MI355X_MICROARCH.md, equal "
-                        "to the FP32 vector peak; the kernel runs on the vector ALU (compute_unit), nothing "
-                        "here is a dense contraction. "
-                        "valu_busy_frac: share of SIMD time with a VALU instruction in flight (PMC "
-                        "SQ_ACTIVE_INST_VALU); wave_time_split: issuing / ready but behind other waves / parked "
-                        "on s_waitcnt (LDS and memory latency), profiles/. The VALU pipe is ~0.9 busy but the "
-                        "launch is not set by VALU issue alone (DESIGN.md §3.1); the FLOP fraction is low "
-                        "because MT/RNG/compare instructions are not FMA-dense. hbm: PMC bytes per launch "
-                        "(traffic) over the kernel time against 8 TB/s"
-                        + ("; frac > 1: the reference's brute-force tests per ray, most of which the tile masks "
-                           "and the BVH skip (DESIGN.md §5)" if achieved_tflops > FP32_PEAK_TFLOPS else ""),
-            },
+            "setup_ms": {k: round(v, 2) for k, v in setup.items()},
+            "roofline": roofline(cfg, args, world, rays_per_launch, kern_avg_ms, iqpt.kernel_name()),
         }
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(cfg, pk, cam, args.cpu_seconds)
         if args.save_frame:
             if frame is None:
                 frame = torch.from_numpy(pt.read()[0])
-            np.save(args.save_frame, frame.cpu().numpy() if hasattr(frame, "cpu") else frame)
+            np.save(args.save_frame, frame.cpu().numpy())
         print(json.dumps(out), flush=True)
     pt.close()
     if world > 1:

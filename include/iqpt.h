@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define IQPT_ABI_VERSION 2
+#define IQPT_ABI_VERSION 3
 
 typedef enum iqpt_status {
     IQPT_OK = 0,
@@ -172,6 +172,23 @@ int iqpt_upload_packet(iqpt_ctx* ctx, const iqpt_packet_desc* packet);
 int iqpt_render(iqpt_ctx* ctx, uint32_t spp);
 int iqpt_sync(iqpt_ctx* ctx);
 
+/* Sample-parallel chains (no reference counterpart: the reference runs one sample per
+ * pixel per launch, path_tracer.cu:330-366). A pixel's samples are one sequential XORWOW stream
+ * (path_tracer.cu:339), so its samples cannot simply be spread over threads; in split mode the pixels
+ * whose camera rays may scatter have a sample evaluated at every even stream offset of a window in
+ * parallel, then the chain is stitched in order — bit-identical results, more parallelism when a
+ * context owns few pixels (a row share of a multi-GPU frame). AUTO (the default) splits when the
+ * owned pixels are few per resident GPU lane; ON / OFF force it (resident scenes only). */
+#define IQPT_SPLIT_AUTO (-1)
+#define IQPT_SPLIT_OFF 0
+#define IQPT_SPLIT_ON 1
+int iqpt_set_split(iqpt_ctx* ctx, int mode);
+
+/* Builds the per-view acceleration state (the tile masks, queue order and split set of the current
+ * camera and packet) now instead of inside the next iqpt_render, and synchronises: lets a caller time
+ * the setup the reference pays on every scene change (path_tracer.cu:389-392). Optional. */
+int iqpt_prepare(iqpt_ctx* ctx);
+
 /* path_tracer::reset: the next sample restarts the running mean at frame 1 and the BGRA frame is
  * cleared; the accumulator and RNG states are kept, exactly as the reference (path_tracer.cu:394-400). */
 int iqpt_reset(iqpt_ctx* ctx);
@@ -185,6 +202,10 @@ int iqpt_read_rng(iqpt_ctx* ctx, uint32_t* states);
 /* Device-to-device copy of the accumulator (npix float4) into a caller device buffer on the
  * ctx's stream (used by the multi-GPU gather). Synchronises. */
 int iqpt_copy_accum_device(iqpt_ctx* ctx, void* dst_device, size_t bytes);
+/* Device-to-device copy of the BGRA8 frame (npix uint32, compact order) into a caller device buffer:
+ * the multi-GPU gather of the presented frame (path_tracer.cu:385 reads this buffer back every
+ * frame). Synchronises. */
+int iqpt_copy_frame_device(iqpt_ctx* ctx, void* dst_device, size_t bytes);
 
 int iqpt_num_pixels(const iqpt_ctx* ctx, uint64_t* npix);
 int iqpt_frame_count(const iqpt_ctx* ctx, uint64_t* frames);

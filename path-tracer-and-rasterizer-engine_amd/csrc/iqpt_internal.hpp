@@ -118,8 +118,75 @@ struct kparams {
     const uint32_t* sbvh_always;
     uint32_t sbvh_nnodes, sbvh_nalways;
     float sbvh_gulp;
+    // kOptSplit: sample-parallel chains. A "split pixel" sp (slot sp of the split set,
+    // split tile sp / 64, pixel sp % 64 of that tile) whose chains are long ("heavy": its last launch
+    // took >= heavy_rho slots per sample) has a sample evaluated speculatively at every even RNG offset
+    // 2j ("slot" j) of a window of M slots in round 1, by runs of R consecutive slots, and the chain is
+    // stitched in order by iqpt_split_stitch_kernel; the split tiles' light pixels run anchored; a chain
+    // that leaves its window is finished by an anchored lane in round 2.
+    uint32_t split_round;            // 1: runs + anchored tiles + light split pixels, 2: anchored leftovers
+    uint32_t n_anchor;               // round 1: the anchored tiles anchor_order[]
+    const uint32_t* anchor_order;
+    uint32_t n_split_tiles;
+    const uint32_t* split_tiles;     // split tile -> tile index
+    const uint32_t* chunks;          // round 1 run chunks (tile, split tile | run << 23), built by the prep
+    const uint32_t* chunk_count;
+    uint32_t split_len;              // R: slots per run
+    uint32_t refill_min;             // idle lanes before a refill (1 = every iteration with an idle lane)
+    uint32_t ns_cap, m_cap;          // split pixel slots (split tiles x 64); window cap (multiple of 16)
+    const uint32_t* sp_win;          // M of a heavy pixel's window this launch, 0 for a light pixel
+    uint32_t* sp_rho;                // slots per sample of the pixel's last chain, x 256 (0 = none)
+    const uint32_t* run_st;          // (G_max + 1) x 6 planes of ns_cap words: state at slot r R, at M (plane G_max)
+    float4_storage* res;             // res[sp * m_cap + j]: clamped colour, slots consumed (uint bits in w)
+    uint8_t* nres;                   // nres[sp * m_cap + j]: slots consumed (the stitch's walk)
+    const uint32_t* left;            // round 2: leftover split slots
+    const uint32_t* left_count;
+    const uint32_t* sp_pix;          // storage index of split slot sp (~0u: no pixel)
+    const uint32_t* sp_st;           // 6 planes of ns_cap: a leftover's state at its chain position
+    const float4_storage* sp_acc;    // a leftover's accumulator, samples done (uint bits in w)
 };
 constexpr int kSphNodeFloat4 = 3;
+
+// iqpt_split_prep_kernel / iqpt_split_stitch_kernel (kOptSplit).
+struct ksplit {
+    uint32_t ns_cap, spp, m_cap, g_max, run_len, heavy_rho;
+    int32_t max_depth;
+    uint64_t frame0;
+    float mean_tiny;
+    uint32_t npix;
+    const uint32_t* sp_pix;
+    uint32_t* sp_win;
+    uint32_t* sp_rho;                // slots per sample of the pixel's last completed chain, x 256 (0 = none)
+    uint32_t* run_st;
+    const uint32_t* split_tiles;
+    uint32_t* chunks;
+    uint32_t* chunk_count;
+    const float4_storage* res;
+    const uint8_t* nres;
+    uint32_t* left;
+    uint32_t* left_count;
+    uint32_t* sp_st;
+    float4_storage* sp_acc;
+    float4_storage* lin;
+    uint32_t* bgra;
+    uint32_t* rng;
+    unsigned long long* rays;
+};
+constexpr uint32_t kSplitMCapMul = 3;    // window cap M <= 3 spp (rounded up to 16)
+constexpr uint32_t kSplitRunLen = 8;     // R: slots per speculative run
+constexpr uint32_t kSplitHeavyRho = 320; // heavy pixel: >= 1.25 slots per sample last launch (x 256)
+
+// The window of a split pixel for a launch of spp samples: its last chain's slots per sample rho
+// (x 256) times spp, plus a margin of an eighth of the extra slots (at least 2), + 2; 1.5 spp without
+// history; within [spp, m_cap]. Round 1 and the stitch both use this value (through sp_win).
+__host__ __device__ inline uint32_t split_window(uint32_t rho256, uint32_t spp, uint32_t m_cap) {
+    if (rho256 == 0u) return spp + spp / 2u > m_cap ? m_cap : spp + spp / 2u;
+    const uint64_t m = ((uint64_t)spp * rho256 + 255u) / 256u;
+    const uint64_t extra = m > spp ? (m - spp) / 8u : 0u;
+    uint64_t w = m + (extra > 2u ? extra : 2u) + 2u;
+    if (w < spp) w = spp;
+    return (uint32_t)(w > m_cap ? m_cap : w);
+}
 
 // Binning launch (iqpt_bin_kernel): the camera and pixel set of the context, the world-space scene.
 struct kbin {
@@ -176,6 +243,7 @@ constexpr int kOptDiag = 1 << 13;      // A/B builds only: timing ablations sele
 constexpr int kOptExp = 1 << 15;       // A/B builds only: an alternative formulation under test (exact)
 constexpr int kOptCamAxis = 1 << 14;   // short camera transform for pitch-only cameras (kparams::cam_ax; the runtime
                                        // checks the zero pattern and the frame-wide normalization bounds)
+constexpr int kOptSplit = 1 << 16;     // sample-parallel chains: speculative runs + anchored lanes (kparams::split_round)
 constexpr int kOptDefault =
     kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull | kOptBvh;
 constexpr uint32_t kStatsHeader = 24;        // kOptStats: 24 counters, then per-wave (start, end, iterations)
@@ -208,6 +276,10 @@ int launch_render(void* stream, const kparams& p, uint32_t grid_blocks, uint32_t
                   int opt);
 // Max resident blocks per CU of the render kernel for the given dynamic LDS (occupancy query).
 int render_occupancy(int max_depth, bool stream_batches, int opt, uint32_t lds_bytes, int* blocks_per_cu);
+// kOptSplit: the windows, run states and run chunks before round 1, the stitch after it (fastdiv:
+// the running mean's short division, as the render variant that produced the slots).
+int launch_split_prep(void* stream, const ksplit& s);
+int launch_split_stitch(void* stream, const ksplit& s, bool fastdiv);
 bool render_variant_exists(int max_depth, bool stream_batches, int opt);
 constexpr int kRenderBlock = 256;
 constexpr uint32_t kQueueChunk = 64;

@@ -33,6 +33,10 @@ constexpr uint32_t kLdsResidentBytes = 32 * 1024;
 // slots and scatter stack a block stays under 32 KB, so 5 blocks fit a CU).
 constexpr uint32_t kTriBatch = 256;   // primitives per LDS batch (128 pairs = 10 KB)
 constexpr uint32_t kSphBatch = 256;
+constexpr int kTuneLaunches = 4;     // timed launches before the camera-ray path is chosen (A, B, A, B)
+// kOptSplit auto mode: split when the owned pixels are fewer than this many per resident lane
+constexpr double kSplitAutoPixelsPerLane = 1.2;
+constexpr size_t kSplitResBudget = size_t(8) << 30;   // speculative results (bytes)
 
 std::once_flag g_tables_once;
 std::vector<uint32_t> g_tables;  // A^(2^(67+i)), i < 32
@@ -127,11 +131,29 @@ struct iqpt_ctx {
     // tools/ab_kernel.py fixes the option set instead (opt_fixed)
     bool opt_fixed = false;
     uint32_t diag = 0;           // kOptDiag ablation bits (tools/ab_kernel.py)
-    int tune_stage = 0;          // 0: next launch times masks, 1: times the BVH, 2: decide, 3: decided
+    // stages 0..kTuneLaunches-1 time masks (even) and the BVH (odd) alternately; stage kTuneLaunches
+    // decides on the fastest launch of each; reset by a packet upload or a camera change
+    int tune_stage = 0;
     bool tune_primary = false;
-    hipEvent_t tune_ev[4] = {nullptr, nullptr, nullptr, nullptr};
+    hipEvent_t tune_ev[2 * 4] = {};
     int last_opt = -1;           // option set of the last render launch (iqpt_debug_last_options)
-    double tune_work[2] = {0.0, 0.0};
+    // kOptSplit, sample-parallel chains: mode (IQPT_SPLIT_*), the split set built with
+    // the masks (tiles whose camera rays may scatter), per-slot buffers sized for the launch
+    int split_mode = IQPT_SPLIT_AUTO;
+    bool split_last = false;     // the last launch ran split
+    uint32_t n_split_tiles = 0, n_anchor = 0;
+    uint32_t* d_split = nullptr;        // anchor_order[n_anchor], split_tiles[nst], sp_pix, sp_win, sp_rho,
+                                        // left (ns_cap each)
+    uint32_t* d_sp_st = nullptr;        // 6 x ns_cap
+    uint32_t* d_run_st = nullptr;       // (g_max + 1) x 6 x ns_cap
+    uint32_t* d_chunks = nullptr;       // 2 x g_max x split tiles: round-1 run chunks
+    float4_storage* d_sp_acc = nullptr; // ns_cap
+    float4_storage* d_res = nullptr;    // m_cap x ns_cap
+    uint8_t* d_nres = nullptr;          // ns_cap x m_cap
+    uint32_t split_refill_min = 16;     // idle lanes before a refill in split launches
+    uint32_t split_heavy_rho = iqpt::kSplitHeavyRho;   // 320 measured best at N = 8 (r02_split_share_v8)
+    size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
+    double tune_work[4] = {0.0, 0.0, 0.0, 0.0};
 };
 
 namespace {
@@ -160,6 +182,61 @@ void free_scene(iqpt_ctx* c) {
     c->cull_valid = false;
     c->tune_stage = 0;
     c->tune_primary = false;
+}
+
+void free_split(iqpt_ctx* c) {
+    for (uint32_t** b : {&c->d_split, &c->d_sp_st, &c->d_run_st, &c->d_chunks}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    for (float4_storage** b : {&c->d_sp_acc, &c->d_res}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    if (c->d_nres) (void)hipFree(c->d_nres);
+    c->d_nres = nullptr;
+    c->n_split_tiles = c->n_anchor = 0;
+    c->res_slots = 0;
+}
+
+// The split set of kOptSplit: the tiles whose camera rays may scatter — a sphere
+// candidate in the masks under the reference's materials (every triangle is emissive), any candidate
+// with a material table — in queue order, and the other tiles' queue order. Slot sp of the split set
+// is pixel sp % 64 of split tile sp / 64 (tile-major storage index, ~0u past a partial tile's end).
+int build_split(iqpt_ctx* c, const std::vector<uint32_t>& order, const std::vector<uint32_t>& cnt) {
+    free_split(c);
+    const uint32_t ntiles = (uint32_t)order.size();
+    std::vector<uint32_t> anchor, split;
+    for (uint32_t t : order) {
+        const bool scatters = c->d_mats ? (cnt[t] + cnt[ntiles + t]) > 0 : cnt[ntiles + t] > 0;
+        (scatters ? split : anchor).push_back(t);
+    }
+    if (split.empty()) return IQPT_OK;
+    const size_t ns = split.size() * (size_t)iqpt::kQueueChunk;
+    if (ns >= (1ull << 31)) return IQPT_OK;
+    std::vector<uint32_t> host(anchor.size() + split.size() + 5 * ns, 0u);
+    std::copy(anchor.begin(), anchor.end(), host.begin());
+    std::copy(split.begin(), split.end(), host.begin() + anchor.size());
+    uint32_t* sp_pix = host.data() + anchor.size() + split.size();
+    for (size_t st = 0; st < split.size(); ++st) {
+        const uint32_t t = split[st];
+        const uint32_t tx = t % c->cull_ntx, ty = t / c->cull_ntx;
+        const uint32_t th = std::min(iqpt::kCullTile, c->set.nrows - ty * iqpt::kCullTile);
+        const uint32_t tw = std::min(iqpt::kCullTile, c->ncols - tx * iqpt::kCullTile);
+        const uint32_t first = ty * iqpt::kCullTile * c->ncols + tx * iqpt::kCullTile * th;
+        for (uint32_t i = 0; i < iqpt::kQueueChunk; ++i)
+            sp_pix[st * iqpt::kQueueChunk + i] = i < tw * th ? first + i : ~0u;
+    }
+    if (hipMalloc(&c->d_split, host.size() * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_sp_st, 6 * ns * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_sp_acc, ns * sizeof(float4_storage)) != hipSuccess) {
+        free_split(c);
+        return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "split buffers");
+    }
+    IQPT_HIP(hipMemcpy(c->d_split, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->n_anchor = (uint32_t)anchor.size();
+    c->n_split_tiles = (uint32_t)split.size();
+    return IQPT_OK;
 }
 
 // (Re)build the kOptCull tile masks of the current camera and packet on the context's stream.
@@ -270,6 +347,9 @@ int build_cull(iqpt_ctx* c) {
     if (!c->d_tile_order && hipMalloc(&c->d_tile_order, (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
         return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "tile order");
     IQPT_HIP(hipMemcpy(c->d_tile_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    c->split_last = false;
+    int st = build_split(c, order, cnt);
+    if (st != IQPT_OK) return st;
     c->cull_valid = true;
     return IQPT_OK;
 }
@@ -454,10 +534,12 @@ struct sbvh_host {
     float gulp;
 };
 constexpr uint32_t kSbvhMinSpheres = 64;
+constexpr size_t kSbvhMaxSpheres = size_t(1) << 24;
 
 bool build_sbvh(const std::vector<float4_storage>& sph, sbvh_host& out) {
     const size_t n = sph.size();
-    if (n < kSbvhMinSpheres) return false;
+    // a leaf packs first << 8 | count (iq_bvh.hpp build_spheres): indices must stay below 2^24
+    if (n < kSbvhMinSpheres || n >= kSbvhMaxSpheres) return false;
     std::vector<float> s4(4 * n), radii(n);
     double maxabs = 0.0;
     for (size_t k = 0; k < n; ++k) {
@@ -609,7 +691,7 @@ int iqpt_create(int device, uint32_t width, uint32_t height, const iqpt_pixel_se
         hipMalloc(&c->d_bgra, n * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_rng, 6 * n * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_rays, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->d_queue, sizeof(uint32_t)) != hipSuccess)
+        hipMalloc(&c->d_queue, 4 * sizeof(uint32_t)) != hipSuccess)
         return cleanup(iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "device allocation of the frame state failed"));
     // path_tracer.cu:134-135: both buffers start at zero
     if (hipMemsetAsync(c->d_lin, 0, n * sizeof(float4_storage), c->stream) != hipSuccess ||
@@ -643,6 +725,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->d_rng) (void)hipFree(c->d_rng);
     if (c->d_rays) (void)hipFree(c->d_rays);
     if (c->d_queue) (void)hipFree(c->d_queue);
+    free_split(c);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
     if (c->d_tile_order) (void)hipFree(c->d_tile_order);
@@ -666,6 +749,7 @@ int iqpt_set_camera(iqpt_ctx* c, const iqpt_camera* cam) {
     c->cam = *cam;   // passed by value to every launch: no device copy to race with
     c->have_camera = true;
     c->cull_valid = false;
+    c->tune_stage = 0;              // the faster camera-ray path depends on the view: time it again
     return IQPT_OK;
 }
 
@@ -690,6 +774,8 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         total += m.num_indices / 3;
     }
     if (total > 0xffffffffull / 4) return iqpt::fail(IQPT_ERR_INVALID_ARG, "too many triangles");
+    // sphere indices, pair counts ((n + 1) / 2) and mask words are 32-bit in the kernels
+    if (nsdc > 0xffffffffu / 4) return iqpt::fail(IQPT_ERR_INVALID_ARG, "too many spheres");
     // material table (iqpt.h): indices in range, known types
     if (pk->materials) {
         if ((ntdc && !pk->tri_dc_material) || (nsdc && !pk->sphere_dc_material))
@@ -961,7 +1047,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     }
     // scene batch + running-mean table (padded to 16 B) + (kOptCull) one uint4 slot per thread +
     // the scatter-record stack (max_depth - 1 records per thread; one float each)
-    const uint32_t lds = p.tri_batch * tri_rec + p.sph_batch * sph_rec +
+    uint32_t lds = p.tri_batch * tri_rec + p.sph_batch * sph_rec +
                          (p.acc_tab ? ((spp + 1u) & ~1u) * 8u + ((spp + 3u) & ~3u) * 4u : 0u) +
                          ((opt & iqpt::kOptCull) ? iqpt::kRenderBlock * 16u : 0u) +
                          (uint32_t)std::max(c->max_depth, 1) * iqpt::kRenderBlock * 4u *
@@ -995,15 +1081,19 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     int tune_slot = -1;
     if (!c->opt_fixed && stream_batches && p.bvh_nodes && p.cull && (opt & iqpt::kOptBvh) &&
         iqpt::render_variant_exists(c->max_depth, true, prim_opt)) {
-        if (c->tune_stage == 2) {
-            float ms_a = 0.0f, ms_b = 0.0f;
-            if (hipEventSynchronize(c->tune_ev[3]) == hipSuccess &&
-                hipEventElapsedTime(&ms_a, c->tune_ev[0], c->tune_ev[1]) == hipSuccess &&
-                hipEventElapsedTime(&ms_b, c->tune_ev[2], c->tune_ev[3]) == hipSuccess)
-                c->tune_primary = (double)ms_b * c->tune_work[0] < (double)ms_a * c->tune_work[1];
-            c->tune_stage = 3;
+        if (c->tune_stage == iqpt::kTuneLaunches) {
+            // per variant the fastest of its timed launches, per sample-pixel of work
+            double best[2] = {1e300, 1e300};
+            bool ok = hipEventSynchronize(c->tune_ev[2 * iqpt::kTuneLaunches - 1]) == hipSuccess;
+            for (int s = 0; ok && s < iqpt::kTuneLaunches; ++s) {
+                float ms = 0.0f;
+                ok = hipEventElapsedTime(&ms, c->tune_ev[2 * s], c->tune_ev[2 * s + 1]) == hipSuccess;
+                if (ok) best[s & 1] = std::min(best[s & 1], (double)ms / std::max(1.0, c->tune_work[s]));
+            }
+            c->tune_primary = ok && best[1] < best[0];
+            c->tune_stage = iqpt::kTuneLaunches + 1;
         }
-        if (c->tune_stage < 2) {
+        if (c->tune_stage < iqpt::kTuneLaunches) {
             tune_slot = c->tune_stage;
             for (int k = 0; k < 2; ++k) {
                 hipEvent_t& ev = c->tune_ev[2 * tune_slot + k];
@@ -1015,17 +1105,130 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
                 (void)iqpt::render_occupancy(c->max_depth, true, prim_opt, lds, &o2);
             }
         }
-        if ((tune_slot == 1) || (tune_slot < 0 && c->tune_primary)) opt = prim_opt;
+        if ((tune_slot >= 0 && (tune_slot & 1)) || (tune_slot < 0 && c->tune_primary)) opt = prim_opt;
+    }
+    // kOptSplit: resident scenes with a split set, when the mode asks for it (auto:
+    // fewer owned pixels than kSplitAutoPixelsPerLane per resident lane, i.e. too few pixel chains to
+    // fill and drain the chip evenly)
+    uint32_t lds_split = lds + iqpt::kRenderBlock * (16u + 24u);   // + lds_sp and the base states
+    bool split = false;
+    if (c->split_mode != IQPT_SPLIT_OFF && !stream_batches && p.cull && c->n_split_tiles > 0 &&
+        tune_slot < 0 && iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptSplit)) {
+        int occ_s = 0;
+        if (iqpt::render_occupancy(c->max_depth, false, opt | iqpt::kOptSplit, lds_split, &occ_s) != 0) occ_s = 0;
+        const double lanes = (double)c->num_cus * std::max(occ_s, 1) * iqpt::kRenderBlock;
+        split = occ_s > 0 && (c->split_mode == IQPT_SPLIT_ON || (double)c->npix < iqpt::kSplitAutoPixelsPerLane * lanes);
+    }
+    const size_t ns_cap = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
+    const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
+    const uint32_t g_max = (m_cap + iqpt::kSplitRunLen - 1) / iqpt::kSplitRunLen;
+    if (split && (size_t)m_cap * ns_cap > c->res_slots) {
+        if (c->d_res || c->d_nres || c->d_run_st || c->d_chunks) {
+            IQPT_HIP(hipStreamSynchronize(c->stream));
+            for (void* b : {(void*)c->d_res, (void*)c->d_nres, (void*)c->d_run_st, (void*)c->d_chunks})
+                if (b) (void)hipFree(b);
+            c->d_res = nullptr;
+            c->d_nres = nullptr;
+            c->d_run_st = nullptr;
+            c->d_chunks = nullptr;
+            c->res_slots = 0;
+        }
+        const size_t slots = (size_t)m_cap * ns_cap;
+        const size_t st_words = (size_t)(g_max + 1) * 6 * ns_cap;
+        const size_t chunk_words = 2 * (size_t)g_max * c->n_split_tiles;
+        if (slots * (sizeof(float4_storage) + 1) + (st_words + chunk_words) * 4 <= iqpt::kSplitResBudget &&
+            hipMalloc(&c->d_res, slots * sizeof(float4_storage)) == hipSuccess &&
+            hipMalloc(&c->d_nres, slots) == hipSuccess &&
+            hipMalloc(&c->d_run_st, st_words * sizeof(uint32_t)) == hipSuccess &&
+            hipMalloc(&c->d_chunks, chunk_words * sizeof(uint32_t)) == hipSuccess) {
+            c->res_slots = slots;
+        } else {
+            (void)hipGetLastError();
+            split = false;     // over the budget: the plain kernel (same bits)
+        }
+    }
+    iqpt::ksplit ks;
+    std::memset(&ks, 0, sizeof ks);
+    if (split) {
+        opt |= iqpt::kOptSplit;
+        lds = lds_split;
+        uint32_t* base = c->d_split;
+        uint32_t* sp_pix = base + c->n_anchor + c->n_split_tiles;
+        p.anchor_order = base;
+        p.n_anchor = c->n_anchor;
+        p.n_split_tiles = c->n_split_tiles;
+        p.split_tiles = base + c->n_anchor;
+        p.chunks = c->d_chunks;
+        p.chunk_count = c->d_queue + 3;
+        p.split_len = iqpt::kSplitRunLen;
+        p.run_st = c->d_run_st;
+        p.refill_min = std::min<uint32_t>(64u, std::max<uint32_t>(1u, c->split_refill_min));
+        p.ns_cap = (uint32_t)ns_cap;
+        p.m_cap = m_cap;
+        p.sp_pix = sp_pix;
+        p.sp_win = sp_pix + ns_cap;
+        p.sp_rho = sp_pix + 2 * ns_cap;
+        p.left = sp_pix + 3 * ns_cap;
+        p.left_count = c->d_queue + 2;
+        p.res = c->d_res;
+        p.nres = c->d_nres;
+        p.sp_st = c->d_sp_st;
+        p.sp_acc = c->d_sp_acc;
+        ks.ns_cap = (uint32_t)ns_cap;
+        ks.spp = spp;
+        ks.m_cap = m_cap;
+        ks.g_max = g_max;
+        ks.run_len = iqpt::kSplitRunLen;
+        ks.heavy_rho = c->split_heavy_rho;
+        ks.run_st = c->d_run_st;
+        ks.split_tiles = base + c->n_anchor;
+        ks.chunks = c->d_chunks;
+        ks.chunk_count = c->d_queue + 3;
+        ks.max_depth = c->max_depth;
+        ks.frame0 = c->frame;
+        ks.mean_tiny = p.mean_tiny;
+        ks.npix = c->npix;
+        ks.sp_pix = sp_pix;
+        ks.sp_win = sp_pix + ns_cap;
+        ks.sp_rho = sp_pix + 2 * ns_cap;
+        ks.left = sp_pix + 3 * ns_cap;
+        ks.left_count = c->d_queue + 2;
+        ks.res = c->d_res;
+        ks.nres = c->d_nres;
+        ks.sp_st = c->d_sp_st;
+        ks.sp_acc = c->d_sp_acc;
+        ks.lin = c->d_lin;
+        ks.bgra = c->d_bgra;
+        ks.rng = c->d_rng;
+        ks.rays = c->d_rays;
+        if (!c->split_last) {
+            // no chain history from the previous launch (new split set or the plain kernel ran)
+            IQPT_HIP(hipMemsetAsync(sp_pix + 2 * ns_cap, 0, ns_cap * sizeof(uint32_t), c->stream));
+        }
     }
     int occ = 0;
     if (iqpt::render_occupancy(c->max_depth, stream_batches, opt, lds, &occ) != 0 || occ < 1) occ = 1;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
-    IQPT_HIP(hipMemsetAsync(c->d_queue, 0, sizeof(uint32_t), c->stream));
+    IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
     hipEvent_t e0 = take_event(c), e1 = take_event(c);
     if (e0) (void)hipEventRecord(e0, c->stream);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
-    int le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
+    int le = 0;
+    if (split) {
+        // prep -> round 1 (runs, anchored tiles, light split pixels) -> stitch -> round 2 (leftovers)
+        le = iqpt::launch_split_prep(c->stream, ks);
+        p.split_round = 1;
+        p.queue = c->d_queue;
+        if (le == 0) le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
+        if (le == 0) le = iqpt::launch_split_stitch(c->stream, ks, (opt & iqpt::kOptFastDiv) != 0);
+        p.split_round = 2;
+        p.queue = c->d_queue + 1;
+        if (le == 0) le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
+    } else {
+        le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
+    }
+    c->split_last = split;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1) (void)hipEventRecord(e1, c->stream);
     if (e0 && e1) c->timed.emplace_back(e0, e1);
@@ -1194,6 +1397,14 @@ int iqpt_checkpoint_load(iqpt_ctx* c, const char* path) {
         sum = fnv1a(bgra.data(), n * sizeof(uint32_t), sum);
         if (fnv1a(rng.data(), n * 6 * sizeof(uint32_t), sum) != h.checksum) why = "checksum mismatch";
     }
+    // the accumulator's w is 0 from iqpt_create on and the kernel stores it as 0 (a whole float4 per
+    // pixel): a checkpoint with another w did not come from a context
+    if (why.empty())
+        for (size_t i = 0; i < n; ++i)
+            if (lin[i].w != 0.0f || std::signbit(lin[i].w)) {
+                why = "accumulator w is not +0 (the kernel never produces another)";
+                break;
+            }
     if (!why.empty()) return iqpt::fail(IQPT_ERR_INVALID_ARG, std::string(path) + ": " + why);
     int st = use_device(c);
     if (st) return st;
@@ -1259,6 +1470,78 @@ int iqpt_debug_set_diag(iqpt_ctx* c, uint32_t bits) {
 
 /* Internal (tools/ab_kernel.py): select the kernel option mask of a context and read the
  * diagnostic counters of kOptStats variants. Not part of include/iqpt.h. */
+int iqpt_copy_frame_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
+    if (!c || !dst_device) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (bytes < (size_t)c->npix * sizeof(uint32_t)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
+    int st = use_device(c);
+    if (st) return st;
+    const int le = iqpt::launch_relayout(c->stream, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
+                                         c->set.nrows, 1, 1, true);
+    if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    return IQPT_OK;
+}
+
+int iqpt_prepare(iqpt_ctx* c) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    if (!c->have_camera || !c->have_packet) return iqpt::fail(IQPT_ERR_NOT_READY, "camera and packet must be set");
+    int st = use_device(c);
+    if (st) return st;
+    if ((c->opt & iqpt::kOptPair) && (c->opt & iqpt::kOptCull) && (c->ntri + c->nsph) > 0 && !c->cull_valid &&
+        (st = build_cull(c)) != IQPT_OK)
+        return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    return IQPT_OK;
+}
+
+// kOptSplit statistics of the last launch (tools/split_share.py): split tiles, anchored tiles, split
+// slots, leftovers of round 1, sum of the windows M, sum of the slots-per-sample estimates (x 256),
+// split pixels, whether the last launch ran split. Synchronises.
+int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
+    if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 8; ++i) out8[i] = 0;
+    out8[0] = c->n_split_tiles;
+    out8[1] = c->n_anchor;
+    const size_t ns = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
+    out8[2] = ns;
+    out8[7] = c->split_last ? 1 : 0;
+    if (!c->d_split || ns == 0) return IQPT_OK;
+    uint32_t left = 0;
+    IQPT_HIP(hipMemcpy(&left, c->d_queue + 2, sizeof left, hipMemcpyDeviceToHost));
+    out8[3] = left;
+    std::vector<uint32_t> v(3 * ns);
+    IQPT_HIP(hipMemcpy(v.data(), c->d_split + c->n_anchor + c->n_split_tiles, v.size() * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < ns; ++i) {
+        if (v[i] == ~0u) continue;
+        out8[4] += v[ns + i];
+        out8[5] += v[2 * ns + i];
+        out8[6] += 1;
+    }
+    return IQPT_OK;
+}
+
+// kOptSplit tuning knobs (tools/split_share.py): the heavy threshold (slots per sample x 256 of a
+// pixel's last launch; 0 keeps the default) and the idle lanes a wave waits for before it refills
+// (1..64). Results do not depend on either.
+int iqpt_debug_set_split_knobs(iqpt_ctx* c, uint32_t heavy_rho, uint32_t refill_min) {
+    if (!c || refill_min == 0 || refill_min > 64)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "refill_min 1..64");
+    if (heavy_rho) c->split_heavy_rho = heavy_rho;
+    c->split_refill_min = refill_min;
+    return IQPT_OK;
+}
+
+int iqpt_set_split(iqpt_ctx* c, int mode) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    if (mode != IQPT_SPLIT_AUTO && mode != IQPT_SPLIT_OFF && mode != IQPT_SPLIT_ON)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "split mode must be IQPT_SPLIT_AUTO, _OFF or _ON");
+    c->split_mode = mode;
+    return IQPT_OK;
+}
+
 int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     if (!iqpt::render_variant_exists(c->max_depth, false, opt) && !iqpt::render_variant_exists(c->max_depth, true, opt))

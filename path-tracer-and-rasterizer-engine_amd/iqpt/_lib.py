@@ -20,6 +20,7 @@ MESH_TRIANGLES = 0
 MESH_SPHERES = 1
 DEFAULT_SEED = 1984
 DEFAULT_MAX_DEPTH = 5
+SPLIT_AUTO, SPLIT_OFF, SPLIT_ON = -1, 0, 1     # IQPT_SPLIT_* (iqpt_set_split)
 
 
 class IqptError(RuntimeError):
@@ -93,6 +94,9 @@ SIGNATURES = [
     ("iqpt_read", C.c_int, [_P, _FP, C.POINTER(C.c_uint8)]),
     ("iqpt_read_rng", C.c_int, [_P, C.POINTER(C.c_uint32)]),
     ("iqpt_copy_accum_device", C.c_int, [_P, _P, C.c_size_t]),
+    ("iqpt_copy_frame_device", C.c_int, [_P, _P, C.c_size_t]),
+    ("iqpt_set_split", C.c_int, [_P, C.c_int]),
+    ("iqpt_prepare", C.c_int, [_P]),
     ("iqpt_num_pixels", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("iqpt_frame_count", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("iqpt_rays_traced", C.c_int, [_P, C.POINTER(C.c_uint64)]),
@@ -123,7 +127,7 @@ SIGNATURES = [
 _lib = None
 
 
-ABI_VERSION = 2      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
+ABI_VERSION = 3      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
 
 
 def load() -> C.CDLL:

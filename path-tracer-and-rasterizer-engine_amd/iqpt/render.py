@@ -93,6 +93,18 @@ class PathTracer:
     def copy_accum_device(self, dst_ptr: int, nbytes: int):
         check(self._lib.iqpt_copy_accum_device(self._h, C.c_void_p(dst_ptr), nbytes), "iqpt_copy_accum_device")
 
+    def copy_frame_device(self, dst_ptr: int, nbytes: int):
+        """BGRA8 frame (npix uint32, compact order) into a device buffer (iqpt_copy_frame_device)."""
+        check(self._lib.iqpt_copy_frame_device(self._h, C.c_void_p(dst_ptr), nbytes), "iqpt_copy_frame_device")
+
+    def set_split(self, mode: int):
+        """Sample-parallel chains: _lib.SPLIT_AUTO (default), SPLIT_OFF or SPLIT_ON (iqpt_set_split)."""
+        check(self._lib.iqpt_set_split(self._h, mode), "iqpt_set_split")
+
+    def prepare(self):
+        """Build the tile masks / queue order / split set now (iqpt_prepare; synchronises)."""
+        check(self._lib.iqpt_prepare(self._h), "iqpt_prepare")
+
     def frames(self) -> int:
         f = C.c_uint64()
         check(self._lib.iqpt_frame_count(self._h, C.byref(f)), "iqpt_frame_count")

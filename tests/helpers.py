@@ -23,10 +23,12 @@ def oracle_render(preset, width, height, spp, max_depth, pixels=None, seed=1984,
     return fr
 
 
-def gpu_render(preset, width, height, spp, max_depth, pixels=None, seed=1984, launches=None):
+def gpu_render(preset, width, height, spp, max_depth, pixels=None, seed=1984, launches=None, split=None):
     sc, pk = scene_for(preset)
     cam = make_camera(width, height)
     pt = PathTracer(width, height, pixels=pixels, seed=seed, max_depth=max_depth)
+    if split is not None:
+        pt.set_split(split)
     pt.set_camera(cam)
     pt.upload_packet(pk)
     for s in (launches or [spp]):

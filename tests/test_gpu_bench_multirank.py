@@ -1,0 +1,40 @@
+"""The product's multi-rank path end to end (C3 of BASELINE.json): bench.py --gpus 2 starts its two rank
+processes itself, each renders its cyclic row share through libiqpt, every step gathers the frame to
+rank 0, and the float accumulators gathered after timing must equal a 1-rank render bit for bit
+(RNG streams are keyed by the global pixel id, path_tracer.cu:36-46/336-339). One GPU: both ranks on
+device 0 with gloo collectives (RCCL refuses two ranks on one device); the driver's runs use RCCL.
+"""
+import json
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+
+pytestmark = pytest.mark.gpu
+
+
+def _bench(tmp_path, gpus, name, extra=()):
+    out = tmp_path / f"{name}.npy"
+    cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", str(gpus), "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline", "--verify-rows", "2", "--save-frame", str(out), *extra]
+    if gpus > 1:
+        cmd += ["--backend", "gloo", "--one-device"]
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    line = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1]
+    return json.loads(line), np.load(out)
+
+
+@pytest.mark.parametrize("gather", ["frame", "accum"])
+def test_two_rank_strong_frame_equals_one_rank(require_gpu, tmp_path, gather):
+    one, f1 = _bench(tmp_path, 1, "one")
+    two, f2 = _bench(tmp_path, 2, "two", ("--gather", gather))
+    assert two["n_gpus"] == 2 and two["n_ranks_seen"] == 2 and two["scaling"] == "strong"
+    assert two["bitexact_frac_vs_oracle"] == 1.0 and one["bitexact_frac_vs_oracle"] == 1.0
+    assert f1.shape == f2.shape == (1920 * 1080, 4)
+    assert np.array_equal(f1.view(np.uint32), f2.view(np.uint32))
+    # same work: the rays of two half frames add up to the rays of the whole frame
+    assert two["rays_per_sample"] == one["rays_per_sample"]

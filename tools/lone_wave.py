@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""Latency of one wave: a single 8x8 tile of the C2 frame (one wave in the whole grid) rendered with the
+plain kernel, kOptStats build (A/B library): kernel time, iterations, us per iteration. Tiles on a wall
+(1 ray per sample) and on a sphere (Oren-Nayar bounces). Also a 64x64 crop (64 waves)."""
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "path-tracer-and-rasterizer-engine_amd"))
+import numpy as np  # noqa: E402
+import iqpt  # noqa: E402
+from iqpt import _build, _lib  # noqa: E402
+from iqpt.scene import Scene, make_camera  # noqa: E402
+
+_lib.LIB_PATH = _build.build_lib(ab=True)
+lb = _lib.load()
+sc = Scene()
+sc.add_preset("cornell")
+pk = sc.build_packet()
+W, H = 1920, 1080
+cam = make_camera(W, H)
+out = {}
+CASES = {"wall_tile": (200, 200, 8), "sphere_tile": (800, 560, 8), "sphere_64": (760, 520, 64),
+         "wall_64": (160, 160, 64)}
+only = [a for a in sys.argv[2:]]
+for name, (x0, y0, n) in CASES.items():
+    if only and name not in only:
+        continue
+    for stats in ((False,) if only else (False, True)):
+        ps = iqpt.pixel_set(W, H, x0, x0 + n, y0, 1, n)
+        pt = iqpt.PathTracer(W, H, pixels=ps, max_depth=8)
+        lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
+        if stats:
+            _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, 2863 | 128), "opts")
+        pt.set_split(_lib.SPLIT_OFF)
+        pt.set_camera(cam)
+        pt.upload_packet(pk)
+        pt.render(64)
+        pt.sync()
+        pt.kernel_time()
+        r0 = pt.rays()
+        ms = []
+        for _ in range(5):
+            pt.render(64)
+            t, k = pt.kernel_time()
+            ms.append(t / k)
+        rays = (pt.rays() - r0) / 5
+        row = {"kernel_ms_median": float(np.median(ms)), "rays_per_launch": rays, "pixels": n * n}
+        if stats:
+            s = (C.c_ulonglong * 24)()
+            lb.iqpt_debug_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+            lb.iqpt_debug_read_stats(pt._h, s)
+            pt.render(64)
+            cap = 4096
+            wt = (C.c_ulonglong * (3 * cap))()
+            nw = C.c_uint32(0)
+            lb.iqpt_debug_read_wave_times.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32,
+                                                      C.POINTER(C.c_uint32)]
+            lb.iqpt_debug_read_wave_times(pt._h, wt, cap, C.byref(nw))
+            a = np.array(wt[:3 * nw.value], dtype=np.float64).reshape(-1, 3)
+            a = a[a[:, 2] > 0]
+            dur = (a[:, 1] - a[:, 0]) / 100.0
+            row["busy_waves"] = int(len(a))
+            row["iters"] = a[:, 2].tolist()[:8]
+            row["us_per_iter"] = (dur / a[:, 2]).round(3).tolist()[:8]
+        out[f"{name}{'_stats' if stats else ''}"] = row
+        pt.close()
+        print(name, stats, json.dumps(row), flush=True)
+if len(sys.argv) > 1 and sys.argv[1] != "-":
+    Path(sys.argv[1]).write_text(json.dumps(out, indent=1))

@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_split.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r02_run16_split.log 2>&1 && \
+timeout -k 10 400 python -u tools/split_share.py --ns 8,4,2,1 --knobs 65535:16,320:16,320:1,257:16 --out gpurun_out/r02_split_share_v8.json > gpurun_out/r02_run16_share.log 2>&1
