@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=60.0,
                     help="wall time of the CPU-baseline sample (BASELINE.md §3: >= 60 s)")
     ap.add_argument("--verify-rows", type=int, default=16)
-    ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r01_pmc_traffic_v2.json"))
+    ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r02" / "pmc_traffic_c2.json"))
     ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r01_c2_pmc_mix_v4.json"),
                     help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy)")
     ap.add_argument("--work-json", default="",

@@ -22,14 +22,17 @@ from iqpt._lib import Camera, PacketDesc, PixelSet  # noqa: E402  (ctypes layout
 
 LIB = _HERE / "liboracle.so"
 LIB_GLIBC = _HERE / "liboracle_glibc.so"
+LIB_FMA = _HERE / "liboracle_fma.so"     # informational flavour: FMA contraction on, glibc libm
 
 _cache: dict[str, C.CDLL] = {}
 _FP = C.POINTER(C.c_float)
 _UP = C.POINTER(C.c_uint32)
 
 
-def load(glibc: bool = False) -> C.CDLL:
-    path = LIB_GLIBC if glibc else LIB
+def load(glibc: bool = False, flavour: str | None = None) -> C.CDLL:
+    """flavour: None / "b" (the parity target), "glibc", "fma" (see DESIGN.md §4)."""
+    flavour = flavour or ("glibc" if glibc else "b")
+    path = {"b": LIB, "glibc": LIB_GLIBC, "fma": LIB_FMA}[flavour]
     key = str(path)
     if key in _cache:
         return _cache[key]
@@ -81,8 +84,8 @@ class OracleFrame:
     """Per-pixel state of one pixel set, advanced on the CPU exactly like the reference kernel."""
 
     def __init__(self, width: int, height: int, pixels: PixelSet | None = None, seed: int = 1984,
-                 max_depth: int = 5, glibc: bool = False):
-        self.lib = load(glibc)
+                 max_depth: int = 5, glibc: bool = False, flavour: str | None = None):
+        self.lib = load(glibc, flavour)
         self.width, self.height = width, height
         self.pixels = pixels if pixels is not None else pixel_set(width, height)
         self.npix = (self.pixels.x1 - self.pixels.x0) * self.pixels.nrows

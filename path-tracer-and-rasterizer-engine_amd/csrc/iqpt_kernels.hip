@@ -73,6 +73,18 @@ __device__ __forceinline__ float rand_real(rng6& s, float lo, float hi) {
     return u * (hi - lo) + lo;
 }
 
+// kOptStats: per-thread counts of the primitive tests executed (Möller–Trumbore triangle tests, sphere
+// tests; a packed pair counts two) for the executed-work roofline (tools/work_counters.py), in LDS.
+template <int OPT>
+__device__ __forceinline__ uint32_t* stat_tests() {
+    __shared__ uint32_t cnt[2 * 256];
+    return cnt;
+}
+template <int OPT>
+__device__ __forceinline__ void stat_add(int which, uint32_t n) {
+    if (OPT & kOptStats) stat_tests<OPT>()[which * 256 + threadIdx.x] += n;
+}
+
 // IEEE 1/x under kOptFastDiv (iq_fastdiv.h), the generic expansion otherwise.
 // rcp_scene: x is a Möller–Trumbore determinant with |det| >= 1e-6 or a sphere radius; the runtime
 // launches kOptFastDiv variants only when every edge component and radius of the packet is within
@@ -246,6 +258,7 @@ __device__ __forceinline__ uint32_t to_u8(float f) {
 template <int OPT>
 __device__ __forceinline__ void test_triangle(const float4 a, const float4 b, const float4 c, const ray3 r,
                                               float& closest, int& kind, uint32_t& idx, uint32_t k) {
+    stat_add<OPT>(0, 1u);
     const float e1x = a.w, e1y = b.x, e1z = b.y;
     const float e2x = b.z, e2y = b.w, e2z = c.x;
     const float px = r.dy * e2z - r.dz * e2y;                   // dir x v0v2
@@ -279,6 +292,7 @@ __device__ __forceinline__ void test_triangle_pair_nb(const float4 q0, const flo
                                                       const float4 q3, const float4 q4, const ray3 r,
                                                       float& closest, int& kind, uint32_t& idx, uint32_t k,
                                                       bool second) {
+    stat_add<OPT>(0, 2u);
     const f2 v0x = {q0.x, q0.y}, v0y = {q0.z, q0.w}, v0z = {q1.x, q1.y};
     const f2 e1x = {q1.z, q1.w}, e1y = {q2.x, q2.y}, e1z = {q2.z, q2.w};
     const f2 e2x = {q3.x, q3.y}, e2y = {q3.z, q3.w}, e2z = {q4.x, q4.y};
@@ -315,6 +329,7 @@ template <int OPT>
 __device__ __forceinline__ void test_triangle_pair(const float4 q0, const float4 q1, const float4 q2,
                                                    const float4 q3, const float4 q4, const ray3 r, float& closest,
                                                    int& kind, uint32_t& idx, uint32_t k, bool second) {
+    stat_add<OPT>(0, 2u);
     const f2 v0x = {q0.x, q0.y}, v0y = {q0.z, q0.w}, v0z = {q1.x, q1.y};
     const f2 e1x = {q1.z, q1.w}, e1y = {q2.x, q2.y}, e1z = {q2.z, q2.w};
     const f2 e2x = {q3.x, q3.y}, e2y = {q3.z, q3.w}, e2z = {q4.x, q4.y};
@@ -371,6 +386,7 @@ __device__ __forceinline__ void sphere_roots(float halfb, float delta, float& cl
 template <int OPT>
 __device__ __forceinline__ void test_sphere(const float4 s, const ray3 r, float& closest, int& kind,
                                             uint32_t& idx, uint32_t k) {
+    stat_add<OPT>(1, 1u);
     const float ocx = s.x - r.ox, ocy = s.y - r.oy, ocz = s.z - r.oz;
     const float halfb = (r.dx * ocx + r.dy * ocy) + r.dz * ocz;
     const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.w * s.w;
@@ -383,6 +399,7 @@ __device__ __forceinline__ void test_sphere(const float4 s, const ray3 r, float&
 template <int OPT>
 __device__ __forceinline__ void test_sphere_pair(const float4 s0, const float4 s1, const ray3 r, float& closest,
                                                  int& kind, uint32_t& idx, uint32_t k, bool second) {
+    stat_add<OPT>(1, 2u);
     const f2 cx = {s0.x, s0.y}, cy = {s0.z, s0.w}, cz = {s1.x, s1.y}, rad = {s1.z, s1.w};
     const f2 ocx = cx - r.ox, ocy = cy - r.oy, ocz = cz - r.oz;
     const f2 halfb = (r.dx * ocx + r.dy * ocy) + r.dz * ocz;
@@ -690,6 +707,7 @@ template <int OPT>
 __device__ __forceinline__ void test_triangle_pair_ix(const float4 q0, const float4 q1, const float4 q2,
                                                       const float4 q3, const float4 q4, const ray3 r, float& closest,
                                                       int& kind, uint32_t& idx, uint32_t ka, uint32_t kb) {
+    stat_add<OPT>(0, 2u);
     const f2 v0x = {q0.x, q0.y}, v0y = {q0.z, q0.w}, v0z = {q1.x, q1.y};
     const f2 e1x = {q1.z, q1.w}, e1y = {q2.x, q2.y}, e1z = {q2.z, q2.w};
     const f2 e2x = {q3.x, q3.y}, e2y = {q3.z, q3.w}, e2z = {q4.x, q4.y};
@@ -861,6 +879,7 @@ struct sph_fold {
 template <int OPT>
 __device__ __forceinline__ void sph_visit(const float4 s, uint32_t k, const ray3 r, uint32_t min_idx, sph_fold& f,
                                           float& bound) {
+    stat_add<OPT>(1, 1u);
     const float ocx = s.x - r.ox, ocy = s.y - r.oy, ocz = s.z - r.oz;
     const float halfb = (r.dx * ocx + r.dy * ocy) + r.dz * ocz;
     const float cc = ((ocx * ocx + ocy * ocy) + ocz * ocz) - s.w * s.w;
@@ -1095,6 +1114,10 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     __syncthreads();
 
     const uint32_t lane = __lane_id();
+    if (OPT & kOptStats) {
+        stat_tests<OPT>()[threadIdx.x] = 0u;
+        stat_tests<OPT>()[256 + threadIdx.x] = 0u;
+    }
     // ---- per-lane state
     // (the compact pixel index, the tile and the mask words live in LDS / are recomputed at the
     // pixel's end, and the accumulator's untouched w is never loaded: registers are the limit at
@@ -1852,16 +1875,17 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             atomicAdd(p.stats + 13, s_refill_lanes);
         }
         {
-            // BVH work, summed over the wave's lanes
-            unsigned long long v[6] = {c_tri_rays, c_tri[0], c_tri[1], c_sph_rays, c_sph[0], c_sph[1]};
+            // BVH work and the primitive tests executed, summed over the wave's lanes
+            unsigned long long v[8] = {c_tri_rays, c_tri[0], c_tri[1], c_sph_rays, c_sph[0], c_sph[1],
+                                       stat_tests<OPT>()[threadIdx.x], stat_tests<OPT>()[256 + threadIdx.x]};
 #pragma unroll
-            for (int k = 0; k < 6; ++k) {
+            for (int k = 0; k < 8; ++k) {
 #pragma unroll
                 for (int off = 32; off > 0; off >>= 1) v[k] += __shfl_xor(v[k], off);
             }
             if (lane == 0 && p.stats) {
 #pragma unroll
-                for (int k = 0; k < 6; ++k) atomicAdd(p.stats + 14 + k, v[k]);
+                for (int k = 0; k < 8; ++k) atomicAdd(p.stats + 14 + k, v[k]);
             }
             // wave timeline (s_memrealtime, 100 MHz): start, end, iterations per wave
             // one record per wave (lane 0; the atomic optimiser would otherwise hand every lane a slot)

@@ -29,6 +29,7 @@ LIB_PATH = PKG_DIR / "libiqpt.so"
 AB_LIB_PATH = PKG_DIR / "libiqpt_ab.so"        # + A/B kernel variants (tools/ab_kernel.py)
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 ORACLE_GLIBC_LIB = ORACLE_DIR / "liboracle_glibc.so"
+ORACLE_FMA_LIB = ORACLE_DIR / "liboracle_fma.so"      # informational: contraction on + glibc libm (nvcc-like)
 CLI_PATH = PKG_DIR / "iqpt_cli"
 FACADE_TEST_PATH = PKG_DIR / "test_facade"
 
@@ -109,10 +110,17 @@ def build_oracle(force: bool = False) -> list[Path]:
     base = [CC, "-O3", "-std=gnu11", "-fPIC", "-shared", "-fopenmp", *FP_FLAGS, "-fno-builtin-sinf",
             f"-I{INCLUDE}", f"-I{CSRC}", str(src)]
     built = []
-    for target, extra in ((ORACLE_LIB, []), (ORACLE_GLIBC_LIB, ["-DIQO_GLIBC_LIBM"])):
+    # flavours: B = the parity target (iq_fp.h, contraction off); A = glibc libm;
+    # FMA = contraction on (-ffp-contract=fast -mfma) with glibc libm, the closest this image gets to
+    # nvcc's default (contraction on, libdevice): an estimate of how far the reference binary may sit
+    for target, extra in ((ORACLE_LIB, []), (ORACLE_GLIBC_LIB, ["-DIQO_GLIBC_LIBM"]),
+                          (ORACLE_FMA_LIB, ["-DIQO_GLIBC_LIBM", "-ffp-contract=fast", "-mfma"])):
         if force or not _newer(target, deps):
             tmp = target.with_suffix(".so.tmp")
-            _run([*base, *extra, "-o", str(tmp), "-lm"])
+            cmd = [*base, *extra, "-o", str(tmp), "-lm"]
+            if "-ffp-contract=fast" in extra:
+                cmd.remove("-ffp-contract=off")
+            _run(cmd)
             os.replace(tmp, target)
         built.append(target)
     return built

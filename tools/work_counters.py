@@ -1,0 +1,102 @@
+#!/usr/bin/env python3
+"""Executed work per ray of the render kernel (the roofline numerator for the BVH / culled configs).
+
+For a config (c2, c4, c5) this runs the production path of the A/B library until its camera-ray path
+choice is made (iqpt_runtime.cpp tune stages), reads the option set it settled on, then renders with the
+kOptStats build of that option set and reads the per-lane counters (iqpt_kernels.hip stat_add and the
+BVH counters): Möller–Trumbore triangle tests, sphere tests, triangle-BVH node tests and sphere-BVH node
+tests, per closest-hit query. Executed FLOPs per ray = 52 MT + 19 sphere (shape.cu:65-92,
+16-25) + 67 per node test (iq bvh_node_test / sbvh_pass: the grown-box slab test, add/sub/mul/div/sqrt
+counted as in §8d). The stats build is slower; only its counts are used. Output JSON feeds
+bench.py --work-json.
+
+    python tools/work_counters.py --config c5 [--spp 1] [--launches 2] --out profiles/r02/work_c5.json
+"""
+import argparse
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "path-tracer-and-rasterizer-engine_amd"))
+
+import iqpt  # noqa: E402
+from iqpt import _build, _lib  # noqa: E402
+from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
+
+K_STATS = 1 << 7
+K_LB5 = 1 << 3
+K_SPLIT = 1 << 16
+FLOP_MT, FLOP_SPHERE, FLOP_NODE = 52, 19, 67
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="c5")
+    ap.add_argument("--spp", type=int, default=0)
+    ap.add_argument("--launches", type=int, default=2)
+    ap.add_argument("--out", default="")
+    args = ap.parse_args()
+    _lib.LIB_PATH = _build.build_lib(ab=True)
+    lb = _lib.load()
+    lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
+    lb.iqpt_debug_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    cfg = CONFIGS[args.config]
+    spp = args.spp or {"c4": 16, "c5": 1}.get(cfg.name, cfg.spp)
+    sc = Scene()
+    sc.add_preset(cfg.preset)
+    pk = sc.build_packet()
+    cam = make_camera(cfg.width, cfg.height)
+    # 1) the production choice
+    pt = iqpt.PathTracer(cfg.width, cfg.height, max_depth=cfg.max_depth)
+    pt.set_split(_lib.SPLIT_OFF)
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    for _ in range(6):
+        pt.render(spp)
+    o = C.c_int()
+    _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(o)), "last options")
+    prod_opt = o.value
+    pt.close()
+    # 2) the stats build of that option set (the 5-wave bound is not part of the algorithm)
+    stats_opt = prod_opt | K_STATS
+    pt = iqpt.PathTracer(cfg.width, cfg.height, max_depth=cfg.max_depth)
+    pt.set_split(_lib.SPLIT_OFF)
+    if lb.iqpt_debug_set_kernel_options(pt._h, stats_opt) != 0:
+        stats_opt &= ~K_LB5
+        _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, stats_opt), "set options (stats)")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    pt.render(spp)                                   # warm (masks / lists built)
+    s = (C.c_ulonglong * 24)()
+    lb.iqpt_debug_read_stats(pt._h, s)               # clears
+    r0 = pt.rays()
+    for _ in range(args.launches):
+        pt.render(spp)
+    pt.sync()
+    rays = pt.rays() - r0
+    lb.iqpt_debug_read_stats(pt._h, s)
+    v = list(s)
+    pt.close()
+    tri_nodes, sph_nodes = v[15], v[18]
+    mt, sph = v[20], v[21]
+    per = {"mt_tests": mt / rays, "sphere_tests": sph / rays, "tri_bvh_node_tests": tri_nodes / rays,
+           "sph_bvh_node_tests": sph_nodes / rays}
+    fpr = FLOP_MT * per["mt_tests"] + FLOP_SPHERE * per["sphere_tests"] + \
+        FLOP_NODE * (per["tri_bvh_node_tests"] + per["sph_bvh_node_tests"])
+    out = {"config": cfg.name, "preset": cfg.preset, "spp_per_launch": spp, "launches": args.launches,
+           "rays": rays, "production_options": prod_opt, "stats_options": stats_opt,
+           "per_ray": {k: round(x, 4) for k, x in per.items()}, "flops_per_ray": round(fpr, 2),
+           "flop_weights": {"mt": FLOP_MT, "sphere": FLOP_SPHERE, "node": FLOP_NODE},
+           "reference_flops_per_ray": cfg.flops_per_ray,
+           "note": "executed tests per closest-hit query (kOptStats counters, all lanes that ran a test); "
+                   "the reference's brute-force price is reference_flops_per_ray (52 T + 19 S)"}
+    print(json.dumps(out, indent=1))
+    if args.out:
+        Path(args.out).write_text(json.dumps(out, indent=1) + "\n")
+
+
+if __name__ == "__main__":
+    main()
