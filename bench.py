@@ -56,11 +56,13 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=60.0,
                     help="wall time of the CPU-baseline sample (BASELINE.md §3: >= 60 s)")
     ap.add_argument("--verify-rows", type=int, default=16)
-    ap.add_argument("--pmc-json", default=str(REPO / "profiles" / "r02" / "pmc_traffic_c2.json"))
+    ap.add_argument("--pmc-json", default="",
+                    help="PMC traffic of the config (tools/pmc_traffic.py; default profiles/r02/pmc_traffic_<config>.json)")
     ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r01_c2_pmc_mix_v4.json"),
                     help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy)")
     ap.add_argument("--work-json", default="",
-                    help="executed-work counters of the config (tools/work_counters.py): prices C4/C5")
+                    help="executed-work counters of the config (tools/work_counters.py; default "
+                         "profiles/r02/work_<config>.json): prices C4/C5, reported beside C2's algorithmic price")
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="collective backend for N > 1 (nccl = RCCL over xGMI; gloo = rehearsal)")
     ap.add_argument("--one-device", action="store_true",
@@ -192,24 +194,33 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name) -> dic
     t = kern_avg_ms * 1e-3
     ref_tflops = f_ray * rays_per_launch / t / 1e12 if t > 0 else 0.0
     traffic = None
-    pmc = load_json(args.pmc_json, cfg.name)
+    pmc = None
+    for cand in ([args.pmc_json] if args.pmc_json else
+                 [str(REPO / "profiles" / "r02" / f"pmc_traffic_{cfg.name}.json"),
+                  str(REPO / "profiles" / f"r01_pmc_traffic_{cfg.name}_v4.json")]):
+        pmc = pmc or load_json(cand, cfg.name)
     if pmc and world == 1:
         traffic = pmc.get("hbm_bytes_per_launch")
     mix = load_json(args.pmc_mix_json, cfg.name)
-    work = load_json(args.work_json, cfg.name)
+    work_path = args.work_json or str(REPO / "profiles" / "r02" / f"work_{cfg.name}.json")
+    work = load_json(work_path, cfg.name)
     out = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "kernel": kernel_name,
            "kernel_avg_ms": round(kern_avg_ms, 4), "traffic": traffic,
            "valu_busy_frac": (mix or {}).get("valu_busy_frac") if world == 1 else None,
            "wave_time_split": (mix or {}).get("wave_time_split") if world == 1 else None}
-    if work and work.get("flops_per_ray"):
-        ex = work["flops_per_ray"] * rays_per_launch / t / 1e12 if t > 0 else 0.0
+    ex = work["flops_per_ray"] * rays_per_launch / t / 1e12 if (work and work.get("flops_per_ray") and t > 0) else None
+    if ex is not None and ref_tflops > FP32_PEAK_TFLOPS:
         out.update(achieved=round(ex, 4), frac=round(ex / FP32_PEAK_TFLOPS, 5),
-                   flops_per_ray=work["flops_per_ray"], work_basis="executed tests per ray (" + args.work_json + ")",
+                   flops_per_ray=work["flops_per_ray"], work_basis="executed tests per ray (" + Path(work_path).name + ")",
                    reference_equivalent={"achieved": round(ref_tflops, 2), "flops_per_ray": f_ray,
                                          "frac": round(ref_tflops / FP32_PEAK_TFLOPS, 4)})
     elif ref_tflops <= FP32_PEAK_TFLOPS:
         out.update(achieved=round(ref_tflops, 4), frac=round(ref_tflops / FP32_PEAK_TFLOPS, 5),
                    flops_per_ray=f_ray, work_basis="algorithmic F_ray = 52 T + 19 S (SURVEY.md §8d)")
+        if ex is not None:
+            # the tests the kernel actually executes (the tile masks skip most of the brute-force ones)
+            out["executed_work"] = {"achieved": round(ex, 4), "frac": round(ex / FP32_PEAK_TFLOPS, 5),
+                                    "flops_per_ray": work["flops_per_ray"], "per_ray": work.get("per_ray")}
     else:
         # the brute-force price exceeds the peak: the kernel skips that work, so it is no roofline
         out.update(achieved=None, frac=None, flops_per_ray=None,

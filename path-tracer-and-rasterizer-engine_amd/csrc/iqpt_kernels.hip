@@ -1068,7 +1068,9 @@ constexpr int min_waves_per_simd() {
     // kOptSplit variants are built for 4 waves/SIMD (<= 128 VGPRs): with 5 their refill and path-end
     // bookkeeping spilled 9 VGPRs to scratch, and at the low occupancy of a multi-GPU row share a scratch
     // reload's latency is not hidden
-    return (OPT & kOptSplit) ? 4 : ((OPT & kOptLB6) ? 6 : ((OPT & kOptLB5) ? 5 : (STREAM ? 4 : 1)));
+    // (A/B builds: kOptExp with kOptSplit keeps the 5-wave bound, spills and all)
+    return (OPT & kOptSplit) ? (((OPT & kOptExp) && (OPT & kOptLB5)) ? 5 : 4)
+                             : ((OPT & kOptLB6) ? 6 : ((OPT & kOptLB5) ? 5 : (STREAM ? 4 : 1)));
 }
 
 template <int MAXD, bool STREAM, int OPT>
@@ -2329,6 +2331,7 @@ const variant kVariants[] = {
     IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptExp),
     IQPT_V(8, true, (kOptDefault | kOptMaterials) & ~kOptBvh),
     IQPT_V(8, false, kOptDefault | kOptSplit | kOptStats),
+    IQPT_V(8, false, kOptDefault | kOptExp), IQPT_V(8, false, kOptDefault | kOptExp | kOptSplit),
 #endif
 };
 #undef IQPT_V

@@ -151,7 +151,8 @@ struct iqpt_ctx {
     float4_storage* d_res = nullptr;    // m_cap x ns_cap
     uint8_t* d_nres = nullptr;          // ns_cap x m_cap
     uint32_t split_refill_min = 16;     // idle lanes before a refill in split launches
-    uint32_t split_heavy_rho = iqpt::kSplitHeavyRho;   // 320 measured best at N = 8 (r02_split_share_v8)
+    uint32_t split_heavy_rho = iqpt::kSplitHeavyRho;
+    bool split_all_tiles = false;       // every tile in the split set (wall tiles: one slot per sample)   // 320 measured best at N = 8 (r02_split_share_v8)
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
     double tune_work[4] = {0.0, 0.0, 0.0, 0.0};
 };
@@ -208,7 +209,8 @@ int build_split(iqpt_ctx* c, const std::vector<uint32_t>& order, const std::vect
     const uint32_t ntiles = (uint32_t)order.size();
     std::vector<uint32_t> anchor, split;
     for (uint32_t t : order) {
-        const bool scatters = c->d_mats ? (cnt[t] + cnt[ntiles + t]) > 0 : cnt[ntiles + t] > 0;
+        const bool scatters = c->split_all_tiles ||
+                              (c->d_mats ? (cnt[t] + cnt[ntiles + t]) > 0 : cnt[ntiles + t] > 0);
         (scatters ? split : anchor).push_back(t);
     }
     if (split.empty()) return IQPT_OK;
@@ -1527,8 +1529,15 @@ int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
 // pixel's last launch; 0 keeps the default) and the idle lanes a wave waits for before it refills
 // (1..64). Results do not depend on either.
 int iqpt_debug_set_split_knobs(iqpt_ctx* c, uint32_t heavy_rho, uint32_t refill_min) {
-    if (!c || refill_min == 0 || refill_min > 64)
+    if (!c || (refill_min & 0xffffu) == 0 || (refill_min & 0xffffu) > 64)
         return iqpt::fail(IQPT_ERR_INVALID_ARG, "refill_min 1..64");
+    // bit 16 of refill_min: every tile joins the split set (rebuilt with the masks)
+    const bool all = (refill_min >> 16) & 1u;
+    if (all != c->split_all_tiles) {
+        c->split_all_tiles = all;
+        c->cull_valid = false;
+    }
+    refill_min &= 0xffffu;
     if (heavy_rho) c->split_heavy_rho = heavy_rho;
     c->split_refill_min = refill_min;
     return IQPT_OK;

@@ -24,6 +24,9 @@ from iqpt import dist as iqdist  # noqa: E402
 from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
 
 
+OPT = 0
+
+
 def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None) -> dict:
     cfg = CONFIGS["c2"]
     sc = Scene()
@@ -33,6 +36,11 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None) -> di
     ps = iqdist.pixel_set_for_rank(cfg.width, cfg.height, 0, n)
     pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
     pt.set_split(mode)
+    if OPT:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, OPT), "iqpt_debug_set_kernel_options")
     if knobs:
         import ctypes as C
         lb = _lib.load()
@@ -136,8 +144,14 @@ def main():
     ap.add_argument("--modes", default="plain,split")
     ap.add_argument("--knobs", default="", help="split knob sets heavy_rho:refill_min[,...] (extra split rows)")
     ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (A/B library)")
+    ap.add_argument("--opt", type=int, default=0, help="kernel option set (A/B library; 0 = production)")
     args = ap.parse_args()
     out = {"config": "c2 rank-0 row share, 64 spp per launch", "launches": args.launches, "rows": []}
+    if args.opt:
+        global OPT
+        from iqpt import _build
+        _lib.LIB_PATH = _build.build_lib(ab=True)
+        OPT = args.opt
     if args.stats:
         from iqpt import _build
         _lib.LIB_PATH = _build.build_lib(ab=True)
