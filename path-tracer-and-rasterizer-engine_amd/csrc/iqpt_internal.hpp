@@ -244,8 +244,10 @@ constexpr int kOptExp = 1 << 15;       // A/B builds only: an alternative formul
 constexpr int kOptCamAxis = 1 << 14;   // short camera transform for pitch-only cameras (kparams::cam_ax; the runtime
                                        // checks the zero pattern and the frame-wide normalization bounds)
 constexpr int kOptSplit = 1 << 16;     // sample-parallel chains: speculative runs + anchored lanes (kparams::split_round)
-constexpr int kOptDefault =
-    kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull | kOptBvh;
+constexpr int kOptScatter2 = 1 << 18;  // Oren–Nayar scatter with packed, branch-free transcendental pairs (iq_fp2.h)
+constexpr int kOptPrio = 1 << 17;      // VALU issue priority for waves on the launch's critical path (no effect on results)
+constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull |
+                            kOptBvh | kOptScatter2;
 constexpr uint32_t kStatsHeader = 24;        // kOptStats: 24 counters, then per-wave (start, end, iterations)
 constexpr uint32_t kStatsWaveSlots = 65536;
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)

@@ -32,6 +32,7 @@
 #define IQ_FP_FASTDIV 1
 #include "iq_fastdiv.h"
 #include "iq_fp.h"
+#include "iq_fp2.h"
 #include "iq_interval.h"
 #include "iq_xorwow.h"
 #include "iqpt_internal.hpp"
@@ -449,9 +450,22 @@ __device__ __forceinline__ void or_scatter_core(float hx, float hy, float hz, fl
     const float u1 = rand_real(s, 0.0f, 1.0f);
     const float u2 = rand_real(s, 0.0f, 1.0f);
     const float phi = (2.0f * IQ_PI) * u1;
-    const float su2 = sqrt_n<OPT>(u2);                          // u2 = k 2^-32: 0 or >= 2^-32
+    float su2, lz;
+    if ((OPT & kOptScatter2) && (OPT & kOptFastDiv)) {
+        // u2 = k 2^-32: 0 or >= 2^-32; 1 - u2: 0 or >= 2^-24 (iq_sqrt_n's domain)
+        const iq_f2 rt = iq_sqrt_n2((iq_f2){u2, 1.0f - u2});
+        su2 = rt.x;
+        lz = rt.y;
+    } else {
+        su2 = sqrt_n<OPT>(u2);                                   // u2 = k 2^-32: 0 or >= 2^-32
+        lz = sqrt_n<OPT>(1.0f - u2);                             // 1 - u2: 0 or >= 2^-24
+    }
     float sphi, cphi;
-    if (OPT & kOptSinCos) {
+    if (OPT & kOptScatter2) {
+        const iq_f2 sc = iq_sin_cos2((iq_f2){phi, phi});
+        sphi = sc.x;
+        cphi = sc.y;
+    } else if (OPT & kOptSinCos) {
         iq_sincosf(phi, &sphi, &cphi);
     } else {
         cphi = iq_cosf(phi);
@@ -459,7 +473,6 @@ __device__ __forceinline__ void or_scatter_core(float hx, float hy, float hz, fl
     }
     const float lx = cphi * su2;
     const float ly = sphi * su2;
-    const float lz = sqrt_n<OPT>(1.0f - u2);                    // 1 - u2: 0 or >= 2^-24
     float dx = (ux * lx + vx * ly) + wx * lz;                    // onb::transform_to_world
     float dy = (uy * lx + vy * ly) + wy * lz;
     float dz = (uz * lx + vz * ly) + wz * lz;
@@ -476,15 +489,27 @@ __device__ __forceinline__ void or_scatter_core(float hx, float hy, float hz, fl
         pdf = 1.0f / IQ_PI;
     }
     const float cosw = iq_fmaxf(0.0f, (nx * dx + ny * dy) + nz * dz);
-    const float phi_o = iq_atan2f(woy, wox);
-    const float phi_i = iq_atan2f(dy, dx);
     const float cto = iq_fmaxf(0.0f, (wox * nx + woy * ny) + woz * nz);
-    const float theta_o = cto > 1.0f ? 0.0f : iq_acosf(cto);
     const float cti = iq_fmaxf(0.0f, (dx * nx + dy * ny) + dz * nz);
-    const float theta_i = cti > 1.0f ? 0.0f : iq_acosf(cti);
-    const float alpha = iq_fmaxf(theta_i, theta_o);
-    const float beta = iq_fminf(theta_i, theta_o);
-    coeff = A + B * iq_cosf(phi_i - phi_o) * iq_sinf(alpha) * iq_tanf(beta);
+    if (OPT & kOptScatter2) {
+        // the independent transcendentals in packed pairs, branch-free (iq_fp2.h; same bits)
+        const iq_f2 ph = iq_atan2f2((iq_f2){woy, dy}, (iq_f2){wox, dx});   // (phi_o, phi_i)
+        const iq_f2 th = iq_acosf2((iq_f2){cto, cti});
+        const float theta_o = cto > 1.0f ? 0.0f : th.x;
+        const float theta_i = cti > 1.0f ? 0.0f : th.y;
+        const float alpha = iq_fmaxf(theta_i, theta_o);
+        const float beta = iq_fminf(theta_i, theta_o);
+        const iq_f2 sc = iq_sin_cos2((iq_f2){alpha, ph.y - ph.x});       // (sin(alpha), cos(phi_i - phi_o))
+        coeff = A + B * sc.y * sc.x * iq_tanf_bf(beta);
+    } else {
+        const float phi_o = iq_atan2f(woy, wox);
+        const float phi_i = iq_atan2f(dy, dx);
+        const float theta_o = cto > 1.0f ? 0.0f : iq_acosf(cto);
+        const float theta_i = cti > 1.0f ? 0.0f : iq_acosf(cti);
+        const float alpha = iq_fmaxf(theta_i, theta_o);
+        const float beta = iq_fminf(theta_i, theta_o);
+        coeff = A + B * iq_cosf(phi_i - phi_o) * iq_sinf(alpha) * iq_tanf(beta);
+    }
     r.ox = hx + nx * 0.0001f;                                    // hr.p + 0.0001f * hr.n
     r.oy = hy + ny * 0.0001f;
     r.oz = hz + nz * 0.0001f;
@@ -1342,6 +1367,12 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             need = __ballot(!active);
         }
         if (kSplit) spec_mask = __ballot(active && lds_sp[threadIdx.x].w == 1u);
+        if ((OPT & kOptPrio) && !(OPT & kOptExp) && kCull && p.cull) {
+            // a wave holding pixels of a tile with sphere candidates (chains that scatter: the launch's
+            // longest) wins VALU arbitration against wall / sky waves
+            if (__ballot(active && lds_cm[threadIdx.x].y != 0u) != 0ull) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
+        }
     };
 
     const uint64_t t_start = (OPT & kOptStats) ? __builtin_amdgcn_s_memrealtime() : 0ull;
@@ -1359,6 +1390,11 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
         if (kSplit && need_cam) {
             camera_ray<OPT>(p, px, py, st, ray);
             need_cam = false;
+        }
+        if ((OPT & kOptPrio) && (OPT & kOptExp)) {
+            // per iteration: a wave tracing a secondary ray wins VALU arbitration
+            if (__any(active && depth != 0)) __builtin_amdgcn_s_setprio(3);
+            else __builtin_amdgcn_s_setprio(0);
         }
         if (OPT & kOptStats) {
             ++s_iter;
@@ -1926,6 +1962,23 @@ __global__ __launch_bounds__(256) void iqpt_libm_kernel(int fn, const float* a, 
     case 11: r = iq_div(x, y); break;
     default: break;
     }
+    if (fn >= 12 && fn <= 19) {
+        // iq_fp2.h pair forms: element 0 from (a[i], b[i]), element 1 from the mirrored index, so every
+        // output is produced once by each lane slot over the two calls (fn even: .x, odd: .y)
+        const uint32_t k = n - 1u - i;
+        const float xk = a[k], yk = b[k];
+        const bool hi = fn & 1;
+        const iq_f2 va = hi ? (iq_f2){xk, x} : (iq_f2){x, xk}, vb = hi ? (iq_f2){yk, y} : (iq_f2){y, yk};
+        iq_f2 v = {0.0f, 0.0f};
+        switch (fn) {
+        case 12: case 13: v = iq_atan2f2(va, vb); break;      // atan2(a, b)
+        case 14: case 15: v = iq_acosf2(va); break;
+        case 16: case 17: v = iq_sin_cos2(va); break;         // 16: sin(a) from .x, 17: cos(a) from .y
+        case 18: v = (iq_f2){iq_tanf_bf(x), 0.0f}; break;
+        default: v = iq_sqrt_n2(va); break;                   // 19: iq_sqrt_n from .y
+        }
+        r = hi ? v.y : v.x;
+    }
     out[i] = r;
 }
 
@@ -2288,21 +2341,24 @@ const variant kVariants[] = {
     // variants keep it (5 waves measured 2.5 % faster on C5 than 4, 6 slower: profiles/ab/r01_ab72).
     // Streamed scenes also get the kOptBvhPrimary form (camera rays through the BVH), chosen per
     // packet by timing (iqpt_runtime.cpp).
-#define IQPT_PROD(O) IQPT_V(8, false, O), IQPT_V(16, false, O), IQPT_V(8, true, (O) & ~kOptLB5), \
+    // Resident variants carry kOptPrio (waves holding scatter-heavy tiles win VALU arbitration: the
+    // launch ends with the longest chains, profiles/r02/ab_prio.json); the runtime adds the bit.
+#define IQPT_PROD(O) IQPT_V(8, false, (O) | kOptPrio), IQPT_V(16, false, (O) | kOptPrio), IQPT_V(8, true, (O) & ~kOptLB5), \
                      IQPT_V(16, true, (O) & ~kOptLB5), IQPT_V(8, true, (O) | kOptBvhPrimary), \
                      IQPT_V(16, true, (O) | kOptBvhPrimary)
     IQPT_PROD(kOptDefault),
     // pitch-only cameras (kOptCamAxis), resident scenes, max_depth <= 8: opt-in only (10.5 % fewer VALU
     // instructions on C2 but no shorter launch); kept for its exactness tests
-    IQPT_V(8, false, kOptDefault | kOptCamAxis), IQPT_V(8, false, kOptDefault | kOptMaterials | kOptCamAxis),
+    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptPrio),
+    IQPT_V(8, false, kOptDefault | kOptMaterials | kOptCamAxis | kOptPrio),
     IQPT_PROD(kOptDefault & ~kOptFastDiv),                  // packets outside the kOptFastDiv range
     IQPT_PROD(kOptDefault | kOptMaterials),                 // packets with a material table
     IQPT_PROD((kOptDefault & ~kOptFastDiv) | kOptMaterials),
     // sample-parallel chains (kOptSplit), resident scenes
-    IQPT_V(8, false, kOptDefault | kOptSplit), IQPT_V(16, false, kOptDefault | kOptSplit),
-    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptSplit),
-    IQPT_V(8, false, kOptDefault | kOptMaterials | kOptSplit),
-    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptMaterials | kOptSplit),
+    IQPT_V(8, false, kOptDefault | kOptSplit | kOptPrio), IQPT_V(16, false, kOptDefault | kOptSplit | kOptPrio),
+    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptSplit | kOptPrio),
+    IQPT_V(8, false, kOptDefault | kOptMaterials | kOptSplit | kOptPrio),
+    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptMaterials | kOptSplit | kOptPrio),
 #undef IQPT_PROD
 #if defined(IQPT_AB_VARIANTS)
     IQPT_V(8, false, 0),
@@ -2332,6 +2388,13 @@ const variant kVariants[] = {
     IQPT_V(8, true, (kOptDefault | kOptMaterials) & ~kOptBvh),
     IQPT_V(8, false, kOptDefault | kOptSplit | kOptStats),
     IQPT_V(8, false, kOptDefault | kOptExp), IQPT_V(8, false, kOptDefault | kOptExp | kOptSplit),
+    // round 2: no priority, per-iteration priority, scalar scatter transcendentals (profiles/r02/ab_prio.json,
+    // ab_scatter2.json)
+    IQPT_V(8, false, kOptDefault), IQPT_V(8, false, kOptDefault | kOptPrio | kOptExp),
+    IQPT_V(8, false, kOptDefault | kOptPrio | kOptStats), IQPT_V(8, false, kOptDefault | kOptSplit),
+    IQPT_V(8, false, (kOptDefault & ~kOptScatter2) | kOptPrio),
+    IQPT_V(8, false, ((kOptDefault & ~kOptScatter2) | kOptPrio | kOptStats)),
+    IQPT_V(8, false, kOptDefault & ~kOptScatter2),
 #endif
 };
 #undef IQPT_V

@@ -1040,6 +1040,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // only where the camera qualifies. Not selected by default: 10 % fewer VALU instructions per
     // wave-iteration on C2 but no shorter launch
     if (!cam_axis) opt &= ~iqpt::kOptCamAxis;
+    // resident production variants carry kOptPrio (VALU priority for scatter-heavy waves; same bits)
+    if (!stream_batches && !iqpt::render_variant_exists(c->max_depth, false, opt) &&
+        iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptPrio))
+        opt |= iqpt::kOptPrio;
     if (stream_batches) {
         p.tri_batch = pair ? iqpt::kTriBatch / 2 : iqpt::kTriBatch;   // records
         p.sph_batch = pair ? iqpt::kSphBatch / 2 : iqpt::kSphBatch;
@@ -1551,9 +1555,15 @@ int iqpt_set_split(iqpt_ctx* c, int mode) {
     return IQPT_OK;
 }
 
+// The production option mask (kOptDefault) for A/B tools and tests.
+int iqpt_debug_default_options(void) { return iqpt::kOptDefault; }
+
 int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    if (!iqpt::render_variant_exists(c->max_depth, false, opt) && !iqpt::render_variant_exists(c->max_depth, true, opt))
+    // (resident launches add kOptPrio when only that form is built, as iqpt_render does)
+    if (!iqpt::render_variant_exists(c->max_depth, false, opt) &&
+        !iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptPrio) &&
+        !iqpt::render_variant_exists(c->max_depth, true, opt))
         return iqpt::fail(IQPT_ERR_UNSUPPORTED, "kernel option set not compiled into this build");
     int st = use_device(c);
     if (st) return st;

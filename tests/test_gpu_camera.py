@@ -63,7 +63,6 @@ def test_device_camera_transforms_bit_identical(require_gpu, which):
     assert np.array_equal(gen.view(np.uint32), host.view(np.uint32))
 
 
-K_OPT_DEFAULT = 2863
 K_OPT_MATERIALS = 1 << 10
 
 
@@ -75,7 +74,7 @@ def render_both(cam, w, h, spp, depth=8, preset="cornell", axis=True):
     if axis:   # opt-in variant (the runtime drops the bit when the camera does not qualify)
         lb = _lib.load()
         lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
-        opt = K_OPT_DEFAULT | K_OPT_CAM_AXIS | (K_OPT_MATERIALS if preset == "cornell_lit" else 0)
+        opt = lb.iqpt_debug_default_options() | K_OPT_CAM_AXIS | (K_OPT_MATERIALS if preset == "cornell_lit" else 0)
         _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, opt), "iqpt_debug_set_kernel_options")
     pt.set_camera(cam)
     pt.upload_packet(pk)

@@ -18,7 +18,9 @@ pytestmark = pytest.mark.gpu
 
 FP = C.POINTER(C.c_float)
 ORACLE_FN = {"sin": 0, "cos": 1, "tan": 2, "acos": 3, "atan2": 4, "asin": 5, "atan": 6}
-GPU_FN = dict(ORACLE_FN, sincos_sin=7, sincos_cos=8, sqrt=9, rcp=10, div=11)
+GPU_FN = dict(ORACLE_FN, sincos_sin=7, sincos_cos=8, sqrt=9, rcp=10, div=11,
+              atan2_x2_lo=12, atan2_x2_hi=13, acos_x2_lo=14, acos_x2_hi=15, sin_x2=16, cos_x2=17, tan_bf=18,
+              sqrt_x2=19)
 
 SPECIAL = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1.0, -1.0, 0.5, -0.5, 1e-45, -1e-45, 1e-38, 3.4e38,
                     -3.4e38, np.pi / 2, np.pi, 2 * np.pi, 1e-4, 1.0001e-4, 0.4142135, 0.41421357, 2.4142137,
@@ -112,3 +114,49 @@ def test_short_sqrt_rcp_div_are_ieee(require_gpu):
         check(gpu("rcp", a), np.float32(1.0) / a, a)
         b = np.concatenate([random_bits(), SPECIAL[::-1]])
         check(gpu("div", a, b), a / b, a, b)
+
+
+# iq_fp2.h: the packed, branch-free pairs of the Oren-Nayar scatter (kOptScatter2). Each lane evaluates
+# element i in one slot of the pair and the mirrored element n-1-i in the other; "_lo"/"_hi" read the
+# two slots, so every input is checked in both.
+def pair_inputs(n=1 << 20):
+    f32 = np.float32
+    sy, sx = np.meshgrid(SPECIAL, SPECIAL)
+    y = np.concatenate([rng.uniform(-1, 1, n).astype(f32), (rng.uniform(-1, 1, n) * 1e-30).astype(f32),
+                        random_bits(n), sy.ravel()])
+    x = np.concatenate([rng.uniform(-1, 1, n).astype(f32), rng.uniform(-1, 1, n).astype(f32), random_bits(n),
+                        sx.ravel()])
+    return y, x
+
+
+def test_atan2_pairs_equal_scalar(require_gpu):
+    y, x = pair_inputs()
+    want = host("atan2", y, x)
+    check(gpu("atan2_x2_lo", y, x), want, y, x)
+    check(gpu("atan2_x2_hi", y, x), want, y, x)
+
+
+@pytest.mark.parametrize("lo,hi", [(0.0, 1.0), (-1.0, 1.0), (-1.1, 1.1)])
+def test_acos_pairs_equal_scalar(require_gpu, lo, hi):
+    a = np.concatenate([args(lo, hi), random_bits()])
+    want = host("acos", a)
+    check(gpu("acos_x2_lo", a), want, a)
+    check(gpu("acos_x2_hi", a), want, a)
+
+
+@pytest.mark.parametrize("lo,hi", [(0.0, 2 * np.pi), (-2 * np.pi, 2 * np.pi), (-1e4, 1e4)])
+def test_sin_cos_pairs_and_tan_equal_scalar(require_gpu, lo, hi):
+    a = np.concatenate([args(lo, hi), random_bits()])
+    check(gpu("sin_x2", a), host("sin", a), a)
+    check(gpu("cos_x2", a), host("cos", a), a)
+    check(gpu("tan_bf", a), host("tan", a), a)
+
+
+def test_sqrt_pair_is_ieee_on_its_domain(require_gpu):
+    a = np.concatenate([random_bits(), SPECIAL])
+    a = a[(np.abs(a) >= 2.0 ** -96) | (a == 0) | np.isnan(a)]
+    with np.errstate(all="ignore"):
+        want = np.sqrt(a)
+    got = gpu("sqrt_x2", a)
+    pos = ~(a < 0)
+    check(got[pos], want[pos], a[pos])

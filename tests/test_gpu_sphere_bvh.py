@@ -23,13 +23,17 @@ def sbvh_info(pt):
     return n.value, a.value
 
 
-PRIM = 6959      # kOptDefault | kOptBvhPrimary (iqpt_internal.hpp), a production variant
+def prim_opt():
+    """kOptDefault | kOptBvhPrimary, a production variant (read from the library: no GPU needed)."""
+    return _lib.load().iqpt_debug_default_options() | (1 << 12)
 
 
 def run_both(scene, w, h, launches, depth, camera=None, pixels=None, opt=None):
     pk = scene.build_packet()
     cam = camera or make_camera(w, h)
     pt = PathTracer(w, h, max_depth=depth, pixels=pixels)
+    if opt == "prim":
+        opt = prim_opt()
     if opt is not None:
         lb = _lib.load()
         lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
@@ -64,7 +68,7 @@ def grid(sc, n, r=0.04, y=0.04, prefix="s"):
         sc.add_model(f"{prefix}{i:04d}", "sphere", r, 0.0, (-1.2 + 0.1 * (i % 25), y, -0.3 + 0.1 * (i // 25)))
 
 
-@pytest.mark.parametrize("opt", [None, PRIM], ids=["auto", "prim"])
+@pytest.mark.parametrize("opt", [None, "prim"], ids=["auto", "prim"])
 def test_grid_with_ground_on_always_list(require_gpu, opt):
     sc = Scene()
     streamed_base(sc)
@@ -74,7 +78,7 @@ def test_grid_with_ground_on_always_list(require_gpu, opt):
     assert nodes > 0 and always == 1
 
 
-@pytest.mark.parametrize("opt", [None, PRIM], ids=["auto", "prim"])
+@pytest.mark.parametrize("opt", [None, "prim"], ids=["auto", "prim"])
 def test_origins_inside_spheres(require_gpu, opt):
     """Camera inside a sphere of the BVH (every camera ray takes that sphere's far root), plus nested and
     overlapping spheres so that bounces also start inside spheres."""
@@ -89,7 +93,7 @@ def test_origins_inside_spheres(require_gpu, opt):
     assert nodes > 0 and always == 0
 
 
-@pytest.mark.parametrize("opt", [None, PRIM], ids=["auto", "prim"])
+@pytest.mark.parametrize("opt", [None, "prim"], ids=["auto", "prim"])
 def test_duplicate_spheres_tie_to_the_later_one(require_gpu, opt):
     """Every sphere twice at the same place: each hit is an exact t tie and the later (second) sphere's
     material must be the one shaded — the duplicates are emissive with different colours."""

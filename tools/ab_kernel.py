@@ -20,7 +20,7 @@ import numpy as np  # noqa: E402
 from iqpt import _build, _lib  # noqa: E402
 
 OPT = {"cam": 1, "acc": 2, "pair": 4, "sincos": 32, "stats": 128}
-DEFAULT = 1 | 2 | 4 | 8 | 32 | 256 | 512 | 2048
+DEFAULT = 0   # the library's production mask (iqpt_debug_default_options), set after loading it
 
 
 def main():
@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--out", default="")
     ap.add_argument("--only", default="", help="run one variant for --frames frames (profiling)")
     ap.add_argument("--frames", type=int, default=3)
-    ap.add_argument("--stats-opt", type=int, default=DEFAULT)
+    ap.add_argument("--stats-opt", type=int, default=-1, help="option mask of the stats run (default: production)")
     ap.add_argument("--crop", default="", help="x0,x1,y0,ystep,nrows pixel set")
     ap.add_argument("--variants", default="", help="comma list of name=optmask")
     ap.add_argument("--scene", default="", help="empty | walls (cornell without spheres) | preset name")
@@ -40,6 +40,10 @@ def main():
     lib_path = Path(args.lib) if args.lib else _build.build_lib(ab=True)
     _lib.LIB_PATH = lib_path                    # load the A/B build instead of the production one
     lib = _lib.load()
+    global DEFAULT
+    DEFAULT = lib.iqpt_debug_default_options()
+    if args.stats_opt < 0:
+        args.stats_opt = DEFAULT
     lib.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
     lib.iqpt_debug_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
     lib.iqpt_debug_set_diag.argtypes = [C.c_void_p, C.c_uint32]

@@ -4,6 +4,7 @@ plain kernel, kOptStats build (A/B library): kernel time, iterations, us per ite
 (1 ray per sample) and on a sphere (Oren-Nayar bounces). Also a 64x64 crop (64 waves)."""
 import ctypes as C
 import json
+import os
 import sys
 from pathlib import Path
 
@@ -33,7 +34,9 @@ for name, (x0, y0, n) in CASES.items():
         pt = iqpt.PathTracer(W, H, pixels=ps, max_depth=8)
         lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
         if stats:
-            _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, 2863 | 128), "opts")
+            _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, int(os.environ.get("LONE_OPT", str(lb.iqpt_debug_default_options()))) | 128), "opts")
+        elif os.environ.get("LONE_OPT"):
+            _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, int(os.environ["LONE_OPT"])), "opts")
         pt.set_split(_lib.SPLIT_OFF)
         pt.set_camera(cam)
         pt.upload_packet(pk)

@@ -88,7 +88,7 @@ def wave_timeline(n: int, spp: int, warm: int, knobs=None) -> dict:
     lb = _lib.load()
     pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
     lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
-    _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, 2863 | 128), "set options (stats)")
+    _lib.check(lb.iqpt_debug_set_kernel_options(pt._h, lb.iqpt_debug_default_options() | 128), "set options (stats)")
     pt.set_split(_lib.SPLIT_ON)
     if knobs:
         lb.iqpt_debug_set_split_knobs.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
