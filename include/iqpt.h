@@ -184,6 +184,16 @@ int iqpt_sync(iqpt_ctx* ctx);
 #define IQPT_SPLIT_ON 1
 int iqpt_set_split(iqpt_ctx* ctx, int mode);
 
+/* Overlapped launches (no reference counterpart: the reference launches one frame at a
+ * time on one stream, path_tracer.cu:370-392). With AUTO (the default) consecutive iqpt_render calls on
+ * a resident scene alternate between two HIP streams, so a launch starts filling the CUs its
+ * predecessor's tail leaves idle; each screen tile is bound to one XCD and waits, per tile, until the
+ * previous launch has finished it — bit-identical results. Every other call joins the streams. OFF
+ * renders every launch on one stream. */
+#define IQPT_OVERLAP_OFF 0
+#define IQPT_OVERLAP_AUTO 1
+int iqpt_set_overlap(iqpt_ctx* ctx, int mode);
+
 /* Builds the per-view acceleration state (the tile masks, queue order and split set of the current
  * camera and packet) now instead of inside the next iqpt_render, and synchronises: lets a caller time
  * the setup the reference pays on every scene change (path_tracer.cu:389-392). Optional. */
@@ -214,6 +224,9 @@ int iqpt_rays_traced(iqpt_ctx* ctx, uint64_t* rays);
 /* Sum of the render-kernel durations measured with HIP events on the ctx stream, and the number
  * of launches, since the last call (then cleared). Synchronises. */
 int iqpt_kernel_time(iqpt_ctx* ctx, double* total_ms, uint64_t* launches);
+/* The launches of the last iqpt_kernel_time call from the first one's start to the last one's end
+ * (equal to total_ms for launches that did not overlap, less when they did). */
+int iqpt_kernel_span(const iqpt_ctx* ctx, double* span_ms);
 /* Name of the render kernel as it appears in rocprofv3 traces. */
 const char* iqpt_kernel_name(void);
 

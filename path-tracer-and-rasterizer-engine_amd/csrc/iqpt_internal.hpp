@@ -144,8 +144,20 @@ struct kparams {
     const uint32_t* sp_pix;          // storage index of split slot sp (~0u: no pixel)
     const uint32_t* sp_st;           // 6 planes of ns_cap: a leftover's state at its chain position
     const float4_storage* sp_acc;    // a leftover's accumulator, samples done (uint bits in w)
+    // kOptOverlap: consecutive launches run concurrently on two streams. Every tile is
+    // bound to one XCD (its L2 is the coherence point of the tile's pixel state): an XCD's waves take
+    // only its own tiles, xcd_order[xcd_off[x] + q] in cost order, from the queue word queue[16 x].
+    // Launch k of an overlap chain takes tile t once tile_done[t] >= k * pixels(t) (every earlier
+    // launch of the chain finished the tile) and adds its completed pixels after their stores.
+    uint32_t* tile_done;
+    uint32_t done_target;            // k: launches of the chain before this one (0: no wait)
+    const uint32_t* xcd_order;
+    uint32_t xcd_off[9];
+    uint32_t* ovl_err;               // bit 0: a wait exceeded kOverlapSpinLimit (never expected)
 };
 constexpr int kSphNodeFloat4 = 3;
+constexpr uint32_t kOverlapSpinLimit = 1u << 23;   // s_sleep(20) polls before a wait gives up (~seconds)
+constexpr uint32_t kOverlapQueueWords = 2 * 8 * 16; // two launch parities x 8 XCD queue words, 64 B apart
 
 // iqpt_split_prep_kernel / iqpt_split_stitch_kernel (kOptSplit).
 struct ksplit {
@@ -245,11 +257,13 @@ constexpr int kOptCamAxis = 1 << 14;   // short camera transform for pitch-only 
                                        // checks the zero pattern and the frame-wide normalization bounds)
 constexpr int kOptSplit = 1 << 16;     // sample-parallel chains: speculative runs + anchored lanes (kparams::split_round)
 constexpr int kOptScatter2 = 1 << 18;  // Oren–Nayar scatter with packed, branch-free transcendental pairs (iq_fp2.h)
-constexpr int kOptPrio = 1 << 17;      // VALU issue priority for waves on the launch's critical path (no effect on results)
+constexpr int kOptPrio = 1 << 17;
+constexpr int kOptOverlap = 1 << 19;   // tiles bound to XCDs, launches overlap through per-tile completion counts      // VALU issue priority for waves on the launch's critical path (no effect on results)
 constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull |
                             kOptBvh | kOptScatter2;
 constexpr uint32_t kStatsHeader = 24;        // kOptStats: 24 counters, then per-wave (start, end, iterations)
 constexpr uint32_t kStatsWaveSlots = 65536;
+constexpr uint32_t kStatsQueueSlots = 65536;   // kOptStats: then the s_memrealtime at which queue position q was taken
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.

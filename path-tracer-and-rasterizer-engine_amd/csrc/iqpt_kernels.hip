@@ -1125,6 +1125,10 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // kOptSplit (resident scenes): round 1 serves anchored tiles and speculative runs, round 2 the
     // chains that left their window
     constexpr bool kSplit = (OPT & kOptSplit) && !STREAM;
+    // kOptOverlap (resident, culled, not split): this XCD's tile list and queue word, per-tile waits
+    constexpr bool kOverlap = (OPT & kOptOverlap) && !STREAM && !kSplit && kCull;
+    const uint32_t xcd = kOverlap ? (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) : 0u;   // HW_REG_XCC_ID
+    uint32_t* const queue_word = kOverlap ? p.queue + 16u * xcd : p.queue;
 
     if (!STREAM) {
         for (uint32_t i = threadIdx.x; i < tri_recs * kTriRec; i += kRenderBlock) lds_tri[i] = g_tri[i];
@@ -1179,6 +1183,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     unsigned long long s_full = 0;            // iterations forced to the full loop (a secondary ray in the wave)
     unsigned long long s_refill = 0, s_refill_lanes = 0;   // refills that started pixels, pixels started
     unsigned long long s_spec_lanes = 0;      // kOptSplit: speculative slots started by this wave
+    uint32_t s_first_q = 0, s_chunks = 0;     // first queue position taken, chunks taken (timeline)
     // per lane (kOptStats): BVH rays, nodes visited, leaf pairs / spheres tested — triangle and sphere BVH
     uint32_t c_tri[2] = {0u, 0u}, c_sph[2] = {0u, 0u}, c_tri_rays = 0u, c_sph_rays = 0u;
 
@@ -1188,7 +1193,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // tile, 2 leftovers [chunk_next, chunk_end) of the leftover list, 3 the light pixels of a split tile
     // (anchored) — and the split tile's first slot and storage index
     uint32_t chunk_kind = 0, chunk_sp0 = 0, chunk_first = 0, chunk_r = 0;
-    uint32_t queue_total = p.ntiles, n_runs = 0;
+    uint32_t queue_total = kOverlap ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : p.ntiles, n_runs = 0;
     if (kSplit) {
         // round 1, longest tasks first: the split tiles' light pixels (anchored chains with scatters, in
         // the masks' cost order), then the heavy pixels' run chunks, then the anchored (wall / sky) tiles
@@ -1230,13 +1235,21 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 if (kSplit && have_next) {
                     q = (uint32_t)__builtin_amdgcn_readfirstlane((int)q_next_v);
                 } else {
-                    if (lane == 0) q = atomicAdd(p.queue, 1u);
+                    if (lane == 0) q = atomicAdd(queue_word, 1u);
                     q = (uint32_t)__builtin_amdgcn_readfirstlane((int)q);   // wave-uniform: scalar registers
                 }
                 have_next = false;
                 if (q >= queue_total) {
                     exhausted = true;
                     break;
+                }
+                if (OPT & kOptStats) {
+                    if (s_chunks == 0) s_first_q = q;
+                    ++s_chunks;
+                    if (lane == 0 && p.stats && q < kStatsQueueSlots)
+                        p.stats[kStatsHeader + 3 * (size_t)kStatsWaveSlots + q] =
+                            (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) |
+                            ((unsigned long long)(blockIdx.x * (kRenderBlock / 64) + threadIdx.x / 64) << 48);
                 }
                 if (kSplit) {
                     if (lane == 0) q_next_v = atomicAdd(p.queue, 1u);
@@ -1265,6 +1278,24 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                             chunk_kind = 0;
                             t = p.anchor_order[q - p.n_split_tiles - n_runs];
                         }
+                    } else if (kOverlap) {
+                        t = p.xcd_order[p.xcd_off[xcd] + q];
+                        if (p.done_target != 0u && lane == 0) {
+                            // wait until the previous launches of the chain have finished tile t: their waves
+                            // ran on this XCD, so the counter and the tile's pixel state meet in its L2 (sc1
+                            // polls and loads bypass this CU's L1)
+                            const uint32_t tx = t % p.ntx, ty = t / p.ntx;
+                            const uint32_t need = p.done_target * (min(kCullTile, p.nrows - ty * kCullTile) *
+                                                                   min(kCullTile, p.ncols - tx * kCullTile));
+                            uint32_t spins = 0;
+                            while (__hip_atomic_load(p.tile_done + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
+                                __builtin_amdgcn_s_sleep(20);
+                                if (++spins > kOverlapSpinLimit) {
+                                    atomicOr(p.ovl_err, 1u);
+                                    break;
+                                }
+                            }
+                        }
                     } else {
                         t = p.tile_order ? p.tile_order[q] : q;
                     }
@@ -1275,6 +1306,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     chunk_next = ty * kCullTile * p.ncols + tx * kCullTile * th;
                     chunk_end = chunk_next + tw * th;
                     chunk_first = chunk_next;
+
                 }
             }
             const uint32_t avail = chunk_end - chunk_next;
@@ -1333,6 +1365,20 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         const float4_storage a = p.sp_acc[p.left[chunk_next + rank]];
                         acc = make_float3(a.x, a.y, a.z);
                         done = __float_as_uint(a.w);
+                    } else if (kOverlap) {
+                        // written by the previous launch of the chain, possibly from another CU of this XCD
+                        auto ld = [](const uint32_t* q) {
+                            return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        };
+                        st.v0 = ld(p.rng + pix);
+                        st.v1 = ld(p.rng + (size_t)p.npix + pix);
+                        st.v2 = ld(p.rng + 2 * (size_t)p.npix + pix);
+                        st.v3 = ld(p.rng + 3 * (size_t)p.npix + pix);
+                        st.v4 = ld(p.rng + 4 * (size_t)p.npix + pix);
+                        st.d = ld(p.rng + 5 * (size_t)p.npix + pix);
+                        const uint32_t* a = reinterpret_cast<const uint32_t*>(p.lin + pix);
+                        acc = make_float3(__uint_as_float(ld(a)), __uint_as_float(ld(a + 1)), __uint_as_float(ld(a + 2)));
+                        done = 0;
                     } else {
                         st.v0 = p.rng[pix];
                         st.v1 = p.rng[(size_t)p.npix + pix];
@@ -1666,6 +1712,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
 
         // ------------------------------------------------ shade (path_tracer.cu:297-316)
         bool term = false;
+        bool finished = false;             // kOptOverlap: the lane stored its pixel this iteration
         uint32_t md_end = 0;               // the path ended on a scatter at max_depth (kOptSplit slot count)
         float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
         // speculative lanes' rays are counted by the stitch, for the slots on the chain only
@@ -1876,6 +1923,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             depth = 0;
             if (done == p.spp) {
                 store_pixel();
+                if (kOverlap) finished = true;
                 if (kSplit && light_sp != ~0u) p.sp_rho[light_sp] = (uint32_t)(((uint64_t)light_slots * 256u) / p.spp);
                 active = false;
             } else if ((OPT & kOptDiag) && (p.diag & 1u)) {
@@ -1886,6 +1934,22 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 if (kSplit) need_cam = true;   // one camera_ray call site per iteration (loop top)
                 else camera_ray<OPT>(p, px, py, st, ray);
             }
+            }
+        }
+        if (kOverlap && p.tile_done) {
+            // pixels completed this iteration: once their stores are done (vmcnt 0), one counter add per tile
+            uint64_t fin = __ballot(finished);
+            if (fin) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                const uint32_t my_tile = lds_cm[threadIdx.x].z;
+                while (fin) {
+                    const int f = __builtin_ctzll(fin);
+                    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)my_tile, f);
+                    const uint64_t m = __ballot(finished && my_tile == t0);
+                    if ((int)lane == f) atomicAdd(p.tile_done + t0, (uint32_t)__popcll(m));
+                    fin &= ~m;
+                }
+                finished = false;
             }
         }
         if (!exhausted && (uint32_t)__popcll(__ballot(!active)) >= refill_min) refill();
@@ -1929,9 +1993,16 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             // one record per wave (lane 0; the atomic optimiser would otherwise hand every lane a slot)
             const uint64_t slot = lane == 0 && p.stats ? atomicAdd(p.stats + 11, 1ull) : ~0ull;
             if (slot < kStatsWaveSlots) {
-                p.stats[kStatsHeader + 3 * slot] = t_start;
+                // start (48 b) | wave id (blockIdx.x * waves per block + wave, 16 b)
+                p.stats[kStatsHeader + 3 * slot] =
+                    (t_start & 0xffffffffffffull) |
+                    ((unsigned long long)(blockIdx.x * (kRenderBlock / 64) + threadIdx.x / 64) << 48);
                 p.stats[kStatsHeader + 3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
-                p.stats[kStatsHeader + 3 * slot + 2] = s_iter | (s_spec_lanes << 32);
+                // iterations | (split: speculative lanes; else first queue position (24 b) | chunks (8 b)) << 32
+                p.stats[kStatsHeader + 3 * slot + 2] =
+                    s_iter | ((kSplit ? s_spec_lanes
+                                      : (unsigned long long)(min(s_first_q, 0xffffffu) | (min(s_chunks, 255u) << 24)))
+                              << 32);
             }
         }
     }
@@ -2354,6 +2425,10 @@ const variant kVariants[] = {
     IQPT_PROD(kOptDefault & ~kOptFastDiv),                  // packets outside the kOptFastDiv range
     IQPT_PROD(kOptDefault | kOptMaterials),                 // packets with a material table
     IQPT_PROD((kOptDefault & ~kOptFastDiv) | kOptMaterials),
+    // overlapped launches (kOptOverlap), resident scenes
+    IQPT_V(8, false, kOptDefault | kOptPrio | kOptOverlap), IQPT_V(16, false, kOptDefault | kOptPrio | kOptOverlap),
+    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptPrio | kOptOverlap),
+    IQPT_V(8, false, kOptDefault | kOptMaterials | kOptPrio | kOptOverlap),
     // sample-parallel chains (kOptSplit), resident scenes
     IQPT_V(8, false, kOptDefault | kOptSplit | kOptPrio), IQPT_V(16, false, kOptDefault | kOptSplit | kOptPrio),
     IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptSplit | kOptPrio),

@@ -155,6 +155,22 @@ struct iqpt_ctx {
     bool split_all_tiles = false;       // every tile in the split set (wall tiles: one slot per sample)   // 320 measured best at N = 8 (r02_split_share_v8)
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
     double tune_work[4] = {0.0, 0.0, 0.0, 0.0};
+    // kOptOverlap: consecutive render launches alternate between `stream` and
+    // `stream2`, so launch k + 1 fills the CUs that launch k's tail leaves idle; it takes a tile only
+    // when launch k has finished it (tile_done). Every other entry point joins the streams first.
+    int overlap_mode = IQPT_OVERLAP_AUTO;
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_pre = nullptr;        // on `stream`, before its last overlapped launch
+    hipEvent_t ev_s2 = nullptr;         // on `stream2`, after its last launch (join)
+    bool s2_pending = false;            // stream2 has work `stream` has not waited for
+    bool next_on_main = true;           // the next overlapped launch goes to `stream`
+    bool ovl_zero = true;               // tile_done must be zeroed before the next overlapped launch
+    uint32_t ovl_epoch = 0;             // overlapped launches since tile_done was zeroed
+    uint32_t* d_tile_done = nullptr;    // ntiles
+    uint32_t* d_xcd_order = nullptr;    // ntiles: XCD x's tiles at [xcd_off[x], xcd_off[x + 1])
+    uint32_t xcd_off[9] = {};
+    uint32_t* d_ovl_err = nullptr;
+    double last_span_ms = 0.0;          // iqpt_kernel_time: first start to last end of the timed launches
 };
 
 namespace {
@@ -162,6 +178,26 @@ namespace {
 int use_device(const iqpt_ctx* c) {
     IQPT_HIP(hipSetDevice(c->device));
     return IQPT_OK;
+}
+
+// kOptOverlap: make `stream` wait for the last launch on `stream2`; the next overlapped launch starts a
+// new chain (tile_done zeroed on `stream`, no waits).
+int join_streams(iqpt_ctx* c) {
+    if (c->s2_pending) {
+        IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
+        IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
+        c->s2_pending = false;
+    }
+    c->next_on_main = true;
+    c->ovl_zero = true;
+    return IQPT_OK;
+}
+
+// Every entry point but iqpt_render: the device, then the streams joined.
+int enter(iqpt_ctx* c) {
+    int st = use_device(c);
+    if (st) return st;
+    return join_streams(c);
 }
 
 void cam_constants(const iqpt_camera& cam, uint32_t* is_const, float* near_rw, float* far_rw);
@@ -349,6 +385,23 @@ int build_cull(iqpt_ctx* c) {
     if (!c->d_tile_order && hipMalloc(&c->d_tile_order, (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
         return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "tile order");
     IQPT_HIP(hipMemcpy(c->d_tile_order, order.data(), order.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    // kOptOverlap: the cost order dealt round-robin to the 8 XCDs (each list in cost order)
+    {
+        std::vector<uint32_t> xo;
+        xo.reserve(ntiles);
+        for (uint32_t x = 0; x < 8; ++x) {
+            c->xcd_off[x] = (uint32_t)xo.size();
+            for (uint32_t r = x; r < ntiles; r += 8) xo.push_back(order[r]);
+        }
+        c->xcd_off[8] = (uint32_t)xo.size();
+        if (!c->d_xcd_order && hipMalloc(&c->d_xcd_order, (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "XCD tile order");
+        if (!c->d_tile_done && hipMalloc(&c->d_tile_done, (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "tile completion counts");
+
+        IQPT_HIP(hipMemcpy(c->d_xcd_order, xo.data(), xo.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        c->ovl_zero = true;
+    }
     c->split_last = false;
     int st = build_split(c, order, cnt);
     if (st != IQPT_OK) return st;
@@ -693,12 +746,14 @@ int iqpt_create(int device, uint32_t width, uint32_t height, const iqpt_pixel_se
         hipMalloc(&c->d_bgra, n * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_rng, 6 * n * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_rays, sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->d_queue, 4 * sizeof(uint32_t)) != hipSuccess)
+        hipMalloc(&c->d_queue, (4 + iqpt::kOverlapQueueWords) * sizeof(uint32_t)) != hipSuccess ||
+        hipMalloc(&c->d_ovl_err, sizeof(uint32_t)) != hipSuccess)
         return cleanup(iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "device allocation of the frame state failed"));
     // path_tracer.cu:134-135: both buffers start at zero
     if (hipMemsetAsync(c->d_lin, 0, n * sizeof(float4_storage), c->stream) != hipSuccess ||
         hipMemsetAsync(c->d_bgra, 0, n * sizeof(uint32_t), c->stream) != hipSuccess ||
-        hipMemsetAsync(c->d_rays, 0, sizeof(unsigned long long), c->stream) != hipSuccess)
+        hipMemsetAsync(c->d_rays, 0, sizeof(unsigned long long), c->stream) != hipSuccess ||
+        hipMemsetAsync(c->d_ovl_err, 0, sizeof(uint32_t), c->stream) != hipSuccess)
         return cleanup(iqpt::fail(IQPT_ERR_HIP, "hipMemsetAsync"));
     // renderer_init_kernel (path_tracer.cu:139): curand_init(seed, pixelid, 0)
     const std::vector<uint32_t>& tables = iqpt::xorwow_tables();
@@ -721,12 +776,18 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (!c) return IQPT_OK;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     free_scene(c);
     if (c->d_lin) (void)hipFree(c->d_lin);
     if (c->d_bgra) (void)hipFree(c->d_bgra);
     if (c->d_rng) (void)hipFree(c->d_rng);
     if (c->d_rays) (void)hipFree(c->d_rays);
     if (c->d_queue) (void)hipFree(c->d_queue);
+    for (uint32_t* b : {c->d_tile_done, c->d_xcd_order, c->d_ovl_err})
+        if (b) (void)hipFree(b);
+    if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
+    if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
+    if (c->stream2) (void)hipStreamDestroy(c->stream2);
     free_split(c);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
@@ -883,7 +944,7 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
         float* dst = &sph_pairs[(k / 2) * iqpt::kSphPairFloat4].x;
         for (int comp = 0; comp < 4; ++comp) dst[2 * comp + (k & 1)] = f[comp];
     }
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));   // a render in flight may still read the old scene
     free_scene(c);
@@ -1059,7 +1120,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
                          (uint32_t)std::max(c->max_depth, 1) * iqpt::kRenderBlock * 4u *
                              ((opt & iqpt::kOptMaterials) ? 3u : 1u);
     if ((opt & iqpt::kOptCull) && (c->ntri + c->nsph) > 0) {
-        if (!c->cull_valid && (st = build_cull(c)) != IQPT_OK) return st;
+        if (!c->cull_valid) {
+            if ((st = join_streams(c)) != IQPT_OK) return st;   // new masks and tile lists: the chain restarts
+            if ((st = build_cull(c)) != IQPT_OK) return st;
+        }
         p.cull = c->d_cull;
         p.tile_order = c->d_tile_order;
         p.cull_ntx = c->cull_ntx;
@@ -1125,6 +1189,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const double lanes = (double)c->num_cus * std::max(occ_s, 1) * iqpt::kRenderBlock;
         split = occ_s > 0 && (c->split_mode == IQPT_SPLIT_ON || (double)c->npix < iqpt::kSplitAutoPixelsPerLane * lanes);
     }
+    if (split && (st = join_streams(c)) != IQPT_OK) return st;   // split launches never overlap
     const size_t ns_cap = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
     const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
     const uint32_t g_max = (m_cap + iqpt::kSplitRunLen - 1) / iqpt::kSplitRunLen;
@@ -1212,16 +1277,67 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             IQPT_HIP(hipMemsetAsync(sp_pix + 2 * ns_cap, 0, ns_cap * sizeof(uint32_t), c->stream));
         }
     }
+    // kOptOverlap: resident, culled, not split, not a tuning launch
+    bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && p.cull != nullptr &&
+               tune_slot < 0 && c->d_tile_done && c->d_xcd_order &&
+               iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptOverlap);
     int occ = 0;
-    if (iqpt::render_occupancy(c->max_depth, stream_batches, opt, lds, &occ) != 0 || occ < 1) occ = 1;
+    if (iqpt::render_occupancy(c->max_depth, stream_batches, ovl ? (opt | iqpt::kOptOverlap) : opt, lds, &occ) != 0 ||
+        occ < 1)
+        occ = 1;
+    // two launches in flight: each keeps one block slot per CU free for the other (occ - 1 per CU), so the
+    // earlier launch, which the later one waits for, can always run
+    if (ovl && occ < 2) ovl = false;
+    if (ovl && !c->stream2) {
+        if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_s2, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            ovl = false;
+            c->overlap_mode = IQPT_OVERLAP_OFF;
+        }
+    }
+    if (!ovl && (st = join_streams(c)) != IQPT_OK) return st;
+    hipStream_t ls = c->stream;                       // the launch's stream
+    if (ovl) {
+        opt |= iqpt::kOptOverlap;
+        if (c->ovl_zero || c->ovl_epoch >= (1u << 24)) {
+            if ((st = join_streams(c)) != IQPT_OK) return st;
+            IQPT_HIP(hipMemsetAsync(c->d_tile_done, 0, (size_t)p.ntiles * sizeof(uint32_t), c->stream));
+            c->ovl_zero = false;
+            c->ovl_epoch = 0;
+        }
+        if (!c->next_on_main) {
+            // after everything `stream` held before its last launch, that launch's list resets included
+            ls = c->stream2;
+            IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
+            c->s2_pending = true;
+        }
+        const uint32_t parity = c->ovl_epoch & 1u;
+        p.queue = c->d_queue + 4 + parity * (iqpt::kOverlapQueueWords / 2);
+        p.tile_done = c->d_tile_done;
+        p.done_target = c->ovl_epoch;
+        p.xcd_order = c->d_xcd_order;
+        std::memcpy(p.xcd_off, c->xcd_off, sizeof p.xcd_off);
+        p.ovl_err = c->d_ovl_err;
+        IQPT_HIP(hipMemsetAsync(p.queue, 0, (iqpt::kOverlapQueueWords / 2) * sizeof(uint32_t), ls));
+        // the next launch (stream2) starts after all of this but not after this launch
+        if (ls == c->stream) IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
+        occ -= 1;
+    }
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
-    IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
+    if (!ovl) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
     hipEvent_t e0 = take_event(c), e1 = take_event(c);
-    if (e0) (void)hipEventRecord(e0, c->stream);
+    if (e0) (void)hipEventRecord(e0, ls);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
     int le = 0;
-    if (split) {
+    if (ovl) {
+        le = iqpt::launch_render(ls, p, grid, lds, stream_batches, opt);
+        c->ovl_epoch += 1;
+        c->next_on_main = !c->next_on_main;
+        if (le != 0) c->ovl_zero = true;     // a failed launch breaks the chain's counts: restart it
+    } else if (split) {
         // prep -> round 1 (runs, anchored tiles, light split pixels) -> stitch -> round 2 (leftovers)
         le = iqpt::launch_split_prep(c->stream, ks);
         p.split_round = 1;
@@ -1236,7 +1352,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     }
     c->split_last = split;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
-    if (e1) (void)hipEventRecord(e1, c->stream);
+    if (e1) (void)hipEventRecord(e1, ls);
     if (e0 && e1) c->timed.emplace_back(e0, e1);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "render kernel launch");
     c->last_opt = opt;
@@ -1251,15 +1367,22 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
 
 int iqpt_sync(iqpt_ctx* c) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
+    // kOptOverlap: a per-tile wait that gave up (never expected) leaves the frame undefined: report it
+    uint32_t err = 0;
+    IQPT_HIP(hipMemcpy(&err, c->d_ovl_err, sizeof err, hipMemcpyDeviceToHost));
+    if (err) {
+        IQPT_HIP(hipMemset(c->d_ovl_err, 0, sizeof err));
+        return iqpt::fail(IQPT_ERR_HIP, "overlapped launch: a per-tile wait timed out (results invalid)");
+    }
     return IQPT_OK;
 }
 
 int iqpt_reset(iqpt_ctx* c) {                                       // path_tracer.cu:394-400
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     IQPT_HIP(hipMemsetAsync(c->d_bgra, 0, (size_t)c->npix * sizeof(uint32_t), c->stream));
@@ -1270,7 +1393,7 @@ int iqpt_reset(iqpt_ctx* c) {                                       // path_trac
 
 int iqpt_read(iqpt_ctx* c, float* lin_rgba, uint8_t* bgra) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     if (lin_rgba && (st = fetch_compact(c, c->d_lin, 4, 1, lin_rgba)) != IQPT_OK) return st;
     if (bgra && (st = fetch_compact(c, c->d_bgra, 1, 1, bgra)) != IQPT_OK) return st;
@@ -1279,7 +1402,7 @@ int iqpt_read(iqpt_ctx* c, float* lin_rgba, uint8_t* bgra) {
 
 int iqpt_read_rng(iqpt_ctx* c, uint32_t* states) {
     if (!c || !states) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     std::vector<uint32_t> planes((size_t)c->npix * 6);
     if ((st = fetch_compact(c, c->d_rng, 1, 6, planes.data())) != IQPT_OK) return st;
@@ -1291,7 +1414,7 @@ int iqpt_read_rng(iqpt_ctx* c, uint32_t* states) {
 int iqpt_copy_accum_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
     if (!c || !dst_device) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     if (bytes < (size_t)c->npix * sizeof(float4_storage)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     const int le = iqpt::launch_relayout(c->stream, reinterpret_cast<const uint32_t*>(c->d_lin),
                                          static_cast<uint32_t*>(dst_device), c->ncols, c->set.nrows, 4, 1, true);
@@ -1328,7 +1451,7 @@ uint64_t fnv1a(const void* data, size_t n, uint64_t h = 1469598103934665603ull) 
 
 int iqpt_checkpoint_save(iqpt_ctx* c, const char* path) {
     if (!c || !path) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     const size_t n = c->npix;
@@ -1412,7 +1535,7 @@ int iqpt_checkpoint_load(iqpt_ctx* c, const char* path) {
                 break;
             }
     if (!why.empty()) return iqpt::fail(IQPT_ERR_INVALID_ARG, std::string(path) + ": " + why);
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     const unsigned long long rays = h.rays;
@@ -1439,7 +1562,7 @@ int iqpt_frame_count(const iqpt_ctx* c, uint64_t* frames) {
 
 int iqpt_rays_traced(iqpt_ctx* c, uint64_t* rays) {
     if (!c || !rays) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     unsigned long long v = 0;
@@ -1450,17 +1573,21 @@ int iqpt_rays_traced(iqpt_ctx* c, uint64_t* rays) {
 
 int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
     if (!c || !total_ms || !launches) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
-    double sum = 0.0;
+    double sum = 0.0, span = 0.0;
     for (auto& pr : c->timed) {
-        float ms = 0.0f;
+        float ms = 0.0f, end = 0.0f;
         IQPT_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+        // span: from the first launch's start to the latest end (launches on two streams overlap)
+        IQPT_HIP(hipEventElapsedTime(&end, c->timed.front().first, pr.second));
         sum += ms;
+        span = std::max(span, (double)end);
         c->event_pool.push_back(pr.first);
         c->event_pool.push_back(pr.second);
     }
+    c->last_span_ms = span;
     *total_ms = sum;
     *launches = c->timed.size();
     c->timed.clear();
@@ -1479,7 +1606,7 @@ int iqpt_debug_set_diag(iqpt_ctx* c, uint32_t bits) {
 int iqpt_copy_frame_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
     if (!c || !dst_device) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     if (bytes < (size_t)c->npix * sizeof(uint32_t)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     const int le = iqpt::launch_relayout(c->stream, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
                                          c->set.nrows, 1, 1, true);
@@ -1491,7 +1618,7 @@ int iqpt_copy_frame_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
 int iqpt_prepare(iqpt_ctx* c) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     if (!c->have_camera || !c->have_packet) return iqpt::fail(IQPT_ERR_NOT_READY, "camera and packet must be set");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     if ((c->opt & iqpt::kOptPair) && (c->opt & iqpt::kOptCull) && (c->ntri + c->nsph) > 0 && !c->cull_valid &&
         (st = build_cull(c)) != IQPT_OK)
@@ -1505,7 +1632,7 @@ int iqpt_prepare(iqpt_ctx* c) {
 // split pixels, whether the last launch ran split. Synchronises.
 int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     for (int i = 0; i < 8; ++i) out8[i] = 0;
@@ -1547,6 +1674,20 @@ int iqpt_debug_set_split_knobs(iqpt_ctx* c, uint32_t heavy_rho, uint32_t refill_
     return IQPT_OK;
 }
 
+int iqpt_kernel_span(const iqpt_ctx* c, double* span_ms) {
+    if (!c || !span_ms) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *span_ms = c->last_span_ms;
+    return IQPT_OK;
+}
+int iqpt_set_overlap(iqpt_ctx* c, int mode) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    if (mode != IQPT_OVERLAP_OFF && mode != IQPT_OVERLAP_AUTO)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "overlap mode must be IQPT_OVERLAP_OFF or _AUTO");
+    int st = enter(c);
+    if (st) return st;
+    c->overlap_mode = mode;
+    return IQPT_OK;
+}
 int iqpt_set_split(iqpt_ctx* c, int mode) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     if (mode != IQPT_SPLIT_AUTO && mode != IQPT_SPLIT_OFF && mode != IQPT_SPLIT_ON)
@@ -1565,10 +1706,10 @@ int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
         !iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptPrio) &&
         !iqpt::render_variant_exists(c->max_depth, true, opt))
         return iqpt::fail(IQPT_ERR_UNSUPPORTED, "kernel option set not compiled into this build");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     if ((opt & iqpt::kOptStats) && !c->d_stats) {
-        const size_t words = iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots;
+        const size_t words = iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots + iqpt::kStatsQueueSlots;
         if (hipMalloc(&c->d_stats, words * sizeof(unsigned long long)) != hipSuccess)
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "stats");
         IQPT_HIP(hipMemset(c->d_stats, 0, words * sizeof(unsigned long long)));
@@ -1729,10 +1870,23 @@ int iqpt_debug_last_options(iqpt_ctx* c, int* opt) {
 /* Internal (tools/ab_kernel.py): the per-wave timeline of the last kOptStats launch: up to `cap`
  * (start, end, iterations) triples (s_memrealtime ticks, 100 MHz); *n = waves recorded. Call before
  * iqpt_debug_read_stats (which clears the buffer). */
+// kOptStats: the s_memrealtime (100 MHz) at which each queue position was taken, 0 for positions not
+// taken (out: kStatsQueueSlots words).
+int iqpt_debug_read_queue_times(iqpt_ctx* c, unsigned long long* out) {
+    if (!c || !out) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = enter(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    if (!c->d_stats) return iqpt::fail(IQPT_ERR_INVALID_ARG, "no stats buffer (kOptStats not set)");
+    IQPT_HIP(hipMemcpy(out, c->d_stats + iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots,
+                       iqpt::kStatsQueueSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return IQPT_OK;
+}
+
 int iqpt_debug_read_wave_times(iqpt_ctx* c, unsigned long long* out, uint32_t cap, uint32_t* n) {
     if (!c || !out || !n) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     *n = 0;
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     if (!c->d_stats) return IQPT_OK;
@@ -1749,7 +1903,7 @@ int iqpt_debug_read_wave_times(iqpt_ctx* c, unsigned long long* out, uint32_t ca
 int iqpt_debug_read_stats(iqpt_ctx* c, unsigned long long* out16) {
     unsigned long long* out8 = out16;   // kStatsHeader (24) counters (tools/ab_kernel.py)
     if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    int st = use_device(c);
+    int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     if (!c->d_stats) {

@@ -21,6 +21,7 @@ MESH_SPHERES = 1
 DEFAULT_SEED = 1984
 DEFAULT_MAX_DEPTH = 5
 SPLIT_AUTO, SPLIT_OFF, SPLIT_ON = -1, 0, 1     # IQPT_SPLIT_* (iqpt_set_split)
+OVERLAP_OFF, OVERLAP_AUTO = 0, 1               # IQPT_OVERLAP_* (iqpt_set_overlap)
 
 
 class IqptError(RuntimeError):
@@ -96,6 +97,8 @@ SIGNATURES = [
     ("iqpt_copy_accum_device", C.c_int, [_P, _P, C.c_size_t]),
     ("iqpt_copy_frame_device", C.c_int, [_P, _P, C.c_size_t]),
     ("iqpt_set_split", C.c_int, [_P, C.c_int]),
+    ("iqpt_set_overlap", C.c_int, [_P, C.c_int]),
+    ("iqpt_kernel_span", C.c_int, [_P, C.POINTER(C.c_double)]),
     ("iqpt_prepare", C.c_int, [_P]),
     ("iqpt_num_pixels", C.c_int, [_P, C.POINTER(C.c_uint64)]),
     ("iqpt_frame_count", C.c_int, [_P, C.POINTER(C.c_uint64)]),

@@ -101,6 +101,16 @@ class PathTracer:
         """Sample-parallel chains: _lib.SPLIT_AUTO (default), SPLIT_OFF or SPLIT_ON (iqpt_set_split)."""
         check(self._lib.iqpt_set_split(self._h, mode), "iqpt_set_split")
 
+    def set_overlap(self, mode: int):
+        """Overlapped launches on two streams: _lib.OVERLAP_AUTO (default) or OVERLAP_OFF (iqpt_set_overlap)."""
+        check(self._lib.iqpt_set_overlap(self._h, mode), "iqpt_set_overlap")
+
+    def kernel_span(self) -> float:
+        """First start to last end (ms) of the launches of the last kernel_time() call (iqpt_kernel_span)."""
+        ms = C.c_double()
+        check(self._lib.iqpt_kernel_span(self._h, C.byref(ms)), "iqpt_kernel_span")
+        return ms.value
+
     def prepare(self):
         """Build the tile masks / queue order / split set now (iqpt_prepare; synchronises)."""
         check(self._lib.iqpt_prepare(self._h), "iqpt_prepare")

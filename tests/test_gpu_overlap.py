@@ -1,0 +1,131 @@
+"""Overlapped launches (kOptOverlap): consecutive iqpt_render calls alternate between two
+HIP streams and each screen tile waits, on its XCD, for the previous launch to finish it. The results must
+be the bits of one stream (and of the oracle): accumulator, BGRA8, XORWOW states and ray counts, for
+chains of launches, chains cut by reads / camera changes / resets, and the full C2 frame."""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import compare, scene_for
+from iqpt import PathTracer, _lib, make_camera
+from iqpt.render import pixel_set
+
+pytestmark = pytest.mark.gpu
+
+K_OPT_OVERLAP = 1 << 19
+
+
+def last_options(pt):
+    lb = _lib.load()
+    lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    o = C.c_int(0)
+    _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(o)), "iqpt_debug_last_options")
+    return o.value
+
+
+def run(preset, w, h, launches, depth=8, pixels=None, overlap=True, cut=None):
+    """launches: spp per render call; cut: {index: action} applied before that render."""
+    _, pk = scene_for(preset)
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, pixels=pixels, max_depth=depth)
+    pt.set_split(_lib.SPLIT_OFF)      # small pixel sets would take the split mode, which never overlaps
+    pt.set_overlap(_lib.OVERLAP_AUTO if overlap else _lib.OVERLAP_OFF)
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    opts = []
+    for i, s in enumerate(launches):
+        if cut and i in cut:
+            cut[i](pt, cam)
+        pt.render(s)
+        opts.append(last_options(pt))
+    pt.sync()
+    lin, bgra = pt.read()
+    out = (lin, bgra, pt.read_rng(), pt.rays(), pt.frames())
+    pt.close()
+    return out, opts
+
+
+def same(a, b):
+    assert np.array_equal(a[0].view(np.uint32), b[0].view(np.uint32))
+    assert np.array_equal(a[1], b[1])
+    assert np.array_equal(a[2], b[2])
+    assert a[3] == b[3] and a[4] == b[4]
+
+
+def test_chain_equals_one_stream_and_oracle(require_gpu):
+    w, h = 256, 144
+    launches = [4, 3, 5, 1, 2, 6, 4, 4]
+    on, opts = run("cornell", w, h, launches)
+    assert all(o & K_OPT_OVERLAP for o in opts), opts
+    off, opts_off = run("cornell", w, h, launches, overlap=False)
+    assert not any(o & K_OPT_OVERLAP for o in opts_off)
+    same(on, off)
+    _, pk = scene_for("cornell")
+    fr = oracle.OracleFrame(w, h, max_depth=8)
+    for s in launches:
+        fr.render(pk, make_camera(w, h), s)
+    c = compare(on[0], fr.lin)
+    assert c["bitexact"] == c["npix"], c
+    assert np.array_equal(on[2], fr.states)
+    assert on[3] == int(fr.rays.sum())
+
+
+def test_chain_cut_by_reads_camera_and_reset(require_gpu):
+    w, h = 200, 120
+    launches = [3] * 9
+
+    def read(pt, cam):
+        pt.read()
+
+    def recam(pt, cam):
+        pt.set_camera(cam)            # same view: masks and XCD tile lists rebuilt, the chain restarts
+
+    def reset(pt, cam):
+        pt.reset()
+
+    cuts = {2: read, 4: recam, 6: reset, 7: read}
+    on, _ = run("cornell", w, h, launches, cut=dict(cuts))
+    off, _ = run("cornell", w, h, launches, overlap=False, cut=dict(cuts))
+    same(on, off)
+
+
+@pytest.mark.parametrize("preset,w,h,depth,crop", [
+    ("app_default", 320, 180, 5, None),
+    ("cornell", 1920, 1080, 8, (640, 1280, 400, 2, 96)),       # a C3-like row share (every other row)
+    ("cornell_lit", 160, 96, 8, None),                         # material table variant
+])
+def test_other_scenes_and_shares(require_gpu, preset, w, h, depth, crop):
+    ps = pixel_set(w, h, *crop) if crop else None
+    launches = [2, 2, 2, 2, 2]
+    on, opts = run(preset, w, h, launches, depth=depth, pixels=ps)
+    off, _ = run(preset, w, h, launches, depth=depth, pixels=ps, overlap=False)
+    same(on, off)
+
+
+def test_full_c2_frame_three_overlapped_launches(require_gpu):
+    """The bench's step sequence: 64-spp launches back to back on the full 1920x1080 frame."""
+    w, h = 1920, 1080
+    on, opts = run("cornell", w, h, [64, 64, 64])
+    assert all(o & K_OPT_OVERLAP for o in opts)
+    off, _ = run("cornell", w, h, [64, 64, 64], overlap=False)
+    same(on, off)
+
+
+def test_kernel_span_not_longer_than_sum(require_gpu):
+    _, pk = scene_for("cornell")
+    w, h = 640, 360
+    pt = PathTracer(w, h, max_depth=8)
+    pt.set_split(_lib.SPLIT_OFF)
+    pt.set_camera(make_camera(w, h))
+    pt.upload_packet(pk)
+    pt.render(8)
+    pt.sync()
+    pt.kernel_time()
+    for _ in range(6):
+        pt.render(8)
+    total, n = pt.kernel_time()
+    span = pt.kernel_span()
+    assert n == 6 and 0.0 < span <= total * 1.0001
+    pt.close()

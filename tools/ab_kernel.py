@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--crop", default="", help="x0,x1,y0,ystep,nrows pixel set")
     ap.add_argument("--variants", default="", help="comma list of name=optmask")
     ap.add_argument("--scene", default="", help="empty | walls (cornell without spheres) | preset name")
+    ap.add_argument("--timeline-npy", default="", help="save the stats run's raw per-wave records (.npy)")
     ap.add_argument("--lib", default="", help="load this prebuilt A/B library (compiler-option runs)")
     args = ap.parse_args()
     lib_path = Path(args.lib) if args.lib else _build.build_lib(ab=True)
@@ -157,7 +158,15 @@ def main():
         lib.iqpt_debug_read_wave_times.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32,
                                                    C.POINTER(C.c_uint32)]
         if lib.iqpt_debug_read_wave_times(pt.handle, wt, cap, C.byref(nw)) == 0 and nw.value:
-            a = np.array(wt[:3 * nw.value], dtype=np.float64).reshape(-1, 3)
+            raw = np.array(wt[:3 * nw.value], dtype=np.uint64).reshape(-1, 3)
+            if args.timeline_npy:
+                np.save(args.timeline_npy, raw)
+                qt = (C.c_ulonglong * 65536)()
+                lib.iqpt_debug_read_queue_times.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+                if lib.iqpt_debug_read_queue_times(pt.handle, qt) == 0:
+                    np.save(args.timeline_npy.replace(".npy", "_queue.npy"), np.array(qt[:], dtype=np.uint64))
+            a = (raw & np.uint64(0xffffffffffff)).astype(np.float64)    # 48-bit times (wave id above)
+            a[:, 2] = (raw[:, 2] & np.uint64(0xffffffff)).astype(np.float64)
             t0 = a[:, 0].min()
             start_us, end_us = (a[:, 0] - t0) / 100.0, (a[:, 1] - t0) / 100.0     # 100 MHz ticks
             kern = end_us.max()

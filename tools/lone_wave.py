@@ -62,7 +62,7 @@ for name, (x0, y0, n) in CASES.items():
             lb.iqpt_debug_read_wave_times.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32,
                                                       C.POINTER(C.c_uint32)]
             lb.iqpt_debug_read_wave_times(pt._h, wt, cap, C.byref(nw))
-            a = np.array(wt[:3 * nw.value], dtype=np.float64).reshape(-1, 3)
+            a = (np.array(wt[:3 * nw.value], dtype=np.uint64).reshape(-1, 3) & np.uint64(0xffffffffffff)).astype(np.float64)
             a = a[a[:, 2] > 0]
             dur = (a[:, 1] - a[:, 0]) / 100.0
             row["busy_waves"] = int(len(a))

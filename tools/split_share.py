@@ -108,7 +108,7 @@ def wave_timeline(n: int, spp: int, warm: int, knobs=None) -> dict:
                                               C.POINTER(C.c_uint32)]
     _lib.check(lb.iqpt_debug_read_wave_times(pt._h, wt, cap, C.byref(nw)), "wave times")
     raw = np.array(wt[:3 * nw.value], dtype=np.uint64).reshape(-1, 3)
-    a = raw.astype(np.float64)
+    a = (raw & np.uint64(0xffffffffffff)).astype(np.float64)     # 48-bit times (wave id above)
     a[:, 2] = (raw[:, 2] & np.uint64(0xffffffff)).astype(np.float64)
     spec = (raw[:, 2] >> np.uint64(32)).astype(np.float64)
     pt.close()
