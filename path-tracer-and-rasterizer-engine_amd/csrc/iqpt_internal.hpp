@@ -257,8 +257,8 @@ constexpr int kOptCamAxis = 1 << 14;   // short camera transform for pitch-only 
                                        // checks the zero pattern and the frame-wide normalization bounds)
 constexpr int kOptSplit = 1 << 16;     // sample-parallel chains: speculative runs + anchored lanes (kparams::split_round)
 constexpr int kOptScatter2 = 1 << 18;  // Oren–Nayar scatter with packed, branch-free transcendental pairs (iq_fp2.h)
-constexpr int kOptPrio = 1 << 17;
-constexpr int kOptOverlap = 1 << 19;   // tiles bound to XCDs, launches overlap through per-tile completion counts      // VALU issue priority for waves on the launch's critical path (no effect on results)
+constexpr int kOptPrio = 1 << 17;      // VALU issue priority for waves on the launch's critical path (no effect on results)
+constexpr int kOptOverlap = 1 << 19;   // tiles bound to XCDs, launches overlap through per-tile completion counts
 constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull |
                             kOptBvh | kOptScatter2;
 constexpr uint32_t kStatsHeader = 24;        // kOptStats: 24 counters, then per-wave (start, end, iterations)
