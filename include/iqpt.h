@@ -182,6 +182,10 @@ int iqpt_sync(iqpt_ctx* ctx);
 #define IQPT_SPLIT_AUTO (-1)
 #define IQPT_SPLIT_OFF 0
 #define IQPT_SPLIT_ON 1
+/* CHAIN: the same set of pixels, each evaluated by a group of lanes at consecutive
+ * stream offsets and folded in sample order as the results arrive, in a kernel that runs beside the
+ * plain kernel over the other tiles (one launch pair, no stitch pass). AUTO picks it for small shares. */
+#define IQPT_SPLIT_CHAIN 2
 int iqpt_set_split(iqpt_ctx* ctx, int mode);
 
 /* Overlapped launches (no reference counterpart: the reference launches one frame at a

@@ -154,6 +154,9 @@ struct kparams {
     const uint32_t* xcd_order;
     uint32_t xcd_off[9];
     uint32_t* ovl_err;               // bit 0: a wait exceeded kOverlapSpinLimit (never expected)
+    // queue length of the plain kernel's tile queue (tile_order[0 .. nqueue)); 0: every tile (ntiles).
+    // Chain launches give the plain kernel the anchored tiles only.
+    uint32_t nqueue;
 };
 constexpr int kSphNodeFloat4 = 3;
 constexpr uint32_t kOverlapSpinLimit = 1u << 23;   // s_sleep(20) polls before a wait gives up (~seconds)
@@ -297,6 +300,13 @@ int render_occupancy(int max_depth, bool stream_batches, int opt, uint32_t lds_b
 int launch_split_prep(void* stream, const ksplit& s);
 int launch_split_stitch(void* stream, const ksplit& s, bool fastdiv);
 bool render_variant_exists(int max_depth, bool stream_batches, int opt);
+// Chain-parallel pixels (iqpt_chain_kernel): the split set's pixels, each evaluated by
+// kChainLanes lanes at consecutive even stream offsets and folded in sample order; reads p.sp_pix /
+// p.ns_cap and takes pixels from p.queue[1]. Resident scenes, reference materials, max_depth <= 16.
+bool chain_variant_exists(int max_depth, int opt);
+uint32_t chain_lds(const kparams& p);
+int chain_occupancy(int max_depth, int opt, uint32_t lds, int* blocks_per_cu);
+int launch_chain(void* stream, const kparams& p, uint32_t grid_blocks, int opt);
 constexpr int kRenderBlock = 256;
 constexpr uint32_t kQueueChunk = 64;
 const char* render_kernel_name();

@@ -1193,7 +1193,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // tile, 2 leftovers [chunk_next, chunk_end) of the leftover list, 3 the light pixels of a split tile
     // (anchored) — and the split tile's first slot and storage index
     uint32_t chunk_kind = 0, chunk_sp0 = 0, chunk_first = 0, chunk_r = 0;
-    uint32_t queue_total = kOverlap ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : p.ntiles, n_runs = 0;
+    uint32_t queue_total = kOverlap ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : (p.nqueue ? p.nqueue : p.ntiles), n_runs = 0;
     if (kSplit) {
         // round 1, longest tasks first: the split tiles' light pixels (anchored chains with scatters, in
         // the masks' cost order), then the heavy pixels' run chunks, then the anchored (wall / sky) tiles
@@ -2385,6 +2385,319 @@ __global__ __launch_bounds__(kStitchBlock) void iqpt_split_stitch_kernel(const k
     if (__lane_id() == 0 && rays) atomicAdd(s.rays, rays);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Chain-parallel pixels (iqpt_chain_kernel). A pixel's samples are one XORWOW stream
+// (path_tracer.cu:339): sample k starts where sample k-1's draws ended, 2 draws for the camera jitter
+// (camera.cu:24-25) plus 2 per Oren-Nayar scatter (material.cu:10). Everything a sample does from even
+// stream offset 2j depends on j alone, so kChainLanes lanes of a wave evaluate one pixel's samples at
+// consecutive "slots" j (lane i: slots i, i + kChainLanes, ...) speculatively, each from the state
+// 2j draws into the pixel's stream, and one lane per group (the walker) follows the chain
+// 0 -> j + n_j -> ... through a ring of results in LDS, applying the running mean in sample order.
+// The chain needs slot ptr next; a lane may start slot c only while c < ptr + kChainRing (the ring
+// entry it overwrites is behind the chain), so the lane holding slot ptr always gets to it and the
+// chain always advances. When the pixel's samples are complete, the state at the chain's end is the
+// start state of slot ptr (stored when the slot started, or stepped there by its lane). Same bits as
+// the anchored kernel: the same per-sample code, the same mean terms, the chain's own slots counted
+// as rays. The pixels come from the split set (tiles whose camera rays may scatter, under the
+// reference's materials); the other tiles run anchored in iqpt_render_kernel beside this kernel.
+constexpr uint32_t kChainLanes = 8;                    // lanes per pixel
+constexpr uint32_t kChainGroups = 64 / kChainLanes;    // pixels per wave
+constexpr uint32_t kChainRing = 2 * kChainLanes;       // slots in flight per pixel (multiple of kChainLanes)
+constexpr uint32_t kChainBlock = 64;                   // one wave per block
+constexpr uint32_t kChainIterLimit = 1u << 22;         // loop iterations before a wave gives up (error bit 2)
+
+__device__ __forceinline__ void xorwow_skip_v(uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& v3, uint32_t& v4,
+                                              uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t t = v0 ^ (v0 >> 2);
+        v0 = v1;
+        v1 = v2;
+        v2 = v3;
+        v3 = v4;
+        v4 = (v4 ^ (v4 << 4)) ^ (t ^ (t << 1));
+    }
+}
+
+template <int MAXD, int OPT>
+__global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
+    float4* lds_tri = lds;
+    float4* lds_sph = lds + (size_t)p.ntri_pairs * kTriPairFloat4;
+    float2* lds_tab = reinterpret_cast<float2*>(lds_sph + (size_t)p.nsph_pairs * kSphPairFloat4);
+    float* lds_tab_n = reinterpret_cast<float*>(lds_tab + ((p.spp + 1u) & ~1u));
+    uint4* lds_cm = reinterpret_cast<uint4*>(lds_tab_n + ((p.spp + 3u) & ~3u));
+    float4* ring_res = reinterpret_cast<float4*>(lds_cm + kChainBlock);        // [group][ring]
+    uint32_t* ring_tag = reinterpret_cast<uint32_t*>(ring_res + kChainGroups * kChainRing);
+    uint32_t* ring_st = ring_tag + kChainGroups * kChainRing;                     // 5 planes [group][ring]
+    // per group: 0 pixel (~0u none), 1 px, 2 py, 3 d0, 4 generation, 5 limit, 6 finishing, 7 ptr, 8 tile
+    uint32_t* grp = ring_st + 5 * kChainGroups * kChainRing;
+    float* lds_stk = reinterpret_cast<float*>(grp + 16 * kChainGroups);         // [depth][lane]
+
+    for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kChainBlock)
+        lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
+    for (uint32_t i = threadIdx.x; i < p.nsph_pairs * kSphPairFloat4; i += kChainBlock)
+        lds_sph[i] = reinterpret_cast<const float4*>(p.sph_pairs)[i];
+    for (uint32_t s = threadIdx.x; s < p.spp; s += kChainBlock) {
+        const uint64_t n = p.frame0 + s + 1;
+        lds_tab[s] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
+        lds_tab_n[s] = (float)n;
+    }
+    for (uint32_t i = threadIdx.x; i < kChainGroups * kChainRing; i += kChainBlock) ring_tag[i] = ~0u;
+    for (uint32_t i = threadIdx.x; i < 16 * kChainGroups; i += kChainBlock) grp[i] = (i % 16u) == 0u ? ~0u : 0u;
+    __syncthreads();
+    if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);     // the longest chains of the launch
+
+    const uint32_t lane = threadIdx.x;
+    const uint32_t g = lane / kChainLanes, li = lane % kChainLanes;
+    const bool walker = li == 0u;
+    uint32_t* const G = grp + 16 * g;
+    // walker registers: the pixel's chain
+    uint32_t w_pix = ~0u, w_ptr = 0u, w_k = 0u;
+    bool w_done = false, w_fin = false;
+    float ax = 0.0f, ay = 0.0f, az = 0.0f;
+    unsigned long long w_rays = 0;
+    // lane registers: the slot being traced (or the next one) and its start state (v0..v4; d follows)
+    bool active = false;
+    int depth = 0;
+    ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
+    uint32_t b0 = 0u, b1 = 0u, b2 = 0u, b3 = 0u, b4 = 0u, cslot = 0u, gen_seen = 0u;
+    uint32_t guard = 0u;               // iterations: a bound every wave reaches (never expected to bind)
+
+    while (true) {
+        if (++guard > kChainIterLimit) {
+            if (lane == 0 && p.ovl_err) atomicOr(p.ovl_err, 2u);
+            break;
+        }
+        // ---- A. walkers: finish a complete chain, take a pixel, follow the chain
+        if (walker) {
+            if (w_fin) {
+                // the state at the chain's end: slot ptr's start state (phase B made sure it is stored)
+                const uint32_t e = g * kChainRing + w_ptr % kChainRing;
+                const uint32_t pix = w_pix;
+                const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
+                const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
+                const uint32_t bb = to_u8(255.0f * iq_sqrtf(az));
+                p.bgra[pix] = bb | (g8 << 8) | (r8 << 16) | (255u << 24);
+                reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
+                p.rng[pix] = ring_st[e];
+                p.rng[(size_t)p.npix + pix] = ring_st[kChainGroups * kChainRing + e];
+                p.rng[2 * (size_t)p.npix + pix] = ring_st[2 * kChainGroups * kChainRing + e];
+                p.rng[3 * (size_t)p.npix + pix] = ring_st[3 * kChainGroups * kChainRing + e];
+                p.rng[4 * (size_t)p.npix + pix] = ring_st[4 * kChainGroups * kChainRing + e];
+                p.rng[5 * (size_t)p.npix + pix] = G[3] + 2u * w_ptr * IQ_XORWOW_WEYL;
+                w_pix = ~0u;
+                w_fin = false;
+                G[0] = ~0u;
+                G[6] = 0u;
+            }
+            if (w_pix == ~0u && !w_done) {
+                uint32_t pix = ~0u;
+                while (true) {
+                    const uint32_t q = atomicAdd(p.queue + 1, 1u);
+                    if (q >= p.ns_cap) {
+                        w_done = true;
+                        break;
+                    }
+                    pix = p.sp_pix[q];
+                    if (pix != ~0u) break;
+                }
+                if (!w_done) {
+                    w_pix = pix;
+                    w_ptr = 0u;
+                    w_k = 0u;
+                    const float* a = reinterpret_cast<const float*>(p.lin + pix);
+                    ax = a[0];
+                    ay = a[1];
+                    az = a[2];
+                    uint32_t col, row;
+                    tile_decode(pix, p.ncols, p.nrows, &col, &row);
+                    G[0] = pix;
+                    G[1] = p.x0 + col;
+                    G[2] = p.y0 + row * p.ystep;
+                    G[3] = p.rng[5 * (size_t)p.npix + pix];
+                    G[4] = G[4] + 1u;
+                    G[6] = 0u;
+                    G[7] = 0u;
+                    G[8] = (row / kCullTile) * p.ntx + col / kCullTile;
+                    for (uint32_t i = 0; i < kChainRing; ++i) ring_tag[g * kChainRing + i] = ~0u;
+                }
+            }
+            if (w_pix != ~0u) {
+                // fold the finished slots on the chain, in sample order (path_tracer.cu:356-358)
+                while (w_k < p.spp) {
+                    const uint32_t e = g * kChainRing + w_ptr % kChainRing;
+                    if (ring_tag[e] != w_ptr) break;
+                    const float4 r = ring_res[e];
+                    const uint32_t nsl = __float_as_uint(r.w);
+                    if (nsl == 0u) break;
+                    const float2 tv = lds_tab[w_k];
+                    float qx, qy, qz;
+                    mean_terms<OPT>(r.x, r.y, r.z, lds_tab_n[w_k], tv.x, p.mean_tiny, qx, qy, qz);
+                    ax = qx + ax * tv.y;
+                    ay = qy + ay * tv.y;
+                    az = qz + az * tv.y;
+                    w_rays += (nsl - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : nsl;
+                    w_ptr += nsl;
+                    ++w_k;
+                }
+                G[7] = w_ptr;
+                const uint32_t rem = p.spp - w_k;
+                const uint32_t ahead = min(kChainRing, max(kChainLanes, rem + rem / 2u + 1u));
+                G[5] = w_ptr + ahead;
+                if (w_k == p.spp) {
+                    G[6] = 1u;
+                    w_fin = true;
+                }
+            }
+        }
+        __syncthreads();
+        // ---- B. lanes: a new pixel, a chain's end, slot starts
+        const uint32_t gpix = G[0];
+        const uint32_t gen = G[4];
+        if (gpix != ~0u && gen != gen_seen) {
+            gen_seen = gen;
+            active = false;
+            cslot = li;
+            b0 = p.rng[gpix];
+            b1 = p.rng[(size_t)p.npix + gpix];
+            b2 = p.rng[2 * (size_t)p.npix + gpix];
+            b3 = p.rng[3 * (size_t)p.npix + gpix];
+            b4 = p.rng[4 * (size_t)p.npix + gpix];
+            xorwow_skip_v(b0, b1, b2, b3, b4, 2u * li);
+            if (kCull && p.cull) {
+                const uint32_t t = G[8];
+                lds_cm[lane] = make_uint4(p.cull[(size_t)t * p.cull_stride], p.cull[(size_t)t * p.cull_stride + p.cull_wt],
+                                          t, 0u);
+            }
+        }
+        if (gpix != ~0u && G[6] != 0u) {
+            // the chain is complete: drop the speculative slots; the lane of slot ptr provides its state
+            active = false;
+            const uint32_t ptr = G[7];
+            const uint32_t e = g * kChainRing + ptr % kChainRing;
+            if (li == ptr % kChainLanes && ring_tag[e] != ptr) {
+                // not started: cslot <= ptr (slots start in order), so step forward
+                xorwow_skip_v(b0, b1, b2, b3, b4, 2u * (ptr - cslot));
+                cslot = ptr;
+                ring_st[e] = b0;
+                ring_st[kChainGroups * kChainRing + e] = b1;
+                ring_st[2 * kChainGroups * kChainRing + e] = b2;
+                ring_st[3 * kChainGroups * kChainRing + e] = b3;
+                ring_st[4 * kChainGroups * kChainRing + e] = b4;
+                ring_tag[e] = ptr;
+            }
+        } else if (gpix != ~0u && !active && cslot < G[5]) {
+            // start slot cslot: the state 2 cslot draws into the pixel's stream
+            const uint32_t e = g * kChainRing + cslot % kChainRing;
+            ring_st[e] = b0;
+            ring_st[kChainGroups * kChainRing + e] = b1;
+            ring_st[2 * kChainGroups * kChainRing + e] = b2;
+            ring_st[3 * kChainGroups * kChainRing + e] = b3;
+            ring_st[4 * kChainGroups * kChainRing + e] = b4;
+            ring_tag[e] = cslot;
+            ring_res[e].w = 0.0f;
+            st = {b0, b1, b2, b3, b4, G[3] + 2u * cslot * IQ_XORWOW_WEYL};
+            camera_ray<OPT>(p, G[1], G[2], st, ray);
+            depth = 0;
+            active = true;
+        }
+        const bool more = walker && !w_done;
+        if (!__any(active) && !__any(more) && !__any(w_fin)) break;
+        __syncthreads();
+        if (!__any(active)) continue;
+
+        // ---- C. one bounce of every traced slot (the anchored kernel's closest hit and shading)
+        float closest = kTMax;
+        int kind = kHitNone;
+        uint32_t hidx = 0;
+        if (kCull && p.cull != nullptr) {
+            const bool cull = !__any(active && depth != 0);
+            const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[lane].z * p.cull_stride : nullptr;
+            uint4 cm = lds_cm[lane];
+            const uint64_t act = __ballot(active);
+            const uint32_t first = (uint32_t)__builtin_ctzll(act);
+            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
+            const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
+            if (uni) {
+                cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
+                cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
+            }
+            const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
+            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray, closest,
+                                  kind, hidx, p.cull_wt, uni_mask);
+        } else if (active) {
+            intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
+        }
+        if (active) {
+            bool term = false;
+            uint32_t md_end = 0;
+            float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
+            if (kind == kHitSphere) {
+                const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
+                const float4 sphr = make_float4(q[0], q[2], q[4], q[6]);
+                const float s = oren_nayar_scatter<OPT>(sphr, closest, ray, st);
+                if (depth + 1 >= p.max_depth) {
+                    term = true;
+                    md_end = 1;
+                    Lx = s;
+                    Ly = s;
+                    Lz = s;
+                } else {
+                    lds_stk[(uint32_t)depth * kChainBlock + lane] = s;
+                    ++depth;
+                }
+            } else if (kind == kHitTri) {
+                term = true;
+                Lx = 10.0f;
+                Ly = 10.0f;
+                Lz = 10.0f;
+            } else {
+                term = true;
+                const float a = (ray.dy + 1.0f) * 0.5f;
+                const float one_a = 1.0f - a;
+                Lx = one_a + a * 0.5f;
+                Ly = one_a + a * 0.7f;
+                Lz = one_a + a * 1.0f;
+            }
+            if (term) {
+                float cx = Lx, cy = Ly, cz = Lz;
+                for (int i = depth - 1; i >= 0; --i) {
+                    const float r = lds_stk[(uint32_t)i * kChainBlock + lane];
+                    cx = cx * r;
+                    cy = cy * r;
+                    cz = cz * r;
+                }
+                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                cx = 0.0f + cx;
+                cy = 0.0f + cy;
+                cz = 0.0f + cz;
+                // slots consumed: 1 + the scatters (two draws each)
+                const uint32_t nsl = (uint32_t)depth + 1u + md_end;
+                ring_res[g * kChainRing + cslot % kChainRing] = make_float4(cx, cy, cz, __uint_as_float(nsl));
+                xorwow_skip_v(b0, b1, b2, b3, b4, 2u * kChainLanes);
+                cslot += kChainLanes;
+                active = false;
+            }
+        }
+        __syncthreads();
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) w_rays += __shfl_xor(w_rays, off);
+    if (lane == 0 && w_rays) atomicAdd(p.rays, w_rays);
+}
+
+// LDS bytes of the chain kernel for a launch (scene pairs, mean table, mask slots, ring, group words,
+// scatter stack)
+__host__ __device__ inline uint32_t chain_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, uint32_t spp, int max_depth) {
+    return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + ((spp + 1u) & ~1u) * 8u +
+           ((spp + 3u) & ~3u) * 4u + kChainBlock * 16u + kChainGroups * kChainRing * (16u + 4u + 20u) +
+           16u * kChainGroups * 4u + (uint32_t)(max_depth > 1 ? max_depth : 1) * kChainBlock * 4u;
+}
+
 template <int MAXD, bool STREAM, int OPT>
 int launch_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
     hipLaunchKernelGGL((iqpt_render_kernel<MAXD, STREAM, OPT>), dim3(grid), dim3(kRenderBlock), lds, stream, p);
@@ -2574,6 +2887,54 @@ int launch_split_stitch(void* stream, const ksplit& s, bool fastdiv) {
         hipLaunchKernelGGL(iqpt_split_stitch_kernel<(kOptDefault & ~kOptFastDiv)>, grid, dim3(kStitchBlock), 0,
                            (hipStream_t)stream, s);
     return (int)hipGetLastError();
+}
+
+
+// kOptChain launches (iqpt_chain_kernel): the resident production option sets, reference materials
+namespace {
+template <int MAXD, int OPT>
+int chain_launch_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
+    hipLaunchKernelGGL((iqpt_chain_kernel<MAXD, OPT>), dim3(grid), dim3(kChainBlock), lds, stream, p);
+    return (int)hipGetLastError();
+}
+template <int MAXD, int OPT>
+int chain_occ_t(uint32_t lds, int* blocks) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_chain_kernel<MAXD, OPT>, kChainBlock, lds);
+}
+struct chain_variant {
+    int maxd, opt;
+    int (*launch)(hipStream_t, const kparams&, uint32_t, uint32_t);
+    int (*occ)(uint32_t, int*);
+};
+#define IQPT_CV(M, O) {M, O, chain_launch_t<M, O>, chain_occ_t<M, O>}
+const chain_variant kChainVariants[] = {
+    IQPT_CV(8, kOptDefault | kOptPrio), IQPT_CV(16, kOptDefault | kOptPrio),
+    IQPT_CV(8, (kOptDefault & ~kOptFastDiv) | kOptPrio), IQPT_CV(16, (kOptDefault & ~kOptFastDiv) | kOptPrio),
+};
+#undef IQPT_CV
+const chain_variant* find_chain(int max_depth, int opt) {
+    const int maxd = max_depth <= 8 ? 8 : 16;
+    for (const chain_variant& v : kChainVariants)
+        if (v.maxd == maxd && v.opt == (opt | kOptPrio)) return &v;
+    return nullptr;
+}
+}  // namespace
+
+bool chain_variant_exists(int max_depth, int opt) { return max_depth <= 16 && find_chain(max_depth, opt) != nullptr; }
+
+uint32_t chain_lds(const kparams& p) { return chain_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.spp, p.max_depth); }
+
+int chain_occupancy(int max_depth, int opt, uint32_t lds, int* blocks) {
+    const chain_variant* v = find_chain(max_depth, opt);
+    if (!v) return (int)hipErrorInvalidDeviceFunction;
+    return v->occ(lds, blocks);
+}
+
+int launch_chain(void* stream, const kparams& p, uint32_t grid, int opt) {
+    const chain_variant* v = find_chain(p.max_depth, opt);
+    if (!v || p.max_depth > 16 || p.spp > kAccTableMax) return (int)hipErrorInvalidDeviceFunction;
+    if (grid == 0) return 0;
+    return v->launch((hipStream_t)stream, p, grid, chain_lds(p));
 }
 
 }  // namespace iqpt

@@ -36,6 +36,11 @@ constexpr uint32_t kSphBatch = 256;
 constexpr int kTuneLaunches = 4;     // timed launches before the camera-ray path is chosen (A, B, A, B)
 // kOptSplit auto mode: split when the owned pixels are fewer than this many per resident lane
 constexpr double kSplitAutoPixelsPerLane = 1.2;
+// chain launches: AUTO takes them below this many owned pixels per resident lane of the
+// plain kernel; chain-kernel waves per CU by default
+constexpr double kChainAutoPixelsPerLane = 4.0;
+constexpr uint32_t kChainWavesPerCu = 8;
+constexpr uint64_t kChainPixelsPerWave = 8;   // iqpt_chain_kernel: pixels in flight per wave (kChainGroups)
 constexpr size_t kSplitResBudget = size_t(8) << 30;   // speculative results (bytes)
 
 std::once_flag g_tables_once;
@@ -152,7 +157,10 @@ struct iqpt_ctx {
     uint8_t* d_nres = nullptr;          // ns_cap x m_cap
     uint32_t split_refill_min = 16;     // idle lanes before a refill in split launches
     uint32_t split_heavy_rho = iqpt::kSplitHeavyRho;
-    bool split_all_tiles = false;       // every tile in the split set (wall tiles: one slot per sample)   // 320 measured best at N = 8 (r02_split_share_v8)
+    bool split_all_tiles = false;       // every tile in the split set (wall tiles: one slot per sample)
+    // chain launches: chain-kernel waves per CU (0: kChainWavesPerCu); the last launch's mode
+    uint32_t chain_waves = 0;
+    bool chain_last = false;
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
     double tune_work[4] = {0.0, 0.0, 0.0, 0.0};
     // kOptOverlap: consecutive render launches alternate between `stream` and
@@ -1180,16 +1188,28 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // kOptSplit: resident scenes with a split set, when the mode asks for it (auto:
     // fewer owned pixels than kSplitAutoPixelsPerLane per resident lane, i.e. too few pixel chains to
     // fill and drain the chip evenly)
+    // chain launches: the split set's pixels in iqpt_chain_kernel, the other tiles in the
+    // plain kernel beside it (resident scenes, reference materials)
+    bool chain = false;
+    if ((c->split_mode == IQPT_SPLIT_CHAIN || c->split_mode == IQPT_SPLIT_AUTO) && !stream_batches && p.cull &&
+        c->n_split_tiles > 0 && tune_slot < 0 && !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax &&
+        iqpt::chain_variant_exists(c->max_depth, opt)) {
+        int occ_p = 0;
+        if (iqpt::render_occupancy(c->max_depth, false, opt, lds, &occ_p) != 0) occ_p = 0;
+        const double lanes = (double)c->num_cus * std::max(occ_p, 1) * iqpt::kRenderBlock;
+        chain = c->split_mode == IQPT_SPLIT_CHAIN || (double)c->npix < iqpt::kChainAutoPixelsPerLane * lanes;
+    }
     uint32_t lds_split = lds + iqpt::kRenderBlock * (16u + 24u);   // + lds_sp and the base states
     bool split = false;
-    if (c->split_mode != IQPT_SPLIT_OFF && !stream_batches && p.cull && c->n_split_tiles > 0 &&
+    if (!chain && c->split_mode != IQPT_SPLIT_OFF && c->split_mode != IQPT_SPLIT_CHAIN && !stream_batches && p.cull &&
+        c->n_split_tiles > 0 &&
         tune_slot < 0 && iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptSplit)) {
         int occ_s = 0;
         if (iqpt::render_occupancy(c->max_depth, false, opt | iqpt::kOptSplit, lds_split, &occ_s) != 0) occ_s = 0;
         const double lanes = (double)c->num_cus * std::max(occ_s, 1) * iqpt::kRenderBlock;
         split = occ_s > 0 && (c->split_mode == IQPT_SPLIT_ON || (double)c->npix < iqpt::kSplitAutoPixelsPerLane * lanes);
     }
-    if (split && (st = join_streams(c)) != IQPT_OK) return st;   // split launches never overlap
+    if ((split || chain) && (st = join_streams(c)) != IQPT_OK) return st;   // split / chain launches never overlap
     const size_t ns_cap = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
     const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
     const uint32_t g_max = (m_cap + iqpt::kSplitRunLen - 1) / iqpt::kSplitRunLen;
@@ -1278,7 +1298,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
     }
     // kOptOverlap: resident, culled, not split, not a tuning launch
-    bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && p.cull != nullptr &&
+    bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && !chain && p.cull != nullptr &&
                tune_slot < 0 && c->d_tile_done && c->d_xcd_order &&
                iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptOverlap);
     int occ = 0;
@@ -1288,11 +1308,12 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // two launches in flight: each keeps one block slot per CU free for the other (occ - 1 per CU), so the
     // earlier launch, which the later one waits for, can always run
     if (ovl && occ < 2) ovl = false;
-    if (ovl && !c->stream2) {
+    if ((ovl || chain) && !c->stream2) {
         if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_s2, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
+            if (chain) return iqpt::fail(IQPT_ERR_HIP, "second stream for the chain kernel");
             ovl = false;
             c->overlap_mode = IQPT_OVERLAP_OFF;
         }
@@ -1337,6 +1358,31 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->ovl_epoch += 1;
         c->next_on_main = !c->next_on_main;
         if (le != 0) c->ovl_zero = true;     // a failed launch breaks the chain's counts: restart it
+    } else if (chain) {
+        // the split set's pixels on stream2 (iqpt_chain_kernel, pixels from queue[1]) beside the plain kernel
+        // over the anchored tiles on stream (queue[0]); stream waits for stream2 before the end event
+        const size_t ns = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
+        p.sp_pix = c->d_split + c->n_anchor + c->n_split_tiles;
+        p.ns_cap = (uint32_t)ns;
+        const uint32_t lds_c = iqpt::chain_lds(p);
+        int occ_c = 0;
+        if (iqpt::chain_occupancy(c->max_depth, opt, lds_c, &occ_c) != 0 || occ_c < 1) occ_c = 1;
+        const uint32_t per_cu = std::min<uint32_t>((uint32_t)occ_c, c->chain_waves ? c->chain_waves : iqpt::kChainWavesPerCu);
+        const uint64_t want_c = (ns + iqpt::kChainPixelsPerWave - 1) / iqpt::kChainPixelsPerWave;
+        const uint32_t grid_c = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_c, (uint64_t)c->num_cus * per_cu));
+        p.ovl_err = c->d_ovl_err;
+        IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
+        IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
+        le = iqpt::launch_chain(c->stream2, p, grid_c, opt);
+        if (le == 0 && c->n_anchor > 0) {
+            p.tile_order = c->d_split;
+            p.nqueue = c->n_anchor;
+            const uint64_t want_p = ((uint64_t)c->n_anchor * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
+            const uint32_t grid_p = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_p, (uint64_t)c->num_cus * occ));
+            le = iqpt::launch_render(c->stream, p, grid_p, lds, stream_batches, opt);
+        }
+        IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
+        IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
     } else if (split) {
         // prep -> round 1 (runs, anchored tiles, light split pixels) -> stitch -> round 2 (leftovers)
         le = iqpt::launch_split_prep(c->stream, ks);
@@ -1351,6 +1397,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
     }
     c->split_last = split;
+    c->chain_last = chain;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1) (void)hipEventRecord(e1, ls);
     if (e0 && e1) c->timed.emplace_back(e0, e1);
@@ -1375,7 +1422,8 @@ int iqpt_sync(iqpt_ctx* c) {
     IQPT_HIP(hipMemcpy(&err, c->d_ovl_err, sizeof err, hipMemcpyDeviceToHost));
     if (err) {
         IQPT_HIP(hipMemset(c->d_ovl_err, 0, sizeof err));
-        return iqpt::fail(IQPT_ERR_HIP, "overlapped launch: a per-tile wait timed out (results invalid)");
+        return iqpt::fail(IQPT_ERR_HIP, (err & 2u) ? "chain launch: a wave exceeded its iteration bound (results invalid)"
+                                                   : "overlapped launch: a per-tile wait timed out (results invalid)");
     }
     return IQPT_OK;
 }
@@ -1640,7 +1688,7 @@ int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
     out8[1] = c->n_anchor;
     const size_t ns = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
     out8[2] = ns;
-    out8[7] = c->split_last ? 1 : 0;
+    out8[7] = c->split_last ? 1 : (c->chain_last ? 2 : 0);
     if (!c->d_split || ns == 0) return IQPT_OK;
     uint32_t left = 0;
     IQPT_HIP(hipMemcpy(&left, c->d_queue + 2, sizeof left, hipMemcpyDeviceToHost));
@@ -1674,6 +1722,13 @@ int iqpt_debug_set_split_knobs(iqpt_ctx* c, uint32_t heavy_rho, uint32_t refill_
     return IQPT_OK;
 }
 
+// Chain launches (tools/split_share.py): chain-kernel waves per CU (0: the default). Results do not depend on it.
+int iqpt_debug_set_chain_waves(iqpt_ctx* c, uint32_t waves_per_cu) {
+    if (!c || waves_per_cu > 64) return iqpt::fail(IQPT_ERR_INVALID_ARG, "waves_per_cu 0..64");
+    c->chain_waves = waves_per_cu;
+    return IQPT_OK;
+}
+
 int iqpt_kernel_span(const iqpt_ctx* c, double* span_ms) {
     if (!c || !span_ms) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     *span_ms = c->last_span_ms;
@@ -1690,8 +1745,8 @@ int iqpt_set_overlap(iqpt_ctx* c, int mode) {
 }
 int iqpt_set_split(iqpt_ctx* c, int mode) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    if (mode != IQPT_SPLIT_AUTO && mode != IQPT_SPLIT_OFF && mode != IQPT_SPLIT_ON)
-        return iqpt::fail(IQPT_ERR_INVALID_ARG, "split mode must be IQPT_SPLIT_AUTO, _OFF or _ON");
+    if (mode != IQPT_SPLIT_AUTO && mode != IQPT_SPLIT_OFF && mode != IQPT_SPLIT_ON && mode != IQPT_SPLIT_CHAIN)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "split mode must be IQPT_SPLIT_AUTO, _OFF, _ON or _CHAIN");
     c->split_mode = mode;
     return IQPT_OK;
 }

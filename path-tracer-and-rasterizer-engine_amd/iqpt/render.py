@@ -98,7 +98,7 @@ class PathTracer:
         check(self._lib.iqpt_copy_frame_device(self._h, C.c_void_p(dst_ptr), nbytes), "iqpt_copy_frame_device")
 
     def set_split(self, mode: int):
-        """Sample-parallel chains: _lib.SPLIT_AUTO (default), SPLIT_OFF or SPLIT_ON (iqpt_set_split)."""
+        """Sample-parallel chains: _lib.SPLIT_AUTO (default), SPLIT_OFF, SPLIT_ON or SPLIT_CHAIN (iqpt_set_split)."""
         check(self._lib.iqpt_set_split(self._h, mode), "iqpt_set_split")
 
     def set_overlap(self, mode: int):

@@ -27,7 +27,7 @@ from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
 OPT = 0
 
 
-def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None) -> dict:
+def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain_waves: int = 0) -> dict:
     cfg = CONFIGS["c2"]
     sc = Scene()
     sc.add_preset(cfg.preset)
@@ -46,6 +46,11 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None) -> di
         lb = _lib.load()
         lb.iqpt_debug_set_split_knobs.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_split_knobs(pt._h, knobs[0], knobs[1]), "iqpt_debug_set_split_knobs")
+    if chain_waves:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_chain_waves.argtypes = [C.c_void_p, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_chain_waves(pt._h, chain_waves), "iqpt_debug_set_chain_waves")
     pt.set_camera(cam)
     pt.upload_packet(pk)
     pt.prepare()
@@ -141,7 +146,8 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--out", default="")
-    ap.add_argument("--modes", default="plain,split")
+    ap.add_argument("--modes", default="plain,split", help="plain, split, chain (IQPT_SPLIT_CHAIN)")
+    ap.add_argument("--chain-waves", default="", help="extra chain rows at these chain-kernel waves per CU")
     ap.add_argument("--knobs", default="", help="split knob sets heavy_rho:refill_min[,...] (extra split rows)")
     ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (A/B library)")
     ap.add_argument("--opt", type=int, default=0, help="kernel option set (A/B library; 0 = production)")
@@ -166,15 +172,25 @@ def main():
     for n in [int(x) for x in args.ns.split(",")]:
         row = {"n": n}
         res = {}
-        modes = [m for m in (("plain", _lib.SPLIT_OFF), ("split", _lib.SPLIT_ON)) if m[0] in args.modes.split(",")]
-        for name, mode in modes:
-            r = run(n, mode, args.launches, args.warm, args.spp)
+        modes = [m for m in (("plain", _lib.SPLIT_OFF, 0), ("split", _lib.SPLIT_ON, 0),
+                             ("chain", _lib.SPLIT_CHAIN, 0)) if m[0] in args.modes.split(",")]
+        modes += [(f"chain_w{w}", _lib.SPLIT_CHAIN, int(w)) for w in args.chain_waves.split(",") if w]
+        for name, mode, cw in modes:
+            r = run(n, mode, args.launches, args.warm, args.spp, chain_waves=cw)
             res[name] = r
             row[name + "_ms_median"] = float(np.median(r["ms"]))
             row[name + "_ms_min"] = float(np.min(r["ms"]))
             row[name + "_mrays_per_s"] = r["rays"] / (sum(r["ms"]) * 1e-3) / 1e6
             if name == "split":
                 row["split_info"] = r["info"]
+            if name.startswith("chain"):
+                row[name + "_ran"] = r["info"]["ran_split"] == 2
+            if name != "plain" and "plain" in res:
+                a = res["plain"]
+                row[name + "_identical"] = bool(
+                    np.array_equal(a["lin"].view(np.uint32), r["lin"].view(np.uint32)) and
+                    np.array_equal(a["bgra"], r["bgra"]) and np.array_equal(a["rng"], r["rng"]) and
+                    a["rays"] == r["rays"])
         for kn in [k for k in args.knobs.split(",") if k]:
             rl, rm = (int(x) for x in kn.split(":"))
             r = run(n, _lib.SPLIT_ON, args.launches, args.warm, args.spp, (rl, rm))
@@ -184,7 +200,7 @@ def main():
                 row[f"split_h{rl}_m{rm}_identical"] = bool(
                     np.array_equal(a["lin"].view(np.uint32), r["lin"].view(np.uint32)) and
                     np.array_equal(a["rng"], r["rng"]) and a["rays"] == r["rays"])
-        if len(res) == 2:
+        if "plain" in res and "split" in res:
             a, b = res["plain"], res["split"]
             row["identical"] = bool(np.array_equal(a["lin"].view(np.uint32), b["lin"].view(np.uint32)) and
                                     np.array_equal(a["bgra"], b["bgra"]) and np.array_equal(a["rng"], b["rng"]) and
