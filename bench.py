@@ -359,6 +359,7 @@ def main():
     # overlapped launches run two at a time: the event span of the timed launches / their
     # number is the kernel time per launch that the throughput sees; each launch's own duration is longer
     kern_span_ms = pt.kernel_span()
+    launch_mode = pt.launch_mode()
 
     # after timing: the float frame on rank 0 (strong: the gathered accumulators de-interleaved, bit-
     # identical to one GPU's frame; weak: the N independent estimates averaged)
@@ -421,7 +422,7 @@ def main():
                                       ("none in the timed region; one reduce of the accumulators after it"
                                        if weak else f"gather of the {gathered} to rank 0 every step")
                                       + (" (rccl)" if on_gpu else " (gloo via host, rehearsal)")),
-                       "split": args.split, "overlap": args.overlap},
+                       "split": args.split, "overlap": args.overlap, "launch_mode": launch_mode},
             "n_ranks_seen": n_ranks_seen,
             "msamples_per_s": round(samples / elapsed / 1e6, 3),
             "rays_per_sample": round(total_rays / samples, 5),

@@ -2389,20 +2389,17 @@ __global__ __launch_bounds__(kStitchBlock) void iqpt_split_stitch_kernel(const k
 // Chain-parallel pixels (iqpt_chain_kernel). A pixel's samples are one XORWOW stream
 // (path_tracer.cu:339): sample k starts where sample k-1's draws ended, 2 draws for the camera jitter
 // (camera.cu:24-25) plus 2 per Oren-Nayar scatter (material.cu:10). Everything a sample does from even
-// stream offset 2j depends on j alone, so kChainLanes lanes of a wave evaluate one pixel's samples at
-// consecutive "slots" j (lane i: slots i, i + kChainLanes, ...) speculatively, each from the state
+// stream offset 2j depends on j alone, so LANES (4 or 8) lanes of a wave evaluate one pixel's samples at
+// consecutive "slots" j (lane i: slots i, i + LANES, ...) speculatively, each from the state
 // 2j draws into the pixel's stream, and one lane per group (the walker) follows the chain
 // 0 -> j + n_j -> ... through a ring of results in LDS, applying the running mean in sample order.
-// The chain needs slot ptr next; a lane may start slot c only while c < ptr + kChainRing (the ring
+// The chain needs slot ptr next; a lane may start slot c only while c < ptr + 2 LANES (the ring
 // entry it overwrites is behind the chain), so the lane holding slot ptr always gets to it and the
 // chain always advances. When the pixel's samples are complete, the state at the chain's end is the
 // start state of slot ptr (stored when the slot started, or stepped there by its lane). Same bits as
 // the anchored kernel: the same per-sample code, the same mean terms, the chain's own slots counted
 // as rays. The pixels come from the split set (tiles whose camera rays may scatter, under the
 // reference's materials); the other tiles run anchored in iqpt_render_kernel beside this kernel.
-constexpr uint32_t kChainLanes = 8;                    // lanes per pixel
-constexpr uint32_t kChainGroups = 64 / kChainLanes;    // pixels per wave
-constexpr uint32_t kChainRing = 2 * kChainLanes;       // slots in flight per pixel (multiple of kChainLanes)
 constexpr uint32_t kChainBlock = 64;                   // one wave per block
 constexpr uint32_t kChainIterLimit = 1u << 22;         // loop iterations before a wave gives up (error bit 2)
 
@@ -2418,8 +2415,11 @@ __device__ __forceinline__ void xorwow_skip_v(uint32_t& v0, uint32_t& v1, uint32
     }
 }
 
-template <int MAXD, int OPT>
+template <int MAXD, int OPT, int LANES>
 __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparams p) {
+    constexpr uint32_t kL = LANES;              // lanes per pixel
+    constexpr uint32_t kG = 64 / kL;            // pixels per wave
+    constexpr uint32_t kR = 2 * kL;             // slots in flight per pixel (ring entries, a multiple of kL)
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
     float4* lds_tri = lds;
@@ -2428,11 +2428,11 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
     float* lds_tab_n = reinterpret_cast<float*>(lds_tab + ((p.spp + 1u) & ~1u));
     uint4* lds_cm = reinterpret_cast<uint4*>(lds_tab_n + ((p.spp + 3u) & ~3u));
     float4* ring_res = reinterpret_cast<float4*>(lds_cm + kChainBlock);        // [group][ring]
-    uint32_t* ring_tag = reinterpret_cast<uint32_t*>(ring_res + kChainGroups * kChainRing);
-    uint32_t* ring_st = ring_tag + kChainGroups * kChainRing;                     // 5 planes [group][ring]
+    uint32_t* ring_tag = reinterpret_cast<uint32_t*>(ring_res + kG * kR);
+    uint32_t* ring_st = ring_tag + kG * kR;                     // 5 planes [group][ring]
     // per group: 0 pixel (~0u none), 1 px, 2 py, 3 d0, 4 generation, 5 limit, 6 finishing, 7 ptr, 8 tile
-    uint32_t* grp = ring_st + 5 * kChainGroups * kChainRing;
-    float* lds_stk = reinterpret_cast<float*>(grp + 16 * kChainGroups);         // [depth][lane]
+    uint32_t* grp = ring_st + 5 * kG * kR;
+    float* lds_stk = reinterpret_cast<float*>(grp + 16 * kG);         // [depth][lane]
 
     for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kChainBlock)
         lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
@@ -2443,13 +2443,13 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
         lds_tab[s] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
         lds_tab_n[s] = (float)n;
     }
-    for (uint32_t i = threadIdx.x; i < kChainGroups * kChainRing; i += kChainBlock) ring_tag[i] = ~0u;
-    for (uint32_t i = threadIdx.x; i < 16 * kChainGroups; i += kChainBlock) grp[i] = (i % 16u) == 0u ? ~0u : 0u;
+    for (uint32_t i = threadIdx.x; i < kG * kR; i += kChainBlock) ring_tag[i] = ~0u;
+    for (uint32_t i = threadIdx.x; i < 16 * kG; i += kChainBlock) grp[i] = (i % 16u) == 0u ? ~0u : 0u;
     __syncthreads();
     if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);     // the longest chains of the launch
 
     const uint32_t lane = threadIdx.x;
-    const uint32_t g = lane / kChainLanes, li = lane % kChainLanes;
+    const uint32_t g = lane / kL, li = lane % kL;
     const bool walker = li == 0u;
     uint32_t* const G = grp + 16 * g;
     // walker registers: the pixel's chain
@@ -2464,6 +2464,13 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
     rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
     uint32_t b0 = 0u, b1 = 0u, b2 = 0u, b3 = 0u, b4 = 0u, cslot = 0u, gen_seen = 0u;
     uint32_t guard = 0u;               // iterations: a bound every wave reaches (never expected to bind)
+#if defined(IQPT_AB_VARIANTS)
+    // timing ablations (A/B library only, NOT exact): 64 fold without the mean, 128 no stream stepping,
+    // 256 no workgroup barriers, 512 no closest hit (every ray misses)
+    const uint32_t dg = p.diag;
+#else
+    constexpr uint32_t dg = 0u;
+#endif
 
     while (true) {
         if (++guard > kChainIterLimit) {
@@ -2474,7 +2481,7 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
         if (walker) {
             if (w_fin) {
                 // the state at the chain's end: slot ptr's start state (phase B made sure it is stored)
-                const uint32_t e = g * kChainRing + w_ptr % kChainRing;
+                const uint32_t e = g * kR + w_ptr % kR;
                 const uint32_t pix = w_pix;
                 const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
                 const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
@@ -2482,10 +2489,10 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
                 p.bgra[pix] = bb | (g8 << 8) | (r8 << 16) | (255u << 24);
                 reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
                 p.rng[pix] = ring_st[e];
-                p.rng[(size_t)p.npix + pix] = ring_st[kChainGroups * kChainRing + e];
-                p.rng[2 * (size_t)p.npix + pix] = ring_st[2 * kChainGroups * kChainRing + e];
-                p.rng[3 * (size_t)p.npix + pix] = ring_st[3 * kChainGroups * kChainRing + e];
-                p.rng[4 * (size_t)p.npix + pix] = ring_st[4 * kChainGroups * kChainRing + e];
+                p.rng[(size_t)p.npix + pix] = ring_st[kG * kR + e];
+                p.rng[2 * (size_t)p.npix + pix] = ring_st[2 * kG * kR + e];
+                p.rng[3 * (size_t)p.npix + pix] = ring_st[3 * kG * kR + e];
+                p.rng[4 * (size_t)p.npix + pix] = ring_st[4 * kG * kR + e];
                 p.rng[5 * (size_t)p.npix + pix] = G[3] + 2u * w_ptr * IQ_XORWOW_WEYL;
                 w_pix = ~0u;
                 w_fin = false;
@@ -2521,30 +2528,32 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
                     G[6] = 0u;
                     G[7] = 0u;
                     G[8] = (row / kCullTile) * p.ntx + col / kCullTile;
-                    for (uint32_t i = 0; i < kChainRing; ++i) ring_tag[g * kChainRing + i] = ~0u;
+                    for (uint32_t i = 0; i < kR; ++i) ring_tag[g * kR + i] = ~0u;
                 }
             }
             if (w_pix != ~0u) {
                 // fold the finished slots on the chain, in sample order (path_tracer.cu:356-358)
                 while (w_k < p.spp) {
-                    const uint32_t e = g * kChainRing + w_ptr % kChainRing;
+                    const uint32_t e = g * kR + w_ptr % kR;
                     if (ring_tag[e] != w_ptr) break;
                     const float4 r = ring_res[e];
                     const uint32_t nsl = __float_as_uint(r.w);
                     if (nsl == 0u) break;
                     const float2 tv = lds_tab[w_k];
-                    float qx, qy, qz;
-                    mean_terms<OPT>(r.x, r.y, r.z, lds_tab_n[w_k], tv.x, p.mean_tiny, qx, qy, qz);
-                    ax = qx + ax * tv.y;
-                    ay = qy + ay * tv.y;
-                    az = qz + az * tv.y;
+                    if (!(dg & 64u)) {
+                        float qx, qy, qz;
+                        mean_terms<OPT>(r.x, r.y, r.z, lds_tab_n[w_k], tv.x, p.mean_tiny, qx, qy, qz);
+                        ax = qx + ax * tv.y;
+                        ay = qy + ay * tv.y;
+                        az = qz + az * tv.y;
+                    }
                     w_rays += (nsl - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : nsl;
                     w_ptr += nsl;
                     ++w_k;
                 }
                 G[7] = w_ptr;
                 const uint32_t rem = p.spp - w_k;
-                const uint32_t ahead = min(kChainRing, max(kChainLanes, rem + rem / 2u + 1u));
+                const uint32_t ahead = min(kR, max(kL, rem + rem / 2u + 1u));
                 G[5] = w_ptr + ahead;
                 if (w_k == p.spp) {
                     G[6] = 1u;
@@ -2552,7 +2561,7 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
                 }
             }
         }
-        __syncthreads();
+        if (!(dg & 256u)) __syncthreads();
         // ---- B. lanes: a new pixel, a chain's end, slot starts
         const uint32_t gpix = G[0];
         const uint32_t gen = G[4];
@@ -2576,26 +2585,26 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
             // the chain is complete: drop the speculative slots; the lane of slot ptr provides its state
             active = false;
             const uint32_t ptr = G[7];
-            const uint32_t e = g * kChainRing + ptr % kChainRing;
-            if (li == ptr % kChainLanes && ring_tag[e] != ptr) {
+            const uint32_t e = g * kR + ptr % kR;
+            if (li == ptr % kL && ring_tag[e] != ptr) {
                 // not started: cslot <= ptr (slots start in order), so step forward
                 xorwow_skip_v(b0, b1, b2, b3, b4, 2u * (ptr - cslot));
                 cslot = ptr;
                 ring_st[e] = b0;
-                ring_st[kChainGroups * kChainRing + e] = b1;
-                ring_st[2 * kChainGroups * kChainRing + e] = b2;
-                ring_st[3 * kChainGroups * kChainRing + e] = b3;
-                ring_st[4 * kChainGroups * kChainRing + e] = b4;
+                ring_st[kG * kR + e] = b1;
+                ring_st[2 * kG * kR + e] = b2;
+                ring_st[3 * kG * kR + e] = b3;
+                ring_st[4 * kG * kR + e] = b4;
                 ring_tag[e] = ptr;
             }
         } else if (gpix != ~0u && !active && cslot < G[5]) {
             // start slot cslot: the state 2 cslot draws into the pixel's stream
-            const uint32_t e = g * kChainRing + cslot % kChainRing;
+            const uint32_t e = g * kR + cslot % kR;
             ring_st[e] = b0;
-            ring_st[kChainGroups * kChainRing + e] = b1;
-            ring_st[2 * kChainGroups * kChainRing + e] = b2;
-            ring_st[3 * kChainGroups * kChainRing + e] = b3;
-            ring_st[4 * kChainGroups * kChainRing + e] = b4;
+            ring_st[kG * kR + e] = b1;
+            ring_st[2 * kG * kR + e] = b2;
+            ring_st[3 * kG * kR + e] = b3;
+            ring_st[4 * kG * kR + e] = b4;
             ring_tag[e] = cslot;
             ring_res[e].w = 0.0f;
             st = {b0, b1, b2, b3, b4, G[3] + 2u * cslot * IQ_XORWOW_WEYL};
@@ -2605,14 +2614,16 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
         }
         const bool more = walker && !w_done;
         if (!__any(active) && !__any(more) && !__any(w_fin)) break;
-        __syncthreads();
+        if (!(dg & 256u)) __syncthreads();
         if (!__any(active)) continue;
 
         // ---- C. one bounce of every traced slot (the anchored kernel's closest hit and shading)
         float closest = kTMax;
         int kind = kHitNone;
         uint32_t hidx = 0;
-        if (kCull && p.cull != nullptr) {
+        if (dg & 512u) {
+            // ablation: every ray misses
+        } else if (kCull && p.cull != nullptr) {
             const bool cull = !__any(active && depth != 0);
             const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[lane].z * p.cull_stride : nullptr;
             uint4 cm = lds_cm[lane];
@@ -2677,13 +2688,13 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
                 cz = 0.0f + cz;
                 // slots consumed: 1 + the scatters (two draws each)
                 const uint32_t nsl = (uint32_t)depth + 1u + md_end;
-                ring_res[g * kChainRing + cslot % kChainRing] = make_float4(cx, cy, cz, __uint_as_float(nsl));
-                xorwow_skip_v(b0, b1, b2, b3, b4, 2u * kChainLanes);
-                cslot += kChainLanes;
+                ring_res[g * kR + cslot % kR] = make_float4(cx, cy, cz, __uint_as_float(nsl));
+                if (!(dg & 128u)) xorwow_skip_v(b0, b1, b2, b3, b4, 2u * kL);
+                cslot += kL;
                 active = false;
             }
         }
-        __syncthreads();
+        if (!(dg & 256u)) __syncthreads();
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) w_rays += __shfl_xor(w_rays, off);
@@ -2692,10 +2703,12 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
 
 // LDS bytes of the chain kernel for a launch (scene pairs, mean table, mask slots, ring, group words,
 // scatter stack)
-__host__ __device__ inline uint32_t chain_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, uint32_t spp, int max_depth) {
+__host__ __device__ inline uint32_t chain_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, uint32_t spp, int max_depth,
+                                                    uint32_t lanes) {
+    const uint32_t groups = 64u / lanes, ring = 2u * lanes;
     return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + ((spp + 1u) & ~1u) * 8u +
-           ((spp + 3u) & ~3u) * 4u + kChainBlock * 16u + kChainGroups * kChainRing * (16u + 4u + 20u) +
-           16u * kChainGroups * 4u + (uint32_t)(max_depth > 1 ? max_depth : 1) * kChainBlock * 4u;
+           ((spp + 3u) & ~3u) * 4u + kChainBlock * 16u + groups * ring * (16u + 4u + 20u) + 16u * groups * 4u +
+           (uint32_t)(max_depth > 1 ? max_depth : 1) * kChainBlock * 4u;
 }
 
 template <int MAXD, bool STREAM, int OPT>
@@ -2892,49 +2905,53 @@ int launch_split_stitch(void* stream, const ksplit& s, bool fastdiv) {
 
 // kOptChain launches (iqpt_chain_kernel): the resident production option sets, reference materials
 namespace {
-template <int MAXD, int OPT>
+template <int MAXD, int OPT, int L>
 int chain_launch_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_chain_kernel<MAXD, OPT>), dim3(grid), dim3(kChainBlock), lds, stream, p);
+    hipLaunchKernelGGL((iqpt_chain_kernel<MAXD, OPT, L>), dim3(grid), dim3(kChainBlock), lds, stream, p);
     return (int)hipGetLastError();
 }
-template <int MAXD, int OPT>
+template <int MAXD, int OPT, int L>
 int chain_occ_t(uint32_t lds, int* blocks) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_chain_kernel<MAXD, OPT>, kChainBlock, lds);
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_chain_kernel<MAXD, OPT, L>, kChainBlock, lds);
 }
 struct chain_variant {
-    int maxd, opt;
+    int maxd, opt, lanes;
     int (*launch)(hipStream_t, const kparams&, uint32_t, uint32_t);
     int (*occ)(uint32_t, int*);
 };
-#define IQPT_CV(M, O) {M, O, chain_launch_t<M, O>, chain_occ_t<M, O>}
+#define IQPT_CV(M, O, L) {M, O, L, chain_launch_t<M, O, L>, chain_occ_t<M, O, L>}
+#define IQPT_CV4(O) IQPT_CV(8, O, 8), IQPT_CV(16, O, 8), IQPT_CV(8, O, 4), IQPT_CV(16, O, 4)
 const chain_variant kChainVariants[] = {
-    IQPT_CV(8, kOptDefault | kOptPrio), IQPT_CV(16, kOptDefault | kOptPrio),
-    IQPT_CV(8, (kOptDefault & ~kOptFastDiv) | kOptPrio), IQPT_CV(16, (kOptDefault & ~kOptFastDiv) | kOptPrio),
+    IQPT_CV4(kOptDefault | kOptPrio),
+    IQPT_CV4((kOptDefault & ~kOptFastDiv) | kOptPrio),
 };
+#undef IQPT_CV4
 #undef IQPT_CV
-const chain_variant* find_chain(int max_depth, int opt) {
+const chain_variant* find_chain(int max_depth, int opt, uint32_t lanes) {
     const int maxd = max_depth <= 8 ? 8 : 16;
     for (const chain_variant& v : kChainVariants)
-        if (v.maxd == maxd && v.opt == (opt | kOptPrio)) return &v;
+        if (v.maxd == maxd && v.opt == (opt | kOptPrio) && v.lanes == (int)lanes) return &v;
     return nullptr;
 }
 }  // namespace
 
-bool chain_variant_exists(int max_depth, int opt) { return max_depth <= 16 && find_chain(max_depth, opt) != nullptr; }
+bool chain_variant_exists(int max_depth, int opt) { return max_depth <= 16 && find_chain(max_depth, opt, 8) != nullptr; }
 
-uint32_t chain_lds(const kparams& p) { return chain_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.spp, p.max_depth); }
+uint32_t chain_lds(const kparams& p, uint32_t lanes) {
+    return chain_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.spp, p.max_depth, lanes);
+}
 
-int chain_occupancy(int max_depth, int opt, uint32_t lds, int* blocks) {
-    const chain_variant* v = find_chain(max_depth, opt);
+int chain_occupancy(int max_depth, int opt, uint32_t lanes, uint32_t lds, int* blocks) {
+    const chain_variant* v = find_chain(max_depth, opt, lanes);
     if (!v) return (int)hipErrorInvalidDeviceFunction;
     return v->occ(lds, blocks);
 }
 
-int launch_chain(void* stream, const kparams& p, uint32_t grid, int opt) {
-    const chain_variant* v = find_chain(p.max_depth, opt);
+int launch_chain(void* stream, const kparams& p, uint32_t grid, int opt, uint32_t lanes) {
+    const chain_variant* v = find_chain(p.max_depth, opt, lanes);
     if (!v || p.max_depth > 16 || p.spp > kAccTableMax) return (int)hipErrorInvalidDeviceFunction;
     if (grid == 0) return 0;
-    return v->launch((hipStream_t)stream, p, grid, chain_lds(p));
+    return v->launch((hipStream_t)stream, p, grid, chain_lds(p, lanes));
 }
 
 }  // namespace iqpt

@@ -37,10 +37,10 @@ constexpr int kTuneLaunches = 4;     // timed launches before the camera-ray pat
 // kOptSplit auto mode: split when the owned pixels are fewer than this many per resident lane
 constexpr double kSplitAutoPixelsPerLane = 1.2;
 // chain launches: AUTO takes them below this many owned pixels per resident lane of the
-// plain kernel; chain-kernel waves per CU by default
-constexpr double kChainAutoPixelsPerLane = 4.0;
-constexpr uint32_t kChainWavesPerCu = 8;
-constexpr uint64_t kChainPixelsPerWave = 8;   // iqpt_chain_kernel: pixels in flight per wave (kChainGroups)
+// plain kernel (C3 shares: N = 4 has 1.6, N = 8 0.8; N = 2, 3.2, is faster plain); chain-kernel waves per
+// CU by default (profiles/r02/split_share_v12_lanes.json: 16 beats 8 at N <= 4, equal at N = 8)
+constexpr double kChainAutoPixelsPerLane = 2.0;
+constexpr uint32_t kChainWavesPerCu = 16;
 constexpr size_t kSplitResBudget = size_t(8) << 30;   // speculative results (bytes)
 
 std::once_flag g_tables_once;
@@ -160,6 +160,7 @@ struct iqpt_ctx {
     bool split_all_tiles = false;       // every tile in the split set (wall tiles: one slot per sample)
     // chain launches: chain-kernel waves per CU (0: kChainWavesPerCu); the last launch's mode
     uint32_t chain_waves = 0;
+    uint32_t chain_lanes = 8;           // lanes per pixel (4 or 8)
     bool chain_last = false;
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
     double tune_work[4] = {0.0, 0.0, 0.0, 0.0};
@@ -1364,16 +1365,18 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const size_t ns = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
         p.sp_pix = c->d_split + c->n_anchor + c->n_split_tiles;
         p.ns_cap = (uint32_t)ns;
-        const uint32_t lds_c = iqpt::chain_lds(p);
+        const uint32_t lanes = c->chain_lanes;
+        const uint32_t lds_c = iqpt::chain_lds(p, lanes);
         int occ_c = 0;
-        if (iqpt::chain_occupancy(c->max_depth, opt, lds_c, &occ_c) != 0 || occ_c < 1) occ_c = 1;
+        if (iqpt::chain_occupancy(c->max_depth, opt, lanes, lds_c, &occ_c) != 0 || occ_c < 1) occ_c = 1;
         const uint32_t per_cu = std::min<uint32_t>((uint32_t)occ_c, c->chain_waves ? c->chain_waves : iqpt::kChainWavesPerCu);
-        const uint64_t want_c = (ns + iqpt::kChainPixelsPerWave - 1) / iqpt::kChainPixelsPerWave;
+        const uint64_t px_per_wave = 64u / lanes;
+        const uint64_t want_c = (ns + px_per_wave - 1) / px_per_wave;
         const uint32_t grid_c = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_c, (uint64_t)c->num_cus * per_cu));
         p.ovl_err = c->d_ovl_err;
         IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
         IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
-        le = iqpt::launch_chain(c->stream2, p, grid_c, opt);
+        le = iqpt::launch_chain(c->stream2, p, grid_c, opt, lanes);
         if (le == 0 && c->n_anchor > 0) {
             p.tile_order = c->d_split;
             p.nqueue = c->n_anchor;
@@ -1723,9 +1726,14 @@ int iqpt_debug_set_split_knobs(iqpt_ctx* c, uint32_t heavy_rho, uint32_t refill_
 }
 
 // Chain launches (tools/split_share.py): chain-kernel waves per CU (0: the default). Results do not depend on it.
+// Bits 8..15 of waves_per_cu: lanes per pixel (4 or 8; 0 keeps the current value).
 int iqpt_debug_set_chain_waves(iqpt_ctx* c, uint32_t waves_per_cu) {
-    if (!c || waves_per_cu > 64) return iqpt::fail(IQPT_ERR_INVALID_ARG, "waves_per_cu 0..64");
+    const uint32_t lanes = (waves_per_cu >> 8) & 0xffu;
+    waves_per_cu &= 0xffu;
+    if (!c || waves_per_cu > 64 || (lanes != 0 && lanes != 4 && lanes != 8))
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "waves_per_cu 0..64, lanes 0, 4 or 8");
     c->chain_waves = waves_per_cu;
+    if (lanes) c->chain_lanes = lanes;
     return IQPT_OK;
 }
 

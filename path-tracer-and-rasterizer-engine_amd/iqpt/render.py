@@ -105,6 +105,15 @@ class PathTracer:
         """Overlapped launches on two streams: _lib.OVERLAP_AUTO (default) or OVERLAP_OFF (iqpt_set_overlap)."""
         check(self._lib.iqpt_set_overlap(self._h, mode), "iqpt_set_overlap")
 
+    def launch_mode(self) -> str:
+        """How the last launch ran: "plain", "split" (speculative runs + stitch) or "chain" (chain kernel
+        beside the plain kernel), from iqpt_debug_split_info. Synchronises."""
+        import ctypes as C
+        self._lib.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+        info = (C.c_ulonglong * 8)()
+        check(self._lib.iqpt_debug_split_info(self._h, info), "iqpt_debug_split_info")
+        return {1: "split", 2: "chain"}.get(int(info[7]), "plain")
+
     def kernel_span(self) -> float:
         """First start to last end (ms) of the launches of the last kernel_time() call (iqpt_kernel_span)."""
         ms = C.c_double()

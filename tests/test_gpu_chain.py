@@ -133,3 +133,27 @@ def test_large_frame_counter_chain(require_gpu):
     lin, bgra = pt.read()
     assert ran_chain(pt)
     _check(pt, lin, bgra, fr)
+
+
+@pytest.mark.parametrize("lanes,waves", [(4, 16), (8, 4), (4, 1)])
+def test_lanes_and_waves_chain(require_gpu, lanes, waves):
+    """4 lanes per pixel (16 pixels per wave) and other chain-kernel grid sizes: the same bits."""
+    from iqpt import PathTracer, _lib, make_camera
+    w, h = 480, 270
+    n = len(range(2, h, 4))
+    ps = pixel_set(w, h, 0, w, 2, 4, n)
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    pt.set_split(SPLIT_CHAIN)
+    lib = _lib.load()
+    lib.iqpt_debug_set_chain_waves.argtypes = [C.c_void_p, C.c_uint32]
+    _lib.check(lib.iqpt_debug_set_chain_waves(pt._h, waves | (lanes << 8)), "iqpt_debug_set_chain_waves")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    for s in (10, 3):
+        pt.render(s)
+    lin, bgra = pt.read()
+    assert ran_chain(pt)
+    fr = oracle_render("cornell", w, h, 0, 8, pixels=ps, launches=[10, 3])
+    _check(pt, lin, bgra, fr)

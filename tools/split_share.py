@@ -25,6 +25,7 @@ from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
 
 
 OPT = 0
+DIAG = 0     # chain-kernel timing ablations (A/B library; NOT exact)
 
 
 def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain_waves: int = 0) -> dict:
@@ -46,6 +47,11 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain
         lb = _lib.load()
         lb.iqpt_debug_set_split_knobs.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_split_knobs(pt._h, knobs[0], knobs[1]), "iqpt_debug_set_split_knobs")
+    if DIAG and mode == _lib.SPLIT_CHAIN:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_diag.argtypes = [C.c_void_p, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_diag(pt._h, DIAG), "iqpt_debug_set_diag")
     if chain_waves:
         import ctypes as C
         lb = _lib.load()
@@ -151,7 +157,15 @@ def main():
     ap.add_argument("--knobs", default="", help="split knob sets heavy_rho:refill_min[,...] (extra split rows)")
     ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (A/B library)")
     ap.add_argument("--opt", type=int, default=0, help="kernel option set (A/B library; 0 = production)")
+    ap.add_argument("--ab", action="store_true", help="load the A/B library (chain ablations: --diag)")
+    ap.add_argument("--diag", type=int, default=0, help="chain-kernel ablation bits (64 mean, 128 stepping, "
+                    "256 barriers, 512 closest hit); results are then NOT exact")
     args = ap.parse_args()
+    if args.ab or args.diag:
+        global DIAG
+        from iqpt import _build
+        _lib.LIB_PATH = _build.build_lib(ab=True)
+        DIAG = args.diag
     out = {"config": "c2 rank-0 row share, 64 spp per launch", "launches": args.launches, "rows": []}
     if args.opt:
         global OPT
@@ -174,9 +188,15 @@ def main():
         res = {}
         modes = [m for m in (("plain", _lib.SPLIT_OFF, 0), ("split", _lib.SPLIT_ON, 0),
                              ("chain", _lib.SPLIT_CHAIN, 0)) if m[0] in args.modes.split(",")]
-        modes += [(f"chain_w{w}", _lib.SPLIT_CHAIN, int(w)) for w in args.chain_waves.split(",") if w]
+        # "16" = 16 chain-kernel waves per CU; "16a" = the same with every tile in the split set (all chains);
+        # "16l4" = 4 lanes per pixel
+        def cw(w):
+            v = w.rstrip("a")
+            return int(v.split("l")[0]) | ((int(v.split("l")[1]) << 8) if "l" in v else 0)
+        modes += [(f"chain_w{w}", _lib.SPLIT_CHAIN, cw(w)) for w in args.chain_waves.split(",") if w]
         for name, mode, cw in modes:
-            r = run(n, mode, args.launches, args.warm, args.spp, chain_waves=cw)
+            kn = (0, 16 | (1 << 16)) if name.endswith("a") else None
+            r = run(n, mode, args.launches, args.warm, args.spp, knobs=kn, chain_waves=cw)
             res[name] = r
             row[name + "_ms_median"] = float(np.median(r["ms"]))
             row[name + "_ms_min"] = float(np.min(r["ms"]))
