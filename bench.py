@@ -74,7 +74,9 @@ def parse():
                     help="what the strong-scaling step gathers to rank 0: the BGRA8 frame or the float accumulators")
     ap.add_argument("--overlap", default="auto", choices=["auto", "off"],
                     help="overlapped launches on two streams (iqpt_set_overlap, DESIGN.md §3.8)")
-    ap.add_argument("--split", default="auto", choices=["auto", "on", "off"],
+    ap.add_argument("--kernel-options", type=lambda v: int(v, 0), default=0,
+                    help="A/B: render-kernel option mask (iqpt_debug_set_kernel_options; 0 = production)")
+    ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain"],
                     help="sample-parallel chains (iqpt_set_split, DESIGN.md §3.7)")
     return ap.parse_args()
 
@@ -289,7 +291,13 @@ def main():
     t0 = time.perf_counter()
     pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, seed=seed, max_depth=cfg.max_depth, device=device)
     setup["create_and_rng_init_ms"] = (time.perf_counter() - t0) * 1e3
-    pt.set_split({"auto": _lib.SPLIT_AUTO, "on": _lib.SPLIT_ON, "off": _lib.SPLIT_OFF}[args.split])
+    pt.set_split({"auto": _lib.SPLIT_AUTO, "on": _lib.SPLIT_ON, "off": _lib.SPLIT_OFF,
+                  "chain": _lib.SPLIT_CHAIN}[args.split])
+    if args.kernel_options:
+        import ctypes as C
+        _lib.load().iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(_lib.load().iqpt_debug_set_kernel_options(pt.handle, args.kernel_options),
+                   "iqpt_debug_set_kernel_options")
     pt.set_overlap(_lib.OVERLAP_AUTO if args.overlap == "auto" else _lib.OVERLAP_OFF)
     pt.set_camera(cam)
     t0 = time.perf_counter()
@@ -422,7 +430,8 @@ def main():
                                       ("none in the timed region; one reduce of the accumulators after it"
                                        if weak else f"gather of the {gathered} to rank 0 every step")
                                       + (" (rccl)" if on_gpu else " (gloo via host, rehearsal)")),
-                       "split": args.split, "overlap": args.overlap, "launch_mode": launch_mode},
+                       "split": args.split, "overlap": args.overlap, "launch_mode": launch_mode,
+                       **({"kernel_options": args.kernel_options} if args.kernel_options else {})},
             "n_ranks_seen": n_ranks_seen,
             "msamples_per_s": round(samples / elapsed / 1e6, 3),
             "rays_per_sample": round(total_rays / samples, 5),

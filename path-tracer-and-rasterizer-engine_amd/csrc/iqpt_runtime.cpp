@@ -1323,6 +1323,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     hipStream_t ls = c->stream;                       // the launch's stream
     if (ovl) {
         opt |= iqpt::kOptOverlap;
+        // pitch-only cameras: the short camera transform (exact, kOptCamAxis) pays once launches overlap
+        if (!c->opt_fixed && cam_axis &&
+            iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptCamAxis))
+            opt |= iqpt::kOptCamAxis;
         if (c->ovl_zero || c->ovl_epoch >= (1u << 24)) {
             if ((st = join_streams(c)) != IQPT_OK) return st;
             IQPT_HIP(hipMemsetAsync(c->d_tile_done, 0, (size_t)p.ntiles * sizeof(uint32_t), c->stream));

@@ -156,7 +156,7 @@ def main():
     ap.add_argument("--chain-waves", default="", help="extra chain rows at these chain-kernel waves per CU")
     ap.add_argument("--knobs", default="", help="split knob sets heavy_rho:refill_min[,...] (extra split rows)")
     ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (A/B library)")
-    ap.add_argument("--opt", type=int, default=0, help="kernel option set (A/B library; 0 = production)")
+    ap.add_argument("--opt", type=lambda v: int(v, 0), default=0, help="kernel option set (A/B library; 0 = production)")
     ap.add_argument("--ab", action="store_true", help="load the A/B library (chain ablations: --diag)")
     ap.add_argument("--diag", type=int, default=0, help="chain-kernel ablation bits (64 mean, 128 stepping, "
                     "256 barriers, 512 closest hit); results are then NOT exact")
