@@ -304,7 +304,7 @@ bool render_variant_exists(int max_depth, bool stream_batches, int opt);
 // kChainLanes lanes at consecutive even stream offsets and folded in sample order; reads p.sp_pix /
 // p.ns_cap and takes pixels from p.queue[1]. Resident scenes, reference materials, max_depth <= 16.
 // lanes: lanes per pixel, 4 or 8.
-bool chain_variant_exists(int max_depth, int opt);
+bool chain_variant_exists(int max_depth, int opt, uint32_t lanes);
 uint32_t chain_lds(const kparams& p, uint32_t lanes);
 int chain_occupancy(int max_depth, int opt, uint32_t lanes, uint32_t lds, int* blocks_per_cu);
 int launch_chain(void* stream, const kparams& p, uint32_t grid_blocks, int opt, uint32_t lanes);

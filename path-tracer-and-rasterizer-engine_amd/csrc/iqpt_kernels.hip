@@ -2511,23 +2511,41 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
                     if (pix != ~0u) break;
                 }
                 if (!w_done) {
+                    // the pixel's accumulator, RNG state and tile mask words in one round of loads; the
+                    // group's lanes read them from G (no second round trip in phase B)
                     w_pix = pix;
                     w_ptr = 0u;
                     w_k = 0u;
+                    uint32_t col, row;
+                    tile_decode(pix, p.ncols, p.nrows, &col, &row);
+                    const uint32_t t = (row / kCullTile) * p.ntx + col / kCullTile;
                     const float* a = reinterpret_cast<const float*>(p.lin + pix);
                     ax = a[0];
                     ay = a[1];
                     az = a[2];
-                    uint32_t col, row;
-                    tile_decode(pix, p.ncols, p.nrows, &col, &row);
+                    const uint32_t r0 = p.rng[pix], r1 = p.rng[(size_t)p.npix + pix], r2 = p.rng[2 * (size_t)p.npix + pix],
+                                   r3 = p.rng[3 * (size_t)p.npix + pix], r4 = p.rng[4 * (size_t)p.npix + pix],
+                                   r5 = p.rng[5 * (size_t)p.npix + pix];
+                    uint32_t cm0 = 0u, cm1 = 0u;
+                    if (kCull && p.cull) {
+                        cm0 = p.cull[(size_t)t * p.cull_stride];
+                        cm1 = p.cull[(size_t)t * p.cull_stride + p.cull_wt];
+                    }
                     G[0] = pix;
                     G[1] = p.x0 + col;
                     G[2] = p.y0 + row * p.ystep;
-                    G[3] = p.rng[5 * (size_t)p.npix + pix];
+                    G[3] = r5;
                     G[4] = G[4] + 1u;
                     G[6] = 0u;
                     G[7] = 0u;
-                    G[8] = (row / kCullTile) * p.ntx + col / kCullTile;
+                    G[8] = t;
+                    G[9] = r0;
+                    G[10] = r1;
+                    G[11] = r2;
+                    G[12] = r3;
+                    G[13] = r4;
+                    G[14] = cm0;
+                    G[15] = cm1;
                     for (uint32_t i = 0; i < kR; ++i) ring_tag[g * kR + i] = ~0u;
                 }
             }
@@ -2569,17 +2587,13 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
             gen_seen = gen;
             active = false;
             cslot = li;
-            b0 = p.rng[gpix];
-            b1 = p.rng[(size_t)p.npix + gpix];
-            b2 = p.rng[2 * (size_t)p.npix + gpix];
-            b3 = p.rng[3 * (size_t)p.npix + gpix];
-            b4 = p.rng[4 * (size_t)p.npix + gpix];
+            b0 = G[9];
+            b1 = G[10];
+            b2 = G[11];
+            b3 = G[12];
+            b4 = G[13];
             xorwow_skip_v(b0, b1, b2, b3, b4, 2u * li);
-            if (kCull && p.cull) {
-                const uint32_t t = G[8];
-                lds_cm[lane] = make_uint4(p.cull[(size_t)t * p.cull_stride], p.cull[(size_t)t * p.cull_stride + p.cull_wt],
-                                          t, 0u);
-            }
+            if (kCull && p.cull) lds_cm[lane] = make_uint4(G[14], G[15], G[8], 0u);
         }
         if (gpix != ~0u && G[6] != 0u) {
             // the chain is complete: drop the speculative slots; the lane of slot ptr provides its state
@@ -2744,9 +2758,10 @@ const variant kVariants[] = {
                      IQPT_V(16, true, (O) & ~kOptLB5), IQPT_V(8, true, (O) | kOptBvhPrimary), \
                      IQPT_V(16, true, (O) | kOptBvhPrimary)
     IQPT_PROD(kOptDefault),
-    // pitch-only cameras (kOptCamAxis), resident scenes, max_depth <= 8: opt-in only (10.5 % fewer VALU
-    // instructions on C2 but no shorter launch); kept for its exactness tests
-    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptPrio),
+    // pitch-only cameras (kOptCamAxis), resident scenes: 10.5 % fewer VALU instructions on C2; chosen by the
+    // runtime wherever the camera qualifies (round 1 measured no gain; after kOptPrio / kOptScatter2 and
+    // with overlapped launches it is -12..-14 %)
+    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptPrio), IQPT_V(16, false, kOptDefault | kOptCamAxis | kOptPrio),
     IQPT_V(8, false, kOptDefault | kOptMaterials | kOptCamAxis | kOptPrio),
     IQPT_PROD(kOptDefault & ~kOptFastDiv),                  // packets outside the kOptFastDiv range
     IQPT_PROD(kOptDefault | kOptMaterials),                 // packets with a material table
@@ -2930,7 +2945,7 @@ struct chain_variant {
 const chain_variant kChainVariants[] = {
     IQPT_CV4(kOptDefault | kOptPrio),
     IQPT_CV4((kOptDefault & ~kOptFastDiv) | kOptPrio),
-    IQPT_CV(8, kOptDefault | kOptCamAxis | kOptPrio, 8), IQPT_CV(16, kOptDefault | kOptCamAxis | kOptPrio, 8),
+    IQPT_CV4(kOptDefault | kOptCamAxis | kOptPrio),
 };
 #undef IQPT_CV4
 #undef IQPT_CV
@@ -2942,7 +2957,9 @@ const chain_variant* find_chain(int max_depth, int opt, uint32_t lanes) {
 }
 }  // namespace
 
-bool chain_variant_exists(int max_depth, int opt) { return max_depth <= 16 && find_chain(max_depth, opt, 8) != nullptr; }
+bool chain_variant_exists(int max_depth, int opt, uint32_t lanes) {
+    return max_depth <= 16 && find_chain(max_depth, opt, lanes) != nullptr;
+}
 
 uint32_t chain_lds(const kparams& p, uint32_t lanes) {
     return chain_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.spp, p.max_depth, lanes);

@@ -1194,7 +1194,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     bool chain = false;
     if ((c->split_mode == IQPT_SPLIT_CHAIN || c->split_mode == IQPT_SPLIT_AUTO) && !stream_batches && p.cull &&
         c->n_split_tiles > 0 && tune_slot < 0 && !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax &&
-        iqpt::chain_variant_exists(c->max_depth, opt)) {
+        iqpt::chain_variant_exists(c->max_depth, opt, c->chain_lanes)) {
         int occ_p = 0;
         if (iqpt::render_occupancy(c->max_depth, false, opt, lds, &occ_p) != 0) occ_p = 0;
         const double lanes = (double)c->num_cus * std::max(occ_p, 1) * iqpt::kRenderBlock;
@@ -1323,10 +1323,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     hipStream_t ls = c->stream;                       // the launch's stream
     if (ovl) {
         opt |= iqpt::kOptOverlap;
-        // pitch-only cameras: the short camera transform (exact, kOptCamAxis) pays once launches overlap
-        if (!c->opt_fixed && cam_axis &&
-            iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptCamAxis))
-            opt |= iqpt::kOptCamAxis;
         if (c->ovl_zero || c->ovl_epoch >= (1u << 24)) {
             if ((st = join_streams(c)) != IQPT_OK) return st;
             IQPT_HIP(hipMemsetAsync(c->d_tile_done, 0, (size_t)p.ntiles * sizeof(uint32_t), c->stream));
@@ -1351,6 +1347,13 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         if (ls == c->stream) IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
         occ -= 1;
     }
+    // pitch-only cameras take the short camera transform (exact, kOptCamAxis) wherever that variant is
+    // built: resident plain, overlapped and chain launches (C2 -14 % overlapped, C3 shares -3..-12 %,
+    // profiles/r02/ab_camaxis_overlap.json, split_share_v17_camaxis.json)
+    if (!c->opt_fixed && cam_axis && !stream_batches && !split &&
+        iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptCamAxis) &&
+        (!chain || iqpt::chain_variant_exists(c->max_depth, opt | iqpt::kOptCamAxis, c->chain_lanes)))
+        opt |= iqpt::kOptCamAxis;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
     if (!ovl) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));

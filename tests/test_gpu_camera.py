@@ -109,6 +109,14 @@ def test_yawed_camera_keeps_general_transform(require_gpu):
     assert not opt & K_OPT_CAM_AXIS
 
 
-def test_default_selection_keeps_general_transform(require_gpu):
+def test_default_selection_takes_short_camera(require_gpu):
+    """The runtime's own choice: a pitch-only camera gets the short transform (same bits as the oracle)."""
     opt = render_both(make_camera(96, 64), 96, 64, 2, axis=False)
+    assert opt & K_OPT_CAM_AXIS
+
+
+def test_default_selection_yawed_camera_general(require_gpu):
+    """The runtime's own choice for a yawed camera: the general transform."""
+    cam = make_camera(96, 64, position=(0.3, 0.5, -3.0, 0.0), forward=(-0.2, -0.5, 3.0, 0.0))
+    opt = render_both(cam, 96, 64, 3, axis=False)
     assert not opt & K_OPT_CAM_AXIS
