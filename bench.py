@@ -76,6 +76,10 @@ def parse():
                     help="overlapped launches on two streams (iqpt_set_overlap, DESIGN.md §3.8)")
     ap.add_argument("--kernel-options", type=lambda v: int(v, 0), default=0,
                     help="A/B: render-kernel option mask (iqpt_debug_set_kernel_options; 0 = production)")
+    ap.add_argument("--gather-sync", action="store_true",
+                    help="N > 1: the blocking frame copy + gather of round 1 instead of the stream-ordered one")
+    ap.add_argument("--self-gather", action="store_true",
+                    help="test: run the per-step gather path at N = 1 (a one-rank process group)")
     ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain"],
                     help="sample-parallel chains (iqpt_set_split, DESIGN.md §3.7)")
     return ap.parse_args()
@@ -264,12 +268,17 @@ def main():
     # gloo through host memory (RCCL refuses two ranks on one GPU). The driver's runs use nccl.
     device = 0 if args.one_device else local_rank
     torch.cuda.set_device(device)
-    if world > 1:
+    use_pg = world > 1 or args.self_gather
+    if use_pg:
+        if world == 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
+            os.environ.setdefault("RANK", "0")
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", device), world_size=world, rank=rank)
         else:
-            dist.init_process_group("gloo")
-    n_ranks_seen = dist.get_world_size() if world > 1 else 1
+            dist.init_process_group("gloo", world_size=world, rank=rank)
+    n_ranks_seen = dist.get_world_size() if use_pg else 1
 
     def barrier():
         if world > 1:
@@ -310,7 +319,7 @@ def main():
     on_gpu = args.backend == "nccl"
     tdev = "cuda" if on_gpu else "cpu"
     max_px = iqdist.max_rows(cfg.height, part_world) * cfg.width
-    strong_multi = world > 1 and not weak
+    strong_multi = (world > 1 or args.self_gather) and not weak
     words = 4 if args.gather == "accum" else 1
     dtype = torch.float32 if args.gather == "accum" else torch.int32
     buf = torch.zeros((max_px, words), dtype=dtype, device=tdev) if strong_multi else None
@@ -331,10 +340,30 @@ def main():
         st = torch.stack(parts).view(world, -1, cfg.width, channels)
         return st.transpose(0, 1).reshape(-1, cfg.width, channels)[: cfg.height]
 
+    # Stream-ordered gather (nccl, BGRA frame): the frame copy is enqueued on the context's stream after the
+    # step's render, the gather on torch's stream waits for it with an event, and the next step's copy
+    # into the same buffer waits for that gather: no host synchronisation inside the timed steps, and
+    # the gather of step k runs while step k + 1 renders.
+    stream_gather = strong_multi and on_gpu and args.gather == "frame" and not args.gather_sync
+    ctx_stream = torch.cuda.ExternalStream(pt.stream_handle()) if stream_gather else None
+    gathered = None                                   # torch-stream event after the last gather
+
     def step():
-        nonlocal assembled
+        nonlocal assembled, gathered
         pt.render(spp_step)
-        if strong_multi:
+        if strong_multi and stream_gather:
+            if gathered is not None:
+                ctx_stream.wait_event(gathered)       # buf is read by the previous gather
+            pt.copy_frame_device_async(buf.data_ptr(), buf.numel() * 4)
+            copied = torch.cuda.Event()
+            copied.record(ctx_stream)
+            torch.cuda.current_stream().wait_event(copied)
+            dist.gather(buf, gather_list, dst=0)
+            if rank == 0:
+                assembled = deinterleave(gather_list, words)
+            gathered = torch.cuda.Event()
+            gathered.record(torch.cuda.current_stream())
+        elif strong_multi:
             fetch(buf, args.gather)
             dist.gather(buf, gather_list, dst=0)
             if rank == 0:
@@ -368,6 +397,14 @@ def main():
     # number is the kernel time per launch that the throughput sees; each launch's own duration is longer
     kern_span_ms = pt.kernel_span()
     launch_mode = pt.launch_mode()
+
+    # the last step's gathered frame: rank 0's own rows of it must be its BGRA frame (checks the gather path)
+    gather_check = None
+    if strong_multi and rank == 0 and assembled is not None:
+        torch.cuda.synchronize()
+        own = pt.read()[1].view(np.int32).reshape(-1, cfg.width)
+        got = assembled.reshape(-1, cfg.width)[0::world].cpu().numpy().view(np.int32)
+        gather_check = bool(own.shape == got.shape and np.array_equal(own, got))
 
     # after timing: the float frame on rank 0 (strong: the gathered accumulators de-interleaved, bit-
     # identical to one GPU's frame; weak: the N independent estimates averaged)
@@ -433,6 +470,8 @@ def main():
                        "split": args.split, "overlap": args.overlap, "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {})},
             "n_ranks_seen": n_ranks_seen,
+            **({"gather": "stream-ordered" if stream_gather else "blocking", "gather_check": gather_check}
+               if strong_multi else {}),
             "msamples_per_s": round(samples / elapsed / 1e6, 3),
             "rays_per_sample": round(total_rays / samples, 5),
             "rmse_vs_oracle": rmse_v,
@@ -450,7 +489,7 @@ def main():
             np.save(args.save_frame, frame.cpu().numpy())
         print(json.dumps(out), flush=True)
     pt.close()
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -220,6 +220,13 @@ int iqpt_copy_accum_device(iqpt_ctx* ctx, void* dst_device, size_t bytes);
  * the multi-GPU gather of the presented frame (path_tracer.cu:385 reads this buffer back every
  * frame). Synchronises. */
 int iqpt_copy_frame_device(iqpt_ctx* ctx, void* dst_device, size_t bytes);
+/* Stream-ordered form of iqpt_copy_frame_device for a pipelined gather: the copy is enqueued on the
+ * context's stream after every render issued so far and the call returns at once (no host sync). The
+ * caller orders its own work against that stream (iqpt_stream). */
+int iqpt_copy_frame_device_async(iqpt_ctx* ctx, void* dst_device, size_t bytes);
+/* The context's HIP stream (hipStream_t): renders, and every copy out, are ordered on it (overlapped
+ * launches join it before any other call). */
+int iqpt_stream(iqpt_ctx* ctx, void** stream);
 
 int iqpt_num_pixels(const iqpt_ctx* ctx, uint64_t* npix);
 int iqpt_frame_count(const iqpt_ctx* ctx, uint64_t* frames);

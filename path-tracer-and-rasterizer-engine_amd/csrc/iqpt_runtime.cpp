@@ -1673,6 +1673,25 @@ int iqpt_copy_frame_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
     return IQPT_OK;
 }
 
+int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
+    if (!c || !dst_device) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (bytes < (size_t)c->npix * sizeof(uint32_t)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
+    int st = enter(c);                    // (joins the overlapped launches' second stream: no host sync)
+    if (st) return st;
+    const int le = iqpt::launch_relayout(c->stream, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
+                                         c->set.nrows, 1, 1, true);
+    if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
+    return IQPT_OK;
+}
+
+int iqpt_stream(iqpt_ctx* c, void** stream) {
+    if (!c || !stream) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = enter(c);
+    if (st) return st;
+    *stream = (void*)c->stream;
+    return IQPT_OK;
+}
+
 int iqpt_prepare(iqpt_ctx* c) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     if (!c->have_camera || !c->have_packet) return iqpt::fail(IQPT_ERR_NOT_READY, "camera and packet must be set");

@@ -97,6 +97,18 @@ class PathTracer:
         """BGRA8 frame (npix uint32, compact order) into a device buffer (iqpt_copy_frame_device)."""
         check(self._lib.iqpt_copy_frame_device(self._h, C.c_void_p(dst_ptr), nbytes), "iqpt_copy_frame_device")
 
+    def copy_frame_device_async(self, dst_ptr: int, nbytes: int):
+        """The BGRA8 frame into a device buffer, enqueued on the context's stream (no host sync;
+        iqpt_copy_frame_device_async). Order other work against stream_handle()."""
+        check(self._lib.iqpt_copy_frame_device_async(self._h, C.c_void_p(dst_ptr), nbytes),
+              "iqpt_copy_frame_device_async")
+
+    def stream_handle(self) -> int:
+        """The context's hipStream_t (iqpt_stream), e.g. for torch.cuda.ExternalStream."""
+        s = C.c_void_p()
+        check(self._lib.iqpt_stream(self._h, C.byref(s)), "iqpt_stream")
+        return int(s.value or 0)
+
     def set_split(self, mode: int):
         """Sample-parallel chains: _lib.SPLIT_AUTO (default), SPLIT_OFF, SPLIT_ON or SPLIT_CHAIN (iqpt_set_split)."""
         check(self._lib.iqpt_set_split(self._h, mode), "iqpt_set_split")
