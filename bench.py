@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--verify-rows", type=int, default=16)
     ap.add_argument("--pmc-json", default="",
                     help="PMC traffic of the config (tools/pmc_traffic.py; default profiles/r02/pmc_traffic_<config>.json)")
-    ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r01" / "r01_c2_pmc_mix_v4.json"),
+    ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r02" / "c2_pmc_mix_v5.json"),
                     help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy)")
     ap.add_argument("--work-json", default="",
                     help="executed-work counters of the config (tools/work_counters.py; default "
