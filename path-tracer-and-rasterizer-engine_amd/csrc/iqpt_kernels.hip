@@ -2402,6 +2402,14 @@ __global__ __launch_bounds__(kStitchBlock) void iqpt_split_stitch_kernel(const k
 // reference's materials); the other tiles run anchored in iqpt_render_kernel beside this kernel.
 constexpr uint32_t kChainBlock = 64;                   // one wave per block
 constexpr uint32_t kChainIterLimit = 1u << 22;         // loop iterations before a wave gives up (error bit 2)
+#ifndef IQPT_CHAIN_WAVES
+#define IQPT_CHAIN_WAVES 4
+#endif
+#ifndef IQPT_CHAIN_RING_MUL
+#define IQPT_CHAIN_RING_MUL 2
+#endif
+constexpr int kChainWaves = IQPT_CHAIN_WAVES;          // __launch_bounds__ waves per SIMD
+constexpr uint32_t kChainRingMul = IQPT_CHAIN_RING_MUL; // ring entries per lane
 
 __device__ __forceinline__ void xorwow_skip_v(uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& v3, uint32_t& v4,
                                               uint32_t n) {
@@ -2416,10 +2424,10 @@ __device__ __forceinline__ void xorwow_skip_v(uint32_t& v0, uint32_t& v1, uint32
 }
 
 template <int MAXD, int OPT, int LANES>
-__global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparams p) {
+__global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(const kparams p) {
     constexpr uint32_t kL = LANES;              // lanes per pixel
     constexpr uint32_t kG = 64 / kL;            // pixels per wave
-    constexpr uint32_t kR = 2 * kL;             // slots in flight per pixel (ring entries, a multiple of kL)
+    constexpr uint32_t kR = kChainRingMul * kL; // slots in flight per pixel (ring entries, a multiple of kL)
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
     float4* lds_tri = lds;
@@ -2719,7 +2727,7 @@ __global__ __launch_bounds__(kChainBlock, 4) void iqpt_chain_kernel(const kparam
 // scatter stack)
 __host__ __device__ inline uint32_t chain_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, uint32_t spp, int max_depth,
                                                     uint32_t lanes) {
-    const uint32_t groups = 64u / lanes, ring = 2u * lanes;
+    const uint32_t groups = 64u / lanes, ring = kChainRingMul * lanes;
     return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + ((spp + 1u) & ~1u) * 8u +
            ((spp + 3u) & ~3u) * 4u + kChainBlock * 16u + groups * ring * (16u + 4u + 20u) + 16u * groups * 4u +
            (uint32_t)(max_depth > 1 ? max_depth : 1) * kChainBlock * 4u;

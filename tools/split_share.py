@@ -160,7 +160,10 @@ def main():
     ap.add_argument("--ab", action="store_true", help="load the A/B library (chain ablations: --diag)")
     ap.add_argument("--diag", type=int, default=0, help="chain-kernel ablation bits (64 mean, 128 stepping, "
                     "256 barriers, 512 closest hit); results are then NOT exact")
+    ap.add_argument("--lib", default="", help="load this prebuilt library (compile-time knob A/B)")
     args = ap.parse_args()
+    if args.lib:
+        _lib.LIB_PATH = Path(args.lib)
     if args.ab or args.diag:
         global DIAG
         from iqpt import _build
