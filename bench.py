@@ -78,6 +78,9 @@ def parse():
                     help="A/B: render-kernel option mask (iqpt_debug_set_kernel_options; 0 = production)")
     ap.add_argument("--gather-sync", action="store_true",
                     help="N > 1: the blocking frame copy + gather of round 1 instead of the stream-ordered one")
+    ap.add_argument("--share-of", type=int, default=0,
+                    help="rehearsal at N = 1: render rank 0's rows of an N-way C3 split (one GPU's share; "
+                         "with --self-gather the per-step gather path too)")
     ap.add_argument("--self-gather", action="store_true",
                     help="test: run the per-step gather path at N = 1 (a one-rank process group)")
     ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain"],
@@ -294,6 +297,10 @@ def main():
     weak = args.scaling == "weak"
     # weak: the whole frame per rank, RNG streams of seed 1984 + rank; strong: cyclic rows of one frame
     part_rank, part_world = (0, 1) if weak else (rank, world)
+    if args.share_of:
+        if world != 1 or weak:
+            raise SystemExit("--share-of is a one-rank strong-scaling rehearsal")
+        part_world = args.share_of
     seed = iqpt.DEFAULT_SEED + (rank if weak else 0)
     ps = iqdist.pixel_set_for_rank(cfg.width, cfg.height, part_rank, part_world)
     setup = {}
@@ -345,18 +352,27 @@ def main():
     # into the same buffer waits for that gather: no host synchronisation inside the timed steps, and
     # the gather of step k runs while step k + 1 renders.
     stream_gather = strong_multi and on_gpu and args.gather == "frame" and not args.gather_sync
-    ctx_stream = torch.cuda.ExternalStream(pt.stream_handle()) if stream_gather else None
+    # With overlapped launches (N = 2 plain shares) the copy goes on the last launch's stream, so the next
+    # render keeps overlapping it (iqpt_frame_stream; the launches write two frame buffers in turn).
+    ext_streams = {}
     gathered = None                                   # torch-stream event after the last gather
+
+    def frame_stream():
+        h = pt.frame_stream_handle()
+        if h not in ext_streams:
+            ext_streams[h] = torch.cuda.ExternalStream(h)
+        return ext_streams[h]
 
     def step():
         nonlocal assembled, gathered
         pt.render(spp_step)
         if strong_multi and stream_gather:
+            fs = frame_stream()
             if gathered is not None:
-                ctx_stream.wait_event(gathered)       # buf is read by the previous gather
+                fs.wait_event(gathered)               # buf is read by the previous gather
             pt.copy_frame_device_async(buf.data_ptr(), buf.numel() * 4)
             copied = torch.cuda.Event()
-            copied.record(ctx_stream)
+            copied.record(fs)
             torch.cuda.current_stream().wait_event(copied)
             dist.gather(buf, gather_list, dst=0)
             if rank == 0:
@@ -462,7 +478,9 @@ def main():
                        "spp_per_step": spp_step, "max_depth": cfg.max_depth, "triangles": stats["triangles"],
                        "spheres": stats["spheres"],
                        "partition": (f"full frame per rank x{world} (seed 1984+rank)" if weak
-                                     else (f"cyclic rows x{world}" if world > 1 else "full frame")),
+                                     else (f"cyclic rows x{world}" if world > 1 else
+                                           (f"rank 0's rows of a cyclic x{args.share_of} split (one-GPU share "
+                                            "rehearsal)" if args.share_of else "full frame"))),
                        "collective": ("none" if world == 1 else
                                       ("none in the timed region; one reduce of the accumulators after it"
                                        if weak else f"gather of the {gathered} to rank 0 every step")

@@ -179,6 +179,14 @@ struct iqpt_ctx {
     uint32_t* d_xcd_order = nullptr;    // ntiles: XCD x's tiles at [xcd_off[x], xcd_off[x + 1])
     uint32_t xcd_off[9] = {};
     uint32_t* d_ovl_err = nullptr;
+    // stream-ordered frame copies across overlapped launches (iqpt_copy_frame_device_async): once the
+    // first such copy is asked for, each overlapped launch writes the BGRA frame into the buffer the
+    // previous launch did not (d_bgra is always the last written, d_bgra_alt the other), so launch k's
+    // copy, queued on launch k's stream, reads a frame launch k + 1 never touches, and launch k + 2
+    // (the same stream) writes it only after that copy
+    uint32_t* d_bgra_alt = nullptr;
+    hipStream_t last_ls = nullptr;      // the stream of the last render launch
+    bool last_ovl = false;              // ... which was overlapped, and no call has joined the streams since
     double last_span_ms = 0.0;          // iqpt_kernel_time: first start to last end of the timed launches
 };
 
@@ -199,6 +207,7 @@ int join_streams(iqpt_ctx* c) {
     }
     c->next_on_main = true;
     c->ovl_zero = true;
+    c->last_ovl = false;
     return IQPT_OK;
 }
 
@@ -789,6 +798,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     free_scene(c);
     if (c->d_lin) (void)hipFree(c->d_lin);
     if (c->d_bgra) (void)hipFree(c->d_bgra);
+    if (c->d_bgra_alt) (void)hipFree(c->d_bgra_alt);
     if (c->d_rng) (void)hipFree(c->d_rng);
     if (c->d_rays) (void)hipFree(c->d_rays);
     if (c->d_queue) (void)hipFree(c->d_queue);
@@ -1342,6 +1352,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         p.xcd_order = c->d_xcd_order;
         std::memcpy(p.xcd_off, c->xcd_off, sizeof p.xcd_off);
         p.ovl_err = c->d_ovl_err;
+        if (c->d_bgra_alt) {
+            std::swap(c->d_bgra, c->d_bgra_alt);
+            p.bgra = c->d_bgra;
+        }
         IQPT_HIP(hipMemsetAsync(p.queue, 0, (iqpt::kOverlapQueueWords / 2) * sizeof(uint32_t), ls));
         // the next launch (stream2) starts after all of this but not after this launch
         if (ls == c->stream) IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
@@ -1408,6 +1422,8 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     }
     c->split_last = split;
     c->chain_last = chain;
+    c->last_ls = ls;
+    c->last_ovl = ovl;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1) (void)hipEventRecord(e1, ls);
     if (e0 && e1) c->timed.emplace_back(e0, e1);
@@ -1676,11 +1692,31 @@ int iqpt_copy_frame_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
 int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
     if (!c || !dst_device) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     if (bytes < (size_t)c->npix * sizeof(uint32_t)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
-    int st = enter(c);                    // (joins the overlapped launches' second stream: no host sync)
+    int st = use_device(c);
     if (st) return st;
-    const int le = iqpt::launch_relayout(c->stream, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
+    hipStream_t cs = c->stream;
+    if (c->last_ovl && c->last_ls) {
+        // overlapped launches in flight: copy on the last launch's stream without joining, so the next
+        // launch still overlaps this one (from here on overlapped launches alternate two frame buffers)
+        if (!c->d_bgra_alt && hipMalloc(&c->d_bgra_alt, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            c->d_bgra_alt = nullptr;
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "second frame buffer for overlapped copies");
+        }
+        cs = c->last_ls;
+        if (cs == c->stream2) c->s2_pending = true;
+    } else if ((st = join_streams(c)) != IQPT_OK) {
+        return st;
+    }
+    const int le = iqpt::launch_relayout(cs, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
                                          c->set.nrows, 1, 1, true);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
+    return IQPT_OK;
+}
+
+int iqpt_frame_stream(iqpt_ctx* c, void** stream) {
+    if (!c || !stream) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *stream = (void*)((c->last_ovl && c->last_ls) ? c->last_ls : c->stream);
     return IQPT_OK;
 }
 

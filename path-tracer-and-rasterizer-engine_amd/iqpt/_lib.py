@@ -98,6 +98,7 @@ SIGNATURES = [
     ("iqpt_copy_frame_device", C.c_int, [_P, _P, C.c_size_t]),
     ("iqpt_copy_frame_device_async", C.c_int, [_P, _P, C.c_size_t]),
     ("iqpt_stream", C.c_int, [_P, C.POINTER(C.c_void_p)]),
+    ("iqpt_frame_stream", C.c_int, [_P, C.POINTER(C.c_void_p)]),
     ("iqpt_set_split", C.c_int, [_P, C.c_int]),
     ("iqpt_set_overlap", C.c_int, [_P, C.c_int]),
     ("iqpt_kernel_span", C.c_int, [_P, C.POINTER(C.c_double)]),

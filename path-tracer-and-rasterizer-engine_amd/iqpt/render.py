@@ -99,7 +99,8 @@ class PathTracer:
 
     def copy_frame_device_async(self, dst_ptr: int, nbytes: int):
         """The BGRA8 frame into a device buffer, enqueued on the context's stream (no host sync;
-        iqpt_copy_frame_device_async). Order other work against stream_handle()."""
+        iqpt_copy_frame_device_async). Order other work against frame_stream_handle(), asked
+        right before this call (overlapped launches keep overlapping across the copy)."""
         check(self._lib.iqpt_copy_frame_device_async(self._h, C.c_void_p(dst_ptr), nbytes),
               "iqpt_copy_frame_device_async")
 
@@ -107,6 +108,13 @@ class PathTracer:
         """The context's hipStream_t (iqpt_stream), e.g. for torch.cuda.ExternalStream."""
         s = C.c_void_p()
         check(self._lib.iqpt_stream(self._h, C.byref(s)), "iqpt_stream")
+        return int(s.value or 0)
+
+    def frame_stream_handle(self) -> int:
+        """The hipStream_t copy_frame_device_async enqueues on now (iqpt_frame_stream): the last
+        render's stream while overlapped launches are in flight, else stream_handle()."""
+        s = C.c_void_p()
+        check(self._lib.iqpt_frame_stream(self._h, C.byref(s)), "iqpt_frame_stream")
         return int(s.value or 0)
 
     def set_split(self, mode: int):

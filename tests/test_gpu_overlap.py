@@ -129,3 +129,54 @@ def test_kernel_span_not_longer_than_sum(require_gpu):
     span = pt.kernel_span()
     assert n == 6 and 0.0 < span <= total * 1.0001
     pt.close()
+
+
+@pytest.mark.parametrize("preset,w,h,crop", [
+    ("cornell", 256, 144, None),
+    ("cornell", 1920, 1080, (640, 1280, 400, 2, 96)),          # the C3 N = 2 share shape
+])
+def test_async_frame_copies_keep_overlap(require_gpu, preset, w, h, crop):
+    """bench.py's stream-ordered gather: after every render a copy of the frame on iqpt_frame_stream,
+    without joining the streams. Launches keep overlapping (two frame buffers in turn) and every copy
+    is the frame of its own launch: the BGRA8 a one-stream context presents after the same launch."""
+    import torch
+    _, pk = scene_for(preset)
+    ps = pixel_set(w, h, *crop) if crop else None
+    launches = [3, 4, 2, 5, 3, 3]
+    cam = make_camera(w, h)
+
+    def ctx(overlap):
+        pt = PathTracer(w, h, pixels=ps, max_depth=8)
+        pt.set_split(_lib.SPLIT_OFF)
+        pt.set_overlap(_lib.OVERLAP_AUTO if overlap else _lib.OVERLAP_OFF)
+        pt.set_camera(cam)
+        pt.upload_packet(pk)
+        return pt
+
+    ref = ctx(False)
+    want = []
+    for s in launches:
+        ref.render(s)
+        want.append(ref.read()[1].view(np.uint32).ravel().copy())
+    ref_state = (ref.read()[0], ref.read()[1], ref.read_rng(), ref.rays(), ref.frames())
+    ref.close()
+
+    pt = ctx(True)
+    npix = want[0].size
+    bufs = [torch.empty(npix, dtype=torch.int32, device="cuda") for _ in launches]
+    opts, streams = [], set()
+    for s, b in zip(launches, bufs):
+        pt.render(s)
+        opts.append(last_options(pt))
+        streams.add(pt.frame_stream_handle())
+        pt.copy_frame_device_async(b.data_ptr(), b.numel() * 4)
+    assert all(o & K_OPT_OVERLAP for o in opts), opts
+    assert len(streams) == 2                   # copies followed their launches on both streams
+    pt.sync()
+    torch.cuda.synchronize()
+    for i, b in enumerate(bufs):
+        got = b.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, want[i]), f"copy after launch {i}"
+    lin, bgra = pt.read()
+    same((lin, bgra, pt.read_rng(), pt.rays(), pt.frames()), ref_state)
+    pt.close()
