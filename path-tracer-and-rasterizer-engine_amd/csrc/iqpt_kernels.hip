@@ -2620,6 +2620,19 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
                 ring_tag[e] = ptr;
             }
         } else if (gpix != ~0u && !active && cslot < G[5]) {
+#if defined(IQPT_CHAIN_NO_DEAD_SKIP)
+            const uint32_t ptr = 0u;
+#else
+            const uint32_t ptr = G[7];
+#endif
+            // slots behind the chain (inside a folded sample's scatter draws) are dead: step past them to
+            // this lane's first slot at or after ptr instead of tracing them (2 kL draws per slot skipped)
+            while (cslot < ptr) {
+                xorwow_skip_v(b0, b1, b2, b3, b4, 2u * kL);
+                cslot += kL;
+            }
+        }
+        if (gpix != ~0u && G[6] == 0u && !active && cslot < G[5]) {
             // start slot cslot: the state 2 cslot draws into the pixel's stream
             const uint32_t e = g * kR + cslot % kR;
             ring_st[e] = b0;
