@@ -2603,6 +2603,11 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
             xorwow_skip_v(b0, b1, b2, b3, b4, 2u * li);
             if (kCull && p.cull) lds_cm[lane] = make_uint4(G[14], G[15], G[8], 0u);
         }
+#if !defined(IQPT_CHAIN_NO_ABORT)
+        // a slot still being traced that the chain has passed was not on it (the walker folds only
+        // finished slots): it is dead, so stop tracing it
+        if (gpix != ~0u && active && G[6] == 0u && cslot < G[7]) active = false;
+#endif
         if (gpix != ~0u && G[6] != 0u) {
             // the chain is complete: drop the speculative slots; the lane of slot ptr provides its state
             active = false;
