@@ -252,6 +252,14 @@ def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
+    # The per-step gather's stream waits must not share a hardware queue with a render stream: with HIP's
+    # 4 queues per process the gather (torch / RCCL stream) and the context's stream land on one queue, and
+    # the gather's wait for launch k + 1's frame copy then holds launch k + 2 behind launch k + 1 (profiles/
+    # r02/c3_share2_gather_kernel_trace.csv). 8 queues give every stream its own: N = 2 share -10 %
+    # (profiles/r02/ab_hw_queues.json). Set before anything initialises HIP.
+    strong_gather = (int(os.environ.get("WORLD_SIZE", "1")) > 1 or args.self_gather) and args.scaling != "weak"
+    if strong_gather:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
     import numpy as np
     import torch
@@ -488,6 +496,7 @@ def main():
                        "split": args.split, "overlap": args.overlap, "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {})},
             "n_ranks_seen": n_ranks_seen,
+            "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             **({"gather": "stream-ordered" if stream_gather else "blocking", "gather_check": gather_check}
                if strong_multi else {}),
             "msamples_per_s": round(samples / elapsed / 1e6, 3),
