@@ -78,6 +78,7 @@ def parse():
                     help="A/B: render-kernel option mask (iqpt_debug_set_kernel_options; 0 = production)")
     ap.add_argument("--gather-sync", action="store_true",
                     help="N > 1: the blocking frame copy + gather of round 1 instead of the stream-ordered one")
+    ap.add_argument("--lib", default="", help="A/B only: load this prebuilt libiqpt (compile-time knob builds)")
     ap.add_argument("--share-of", type=int, default=0,
                     help="rehearsal at N = 1: render rank 0's rows of an N-way C3 split (one GPU's share; "
                          "with --self-gather the per-step gather path too)")
@@ -268,6 +269,8 @@ def main():
     import iqpt
     from iqpt import _lib
     from iqpt import dist as iqdist
+    if args.lib:
+        _lib.LIB_PATH = Path(args.lib).resolve()
     from iqpt.scene import CONFIGS, Scene, make_camera, packet_stats
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

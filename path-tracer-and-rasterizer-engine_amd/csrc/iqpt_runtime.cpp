@@ -162,6 +162,8 @@ struct iqpt_ctx {
     uint32_t chain_waves = 0;
     uint32_t chain_lanes = 8;           // lanes per pixel (4 or 8)
     bool chain_last = false;
+    uint32_t chain_par = 0;             // the queue-counter set of the next chain launch
+    bool chain_q_ready[2] = {false, false};   // that set is zeroed (in stream order)
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
     double tune_work[4] = {0.0, 0.0, 0.0, 0.0};
     // kOptOverlap: consecutive render launches alternate between `stream` and
@@ -1352,6 +1354,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         p.xcd_order = c->d_xcd_order;
         std::memcpy(p.xcd_off, c->xcd_off, sizeof p.xcd_off);
         p.ovl_err = c->d_ovl_err;
+        c->chain_q_ready[0] = c->chain_q_ready[1] = false;   // the overlapped launches' words (chain sets)
         if (c->d_bgra_alt) {
             std::swap(c->d_bgra, c->d_bgra_alt);
             p.bgra = c->d_bgra;
@@ -1370,7 +1373,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         opt |= iqpt::kOptCamAxis;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
+#if defined(IQPT_CHAIN_OLD_STREAMS)
     if (!ovl) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
+#else
+    if (!ovl && !chain) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
+#endif
     hipEvent_t e0 = take_event(c), e1 = take_event(c);
     if (e0) (void)hipEventRecord(e0, ls);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
@@ -1395,6 +1402,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const uint64_t want_c = (ns + px_per_wave - 1) / px_per_wave;
         const uint32_t grid_c = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_c, (uint64_t)c->num_cus * per_cu));
         p.ovl_err = c->d_ovl_err;
+#if defined(IQPT_CHAIN_OLD_STREAMS)
         IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
         IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
         le = iqpt::launch_chain(c->stream2, p, grid_c, opt, lanes);
@@ -1405,6 +1413,30 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             const uint32_t grid_p = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_p, (uint64_t)c->num_cus * occ));
             le = iqpt::launch_render(c->stream, p, grid_p, lds, stream_batches, opt);
         }
+#else
+        // The chain kernel (the launch's critical path) goes first on the context stream; the anchored
+        // kernel (shorter) follows on stream2 behind a cross-queue event, whose latency it absorbs. The
+        // queue counters alternate between two sets in the overlapped launches' words: this launch's set
+        // was zeroed behind the previous chain launch's anchored kernel, off the critical path.
+        uint32_t* const qset = c->d_queue + 4 + c->chain_par * (iqpt::kOverlapQueueWords / 2);
+        if (!c->chain_q_ready[c->chain_par]) IQPT_HIP(hipMemsetAsync(qset, 0, 4 * sizeof(uint32_t), c->stream));
+        p.queue = qset;
+        IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
+        IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
+        le = iqpt::launch_chain(c->stream, p, grid_c, opt, lanes);
+        if (le == 0 && c->n_anchor > 0) {
+            p.tile_order = c->d_split;
+            p.nqueue = c->n_anchor;
+            const uint64_t want_p = ((uint64_t)c->n_anchor * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
+            const uint32_t grid_p = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_p, (uint64_t)c->num_cus * occ));
+            le = iqpt::launch_render(c->stream2, p, grid_p, lds, stream_batches, opt);
+        }
+        const uint32_t nxt = c->chain_par ^ 1u;
+        IQPT_HIP(hipMemsetAsync(c->d_queue + 4 + nxt * (iqpt::kOverlapQueueWords / 2), 0, 4 * sizeof(uint32_t), c->stream2));
+        c->chain_q_ready[nxt] = true;
+        c->chain_q_ready[c->chain_par] = false;
+        c->chain_par = nxt;
+#endif
         IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
         IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
     } else if (split) {
