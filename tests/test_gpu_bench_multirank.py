@@ -38,3 +38,15 @@ def test_two_rank_strong_frame_equals_one_rank(require_gpu, tmp_path, gather):
     assert np.array_equal(f1.view(np.uint32), f2.view(np.uint32))
     # same work: the rays of two half frames add up to the rays of the whole frame
     assert two["rays_per_sample"] == one["rays_per_sample"]
+
+
+@pytest.mark.parametrize("share,mode", [(2, "plain"), (8, "chain")])
+def test_stream_ordered_gather_on_one_gpu(require_gpu, tmp_path, share, mode):
+    """The RCCL path the driver's N-GPU runs take, on one GPU: a one-rank nccl process group, rank 0's
+    rows of an N-way split, the stream-ordered frame copy + gather every step (copies that keep
+    overlapped launches overlapped at N = 2, chain launches at N = 8), 8 hardware queues."""
+    res, _ = _bench(tmp_path, 1, f"self{share}", ("--self-gather", "--share-of", str(share)))
+    assert res["gather"] == "stream-ordered" and res["gather_check"] is True
+    assert res["hw_queues"] == 8 and res["n_ranks_seen"] == 1
+    assert res["config"]["launch_mode"] == mode
+    assert res["bitexact_frac_vs_oracle"] == 1.0
