@@ -57,7 +57,8 @@ def parse():
                     help="wall time of the CPU-baseline sample (BASELINE.md §3: >= 60 s)")
     ap.add_argument("--verify-rows", type=int, default=16)
     ap.add_argument("--pmc-json", default="",
-                    help="PMC traffic of the config (tools/pmc_traffic.py; default profiles/r02/pmc_traffic_<config>.json)")
+                    help="PMC traffic of the config's launch (tools/pmc_traffic.py; default: the newest "
+                         "profiles/r0*/pmc_traffic_<config>*.json whose spp_per_launch equals this run's)")
     ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r02" / "c2_pmc_mix_v5.json"),
                     help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy)")
     ap.add_argument("--work-json", default="",
@@ -194,7 +195,28 @@ def load_json(path: str, cfg_name: str):
     return d if d.get("config") == cfg_name else None
 
 
-def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name) -> dict:
+BYTES_PER_PIXEL_LAUNCH = 84     # RNG 24 read + 24 written, accumulator 16 + 16, BGRA8 4
+
+
+def find_pmc(cfg_name: str, spp: int, explicit: str):
+    """The PMC traffic profile of THIS launch shape: same config and same samples per launch (traffic
+    per launch grows with spp only through the kernel's own re-reads, but a 1-spp profile divided by a
+    16-spp kernel time is meaningless). Returns (profile, path) or (None, why)."""
+    cands = [Path(explicit)] if explicit else sorted(
+        (REPO / "profiles").glob(f"r0*/pmc_traffic_{cfg_name}*.json"), key=lambda q: q.parent.name, reverse=True)
+    why = "no PMC profile of this config"
+    for c in cands:
+        d = load_json(str(c), cfg_name)
+        if not d:
+            continue
+        if d.get("spp_per_launch") != spp:
+            why = f"{c.relative_to(REPO)} was taken at {d.get('spp_per_launch')} spp per launch, this run launches {spp}"
+            continue
+        return d, str(c.relative_to(REPO))
+    return None, why
+
+
+def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name, spp: int, npix_owned: int) -> dict:
     """The dominant kernel against the FP32 vector (VALU) peak.
 
     C1/C2/C3: algorithmic FLOPs F_ray = 52 T + 19 S per ray (the reference's brute-force
@@ -205,14 +227,10 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name) -> dic
     f_ray = cfg.flops_per_ray
     t = kern_avg_ms * 1e-3
     ref_tflops = f_ray * rays_per_launch / t / 1e12 if t > 0 else 0.0
-    traffic = None
-    pmc = None
-    for cand in ([args.pmc_json] if args.pmc_json else
-                 [str(REPO / "profiles" / "r02" / f"pmc_traffic_{cfg.name}.json"),
-                  str(REPO / "profiles" / f"r01_pmc_traffic_{cfg.name}_v4.json")]):
-        pmc = pmc or load_json(cand, cfg.name)
-    if pmc and world == 1:
-        traffic = pmc.get("hbm_bytes_per_launch")
+    # PMC bytes only for the launch shape they were measured on (one GPU's full frame at this spp); the
+    # algorithmic bytes (84 B per owned pixel per launch) for every line, rank 0's share at N > 1
+    pmc, pmc_src = find_pmc(cfg.name, spp, args.pmc_json) if world == 1 and not args.share_of else (None, "N > 1: per-rank PMC not collected")
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     mix = load_json(args.pmc_mix_json, cfg.name)
     work_path = args.work_json or str(REPO / "profiles" / "r02" / f"work_{cfg.name}.json")
     work = load_json(work_path, cfg.name)
@@ -238,15 +256,33 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name) -> dic
         out.update(achieved=None, frac=None, flops_per_ray=None,
                    work_basis="none: run tools/work_counters.py for the executed-work price",
                    reference_equivalent={"achieved": round(ref_tflops, 2), "flops_per_ray": f_ray})
-    if traffic and t > 0:
-        out["hbm"] = {"achieved": round(traffic / t / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                      "frac": round(traffic / t / 1e9 / HBM_PEAK_GBPS, 5)}
+    if t > 0:
+        alg = BYTES_PER_PIXEL_LAUNCH * npix_owned
+        out["hbm"] = {"achieved": round(alg / t / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                      "frac": round(alg / t / 1e9 / HBM_PEAK_GBPS, 6), "basis": "algorithmic",
+                      "bytes_per_launch": alg, "pixels_per_launch": npix_owned}
+        if traffic:
+            out["hbm"].update(pmc_bytes_per_launch=round(traffic), pmc_achieved=round(traffic / t / 1e9, 2),
+                              pmc_frac=round(traffic / t / 1e9 / HBM_PEAK_GBPS, 6), pmc_source=pmc_src)
+        else:
+            out["hbm"]["pmc_source"] = None
+            out["hbm"]["pmc_missing"] = pmc_src
     out["note"] = ("achieved = FLOPs per launch / kernel_avg_ms (the HIP-event span of the timed launches / their "
                    "number: overlapped launches run two at a time, launch_duration_ms is one launch's own) against the FP32 "
                    "vector peak; the path runs on the VALU, nothing is a dense contraction (no MFMA). traffic: "
                    "PMC HBM bytes per launch (tools/pmc_traffic.py); valu_busy_frac / wave_time_split: PMC "
                    "instruction-mix pass (tools/pmc_mix.py), profiles/.")
     return out
+
+
+def fma_flavour_rmse():
+    """How far a contracting (nvcc-default-like) build of the same algorithm sits from the parity target on
+    the full C2 frame (tools/fp_flavours.py): the size of the unpinned part."""
+    try:
+        d = json.loads((REPO / "profiles" / "r02" / "fp_flavours.json").read_text())
+        return d["cases"]["c2_full"]["FMA_vs_B"]["rmse"]
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def main():
@@ -472,6 +508,7 @@ def main():
         gathered = "BGRA8 frame" if args.gather == "frame" else "float4 accumulators"
         out = {
             "metric": "Mrays/sec at 1920x1080 8-bounce; per-pixel RMSE vs reference",
+            # "RMSE vs reference" is measured against the oracle restatement (parity_basis below)
             "value": round(mrays, 3),
             "unit": "Mrays/s",
             "n_gpus": world,
@@ -507,7 +544,12 @@ def main():
             "rmse_vs_oracle": rmse_v,
             "bitexact_frac_vs_oracle": bitexact,
             "setup_ms": {k: round(v, 2) for k, v in setup.items()},
-            "roofline": roofline(cfg, args, world, rays_per_launch, kern_avg_ms, iqpt.kernel_name()),
+            "parity_basis": ("bit-exact vs the CPU oracle (oracle/iqpt_oracle.c: the reference restated with "
+                             "FMA contraction off and shared iq_fp.h transcendentals); unpinned vs the nvcc/cuRAND "
+                             "reference binary, which cannot be built here"),
+            "fma_flavour_rmse_c2": fma_flavour_rmse(),
+            "roofline": roofline(cfg, args, world, rays_per_launch, kern_avg_ms, iqpt.kernel_name(), spp_step,
+                                 (ps.x1 - ps.x0) * ps.nrows),
         }
         out["roofline"]["launch_duration_ms"] = round(kern_ms / max(1, launches), 4)
         out["roofline"]["overlapped_launches"] = bool(kern_span_ms < 0.98 * kern_ms)

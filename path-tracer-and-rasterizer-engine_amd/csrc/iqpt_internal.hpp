@@ -60,7 +60,6 @@ struct kparams {
     // (z_n, z_f: unprojected z of the near / far point divided by its w)
     float cam_ax[16];
     uint32_t acc_tab;                // build the per-launch (1/n, (n-1)/n) table in LDS
-    uint32_t diag;                   // kOptDiag ablation bits (A/B builds): 1 camera ray, 2 intersection, 4 mean
     uint32_t frames32;               // frame0 + spp < 2^32: 32-bit frame-counter conversions
     float mean_tiny;                 // kOptFastDiv running mean: c below this takes the IEEE division
     const float4_storage* tris;      // ntri * kTriFloat4 (single layout)
@@ -153,14 +152,20 @@ struct kparams {
     uint32_t done_target;            // k: launches of the chain before this one (0: no wait)
     const uint32_t* xcd_order;
     uint32_t xcd_off[9];
-    uint32_t* ovl_err;               // bit 0: a wait exceeded kOverlapSpinLimit (never expected)
+    uint32_t* ovl_err;               // bit 0: a wait exceeded spin_limit, bit 1: a chain wave exceeded iter_limit,
+                                     // bit 2: an XCD's tile list was never taken (no workgroup ran there)
+    // forward-progress bounds (never reached by a real launch; iqpt_debug_set_limits lowers them so that
+    // tests can force each one): s_sleep polls of one per-tile wait, loop iterations of one chain wave
+    uint32_t spin_limit, iter_limit;
     // queue length of the plain kernel's tile queue (tile_order[0 .. nqueue)); 0: every tile (ntiles).
     // Chain launches give the plain kernel the anchored tiles only.
     uint32_t nqueue;
 };
 constexpr int kSphNodeFloat4 = 3;
 constexpr uint32_t kOverlapSpinLimit = 1u << 23;   // s_sleep(20) polls before a wait gives up (~seconds)
-constexpr uint32_t kOverlapQueueWords = 2 * 8 * 16; // two launch parities x 8 XCD queue words, 64 B apart
+constexpr uint32_t kChainIterLimit = 1u << 22;     // chain-kernel loop iterations before a wave gives up
+// two launch parities x (8 XCD queue words + the finished-block count), 64 B apart
+constexpr uint32_t kOverlapQueueWords = 2 * 9 * 16;
 
 // iqpt_split_prep_kernel / iqpt_split_stitch_kernel (kOptSplit).
 struct ksplit {
@@ -254,8 +259,6 @@ constexpr int kOptMaterials = 1 << 10; // per-primitive material table (RGB scat
 constexpr int kOptBvh = 1 << 11;       // secondary rays traverse the exact BVH (streamed scenes; inert
                                        // when the packet has none)
 constexpr int kOptBvhPrimary = 1 << 12; // camera rays take the BVH too (instead of the tile masks)
-constexpr int kOptDiag = 1 << 13;      // A/B builds only: timing ablations selected by kparams::diag (NOT exact)
-constexpr int kOptExp = 1 << 15;       // A/B builds only: an alternative formulation under test (exact)
 constexpr int kOptCamAxis = 1 << 14;   // short camera transform for pitch-only cameras (kparams::cam_ax; the runtime
                                        // checks the zero pattern and the frame-wide normalization bounds)
 constexpr int kOptSplit = 1 << 16;     // sample-parallel chains: speculative runs + anchored lanes (kparams::split_round)

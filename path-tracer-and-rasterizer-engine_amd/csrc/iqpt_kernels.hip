@@ -202,23 +202,14 @@ __device__ __forceinline__ void camera_ndc(const kparams& p, float x_ndc, float 
 template <int OPT>
 __device__ __forceinline__ void camera_ray_axis(const kparams& p, float x_ndc, float y_ndc, ray3& r) {
     const float* k = p.cam_ax;
-    f2 wx, wy, wz;                                  // (near, far) world-space points
-    if (OPT & kOptExp) {
-        // scalar form (A/B)
-        const float xp = x_ndc * k[0] + k[2], yp = y_ndc * k[1] + k[3];
-        const float xn = xp * k[4], xf = xp * k[5], yn = yp * k[4], yf = yp * k[5];
-        wx = (f2){xn * k[6] + k[7], xf * k[6] + k[7]};
-        wy = (f2){(yn * k[8] + k[12]) + k[10], (yf * k[8] + k[13]) + k[10]};
-        wz = (f2){(yn * k[9] + k[14]) + k[11], (yf * k[9] + k[15]) + k[11]};
-    } else {
-        const f2 nf_rw = {k[4], k[5]};              // 1 / w_near, 1 / w_far
-        const f2 xw = (x_ndc * k[0] + k[2]) * nf_rw;   // (((x P[0] + y P[4]) + z P[8]) + P[12]) / w
-        const f2 yw = (y_ndc * k[1] + k[3]) * nf_rw;   // (((x P[1] + y P[5]) + z P[9]) + P[13]) / w
-        const f2 kzy = {k[12], k[13]}, kzz = {k[14], k[15]};
-        wx = xw * k[6] + k[7];                      // ((x V[0] + y V[4]) + z V[8]) + V[12]
-        wy = (yw * k[8] + kzy) + k[10];             // ((x V[1] + y V[5]) + z V[9]) + V[13]
-        wz = (yw * k[9] + kzz) + k[11];             // ((x V[2] + y V[6]) + z V[10]) + V[14]
-    }
+    // (near, far) world-space points, both in one packed register pair
+    const f2 nf_rw = {k[4], k[5]};                  // 1 / w_near, 1 / w_far
+    const f2 xw = (x_ndc * k[0] + k[2]) * nf_rw;    // (((x P[0] + y P[4]) + z P[8]) + P[12]) / w
+    const f2 yw = (y_ndc * k[1] + k[3]) * nf_rw;    // (((x P[1] + y P[5]) + z P[9]) + P[13]) / w
+    const f2 kzy = {k[12], k[13]}, kzz = {k[14], k[15]};
+    const f2 wx = xw * k[6] + k[7];                 // ((x V[0] + y V[4]) + z V[8]) + V[12]
+    const f2 wy = (yw * k[8] + kzy) + k[10];        // ((x V[1] + y V[5]) + z V[9]) + V[13]
+    const f2 wz = (yw * k[9] + kzz) + k[11];        // ((x V[2] + y V[6]) + z V[10]) + V[14]
     float dx = wx.y - wx.x, dy = wy.y - wy.x, dz = wz.y - wz.x;
     // normalize3 without the zero branch; len in [1e-5, 2^100): iq_rcp is exact (kOptFastDiv)
     const float len = sqrt_n<OPT>((dx * dx + dy * dy) + dz * dz);
@@ -1093,8 +1084,7 @@ constexpr int min_waves_per_simd() {
     // kOptSplit variants are built for 4 waves/SIMD (<= 128 VGPRs): with 5 their refill and path-end
     // bookkeeping spilled 9 VGPRs to scratch, and at the low occupancy of a multi-GPU row share a scratch
     // reload's latency is not hidden
-    // (A/B builds: kOptExp with kOptSplit keeps the 5-wave bound, spills and all)
-    return (OPT & kOptSplit) ? (((OPT & kOptExp) && (OPT & kOptLB5)) ? 5 : 4)
+    return (OPT & kOptSplit) ? 4
                              : ((OPT & kOptLB6) ? 6 : ((OPT & kOptLB5) ? 5 : (STREAM ? 4 : 1)));
 }
 
@@ -1290,7 +1280,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                             uint32_t spins = 0;
                             while (__hip_atomic_load(p.tile_done + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < need) {
                                 __builtin_amdgcn_s_sleep(20);
-                                if (++spins > kOverlapSpinLimit) {
+                                if (++spins > p.spin_limit) {
                                     atomicOr(p.ovl_err, 1u);
                                     break;
                                 }
@@ -1413,7 +1403,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             need = __ballot(!active);
         }
         if (kSplit) spec_mask = __ballot(active && lds_sp[threadIdx.x].w == 1u);
-        if ((OPT & kOptPrio) && !(OPT & kOptExp) && kCull && p.cull) {
+        if ((OPT & kOptPrio) && kCull && p.cull) {
             // a wave holding pixels of a tile with sphere candidates (chains that scatter: the launch's
             // longest) wins VALU arbitration against wall / sky waves
             if (__ballot(active && lds_cm[threadIdx.x].y != 0u) != 0ull) __builtin_amdgcn_s_setprio(3);
@@ -1436,11 +1426,6 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
         if (kSplit && need_cam) {
             camera_ray<OPT>(p, px, py, st, ray);
             need_cam = false;
-        }
-        if ((OPT & kOptPrio) && (OPT & kOptExp)) {
-            // per iteration: a wave tracing a secondary ray wins VALU arbitration
-            if (__any(active && depth != 0)) __builtin_amdgcn_s_setprio(3);
-            else __builtin_amdgcn_s_setprio(0);
         }
         if (OPT & kOptStats) {
             ++s_iter;
@@ -1508,11 +1493,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             const bool tri_all = active && tile_mask == nullptr && !bvh_lane;
             // the spheres through the sphere BVH (same rays as the triangle BVH) instead of the batches
             const bool sbvh_lane = bvh_ray && p.sbvh_nodes != nullptr;
-            // kOptDiag timing ablations (A/B builds, not exact): 8 = secondary rays skip the spheres,
-            // 16 = secondary rays skip the triangle BVH
-            const bool diag_nosph = (OPT & kOptDiag) && (p.diag & 8u) && depth != 0;
-            const bool diag_nobvh = (OPT & kOptDiag) && (p.diag & 16u) && depth != 0;
-            const bool sph_all = active && tile_mask == nullptr && !diag_nosph && !sbvh_lane;
+            const bool sph_all = active && tile_mask == nullptr && !sbvh_lane;
             const uint32_t* sph_mask = sbvh_lane ? nullptr : tile_mask;
             // One tile for every lane that contributes mask words (and no lane that needs every pair): the
             // wave's OR is that tile's mask, read with uniform loads instead of a DPP OR per word
@@ -1596,7 +1577,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 for (uint32_t i = threadIdx.x; i < n * kTriRec; i += kRenderBlock)
                     lds_tri[i] = g_tri[(size_t)base * kTriRec + i];
                 __syncthreads();
-                if (active && !bvh_lane && !list_tri && !((OPT & kOptDiag) && (p.diag & 32u))) {   // diag 32: no pair tests
+                if (active && !bvh_lane && !list_tri) {
                     const uint32_t first = base * kTriPer;
                     const uint32_t cnt = min(n * kTriPer, p.ntri - first);
                     if (kWords) {
@@ -1618,7 +1599,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 }
             }
             // secondary rays: triangles through the exact BVH (iq_bvh.hpp), before the spheres
-            if (bvh_lane && !diag_nobvh) {
+            if (bvh_lane) {
                 if (OPT & kOptStats) ++c_tri_rays;
                 bvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_tri : nullptr);
             }
@@ -1657,7 +1638,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 for (uint32_t i = threadIdx.x; i < n * kSphRec; i += kRenderBlock)
                     lds_sph[i] = g_sph[(size_t)base * kSphRec + i];
                 __syncthreads();
-                if (active && !diag_nosph && !sbvh_lane && !list_sph) {
+                if (active && !sbvh_lane && !list_sph) {
                     const uint32_t first = base * kSphPer;
                     const uint32_t cnt = min(n * kSphPer, p.nsph - first);
                     if (kWords) {
@@ -1678,16 +1659,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     }
                 }
             }
-            if (sbvh_lane && !diag_nosph) {
+            if (sbvh_lane) {
                 if (OPT & kOptStats) ++c_sph_rays;
                 sbvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_sph : nullptr);
-            }
-        } else if ((OPT & kOptDiag) && (p.diag & 2u)) {
-            // diagnostic: no intersection; every ray hits triangle 0 at t = 1
-            if (active) {
-                closest = 1.0f;
-                kind = kHitTri;
-                hidx = 0;
             }
         } else if (kCull && p.cull != nullptr) {
             uint4 cm = lds_cm[threadIdx.x];
@@ -1895,9 +1869,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 nf = p.frames32 ? (float)(uint32_t)n : (float)n;
                 keep = (p.frames32 ? (float)(uint32_t)(n - 1) : (float)(n - 1)) / nf;
             }
-            if ((OPT & kOptDiag) && (p.diag & 4u)) {
-                acc.x += cx;                     // diagnostic: no running-mean arithmetic
-            } else if (use_tab) {
+            if (use_tab) {
                 float qx, qy, qz;
                 mean_terms<OPT>(cx, cy, cz, nf, rc, p.mean_tiny, qx, qy, qz);
                 acc.x = qx + acc.x * keep;
@@ -1926,10 +1898,6 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 if (kOverlap) finished = true;
                 if (kSplit && light_sp != ~0u) p.sp_rho[light_sp] = (uint32_t)(((uint64_t)light_slots * 256u) / p.spp);
                 active = false;
-            } else if ((OPT & kOptDiag) && (p.diag & 1u)) {
-                // diagnostic (timing ablation, not the reference): keep the RNG draws, reuse the ray
-                ray.dx += 1e-7f * (float)xorwow_next(st);
-                ray.dy += 1e-7f * (float)xorwow_next(st);
             } else {
                 if (kSplit) need_cam = true;   // one camera_ray call site per iteration (loop top)
                 else camera_ray<OPT>(p, px, py, st, ray);
@@ -1957,6 +1925,20 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
 
     // closest-hit query count: one atomic per wave
     if (lane == 0 && wave_rays) atomicAdd(p.rays, (unsigned long long)wave_rays);
+    if (kOverlap && p.ovl_err) {
+        // HIP promises no workgroup -> XCD placement: the last block to finish checks that every XCD's
+        // tile list was taken to its end (a list no wave ran on would leave its tiles unrendered, silently)
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t fin = atomicAdd(p.queue + 16u * 8u, 1u);
+            if (fin == gridDim.x - 1u) {
+                for (uint32_t x = 0; x < 8u; ++x)
+                    if (__hip_atomic_load(p.queue + 16u * x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) <
+                        p.xcd_off[x + 1] - p.xcd_off[x])
+                        atomicOr(p.ovl_err, 4u);
+            }
+        }
+    }
     if (OPT & kOptStats) {
         unsigned long long scat = s_scatter_lanes;
 #pragma unroll
@@ -2401,15 +2383,8 @@ __global__ __launch_bounds__(kStitchBlock) void iqpt_split_stitch_kernel(const k
 // as rays. The pixels come from the split set (tiles whose camera rays may scatter, under the
 // reference's materials); the other tiles run anchored in iqpt_render_kernel beside this kernel.
 constexpr uint32_t kChainBlock = 64;                   // one wave per block
-constexpr uint32_t kChainIterLimit = 1u << 22;         // loop iterations before a wave gives up (error bit 2)
-#ifndef IQPT_CHAIN_WAVES
-#define IQPT_CHAIN_WAVES 4
-#endif
-#ifndef IQPT_CHAIN_RING_MUL
-#define IQPT_CHAIN_RING_MUL 2
-#endif
-constexpr int kChainWaves = IQPT_CHAIN_WAVES;          // __launch_bounds__ waves per SIMD
-constexpr uint32_t kChainRingMul = IQPT_CHAIN_RING_MUL; // ring entries per lane
+constexpr int kChainWaves = 4;                         // __launch_bounds__ waves per SIMD
+constexpr uint32_t kChainRingMul = 2;                  // ring entries per lane
 
 __device__ __forceinline__ void xorwow_skip_v(uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& v3, uint32_t& v4,
                                               uint32_t n) {
@@ -2472,16 +2447,9 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
     rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
     uint32_t b0 = 0u, b1 = 0u, b2 = 0u, b3 = 0u, b4 = 0u, cslot = 0u, gen_seen = 0u;
     uint32_t guard = 0u;               // iterations: a bound every wave reaches (never expected to bind)
-#if defined(IQPT_AB_VARIANTS)
-    // timing ablations (A/B library only, NOT exact): 64 fold without the mean, 128 no stream stepping,
-    // 256 no workgroup barriers, 512 no closest hit (every ray misses)
-    const uint32_t dg = p.diag;
-#else
-    constexpr uint32_t dg = 0u;
-#endif
 
     while (true) {
-        if (++guard > kChainIterLimit) {
+        if (++guard > p.iter_limit) {
             if (lane == 0 && p.ovl_err) atomicOr(p.ovl_err, 2u);
             break;
         }
@@ -2566,13 +2534,11 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
                     const uint32_t nsl = __float_as_uint(r.w);
                     if (nsl == 0u) break;
                     const float2 tv = lds_tab[w_k];
-                    if (!(dg & 64u)) {
-                        float qx, qy, qz;
-                        mean_terms<OPT>(r.x, r.y, r.z, lds_tab_n[w_k], tv.x, p.mean_tiny, qx, qy, qz);
-                        ax = qx + ax * tv.y;
-                        ay = qy + ay * tv.y;
-                        az = qz + az * tv.y;
-                    }
+                    float qx, qy, qz;
+                    mean_terms<OPT>(r.x, r.y, r.z, lds_tab_n[w_k], tv.x, p.mean_tiny, qx, qy, qz);
+                    ax = qx + ax * tv.y;
+                    ay = qy + ay * tv.y;
+                    az = qz + az * tv.y;
                     w_rays += (nsl - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : nsl;
                     w_ptr += nsl;
                     ++w_k;
@@ -2587,7 +2553,7 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
                 }
             }
         }
-        if (!(dg & 256u)) __syncthreads();
+        __syncthreads();
         // ---- B. lanes: a new pixel, a chain's end, slot starts
         const uint32_t gpix = G[0];
         const uint32_t gen = G[4];
@@ -2603,11 +2569,9 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
             xorwow_skip_v(b0, b1, b2, b3, b4, 2u * li);
             if (kCull && p.cull) lds_cm[lane] = make_uint4(G[14], G[15], G[8], 0u);
         }
-#if !defined(IQPT_CHAIN_NO_ABORT)
         // a slot still being traced that the chain has passed was not on it (the walker folds only
         // finished slots): it is dead, so stop tracing it
         if (gpix != ~0u && active && G[6] == 0u && cslot < G[7]) active = false;
-#endif
         if (gpix != ~0u && G[6] != 0u) {
             // the chain is complete: drop the speculative slots; the lane of slot ptr provides its state
             active = false;
@@ -2625,11 +2589,7 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
                 ring_tag[e] = ptr;
             }
         } else if (gpix != ~0u && !active && cslot < G[5]) {
-#if defined(IQPT_CHAIN_NO_DEAD_SKIP)
-            const uint32_t ptr = 0u;
-#else
             const uint32_t ptr = G[7];
-#endif
             // slots behind the chain (inside a folded sample's scatter draws) are dead: step past them to
             // this lane's first slot at or after ptr instead of tracing them (2 kL draws per slot skipped)
             while (cslot < ptr) {
@@ -2654,16 +2614,14 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
         }
         const bool more = walker && !w_done;
         if (!__any(active) && !__any(more) && !__any(w_fin)) break;
-        if (!(dg & 256u)) __syncthreads();
+        __syncthreads();
         if (!__any(active)) continue;
 
         // ---- C. one bounce of every traced slot (the anchored kernel's closest hit and shading)
         float closest = kTMax;
         int kind = kHitNone;
         uint32_t hidx = 0;
-        if (dg & 512u) {
-            // ablation: every ray misses
-        } else if (kCull && p.cull != nullptr) {
+        if (kCull && p.cull != nullptr) {
             const bool cull = !__any(active && depth != 0);
             const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[lane].z * p.cull_stride : nullptr;
             uint4 cm = lds_cm[lane];
@@ -2729,12 +2687,12 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
                 // slots consumed: 1 + the scatters (two draws each)
                 const uint32_t nsl = (uint32_t)depth + 1u + md_end;
                 ring_res[g * kR + cslot % kR] = make_float4(cx, cy, cz, __uint_as_float(nsl));
-                if (!(dg & 128u)) xorwow_skip_v(b0, b1, b2, b3, b4, 2u * kL);
+                xorwow_skip_v(b0, b1, b2, b3, b4, 2u * kL);
                 cslot += kL;
                 active = false;
             }
         }
-        if (!(dg & 256u)) __syncthreads();
+        __syncthreads();
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) w_rays += __shfl_xor(w_rays, off);
@@ -2762,8 +2720,8 @@ int occ_t(uint32_t lds, int* blocks) {
                                                              kRenderBlock, lds);
 }
 
-// Variant table: the production option set for every (MAXD, STREAM), plus (in IQPT_AB_VARIANTS
-// builds) the A/B set used by tools/ab_kernel.py.
+// Variant table: the production option set for every (MAXD, STREAM), plus (IQPT_STATS_VARIANTS builds)
+// the instrumented kOptStats variants.
 struct variant {
     int maxd;
     bool stream;
@@ -2808,41 +2766,16 @@ const variant kVariants[] = {
     IQPT_V(8, false, kOptDefault | kOptMaterials | kOptSplit | kOptPrio),
     IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptMaterials | kOptSplit | kOptPrio),
 #undef IQPT_PROD
-#if defined(IQPT_AB_VARIANTS)
-    IQPT_V(8, false, 0),
-    IQPT_V(8, true, 0),
-    IQPT_V(8, false, kOptDefault & ~kOptPair),
-    IQPT_V(8, true, kOptDefault & ~kOptPair),
-    IQPT_V(8, false, kOptDefault & ~kOptSinCos),
-    IQPT_V(8, false, kOptDefault | kOptLB5),
-    IQPT_V(8, false, kOptDefault | kOptLB6),
-    IQPT_V(8, false, kOptDefault | kOptBranchless),
-    IQPT_V(8, false, kOptDefault | kOptBranchless | kOptLB5),
-    IQPT_V(8, false, (kOptDefault & ~kOptPair) | kOptLB6),
-    IQPT_V(8, true, kOptDefault | kOptLB5),
+#if defined(IQPT_STATS_VARIANTS)
+    // instrumented build (libiqpt_stats.so, tools/work_counters.py and the wave timelines of tools/):
+    // kOptStats counts the primitive and node tests each query executes (the executed-work roofline)
     IQPT_V(8, false, kOptDefault | kOptStats),
-    IQPT_V(8, true, kOptDefault | kOptStats),
-    IQPT_V(8, true, ((kOptDefault | kOptStats | kOptBvhPrimary) & ~kOptLB5)),
-    IQPT_V(8, true, ((kOptDefault | kOptBvhPrimary) & ~kOptLB5)),       // BVH-primary at 4 waves/SIMD
+    IQPT_V(8, false, kOptDefault | kOptPrio | kOptStats),
     IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptStats),
-    IQPT_V(8, false, kOptDefault & ~kOptCull),
-    IQPT_V(8, true, kOptDefault & ~kOptCull),
-    IQPT_V(8, false, kOptDefault & ~kOptCull & ~kOptFastDiv),
-    IQPT_V(8, true, kOptDefault & ~kOptBvh),
-    IQPT_V(8, false, kOptDefault | kOptDiag),
-    IQPT_V(8, true, ((kOptDefault | kOptBvhPrimary | kOptDiag) & ~kOptLB5)),
-    IQPT_V(8, true, ((kOptDefault | kOptDiag) & ~kOptLB5)),
-    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptExp),
-    IQPT_V(8, true, (kOptDefault | kOptMaterials) & ~kOptBvh),
+    IQPT_V(8, true, (kOptDefault | kOptStats) & ~kOptLB5),
+    IQPT_V(8, true, kOptDefault | kOptStats | kOptBvhPrimary),
+    IQPT_V(8, true, (kOptDefault | kOptStats | kOptBvhPrimary) & ~kOptLB5),
     IQPT_V(8, false, kOptDefault | kOptSplit | kOptStats),
-    IQPT_V(8, false, kOptDefault | kOptExp), IQPT_V(8, false, kOptDefault | kOptExp | kOptSplit),
-    // round 2: no priority, per-iteration priority, scalar scatter transcendentals (profiles/r02/ab_prio.json,
-    // ab_scatter2.json)
-    IQPT_V(8, false, kOptDefault), IQPT_V(8, false, kOptDefault | kOptPrio | kOptExp),
-    IQPT_V(8, false, kOptDefault | kOptPrio | kOptStats), IQPT_V(8, false, kOptDefault | kOptSplit),
-    IQPT_V(8, false, (kOptDefault & ~kOptScatter2) | kOptPrio),
-    IQPT_V(8, false, ((kOptDefault & ~kOptScatter2) | kOptPrio | kOptStats)),
-    IQPT_V(8, false, kOptDefault & ~kOptScatter2),
 #endif
 };
 #undef IQPT_V

@@ -85,6 +85,7 @@ struct iqpt_ctx {
     int max_depth = 0;
     uint64_t frame = 0;
     int num_cus = 0;
+    int num_xcc = 0;              // XCDs of the device (overlapped launches bind tiles to the 8 XCDs)
     int opt = iqpt::kOptDefault;
     bool have_camera = false, have_packet = false;
     iqpt_camera cam{};
@@ -135,7 +136,6 @@ struct iqpt_ctx {
     // the first two launches after a packet upload time faster per sample (results are identical);
     // tools/ab_kernel.py fixes the option set instead (opt_fixed)
     bool opt_fixed = false;
-    uint32_t diag = 0;           // kOptDiag ablation bits (tools/ab_kernel.py)
     // stages 0..kTuneLaunches-1 time masks (even) and the BVH (odd) alternately; stage kTuneLaunches
     // decides on the fastest launch of each; reset by a packet upload or a camera change
     int tune_stage = 0;
@@ -190,6 +190,13 @@ struct iqpt_ctx {
     hipStream_t last_ls = nullptr;      // the stream of the last render launch
     bool last_ovl = false;              // ... which was overlapped, and no call has joined the streams since
     double last_span_ms = 0.0;          // iqpt_kernel_time: first start to last end of the timed launches
+    // forward-progress bounds of the kernels (iqpt_debug_set_limits lowers them in tests) and a bias added
+    // to the per-tile wait targets of overlapped launches (tests: a wait that can never be satisfied)
+    uint32_t spin_limit = iqpt::kOverlapSpinLimit, iter_limit = iqpt::kChainIterLimit, wait_bias = 0;
+    // the kernels' error word, latched at the first synchronising call that sees it: after a wait that
+    // gave up or a chain wave past its bound the pixel state is undefined, so every later call that
+    // returns or persists pixel state fails until iqpt_checkpoint_load replaces the whole state
+    uint32_t dev_err = 0;
 };
 
 namespace {
@@ -689,6 +696,21 @@ int store_compact(iqpt_ctx* c, const void* host, uint32_t words, uint32_t planes
     return e == hipSuccess ? IQPT_OK : iqpt::hip_fail(e, "upload");
 }
 
+// After the context's streams are synchronised: read the kernels' error word and latch it (see
+// iqpt_ctx::dev_err). Returns IQPT_ERR_HIP while an error is latched.
+int check_dev_err(iqpt_ctx* c) {
+    if (!c->dev_err) {
+        uint32_t err = 0;
+        IQPT_HIP(hipMemcpy(&err, c->d_ovl_err, sizeof err, hipMemcpyDeviceToHost));
+        c->dev_err = err;
+    }
+    if (!c->dev_err) return IQPT_OK;
+    return iqpt::fail(IQPT_ERR_HIP, std::string((c->dev_err & 2u)   ? "chain launch: a wave exceeded its iteration bound"
+                                                : (c->dev_err & 4u) ? "overlapped launch: an XCD's tiles were never taken"
+                                                                    : "overlapped launch: a per-tile wait timed out") +
+                                        " (pixel state undefined until iqpt_checkpoint_load)");
+}
+
 hipEvent_t take_event(iqpt_ctx* c) {
     if (!c->event_pool.empty()) {
         hipEvent_t e = c->event_pool.back();
@@ -759,6 +781,10 @@ int iqpt_create(int device, uint32_t width, uint32_t height, const iqpt_pixel_se
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return cleanup(iqpt::fail(IQPT_ERR_HIP, "hipGetDeviceProperties"));
     c->num_cus = prop.multiProcessorCount;
+    if (hipDeviceGetAttribute(&c->num_xcc, hipDeviceAttributeNumberOfXccs, device) != hipSuccess) {
+        (void)hipGetLastError();
+        c->num_xcc = 0;
+    }
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
         return cleanup(iqpt::fail(IQPT_ERR_HIP, "hipStreamCreate"));
     const size_t n = c->npix;
@@ -830,6 +856,9 @@ int iqpt_set_camera(iqpt_ctx* c, const iqpt_camera* cam) {
     if (!c || !cam) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     if (cam->width != c->width || cam->height != c->height)
         return iqpt::fail(IQPT_ERR_INVALID_ARG, "camera size differs from the context frame");
+    // an interactive loop sets the camera every frame: the same view keeps its tile masks and the
+    // camera-ray path decision (only a changed view is binned and timed again)
+    if (c->have_camera && std::memcmp(&c->cam, cam, sizeof *cam) == 0) return IQPT_OK;
     c->cam = *cam;   // passed by value to every launch: no device copy to race with
     c->have_camera = true;
     c->cull_valid = false;
@@ -1058,7 +1087,8 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     std::memcpy(p.inv_view, c->cam.inv_view, sizeof p.inv_view);
     cam_constants(c->cam, &p.cam_const, &p.cam_near_rw, &p.cam_far_rw);
     p.acc_tab = spp <= iqpt::kAccTableMax ? 1u : 0u;
-    p.diag = c->diag;
+    p.spin_limit = c->spin_limit;
+    p.iter_limit = c->iter_limit;
     p.frames32 = (c->frame + (uint64_t)spp) < (1ull << 32) ? 1u : 0u;
     // running mean under kOptFastDiv: c / n by Markstein's correction is exact while the quotient is
     // normal, c >= 2^-125 n; with n <= frame0 + spp the threshold 2^-124 (frame0 + spp) (rounded up,
@@ -1311,8 +1341,12 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
     }
     // kOptOverlap: resident, culled, not split, not a tuning launch
+    // Tiles are bound to the 8 XCDs (HW_REG_XCC_ID): only on a device that exposes 8 (not a partition
+    // mode) and with at least 64 blocks, so that the observed round-robin dispatch puts blocks on every
+    // XCD (HIP promises no placement; the kernel's last block checks it and raises an error bit if not)
     bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && !chain && p.cull != nullptr &&
-               tune_slot < 0 && c->d_tile_done && c->d_xcd_order &&
+               tune_slot < 0 && c->d_tile_done && c->d_xcd_order && c->num_xcc == 8 && c->num_cus >= 64 &&
+               (uint64_t)c->npix >= 64ull * iqpt::kRenderBlock &&
                iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptOverlap);
     int occ = 0;
     if (iqpt::render_occupancy(c->max_depth, stream_batches, ovl ? (opt | iqpt::kOptOverlap) : opt, lds, &occ) != 0 ||
@@ -1350,7 +1384,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const uint32_t parity = c->ovl_epoch & 1u;
         p.queue = c->d_queue + 4 + parity * (iqpt::kOverlapQueueWords / 2);
         p.tile_done = c->d_tile_done;
-        p.done_target = c->ovl_epoch;
+        p.done_target = c->ovl_epoch ? c->ovl_epoch + c->wait_bias : 0u;
         p.xcd_order = c->d_xcd_order;
         std::memcpy(p.xcd_off, c->xcd_off, sizeof p.xcd_off);
         p.ovl_err = c->d_ovl_err;
@@ -1373,11 +1407,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         opt |= iqpt::kOptCamAxis;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
-#if defined(IQPT_CHAIN_OLD_STREAMS)
-    if (!ovl) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
-#else
     if (!ovl && !chain) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
-#endif
     hipEvent_t e0 = take_event(c), e1 = take_event(c);
     if (e0) (void)hipEventRecord(e0, ls);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
@@ -1402,18 +1432,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const uint64_t want_c = (ns + px_per_wave - 1) / px_per_wave;
         const uint32_t grid_c = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_c, (uint64_t)c->num_cus * per_cu));
         p.ovl_err = c->d_ovl_err;
-#if defined(IQPT_CHAIN_OLD_STREAMS)
-        IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
-        IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
-        le = iqpt::launch_chain(c->stream2, p, grid_c, opt, lanes);
-        if (le == 0 && c->n_anchor > 0) {
-            p.tile_order = c->d_split;
-            p.nqueue = c->n_anchor;
-            const uint64_t want_p = ((uint64_t)c->n_anchor * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
-            const uint32_t grid_p = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_p, (uint64_t)c->num_cus * occ));
-            le = iqpt::launch_render(c->stream, p, grid_p, lds, stream_batches, opt);
-        }
-#else
         // The chain kernel (the launch's critical path) goes first on the context stream; the anchored
         // kernel (shorter) follows on stream2 behind a cross-queue event, whose latency it absorbs. The
         // queue counters alternate between two sets in the overlapped launches' words: this launch's set
@@ -1436,7 +1454,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->chain_q_ready[nxt] = true;
         c->chain_q_ready[c->chain_par] = false;
         c->chain_par = nxt;
-#endif
         IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
         IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
     } else if (split) {
@@ -1475,15 +1492,9 @@ int iqpt_sync(iqpt_ctx* c) {
     int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
-    // kOptOverlap: a per-tile wait that gave up (never expected) leaves the frame undefined: report it
-    uint32_t err = 0;
-    IQPT_HIP(hipMemcpy(&err, c->d_ovl_err, sizeof err, hipMemcpyDeviceToHost));
-    if (err) {
-        IQPT_HIP(hipMemset(c->d_ovl_err, 0, sizeof err));
-        return iqpt::fail(IQPT_ERR_HIP, (err & 2u) ? "chain launch: a wave exceeded its iteration bound (results invalid)"
-                                                   : "overlapped launch: a per-tile wait timed out (results invalid)");
-    }
-    return IQPT_OK;
+    // a per-tile wait that gave up or a chain wave past its bound (never expected) leaves the frame
+    // undefined: report it (and keep reporting it, iqpt_ctx::dev_err)
+    return check_dev_err(c);
 }
 
 int iqpt_reset(iqpt_ctx* c) {                                       // path_tracer.cu:394-400
@@ -1503,7 +1514,8 @@ int iqpt_read(iqpt_ctx* c, float* lin_rgba, uint8_t* bgra) {
     if (st) return st;
     if (lin_rgba && (st = fetch_compact(c, c->d_lin, 4, 1, lin_rgba)) != IQPT_OK) return st;
     if (bgra && (st = fetch_compact(c, c->d_bgra, 1, 1, bgra)) != IQPT_OK) return st;
-    return IQPT_OK;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    return check_dev_err(c);
 }
 
 int iqpt_read_rng(iqpt_ctx* c, uint32_t* states) {
@@ -1512,6 +1524,7 @@ int iqpt_read_rng(iqpt_ctx* c, uint32_t* states) {
     if (st) return st;
     std::vector<uint32_t> planes((size_t)c->npix * 6);
     if ((st = fetch_compact(c, c->d_rng, 1, 6, planes.data())) != IQPT_OK) return st;
+    if ((st = check_dev_err(c)) != IQPT_OK) return st;
     for (size_t p = 0; p < c->npix; ++p)
         for (int k = 0; k < 6; ++k) states[p * 6 + k] = planes[(size_t)k * c->npix + p];
     return IQPT_OK;
@@ -1526,7 +1539,7 @@ int iqpt_copy_accum_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
                                          static_cast<uint32_t*>(dst_device), c->ncols, c->set.nrows, 4, 1, true);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "accumulator reorder");
     IQPT_HIP(hipStreamSynchronize(c->stream));
-    return IQPT_OK;
+    return check_dev_err(c);
 }
 
 namespace {
@@ -1565,6 +1578,7 @@ int iqpt_checkpoint_save(iqpt_ctx* c, const char* path) {
     std::vector<uint32_t> bgra(n), rng(n * 6);
     unsigned long long rays = 0;
     // the file holds the compact row-major order (independent of the device layout)
+    if ((st = check_dev_err(c)) != IQPT_OK) return st;     // never persist undefined state
     if ((st = fetch_compact(c, c->d_lin, 4, 1, lin.data())) != IQPT_OK ||
         (st = fetch_compact(c, c->d_bgra, 1, 1, bgra.data())) != IQPT_OK ||
         (st = fetch_compact(c, c->d_rng, 1, 6, rng.data())) != IQPT_OK)
@@ -1651,6 +1665,9 @@ int iqpt_checkpoint_load(iqpt_ctx* c, const char* path) {
         return st;
     IQPT_HIP(hipMemcpy(c->d_rays, &rays, sizeof rays, hipMemcpyHostToDevice));
     c->frame = h.frame;
+    // the whole pixel state is replaced: a latched kernel error no longer applies
+    IQPT_HIP(hipMemset(c->d_ovl_err, 0, sizeof(uint32_t)));
+    c->dev_err = 0;
     return IQPT_OK;
 }
 
@@ -1700,10 +1717,13 @@ int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
     return IQPT_OK;
 }
 
-/* Internal (tools/ab_kernel.py): kOptDiag timing ablations (A/B builds; results are not the reference's). */
-int iqpt_debug_set_diag(iqpt_ctx* c, uint32_t bits) {
+/* Internal (tests): lower the kernels' forward-progress bounds (0 keeps a bound's default) and bias the
+ * per-tile wait targets of overlapped launches, so that tests can force each error path. */
+int iqpt_debug_set_limits(iqpt_ctx* c, uint32_t spin_limit, uint32_t iter_limit, uint32_t wait_bias) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    c->diag = bits;
+    c->spin_limit = spin_limit ? spin_limit : iqpt::kOverlapSpinLimit;
+    c->iter_limit = iter_limit ? iter_limit : iqpt::kChainIterLimit;
+    c->wait_bias = wait_bias;
     return IQPT_OK;
 }
 
@@ -1718,7 +1738,7 @@ int iqpt_copy_frame_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
                                          c->set.nrows, 1, 1, true);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
     IQPT_HIP(hipStreamSynchronize(c->stream));
-    return IQPT_OK;
+    return check_dev_err(c);
 }
 
 int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
@@ -1726,6 +1746,9 @@ int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
     if (bytes < (size_t)c->npix * sizeof(uint32_t)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
     int st = use_device(c);
     if (st) return st;
+    // no synchronisation here: an error the kernels raise for this launch is reported by the next
+    // synchronising call (iqpt_sync, iqpt_read, ...); one already latched fails the copy now
+    if (c->dev_err) return check_dev_err(c);
     hipStream_t cs = c->stream;
     if (c->last_ovl && c->last_ls) {
         // overlapped launches in flight: copy on the last launch's stream without joining, so the next

@@ -26,7 +26,7 @@ ORACLE_DIR = REPO / "oracle"
 BUILD_DIR = PROJ_DIR / "build"
 
 LIB_PATH = PKG_DIR / "libiqpt.so"
-AB_LIB_PATH = PKG_DIR / "libiqpt_ab.so"        # + A/B kernel variants (tools/ab_kernel.py)
+STATS_LIB_PATH = PKG_DIR / "libiqpt_stats.so"  # + the instrumented kOptStats variants (tools/work_counters.py)
 ORACLE_LIB = ORACLE_DIR / "liboracle.so"
 ORACLE_GLIBC_LIB = ORACLE_DIR / "liboracle_glibc.so"
 ORACLE_FMA_LIB = ORACLE_DIR / "liboracle_fma.so"      # informational: contraction on + glibc libm (nvcc-like)
@@ -63,19 +63,20 @@ def _headers() -> list[Path]:
     return sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("*.hpp")) + sorted(INCLUDE.glob("*.h"))
 
 
-def build_lib(force: bool = False, ab: bool = False, flags: tuple[str, ...] = (),
+def build_lib(force: bool = False, stats: bool = False, flags: tuple[str, ...] = (),
               target: Path | None = None) -> Path:
-    """Compile the HIP kernels + runtime into libiqpt.so (gfx950); ab=True adds the A/B variants.
+    """Compile the HIP kernels + runtime into libiqpt.so (gfx950); stats=True adds the instrumented
+    kOptStats variants (a separate library: measurement only).
     ``flags``/``target``: extra compiler flags into another library (compiler-option A/B runs)."""
-    target = target or (AB_LIB_PATH if ab else LIB_PATH)
+    target = target or (STATS_LIB_PATH if stats else LIB_PATH)
     srcs = [CSRC / s for s in LIB_SOURCES]
     if not force and _newer(target, srcs + _headers() + [Path(__file__)]):
         return target
-    bdir = BUILD_DIR / (target.stem if flags else ("ab" if ab else "prod"))
+    bdir = BUILD_DIR / (target.stem if flags else ("stats" if stats else "prod"))
     bdir.mkdir(parents=True, exist_ok=True)
     objs = []
     cmds = []
-    extra = (["-DIQPT_AB_VARIANTS"] if ab else []) + list(flags)
+    extra = (["-DIQPT_STATS_VARIANTS"] if stats else []) + list(flags)
     for s in srcs:
         o = bdir / (s.name + ".o")
         cmds.append([HIPCC, *HIP_FLAGS, *extra, "-x", "hip", "-c", str(s), "-o", str(o)])

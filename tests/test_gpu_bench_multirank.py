@@ -16,13 +16,13 @@ from conftest import REPO
 pytestmark = pytest.mark.gpu
 
 
-def _bench(tmp_path, gpus, name, extra=()):
+def _bench(tmp_path, gpus, name, extra=(), timeout=240):
     out = tmp_path / f"{name}.npy"
     cmd = [sys.executable, str(REPO / "bench.py"), "--gpus", str(gpus), "--steps", "2", "--warmup", "1",
            "--no-cpu-baseline", "--verify-rows", "2", "--save-frame", str(out), *extra]
     if gpus > 1:
         cmd += ["--backend", "gloo", "--one-device"]
-    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=REPO)
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=REPO)
     assert proc.returncode == 0, proc.stderr[-3000:]
     line = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1]
     return json.loads(line), np.load(out)
@@ -50,3 +50,20 @@ def test_stream_ordered_gather_on_one_gpu(require_gpu, tmp_path, share, mode):
     assert res["hw_queues"] == 8 and res["n_ranks_seen"] == 1
     assert res["config"]["launch_mode"] == mode
     assert res["bitexact_frac_vs_oracle"] == 1.0
+
+
+@pytest.mark.parametrize("gpus", [4, 8])
+def test_c3_assembly_at_4_and_8_ranks(require_gpu, tmp_path, gpus):
+    """C3 as the driver's N-GPU runs split it, at N = 4 and 8: bench.py --gpus N starts N fresh rank
+    processes (here all on GPU 0, gloo through host memory), each renders its cyclic rows through the
+    sample-parallel launches of small shares, every step gathers the BGRA frame to rank 0, and the float
+    accumulators gathered after timing must equal the 1-rank frame bit for bit."""
+    one, f1 = _bench(tmp_path, 1, "one")
+    res, fn = _bench(tmp_path, gpus, f"n{gpus}", timeout=600)
+    assert res["n_gpus"] == gpus and res["n_ranks_seen"] == gpus and res["scaling"] == "strong"
+    assert res["gather_check"] is True
+    assert res["config"]["launch_mode"] != "plain", res["config"]
+    assert res["bitexact_frac_vs_oracle"] == 1.0
+    assert fn.shape == f1.shape == (1920 * 1080, 4)
+    assert np.array_equal(f1.view(np.uint32), fn.view(np.uint32))
+    assert res["rays_per_sample"] == one["rays_per_sample"]

@@ -38,8 +38,8 @@ def main():
     ap.add_argument("--timeline-npy", default="", help="save the stats run's raw per-wave records (.npy)")
     ap.add_argument("--lib", default="", help="load this prebuilt A/B library (compiler-option runs)")
     args = ap.parse_args()
-    lib_path = Path(args.lib) if args.lib else _build.build_lib(ab=True)
-    _lib.LIB_PATH = lib_path                    # load the A/B build instead of the production one
+    lib_path = Path(args.lib) if args.lib else _build.build_lib(stats=True)
+    _lib.LIB_PATH = lib_path                    # load the instrumented build instead of the production one
     lib = _lib.load()
     global DEFAULT
     DEFAULT = lib.iqpt_debug_default_options()
@@ -47,7 +47,6 @@ def main():
         args.stats_opt = DEFAULT
     lib.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
     lib.iqpt_debug_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
-    lib.iqpt_debug_set_diag.argtypes = [C.c_void_p, C.c_uint32]
     import iqpt
     from iqpt.scene import CONFIGS
     cfg = CONFIGS[args.config]
@@ -70,15 +69,11 @@ def main():
     variants = {"default": DEFAULT, "none": 0, "-cull": DEFAULT & ~512, "-fastdiv": DEFAULT & ~256,
                 "-pair": DEFAULT & ~4, "-sincos": DEFAULT & ~32,
                 "-bvh": DEFAULT & ~2048}
-    diag = {}
     if args.variants:
-        # name=optmask or name=optmask#d (d: kOptDiag timing-ablation bits, iqpt_debug_set_diag)
+        # name=optmask (option sets the loaded library builds)
         variants = {}
         for kv in args.variants.split(","):
             name, val = kv.split("=")
-            if "#" in val:
-                val, dbits = val.split("#")
-                diag[name] = int(dbits)
             variants[name] = int(val, 0)
     ps = None
     if args.crop:
@@ -100,8 +95,6 @@ def main():
     for name, opt in list(variants.items()):
         pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
         st = lib.iqpt_debug_set_kernel_options(pt.handle, opt)
-        if st == 0 and name in diag:
-            st = lib.iqpt_debug_set_diag(pt.handle, diag[name])
         if st != 0:
             print(f"skip {name}: {lib.iqpt_last_error().decode()}", file=sys.stderr)
             pt.close()

@@ -15,7 +15,7 @@ import iqpt  # noqa: E402
 from iqpt import _build, _lib  # noqa: E402
 from iqpt.scene import Scene, make_camera  # noqa: E402
 
-_lib.LIB_PATH = _build.build_lib(ab=True)
+_lib.LIB_PATH = _build.build_lib(stats=True)
 lb = _lib.load()
 sc = Scene()
 sc.add_preset("cornell")

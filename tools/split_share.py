@@ -25,7 +25,6 @@ from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
 
 
 OPT = 0
-DIAG = 0     # chain-kernel timing ablations (A/B library; NOT exact)
 
 
 def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain_waves: int = 0) -> dict:
@@ -47,11 +46,6 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain
         lb = _lib.load()
         lb.iqpt_debug_set_split_knobs.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_split_knobs(pt._h, knobs[0], knobs[1]), "iqpt_debug_set_split_knobs")
-    if DIAG and mode == _lib.SPLIT_CHAIN:
-        import ctypes as C
-        lb = _lib.load()
-        lb.iqpt_debug_set_diag.argtypes = [C.c_void_p, C.c_uint32]
-        _lib.check(lb.iqpt_debug_set_diag(pt._h, DIAG), "iqpt_debug_set_diag")
     if chain_waves:
         import ctypes as C
         lb = _lib.load()
@@ -155,29 +149,21 @@ def main():
     ap.add_argument("--modes", default="plain,split", help="plain, split, chain (IQPT_SPLIT_CHAIN)")
     ap.add_argument("--chain-waves", default="", help="extra chain rows at these chain-kernel waves per CU")
     ap.add_argument("--knobs", default="", help="split knob sets heavy_rho:refill_min[,...] (extra split rows)")
-    ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (A/B library)")
-    ap.add_argument("--opt", type=lambda v: int(v, 0), default=0, help="kernel option set (A/B library; 0 = production)")
-    ap.add_argument("--ab", action="store_true", help="load the A/B library (chain ablations: --diag)")
-    ap.add_argument("--diag", type=int, default=0, help="chain-kernel ablation bits (64 mean, 128 stepping, "
-                    "256 barriers, 512 closest hit); results are then NOT exact")
+    ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (instrumented library)")
+    ap.add_argument("--opt", type=lambda v: int(v, 0), default=0, help="kernel option set (instrumented library; 0 = production)")
     ap.add_argument("--lib", default="", help="load this prebuilt library (compile-time knob A/B)")
     args = ap.parse_args()
     if args.lib:
         _lib.LIB_PATH = Path(args.lib)
-    if args.ab or args.diag:
-        global DIAG
-        from iqpt import _build
-        _lib.LIB_PATH = _build.build_lib(ab=True)
-        DIAG = args.diag
     out = {"config": "c2 rank-0 row share, 64 spp per launch", "launches": args.launches, "rows": []}
     if args.opt:
         global OPT
         from iqpt import _build
-        _lib.LIB_PATH = _build.build_lib(ab=True)
+        _lib.LIB_PATH = _build.build_lib(stats=True)
         OPT = args.opt
     if args.stats:
         from iqpt import _build
-        _lib.LIB_PATH = _build.build_lib(ab=True)
+        _lib.LIB_PATH = _build.build_lib(stats=True)
         for n in [int(x) for x in args.ns.split(",")]:
             tl = wave_timeline(n, args.spp, args.warm)
             print(json.dumps({"n": n, "timeline": tl}), flush=True)

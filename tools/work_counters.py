@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--launches", type=int, default=2)
     ap.add_argument("--out", default="")
     args = ap.parse_args()
-    _lib.LIB_PATH = _build.build_lib(ab=True)
+    _lib.LIB_PATH = _build.build_lib(stats=True)
     lb = _lib.load()
     lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
     lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
