@@ -85,7 +85,7 @@ def parse():
                          "with --self-gather the per-step gather path too)")
     ap.add_argument("--self-gather", action="store_true",
                     help="test: run the per-step gather path at N = 1 (a one-rank process group)")
-    ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain"],
+    ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain", "fan", "spec"],
                     help="sample-parallel chains (iqpt_set_split, DESIGN.md §3.7)")
     return ap.parse_args()
 
@@ -355,7 +355,8 @@ def main():
     pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, seed=seed, max_depth=cfg.max_depth, device=device)
     setup["create_and_rng_init_ms"] = (time.perf_counter() - t0) * 1e3
     pt.set_split({"auto": _lib.SPLIT_AUTO, "on": _lib.SPLIT_ON, "off": _lib.SPLIT_OFF,
-                  "chain": _lib.SPLIT_CHAIN}[args.split])
+                  "chain": _lib.SPLIT_CHAIN, "fan": _lib.SPLIT_FAN,
+                  "spec": _lib.SPLIT_SPEC}[args.split])
     if args.kernel_options:
         import ctypes as C
         _lib.load().iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]

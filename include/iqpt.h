@@ -186,6 +186,15 @@ int iqpt_sync(iqpt_ctx* ctx);
  * stream offsets and folded in sample order as the results arrive, in a kernel that runs beside the
  * plain kernel over the other tiles (one launch pair, no stitch pass). AUTO picks it for small shares. */
 #define IQPT_SPLIT_CHAIN 2
+/* FAN: the tiles whose camera rays cannot reach a sphere (every sample one ray and two
+ * draws, so sample k starts 2k draws into the pixel's stream) spread each pixel's samples over four
+ * waves and fold them in order; the other tiles run in the plain kernel beside them. Chain launches
+ * run their anchored tiles this way too. */
+#define IQPT_SPLIT_FAN 3
+/* SPEC: the pixels whose own camera rays may reach a sphere (the only ones whose samples
+ * take more than two draws) have every slot of a window evaluated in parallel and their chains walked in
+ * order afterwards; every other pixel runs as in FAN. AUTO picks it for small shares. */
+#define IQPT_SPLIT_SPEC 4
 int iqpt_set_split(iqpt_ctx* ctx, int mode);
 
 /* Overlapped launches (no reference counterpart: the reference launches one frame at a

@@ -157,6 +157,10 @@ struct kparams {
     // forward-progress bounds (never reached by a real launch; iqpt_debug_set_limits lowers them so that
     // tests can force each one): s_sleep polls of one per-tile wait, loop iterations of one chain wave
     uint32_t spin_limit, iter_limit;
+    // iqpt_fan_kernel: the lanes of fan tile b that it renders (bit i: pixel i of the tile); null = all.
+    // Chain launches give the fan kernel every pixel whose camera rays provably miss every sphere, also
+    // inside tiles with sphere candidates (the other pixels of those tiles are the chain kernel's).
+    const uint64_t* fan_lanes;
     // queue length of the plain kernel's tile queue (tile_order[0 .. nqueue)); 0: every tile (ntiles).
     // Chain launches give the plain kernel the anchored tiles only.
     uint32_t nqueue;
@@ -166,6 +170,32 @@ constexpr uint32_t kOverlapSpinLimit = 1u << 23;   // s_sleep(20) polls before a
 constexpr uint32_t kChainIterLimit = 1u << 22;     // chain-kernel loop iterations before a wave gives up
 // two launch parities x (8 XCD queue words + the finished-block count), 64 B apart
 constexpr uint32_t kOverlapQueueWords = 2 * 9 * 16;
+
+// Slot-parallel sphere pixels (IQPT_SPLIT_SPEC): the pixels whose own camera-ray bundle
+// may reach a sphere. Per launch a window of M slots per pixel (M from the pixel's last chain), every
+// slot j (the sample that starts 2j draws into the pixel's stream) evaluated in parallel by runs of
+// run_len consecutive slots, then the chain walked in order. Kernels: iqpt_spec_prep_kernel (windows,
+// states, run list), iqpt_spec_kernel (the slots), iqpt_spec_stitch_kernel (walk, fold, finish chains
+// that left their window, store the pixel).
+struct kspec {
+    uint32_t n;                      // sphere pixels q < n
+    uint32_t m_cap;                  // window cap (a multiple of 16)
+    uint32_t run_len;                // R: slots per run
+    uint32_t g_max;                  // state plane of slot M (planes r < g_max: slot r R)
+    uint32_t rho0;                   // slots per sample x 256 assumed for a pixel without history
+    const uint32_t* pix;             // tile-major storage index of sphere pixel q
+    uint32_t* m;                     // this launch's window of q
+    uint32_t* rho;                   // slots per sample x 256 of q's last chain (0: none)
+    uint32_t* st;                    // (g_max + 1) x 5 planes x n: v0..v4 at slots 0, R, 2R, ... and at M
+    // run list, 48 B per run, everything a lane needs to start it in one round of loads: (v0, v1, v2, v3),
+    // (v4, d, storage index, q), (first slot | end slot << 16, tile, tile mask words 0 of triangles, spheres)
+    uint32_t* runs;
+    uint32_t* run_count;             // runs in the list; run_count[1]: the spec kernel's dequeue head
+    float4_storage* res;             // res[q m_cap + j]: clamped colour of slot j (w unused)
+    uint8_t* nres;                   // nres[q m_cap + j]: slots slot j's sample consumed
+};
+constexpr uint32_t kSpecRunLen = 4;      // slots per run (a run starts on a state the prep kernel stored)
+constexpr uint32_t kSpecRho0 = 576;      // 2.25 slots per sample before a pixel has a history (sphere pixels take ~2)
 
 // iqpt_split_prep_kernel / iqpt_split_stitch_kernel (kOptSplit).
 struct ksplit {
@@ -306,11 +336,24 @@ bool render_variant_exists(int max_depth, bool stream_batches, int opt);
 // Chain-parallel pixels (iqpt_chain_kernel): the split set's pixels, each evaluated by
 // kChainLanes lanes at consecutive even stream offsets and folded in sample order; reads p.sp_pix /
 // p.ns_cap and takes pixels from p.queue[1]. Resident scenes, reference materials, max_depth <= 16.
-// lanes: lanes per pixel, 4 or 8.
+// lanes: lanes per pixel, 4, 8 or 16.
 bool chain_variant_exists(int max_depth, int opt, uint32_t lanes);
 uint32_t chain_lds(const kparams& p, uint32_t lanes);
 int chain_occupancy(int max_depth, int opt, uint32_t lanes, uint32_t lds, int* blocks_per_cu);
 int launch_chain(void* stream, const kparams& p, uint32_t grid_blocks, int opt, uint32_t lanes);
+// Slot-parallel sphere pixels: prep (zeroes nothing: run_count must be 0), slots, stitch.
+// The slot and stitch kernels need a resident scene, reference materials, max_depth <= 16, spp <= kAccTableMax.
+int launch_spec_prep(void* stream, const kparams& p, const kspec& s);
+bool spec_variant_exists(int max_depth, int opt);
+int spec_occupancy(int max_depth, int opt, const kparams& p, int* blocks_per_cu);
+int launch_spec(void* stream, const kparams& p, const kspec& s, uint32_t grid_blocks, int opt);
+int launch_spec_stitch(void* stream, const kparams& p, const kspec& s, int opt);
+// Sample-parallel anchored tiles (iqpt_fan_kernel): one block per tile of
+// p.tile_order[0 .. ntiles) — tiles without sphere candidates, reference materials, resident scene
+// (p.cull set, p.cull_wt <= 16), spp <= kAccTableMax.
+bool fan_variant_exists(int opt);
+uint32_t fan_lds(const kparams& p);
+int launch_fan(void* stream, const kparams& p, uint32_t ntiles, int opt);
 constexpr int kRenderBlock = 256;
 constexpr uint32_t kQueueChunk = 64;
 const char* render_kernel_name();

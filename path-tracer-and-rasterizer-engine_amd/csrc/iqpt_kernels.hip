@@ -2699,6 +2699,529 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
     if (lane == 0 && w_rays) atomicAdd(p.rays, w_rays);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Sample-parallel anchored tiles (iqpt_fan_kernel). A tile whose camera rays cannot
+// reach a sphere (no sphere bit in its §3.3 mask) under the reference's materials (every triangle
+// emissive, path_tracer.cu:248-249, 278) ends every path on its first ray: an emissive hit or the sky
+// (path_tracer.cu:297-316). Every sample of such a pixel takes exactly the two jitter draws of
+// camera::get_ray (camera.cu:24-25), so sample k starts at stream offset 2k with certainty, and the
+// samples of a pixel are independent but for the ordered running mean (path_tracer.cu:356-358).
+// One block = one 8x8 tile = four waves, lane = pixel in every wave: wave w evaluates a contiguous range
+// of samples of each chunk of C <= 64 samples from the state 2 s draws into the pixel's stream (stepped
+// there once per chunk), and leaves per sample a triangle-hit bit (a ballot) and the sky parameter
+// a = (dir.y + 1) / 2 in LDS; wave 0 then folds the chunk in sample order with the plain kernel's table
+// values and mean_terms. The ranges (fan_range) are sized so that wave 0's fold and the later waves'
+// stream stepping even out the four waves' instruction counts. The pixel's chain is 16 samples per lane instead of 64, and no
+// sample is evaluated that the pixel does not use. Same bits as the plain kernel: the same camera
+// ray, the tile's mask pairs in index order (no sphere candidate: no sphere test), the same colour,
+// clamp and mean, the state 2 spp draws on, spp rays per pixel.
+constexpr uint32_t kFanBlock = 256;                    // four waves, one tile
+constexpr uint32_t kFanChunk = 64;                     // samples per chunk (LDS: [chunk][pixel])
+
+// First sample of wave w's range in a chunk of cn samples: 0, 14 %, 44 %, 72 % of the chunk (wave 0 also
+// folds the chunk, about a sixth of a sample per fold; a later wave first steps 2 s draws, about 7 % of a
+// sample per sample skipped), so that the four ranges cost about the same.
+__device__ __forceinline__ uint32_t fan_range(uint32_t cn, uint32_t w) {
+    return w == 0u ? 0u : (w == 1u ? (cn * 9u) / 64u : (w == 2u ? (cn * 28u) / 64u : (w == 3u ? (cn * 46u) / 64u : cn)));
+}
+
+__host__ __device__ inline uint32_t fan_lds_bytes(uint32_t ntri_pairs, uint32_t spp) {
+    return ntri_pairs * kTriPairFloat4 * 16u + ((spp + 1u) & ~1u) * 8u + ((spp + 3u) & ~3u) * 4u + 16u * 4u +
+           kFanChunk * 64u * 4u + kFanChunk * 8u;
+}
+
+template <int OPT>
+__global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    float4* lds_tri = lds;
+    float2* lds_tab = reinterpret_cast<float2*>(lds_tri + (size_t)p.ntri_pairs * kTriPairFloat4);
+    float* lds_tab_n = reinterpret_cast<float*>(lds_tab + ((p.spp + 1u) & ~1u));
+    uint32_t* lds_mask = reinterpret_cast<uint32_t*>(lds_tab_n + ((p.spp + 3u) & ~3u));   // the tile's words
+    float* lds_sky = reinterpret_cast<float*>(lds_mask + 16);                             // [sample][lane]
+    uint64_t* lds_hit = reinterpret_cast<uint64_t*>(lds_sky + kFanChunk * 64u);           // [sample]
+
+    const uint32_t t = p.tile_order[blockIdx.x];
+    for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kFanBlock)
+        lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
+    for (uint32_t s = threadIdx.x; s < p.spp; s += kFanBlock) {
+        const uint64_t n = p.frame0 + s + 1;
+        lds_tab[s] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
+        lds_tab_n[s] = (float)n;
+    }
+    if (threadIdx.x < p.cull_wt) lds_mask[threadIdx.x] = p.cull[(size_t)t * p.cull_stride + threadIdx.x];
+    __syncthreads();
+
+    const uint32_t lane = __lane_id(), wave = threadIdx.x / 64u;
+    const uint32_t tx = t % p.ntx, ty = t / p.ntx;
+    const uint32_t th = min(kCullTile, p.nrows - ty * kCullTile), tw = min(kCullTile, p.ncols - tx * kCullTile);
+    const uint32_t npt = tw * th;
+    const bool inside = lane < npt;                     // partial tiles at the right / bottom edge
+    // the pixels of this tile the fan kernel owns (chain launches: the others are the chain kernel's)
+    const uint64_t own = p.fan_lanes ? p.fan_lanes[blockIdx.x] : ~0ull;
+    const bool has = inside && ((own >> lane) & 1ull);
+    const uint32_t pix = ty * kCullTile * p.ncols + tx * kCullTile * th + (inside ? lane : 0u);
+    const uint32_t px = p.x0 + tx * kCullTile + (inside ? lane % tw : 0u);
+    const uint32_t py = p.y0 + (ty * kCullTile + (inside ? lane / tw : 0u)) * p.ystep;
+    rng6 st = {p.rng[pix], p.rng[(size_t)p.npix + pix], p.rng[2 * (size_t)p.npix + pix],
+               p.rng[3 * (size_t)p.npix + pix], p.rng[4 * (size_t)p.npix + pix], p.rng[5 * (size_t)p.npix + pix]};
+    float ax = 0.0f, ay = 0.0f, az = 0.0f;
+    if (wave == 0) {
+        const float* a = reinterpret_cast<const float*>(p.lin + pix);
+        ax = a[0];
+        ay = a[1];
+        az = a[2];
+    }
+    const uint32_t tp = (p.ntri + 1) / 2;
+    uint32_t pos = 0;                                   // samples whose draws this lane's state has passed
+
+    for (uint32_t c0 = 0; c0 < p.spp; c0 += kFanChunk) {
+        const uint32_t cn = min(kFanChunk, p.spp - c0);
+        const uint32_t s0 = c0 + fan_range(cn, wave), s1 = c0 + fan_range(cn, wave + 1u);
+        // to sample s0: 2 (s0 - pos) draws (d follows from the count)
+        xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * (s0 - pos));
+        st.d += 2u * (s0 - pos) * IQ_XORWOW_WEYL;
+        for (uint32_t s = s0; s < s1; ++s) {
+            ray3 ray;
+            camera_ray<OPT>(p, px, py, st, ray);
+            // closest hit over the tile's candidate pairs, in index order (path_tracer.cu:257-275); the
+            // lane's pixel has no sphere candidate (its tile's mask, or its own bundle in chain launches), so no
+            // sphere test can accept (iq_interval.h)
+            float closest = kTMax;
+            int kind = kHitNone;
+            uint32_t hidx = 0;
+            for (uint32_t w = 0; w * 32u < tp; ++w) {
+                uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_mask[w]);
+                while (m) {
+                    const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
+                    m &= m - 1u;
+                    if (j >= tp) break;
+                    const float4* q = lds_tri + (size_t)j * kTriPairFloat4;
+                    test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
+                                            2 * j + 1 < p.ntri);
+                }
+            }
+            const uint64_t hit = __ballot(kind == kHitTri);
+            if (lane == 0) lds_hit[s - c0] = hit;
+            lds_sky[(s - c0) * 64u + lane] = (ray.dy + 1.0f) * 0.5f;   // sky gradient parameter (:308-313)
+        }
+        pos = s1;
+        __syncthreads();
+        if (wave == 0) {
+            // the running mean in sample order (path_tracer.cu:341-358): an emissive hit is 10 clamped to 1
+            for (uint32_t k = 0; k < cn; ++k) {
+                float cx, cy, cz;
+                if ((lds_hit[k] >> lane) & 1ull) {
+                    cx = 1.0f;
+                    cy = 1.0f;
+                    cz = 1.0f;
+                } else {
+                    const float a = lds_sky[k * 64u + lane];
+                    const float one_a = 1.0f - a;
+                    cx = one_a + a * 0.5f;
+                    cy = one_a + a * 0.7f;
+                    cz = one_a + a * 1.0f;
+                    cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                    cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                    cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                    cx = 0.0f + cx;
+                    cy = 0.0f + cy;
+                    cz = 0.0f + cz;
+                }
+                const float2 tv = lds_tab[c0 + k];
+                float qx, qy, qz;
+                mean_terms<OPT>(cx, cy, cz, lds_tab_n[c0 + k], tv.x, p.mean_tiny, qx, qy, qz);
+                ax = qx + ax * tv.y;
+                ay = qy + ay * tv.y;
+                az = qz + az * tv.y;
+            }
+        }
+        __syncthreads();
+    }
+    if (has) {
+        if (pos == p.spp) {
+            // the lane whose last sample is the launch's last: its state is 2 spp draws on
+            p.rng[pix] = st.v0;
+            p.rng[(size_t)p.npix + pix] = st.v1;
+            p.rng[2 * (size_t)p.npix + pix] = st.v2;
+            p.rng[3 * (size_t)p.npix + pix] = st.v3;
+            p.rng[4 * (size_t)p.npix + pix] = st.v4;
+            p.rng[5 * (size_t)p.npix + pix] = st.d;
+        }
+        if (wave == 0) {
+            const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
+            const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
+            const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
+            p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+            reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
+        }
+    }
+    if (threadIdx.x == 0)   // one query per sample
+        atomicAdd(p.rays, (unsigned long long)__popcll(own & (npt == 64u ? ~0ull : ((1ull << npt) - 1ull))) * p.spp);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Slot-parallel sphere pixels (IQPT_SPLIT_SPEC). Only the pixels whose own camera-ray
+// bundle may reach a sphere take more than one slot per sample, so only their chains need speculation.
+// Sample k of a pixel starts where sample k - 1's draws ended (path_tracer.cu:339): 2 draws for the
+// jitter (camera.cu:24-25) plus 2 per Oren-Nayar scatter (material.cu:10), and what a sample does from
+// stream offset 2j depends on j alone. So every slot j < M of a window is evaluated in parallel — runs of
+// R consecutive slots per lane, a run starting on a state the prep kernel stored, the next slot's state
+// being the one the camera draws of the current slot leave — and the stitch kernel then follows the chain
+// 0 -> j + n_j -> ... and folds its samples in order with the plain kernel's table values (the running
+// mean of path_tracer.cu:356-358). A chain that leaves its window is finished by the stitch thread itself.
+// Same bits as the plain kernel: the same per-sample code, the chain's own slots counted as rays.
+
+// Per sphere pixel: the window M (the last chain's slots per sample, split_window), the states at slots
+// 0, R, 2R, ... and at M, and the pixel's runs appended to the run list (one atomic per wave).
+__global__ __launch_bounds__(256) void iqpt_spec_prep_kernel(const kparams p, const kspec s) {
+    const uint32_t q = blockIdx.x * 256u + threadIdx.x, lane = __lane_id();
+    uint32_t nr = 0, M = 0, pix = 0;
+    if (q < s.n) {
+        pix = s.pix[q];
+        const uint32_t rho = s.rho[q];
+        M = split_window(rho ? rho : s.rho0, p.spp, s.m_cap);
+        s.m[q] = M;
+        nr = (M + s.run_len - 1u) / s.run_len;
+    }
+    uint32_t incl = nr;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, off);
+        if ((int)lane >= off) incl += t;
+    }
+    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
+    uint32_t base = 0;
+    if (lane == 0 && total) base = atomicAdd(s.run_count, total);
+    base = (uint32_t)__shfl((int)base, 0) + incl - nr;
+    if (q >= s.n) return;
+    // the states at slots 0, R, 2R, ... (each run's start) and at M; each run's record
+    const uint32_t R = s.run_len;
+    uint32_t v0 = p.rng[pix], v1 = p.rng[(size_t)p.npix + pix], v2 = p.rng[2 * (size_t)p.npix + pix],
+             v3 = p.rng[3 * (size_t)p.npix + pix], v4 = p.rng[4 * (size_t)p.npix + pix];
+    const uint32_t d0 = p.rng[5 * (size_t)p.npix + pix];
+    uint32_t col, row;
+    tile_decode(pix, p.ncols, p.nrows, &col, &row);
+    const uint32_t t = (row / kCullTile) * p.ntx + col / kCullTile;
+    const uint32_t cm0 = p.cull[(size_t)t * p.cull_stride], cm1 = p.cull[(size_t)t * p.cull_stride + p.cull_wt];
+    for (uint32_t r = 0; r < nr; ++r) {
+        const uint32_t j0 = r * R;
+        uint4* e = reinterpret_cast<uint4*>(s.runs) + 3 * (size_t)(base + r);
+        e[0] = make_uint4(v0, v1, v2, v3);
+        e[1] = make_uint4(v4, d0 + 2u * j0 * IQ_XORWOW_WEYL, pix, q);
+        e[2] = make_uint4(j0 | (min(j0 + R, M) << 16), t, cm0, cm1);
+        uint32_t* d = s.st + (size_t)r * 5u * s.n + q;
+        d[0] = v0;
+        d[s.n] = v1;
+        d[2 * (size_t)s.n] = v2;
+        d[3 * (size_t)s.n] = v3;
+        d[4 * (size_t)s.n] = v4;
+        xorwow_skip_v(v0, v1, v2, v3, v4, 2u * (min(j0 + R, M) - j0));
+    }
+    uint32_t* d = s.st + (size_t)s.g_max * 5u * s.n + q;
+    d[0] = v0;
+    d[s.n] = v1;
+    d[2 * (size_t)s.n] = v2;
+    d[3 * (size_t)s.n] = v3;
+    d[4 * (size_t)s.n] = v4;
+}
+
+constexpr uint32_t kSpecBlock = 256;
+
+__host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth) {
+    return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + kSpecBlock * 16u +
+           (uint32_t)(max_depth > 1 ? max_depth : 1) * kSpecBlock * 4u;
+}
+
+// The slots: persistent waves, lane = one run at a time, one ray per live lane per iteration (a lane
+// whose slot ends starts its next one at once, its run's end takes a new run). Camera rays test their
+// tile's mask pairs, as in the plain kernel; a wave holding a secondary ray tests every pair.
+template <int MAXD, int OPT>
+__global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams p, const kspec s) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    float4* lds_tri = lds;
+    float4* lds_sph = lds + (size_t)p.ntri_pairs * kTriPairFloat4;
+    uint4* lds_cm = reinterpret_cast<uint4*>(lds_sph + (size_t)p.nsph_pairs * kSphPairFloat4);
+    float* lds_stk = reinterpret_cast<float*>(lds_cm + kSpecBlock);     // [depth][thread]
+    for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kSpecBlock)
+        lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
+    for (uint32_t i = threadIdx.x; i < p.nsph_pairs * kSphPairFloat4; i += kSpecBlock)
+        lds_sph[i] = reinterpret_cast<const float4*>(p.sph_pairs)[i];
+    __syncthreads();
+    if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);   // these chains are the launch's longest
+
+    const uint32_t lane = __lane_id();
+    const uint32_t nruns = *s.run_count;                  // final: the prep kernel ran before this one
+    bool active = false, exhausted = false;
+    uint32_t q = 0, j = 0, jend = 0, px = 0, py = 0;
+    rng6 st = {0u, 0u, 0u, 0u, 0u, 0u}, base = {0u, 0u, 0u, 0u, 0u, 0u};
+    ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    int depth = 0;
+    // a slot's sample starts here: its camera ray, and the state its two draws leave (the next slot's)
+    auto start_slot = [&]() {
+        camera_ray<OPT>(p, px, py, st, ray);
+        base = st;
+        depth = 0;
+    };
+    auto refill = [&]() {
+        const uint64_t need = __ballot(!active);
+        if (need == 0ull || exhausted) return;
+        uint32_t b = 0;
+        if (lane == 0) b = atomicAdd(s.run_count + 1, (uint32_t)__popcll(need));
+        b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
+        if (b + (uint32_t)__popcll(need) >= nruns) exhausted = true;
+        const uint32_t idx = b + prefix_below(need);
+        if (!active && idx < nruns) {
+            // the run's record: one round of three independent 16-byte loads
+            const uint4* e = reinterpret_cast<const uint4*>(s.runs) + 3 * (size_t)idx;
+            const uint4 e0 = e[0], e1 = e[1], e2 = e[2];
+            q = e1.w;
+            j = e2.x & 0xffffu;
+            jend = e2.x >> 16;
+            st = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y};
+            uint32_t col, row;
+            tile_decode(e1.z, p.ncols, p.nrows, &col, &row);
+            px = p.x0 + col;
+            py = p.y0 + row * p.ystep;
+            lds_cm[threadIdx.x] = make_uint4(e2.z, e2.w, e2.y, 0u);
+            start_slot();
+            active = true;
+        }
+    };
+    refill();
+    while (__any(active)) {
+        // closest hit (path_tracer.cu:253-295): camera rays over their tile's mask pairs in index order
+        float closest = kTMax;
+        int kind = kHitNone;
+        uint32_t hidx = 0;
+        {
+            const bool cull = !__any(active && depth != 0);
+            const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
+            uint4 cm = lds_cm[threadIdx.x];
+            const uint64_t act = __ballot(active);
+            const uint32_t first = (uint32_t)__builtin_ctzll(act);
+            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
+            const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
+            if (uni) {
+                cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
+                cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
+            }
+            const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
+            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray, closest,
+                                  kind, hidx, p.cull_wt, uni_mask);
+        }
+        if (active) {
+            // shade (path_tracer.cu:297-316) under the reference's materials
+            bool term = false;
+            uint32_t md_end = 0;
+            float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
+            if (kind == kHitSphere) {
+                const float* sq = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
+                const float sc = oren_nayar_scatter<OPT>(make_float4(sq[0], sq[2], sq[4], sq[6]), closest, ray, st);
+                if (depth + 1 >= p.max_depth) {
+                    term = true;                 // the last record is this scatter (biased, :252)
+                    md_end = 1;
+                    Lx = sc;
+                    Ly = sc;
+                    Lz = sc;
+                } else {
+                    lds_stk[(uint32_t)depth * kSpecBlock + threadIdx.x] = sc;
+                    ++depth;
+                }
+            } else if (kind == kHitTri) {
+                term = true;                     // emissive(1, 10)
+                Lx = 10.0f;
+                Ly = 10.0f;
+                Lz = 10.0f;
+            } else {
+                term = true;                     // sky gradient, :308-313
+                const float a = (ray.dy + 1.0f) * 0.5f;
+                const float one_a = 1.0f - a;
+                Lx = one_a + a * 0.5f;
+                Ly = one_a + a * 0.7f;
+                Lz = one_a + a * 1.0f;
+            }
+            if (term) {
+                // backward product (:321-324), clamp (:345-347), 0 + colour (:341, 348)
+                float cx = Lx, cy = Ly, cz = Lz;
+                for (int i = depth - 1; i >= 0; --i) {
+                    const float rr = lds_stk[(uint32_t)i * kSpecBlock + threadIdx.x];
+                    cx = cx * rr;
+                    cy = cy * rr;
+                    cz = cz * rr;
+                }
+                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                const size_t at = (size_t)q * s.m_cap + j;
+                reinterpret_cast<float4*>(s.res)[at] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                s.nres[at] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
+                if (++j == jend) {
+                    active = false;
+                } else {
+                    st = base;                   // slot j starts where slot j - 1's camera draws ended
+                    start_slot();
+                }
+            }
+        }
+        if (!exhausted && __ballot(!active) != 0ull) refill();
+    }
+}
+
+// The chain of one sphere pixel's slots, finished sequentially from slot j when it leaves the window:
+// one whole sample (camera ray, every bounce over every primitive from global memory, shading), its
+// clamped colour and the slots it consumed.
+template <int MAXD, int OPT>
+__device__ void spec_trace_one(const kparams& p, uint32_t px, uint32_t py, rng6& st, float& cx, float& cy,
+                               float& cz, uint32_t& nsl) {
+    float stk[MAXD];
+    ray3 ray;
+    camera_ray<OPT>(p, px, py, st, ray);
+    int depth = 0;
+    const float4* gtri = reinterpret_cast<const float4*>(p.tri_pairs);
+    const float4* gsph = reinterpret_cast<const float4*>(p.sph_pairs);
+    while (true) {
+        float closest = kTMax;
+        int kind = kHitNone;
+        uint32_t hidx = 0;
+        intersect_range<OPT>(gtri, 0, p.ntri, gsph, 0, p.nsph, ray, closest, kind, hidx);
+        uint32_t md_end = 0;
+        float Lx, Ly, Lz;
+        if (kind == kHitSphere) {
+            const float4_storage c = p.spheres[hidx];
+            const float sc = oren_nayar_scatter<OPT>(make_float4(c.x, c.y, c.z, c.w), closest, ray, st);
+            if (depth + 1 < p.max_depth) {
+                stk[depth++] = sc;
+                continue;
+            }
+            md_end = 1;
+            Lx = sc;
+            Ly = sc;
+            Lz = sc;
+        } else if (kind == kHitTri) {
+            Lx = 10.0f;
+            Ly = 10.0f;
+            Lz = 10.0f;
+        } else {
+            const float a = (ray.dy + 1.0f) * 0.5f;
+            const float one_a = 1.0f - a;
+            Lx = one_a + a * 0.5f;
+            Ly = one_a + a * 0.7f;
+            Lz = one_a + a * 1.0f;
+        }
+        for (int i = depth - 1; i >= 0; --i) {
+            Lx = Lx * stk[i];
+            Ly = Ly * stk[i];
+            Lz = Lz * stk[i];
+        }
+        cx = 0.0f + (Lx > 1.0f ? 1.0f : (Lx < 0.0f ? 0.0f : Lx));
+        cy = 0.0f + (Ly > 1.0f ? 1.0f : (Ly < 0.0f ? 0.0f : Ly));
+        cz = 0.0f + (Lz > 1.0f ? 1.0f : (Lz < 0.0f ? 0.0f : Lz));
+        nsl = (uint32_t)depth + 1u + md_end;
+        return;
+    }
+}
+
+// The walk (one thread per sphere pixel): slot counts 16 at a time, the colours of 8 chain samples in
+// flight at once, the running mean in sample order, the ray count (a sample's rays are its slots, or
+// max_depth when it ended on a scatter at max_depth), the state where the chain stops, the pixel.
+template <int MAXD, int OPT>
+__global__ __launch_bounds__(64) void iqpt_spec_stitch_kernel(const kparams p, const kspec s) {
+    __shared__ float2 tab[kAccTableMax];
+    __shared__ float tab_n[kAccTableMax];
+    for (uint32_t k = threadIdx.x; k < p.spp; k += 64u) {
+        const uint64_t n = p.frame0 + k + 1;
+        tab[k] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
+        tab_n[k] = (float)n;
+    }
+    __syncthreads();
+    const uint32_t q = blockIdx.x * 64u + threadIdx.x;
+    unsigned long long rays = 0;
+    if (q < s.n) {
+        const uint32_t pix = s.pix[q], M = s.m[q];
+        const float* a = reinterpret_cast<const float*>(p.lin + pix);
+        float ax = a[0], ay = a[1], az = a[2];
+        uint32_t k = 0, j = 0;
+        const float4* res = reinterpret_cast<const float4*>(s.res) + (size_t)q * s.m_cap;
+        const uint8_t* nr = s.nres + (size_t)q * s.m_cap;     // m_cap is a multiple of 16
+        uint32_t nbase = ~0u;
+        uint4 nb = make_uint4(0u, 0u, 0u, 0u);
+        auto fold = [&](float cx, float cy, float cz, uint32_t n) {
+            const float2 tv = tab[k];
+            float qx, qy, qz;
+            mean_terms<OPT>(cx, cy, cz, tab_n[k], tv.x, p.mean_tiny, qx, qy, qz);
+            ax = qx + ax * tv.y;
+            ay = qy + ay * tv.y;
+            az = qz + az * tv.y;
+            rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
+            ++k;
+        };
+        constexpr int kBatch = 8;
+        while (k < p.spp && j < M) {
+            uint32_t cj[kBatch], cn[kBatch];
+            int cnt = 0;
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b) {
+                cj[b] = 0u;
+                cn[b] = 0u;
+                if (k + (uint32_t)b < p.spp && j < M) {
+                    if ((j & ~15u) != nbase) {
+                        nbase = j & ~15u;
+                        nb = *reinterpret_cast<const uint4*>(nr + nbase);
+                    }
+                    const uint32_t o = j - nbase, w = o >> 2;
+                    const uint32_t word = w == 0u ? nb.x : (w == 1u ? nb.y : (w == 2u ? nb.z : nb.w));
+                    cj[b] = j;
+                    cn[b] = (word >> ((o & 3u) * 8u)) & 0xffu;
+                    j += cn[b];
+                    cnt = b + 1;
+                }
+            }
+            float4 v[kBatch];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b)
+                if (b < cnt) v[b] = res[cj[b]];
+#pragma unroll
+            for (int b = 0; b < kBatch; ++b)
+                if (b < cnt) fold(v[b].x, v[b].y, v[b].z, cn[b]);
+        }
+        // the state at slot j: from the nearest stored state at or below it (slot M when past the window)
+        const uint32_t plane = j >= M ? s.g_max : j / s.run_len;
+        const uint32_t steps = j >= M ? j - M : j - plane * s.run_len;
+        const uint32_t* sv = s.st + (size_t)plane * 5u * s.n + q;
+        rng6 st = {sv[0], sv[s.n], sv[2 * (size_t)s.n], sv[3 * (size_t)s.n], sv[4 * (size_t)s.n],
+                   p.rng[5 * (size_t)p.npix + pix] + 2u * j * IQ_XORWOW_WEYL};
+        xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * steps);
+        if (k < p.spp) {
+            // the chain left its window: finish its samples here, in order
+            uint32_t col, row;
+            tile_decode(pix, p.ncols, p.nrows, &col, &row);
+            const uint32_t px = p.x0 + col, py = p.y0 + row * p.ystep;
+            while (k < p.spp) {
+                float cx, cy, cz;
+                uint32_t n;
+                spec_trace_one<MAXD, OPT>(p, px, py, st, cx, cy, cz, n);
+                fold(cx, cy, cz, n);
+                j += n;
+            }
+        }
+        const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
+        const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
+        const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
+        p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+        reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
+        p.rng[pix] = st.v0;
+        p.rng[(size_t)p.npix + pix] = st.v1;
+        p.rng[2 * (size_t)p.npix + pix] = st.v2;
+        p.rng[3 * (size_t)p.npix + pix] = st.v3;
+        p.rng[4 * (size_t)p.npix + pix] = st.v4;
+        p.rng[5 * (size_t)p.npix + pix] = st.d;
+        s.rho[q] = (uint32_t)(((uint64_t)j * 256u) / p.spp);
+    }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
+    if (__lane_id() == 0 && rays) atomicAdd(p.rays, rays);
+}
+
 // LDS bytes of the chain kernel for a launch (scene pairs, mean table, mask slots, ring, group words,
 // scatter stack)
 __host__ __device__ inline uint32_t chain_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, uint32_t spp, int max_depth,
@@ -2900,7 +3423,8 @@ struct chain_variant {
     int (*occ)(uint32_t, int*);
 };
 #define IQPT_CV(M, O, L) {M, O, L, chain_launch_t<M, O, L>, chain_occ_t<M, O, L>}
-#define IQPT_CV4(O) IQPT_CV(8, O, 8), IQPT_CV(16, O, 8), IQPT_CV(8, O, 4), IQPT_CV(16, O, 4)
+#define IQPT_CV4(O) IQPT_CV(8, O, 8), IQPT_CV(16, O, 8), IQPT_CV(8, O, 4), IQPT_CV(16, O, 4), IQPT_CV(8, O, 16), \
+                    IQPT_CV(16, O, 16)
 const chain_variant kChainVariants[] = {
     IQPT_CV4(kOptDefault | kOptPrio),
     IQPT_CV4((kOptDefault & ~kOptFastDiv) | kOptPrio),
@@ -2915,6 +3439,114 @@ const chain_variant* find_chain(int max_depth, int opt, uint32_t lanes) {
     return nullptr;
 }
 }  // namespace
+
+// iqpt_fan_kernel launches: the option bits it depends on are the camera form and the division forms
+namespace {
+template <int OPT>
+int fan_launch_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
+    hipLaunchKernelGGL((iqpt_fan_kernel<OPT>), dim3(grid), dim3(kFanBlock), lds, stream, p);
+    return (int)hipGetLastError();
+}
+struct fan_variant {
+    int key;
+    int (*launch)(hipStream_t, const kparams&, uint32_t, uint32_t);
+};
+constexpr int kFanKeyBits = kOptFastDiv | kOptCamAxis;
+const fan_variant kFanVariants[] = {
+    {kOptFastDiv, fan_launch_t<kOptDefault>},
+    {0, fan_launch_t<kOptDefault & ~kOptFastDiv>},
+    {kOptFastDiv | kOptCamAxis, fan_launch_t<kOptDefault | kOptCamAxis>},
+};
+const fan_variant* find_fan(int opt) {
+    // the production option sets differ from kOptDefault only in these bits (and in bits the fan
+    // kernel does not read: priority, overlap, split)
+    if ((opt & (kOptPair | kOptCull | kOptAccTable | kOptCamConst)) !=
+            (kOptPair | kOptCull | kOptAccTable | kOptCamConst) || (opt & (kOptMaterials | kOptStats)))
+        return nullptr;
+    for (const fan_variant& v : kFanVariants)
+        if (v.key == (opt & kFanKeyBits)) return &v;
+    return nullptr;
+}
+}  // namespace
+
+bool fan_variant_exists(int opt) { return find_fan(opt) != nullptr; }
+
+uint32_t fan_lds(const kparams& p) { return fan_lds_bytes(p.ntri_pairs, p.spp); }
+
+int launch_fan(void* stream, const kparams& p, uint32_t ntiles, int opt) {
+    const fan_variant* v = find_fan(opt);
+    if (!v || p.spp > kAccTableMax || p.cull == nullptr || p.cull_wt > 16u || p.tile_order == nullptr)
+        return (int)hipErrorInvalidDeviceFunction;
+    if (ntiles == 0 || p.spp == 0) return 0;
+    return v->launch((hipStream_t)stream, p, ntiles, fan_lds(p));
+}
+
+// Slot-parallel sphere pixels (IQPT_SPLIT_SPEC): the resident production option sets, reference materials
+namespace {
+template <int MAXD, int OPT>
+int spec_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t grid, uint32_t lds) {
+    hipLaunchKernelGGL((iqpt_spec_kernel<MAXD, OPT>), dim3(grid), dim3(kSpecBlock), lds, stream, p, s);
+    return (int)hipGetLastError();
+}
+template <int MAXD, int OPT>
+int spec_occ_t(uint32_t lds, int* blocks) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_spec_kernel<MAXD, OPT>, kSpecBlock, lds);
+}
+template <int MAXD, int OPT>
+int spec_stitch_t(hipStream_t stream, const kparams& p, const kspec& s) {
+    hipLaunchKernelGGL((iqpt_spec_stitch_kernel<MAXD, OPT>), dim3((s.n + 63u) / 64u), dim3(64), 0, stream, p, s);
+    return (int)hipGetLastError();
+}
+struct spec_variant {
+    int maxd, opt;
+    int (*launch)(hipStream_t, const kparams&, const kspec&, uint32_t, uint32_t);
+    int (*occ)(uint32_t, int*);
+    int (*stitch)(hipStream_t, const kparams&, const kspec&);
+};
+#define IQPT_SV(M, O) {M, O, spec_launch_t<M, O>, spec_occ_t<M, O>, spec_stitch_t<M, O>}
+#define IQPT_SV2(O) IQPT_SV(8, O), IQPT_SV(16, O)
+const spec_variant kSpecVariants[] = {
+    IQPT_SV2(kOptDefault | kOptPrio),
+    IQPT_SV2((kOptDefault & ~kOptFastDiv) | kOptPrio),
+    IQPT_SV2(kOptDefault | kOptCamAxis | kOptPrio),
+};
+#undef IQPT_SV2
+#undef IQPT_SV
+const spec_variant* find_spec(int max_depth, int opt) {
+    const int maxd = max_depth <= 8 ? 8 : 16;
+    for (const spec_variant& v : kSpecVariants)
+        if (v.maxd == maxd && v.opt == ((opt | kOptPrio) & ~(kOptOverlap | kOptSplit))) return &v;
+    return nullptr;
+}
+}  // namespace
+
+int launch_spec_prep(void* stream, const kparams& p, const kspec& s) {
+    if (s.n == 0) return 0;
+    hipLaunchKernelGGL(iqpt_spec_prep_kernel, dim3((s.n + 255u) / 256u), dim3(256), 0, (hipStream_t)stream, p, s);
+    return (int)hipGetLastError();
+}
+
+bool spec_variant_exists(int max_depth, int opt) { return max_depth <= 16 && find_spec(max_depth, opt) != nullptr; }
+
+int spec_occupancy(int max_depth, int opt, const kparams& p, int* blocks) {
+    const spec_variant* v = find_spec(max_depth, opt);
+    if (!v) return (int)hipErrorInvalidDeviceFunction;
+    return v->occ(spec_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.max_depth), blocks);
+}
+
+int launch_spec(void* stream, const kparams& p, const kspec& s, uint32_t grid, int opt) {
+    const spec_variant* v = find_spec(p.max_depth, opt);
+    if (!v || p.max_depth > 16 || p.cull == nullptr) return (int)hipErrorInvalidDeviceFunction;
+    if (s.n == 0 || grid == 0) return 0;
+    return v->launch((hipStream_t)stream, p, s, grid, spec_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.max_depth));
+}
+
+int launch_spec_stitch(void* stream, const kparams& p, const kspec& s, int opt) {
+    const spec_variant* v = find_spec(p.max_depth, opt);
+    if (!v || p.spp > kAccTableMax) return (int)hipErrorInvalidDeviceFunction;
+    if (s.n == 0) return 0;
+    return v->stitch((hipStream_t)stream, p, s);
+}
 
 bool chain_variant_exists(int max_depth, int opt, uint32_t lanes) {
     return max_depth <= 16 && find_chain(max_depth, opt, lanes) != nullptr;

@@ -103,6 +103,7 @@ struct iqpt_ctx {
     float4_storage* d_sph = nullptr;
     float4_storage* d_sph_pairs = nullptr;
     uint32_t ntri = 0, nsph = 0;
+    std::vector<float4_storage> h_sph;   // world-space spheres (host copy: per-pixel sphere bundles, build_split)
     // material table (§8f.3), null without one
     uint32_t* d_tri_mat = nullptr;
     uint32_t* d_sph_mat = nullptr;
@@ -162,6 +163,27 @@ struct iqpt_ctx {
     uint32_t chain_waves = 0;
     uint32_t chain_lanes = 8;           // lanes per pixel (4 or 8)
     bool chain_last = false;
+    bool fan_last = false;              // the last launch ran the anchored tiles in iqpt_fan_kernel
+    bool fan_anchored = true;           // chain / fan launches: anchored tiles in the fan kernel (else plain)
+    // chain launches with the fan kernel: the pixels of split tiles whose own camera-ray
+    // bundle may reach a sphere (the chain kernel's pixel list), and the fan kernel's tiles with the lanes
+    // it owns (anchored tiles whole; split tiles without their sphere pixels)
+    uint32_t* d_chain_pix = nullptr;
+    uint32_t n_chain_pix = 0;
+    uint32_t* d_fan_tiles = nullptr;
+    uint64_t* d_fan_lanes = nullptr;
+    uint32_t n_fan_tiles = 0;
+    // spec launches: per sphere pixel (d_chain_pix) the window, the chain's slots per
+    // sample (history, zeroed when the pixel list changes), states every kSpecRunLen slots, the run list,
+    // the slot results; sized for (spec_n, spec_mcap)
+    uint32_t* d_spec = nullptr;         // m, rho (spec_n each), run_count (2), pad, runs (12 x spec_n x runs per pixel)
+    uint32_t* d_spec_st = nullptr;
+    float4_storage* d_spec_res = nullptr;
+    uint8_t* d_spec_nres = nullptr;
+    uint32_t spec_n = 0, spec_mcap = 0;
+    bool spec_rho_valid = false;
+    bool spec_last = false;
+    uint32_t spec_rho0 = iqpt::kSpecRho0;   // window of a pixel without history (iqpt_debug_set_spec)
     uint32_t chain_par = 0;             // the queue-counter set of the next chain launch
     bool chain_q_ready[2] = {false, false};   // that set is zeroed (in stream order)
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
@@ -259,8 +281,79 @@ void free_split(iqpt_ctx* c) {
     }
     if (c->d_nres) (void)hipFree(c->d_nres);
     c->d_nres = nullptr;
+    for (uint32_t** b : {&c->d_chain_pix, &c->d_fan_tiles}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    if (c->d_fan_lanes) (void)hipFree(c->d_fan_lanes);
+    c->d_fan_lanes = nullptr;
+    c->n_chain_pix = c->n_fan_tiles = 0;
+    c->spec_rho_valid = false;           // a new pixel list: no chain history
     c->n_split_tiles = c->n_anchor = 0;
     c->res_slots = 0;
+}
+
+// Chain launches with the fan kernel: which pixels of the split tiles can reach a sphere at all. The
+// interval bundle of iq_interval.h (the same RN operation chain as the kernel's camera ray and sphere
+// test, compiled for the host with contraction off) is evaluated per pixel over its jitter square: a
+// pixel whose bundle rejects every sphere ends every sample on its first ray (every triangle is emissive
+// under the reference's materials) and goes to the fan kernel with its tile's triangle mask; the rest
+// are the chain kernel's. Without a material table and with at most 64 spheres (otherwise every pixel
+// of a split tile stays with the chain kernel).
+int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const std::vector<uint32_t>& split,
+                      const uint32_t* sp_pix) {
+    std::vector<uint32_t> chain_pix, fan_tiles(anchor);
+    std::vector<uint64_t> fan_lanes(anchor.size(), ~0ull);
+    const bool per_pixel = !c->d_mats && c->h_sph.size() == c->nsph && c->nsph <= 64;
+    iqiv::camera_in ci;
+    ci.width = c->width;
+    ci.height = c->height;
+    ci.rcp_width = 0.0f;
+    ci.rcp_height = 0.0f;
+    ci.inv_proj = c->cam.inv_proj;
+    ci.inv_view = c->cam.inv_view;
+    uint32_t cc = 0;
+    cam_constants(c->cam, &cc, &ci.near_rw, &ci.far_rw);
+    ci.cam_const = (int)cc;
+    for (size_t st = 0; st < split.size(); ++st) {
+        uint64_t lanes = 0;
+        for (uint32_t i = 0; i < iqpt::kQueueChunk; ++i) {
+            const uint32_t pix = sp_pix[st * iqpt::kQueueChunk + i];
+            if (pix == ~0u) continue;
+            bool sphere = !per_pixel;
+            if (per_pixel) {
+                uint32_t col, row;
+                iqpt::tile_decode(pix, c->ncols, c->set.nrows, &col, &row);
+                const uint32_t x = c->set.x0 + col, y = c->set.y0 + row * c->set.ystep;
+                const iqiv::bundle b = iqiv::camera_bundle(ci, x, x, y, y);
+                for (uint32_t k = 0; k < c->nsph && !sphere; ++k) {
+                    const float ctr[3] = {c->h_sph[k].x, c->h_sph[k].y, c->h_sph[k].z};
+                    sphere = !(b.ok && iqiv::sphere_culled(b, ctr, c->h_sph[k].w));
+                }
+            }
+            if (sphere) chain_pix.push_back(pix);
+            else lanes |= 1ull << i;
+        }
+        if (lanes) {
+            fan_tiles.push_back(split[st]);
+            fan_lanes.push_back(lanes);
+        }
+    }
+    if (!chain_pix.empty()) {
+        if (hipMalloc(&c->d_chain_pix, chain_pix.size() * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "chain pixel list");
+        IQPT_HIP(hipMemcpy(c->d_chain_pix, chain_pix.data(), chain_pix.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    if (!fan_tiles.empty()) {
+        if (hipMalloc(&c->d_fan_tiles, fan_tiles.size() * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&c->d_fan_lanes, fan_lanes.size() * sizeof(uint64_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "fan tile list");
+        IQPT_HIP(hipMemcpy(c->d_fan_tiles, fan_tiles.data(), fan_tiles.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        IQPT_HIP(hipMemcpy(c->d_fan_lanes, fan_lanes.data(), fan_lanes.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    }
+    c->n_chain_pix = (uint32_t)chain_pix.size();
+    c->n_fan_tiles = (uint32_t)fan_tiles.size();
+    return IQPT_OK;
 }
 
 // The split set of kOptSplit: the tiles whose camera rays may scatter — a sphere
@@ -276,7 +369,8 @@ int build_split(iqpt_ctx* c, const std::vector<uint32_t>& order, const std::vect
                               (c->d_mats ? (cnt[t] + cnt[ntiles + t]) > 0 : cnt[ntiles + t] > 0);
         (scatters ? split : anchor).push_back(t);
     }
-    if (split.empty()) return IQPT_OK;
+    if (anchor.empty() && split.empty()) return IQPT_OK;
+    // (no split tile: the anchored list alone, for fan launches; every split launch needs split tiles)
     const size_t ns = split.size() * (size_t)iqpt::kQueueChunk;
     if (ns >= (1ull << 31)) return IQPT_OK;
     std::vector<uint32_t> host(anchor.size() + split.size() + 5 * ns, 0u);
@@ -293,15 +387,15 @@ int build_split(iqpt_ctx* c, const std::vector<uint32_t>& order, const std::vect
             sp_pix[st * iqpt::kQueueChunk + i] = i < tw * th ? first + i : ~0u;
     }
     if (hipMalloc(&c->d_split, host.size() * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&c->d_sp_st, 6 * ns * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&c->d_sp_acc, ns * sizeof(float4_storage)) != hipSuccess) {
+        (ns && hipMalloc(&c->d_sp_st, 6 * ns * sizeof(uint32_t)) != hipSuccess) ||
+        (ns && hipMalloc(&c->d_sp_acc, ns * sizeof(float4_storage)) != hipSuccess)) {
         free_split(c);
         return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "split buffers");
     }
     IQPT_HIP(hipMemcpy(c->d_split, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     c->n_anchor = (uint32_t)anchor.size();
     c->n_split_tiles = (uint32_t)split.size();
-    return IQPT_OK;
+    return build_pixel_split(c, anchor, split, sp_pix);
 }
 
 // (Re)build the kOptCull tile masks of the current camera and packet on the context's stream.
@@ -836,6 +930,8 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     free_split(c);
+    for (void* b : {(void*)c->d_spec, (void*)c->d_spec_st, (void*)c->d_spec_res, (void*)c->d_spec_nres})
+        if (b) (void)hipFree(b);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
     if (c->d_tile_order) (void)hipFree(c->d_tile_order);
@@ -1042,6 +1138,7 @@ int iqpt_upload_packet(iqpt_ctx* c, const iqpt_packet_desc* pk) {
     }
     c->ntri = (uint32_t)total;
     c->nsph = nsdc;
+    c->h_sph = sph;
     c->fast_rcp_ok = fast_rcp_ok;
     c->have_packet = true;
     return IQPT_OK;
@@ -1242,9 +1339,21 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const double lanes = (double)c->num_cus * std::max(occ_p, 1) * iqpt::kRenderBlock;
         chain = c->split_mode == IQPT_SPLIT_CHAIN || (double)c->npix < iqpt::kChainAutoPixelsPerLane * lanes;
     }
+    // fan launches: the anchored tiles (no sphere candidate) in iqpt_fan_kernel, the split
+    // set's tiles in the plain kernel beside it
+    const bool fan_ok = !stream_batches && p.cull && (c->n_anchor > 0 || c->n_fan_tiles > 0) && tune_slot < 0 &&
+                        !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax && c->cull_wt <= 16 &&
+                        iqpt::fan_variant_exists(opt);
+    const bool fan = !chain && fan_ok && c->split_mode == IQPT_SPLIT_FAN;
+    // spec launches: sphere pixels slot-parallel, every other pixel in the fan kernel
+    const bool spec = !chain && fan_ok && c->split_mode == IQPT_SPLIT_SPEC && c->n_split_tiles > 0 &&
+                      iqpt::spec_variant_exists(c->max_depth, opt) &&
+                      (size_t)c->n_chain_pix * ((iqpt::kSplitMCapMul * spp + 15u) & ~15u) * 22u <= iqpt::kSplitResBudget;
+    const bool fan_beside_chain = chain && fan_ok && c->fan_anchored;
     uint32_t lds_split = lds + iqpt::kRenderBlock * (16u + 24u);   // + lds_sp and the base states
     bool split = false;
-    if (!chain && c->split_mode != IQPT_SPLIT_OFF && c->split_mode != IQPT_SPLIT_CHAIN && !stream_batches && p.cull &&
+    if (!chain && !fan && !spec && c->split_mode != IQPT_SPLIT_OFF && c->split_mode != IQPT_SPLIT_CHAIN &&
+        c->split_mode != IQPT_SPLIT_FAN && c->split_mode != IQPT_SPLIT_SPEC && !stream_batches && p.cull &&
         c->n_split_tiles > 0 &&
         tune_slot < 0 && iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptSplit)) {
         int occ_s = 0;
@@ -1252,7 +1361,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const double lanes = (double)c->num_cus * std::max(occ_s, 1) * iqpt::kRenderBlock;
         split = occ_s > 0 && (c->split_mode == IQPT_SPLIT_ON || (double)c->npix < iqpt::kSplitAutoPixelsPerLane * lanes);
     }
-    if ((split || chain) && (st = join_streams(c)) != IQPT_OK) return st;   // split / chain launches never overlap
+    if ((split || chain || fan || spec) && (st = join_streams(c)) != IQPT_OK) return st;   // these never overlap
+    // split launches with the anchored tiles in the fan kernel beside the four split passes
+    const bool fan_split = split && fan_ok && c->fan_anchored;
     const size_t ns_cap = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
     const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
     const uint32_t g_max = (m_cap + iqpt::kSplitRunLen - 1) / iqpt::kSplitRunLen;
@@ -1344,7 +1455,8 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // Tiles are bound to the 8 XCDs (HW_REG_XCC_ID): only on a device that exposes 8 (not a partition
     // mode) and with at least 64 blocks, so that the observed round-robin dispatch puts blocks on every
     // XCD (HIP promises no placement; the kernel's last block checks it and raises an error bit if not)
-    bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && !chain && p.cull != nullptr &&
+    bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && !chain && !fan && !spec &&
+               p.cull != nullptr &&
                tune_slot < 0 && c->d_tile_done && c->d_xcd_order && c->num_xcc == 8 && c->num_cus >= 64 &&
                (uint64_t)c->npix >= 64ull * iqpt::kRenderBlock &&
                iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptOverlap);
@@ -1355,12 +1467,12 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // two launches in flight: each keeps one block slot per CU free for the other (occ - 1 per CU), so the
     // earlier launch, which the later one waits for, can always run
     if (ovl && occ < 2) ovl = false;
-    if ((ovl || chain) && !c->stream2) {
+    if ((ovl || chain || fan || fan_split || spec) && !c->stream2) {
         if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_s2, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
-            if (chain) return iqpt::fail(IQPT_ERR_HIP, "second stream for the chain kernel");
+            if (chain || fan || fan_split || spec) return iqpt::fail(IQPT_ERR_HIP, "second stream for the chain / fan kernel");
             ovl = false;
             c->overlap_mode = IQPT_OVERLAP_OFF;
         }
@@ -1403,11 +1515,12 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // profiles/r02/ab_camaxis_overlap.json, split_share_v17_camaxis.json)
     if (!c->opt_fixed && cam_axis && !stream_batches && !split &&
         iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptCamAxis) &&
-        (!chain || iqpt::chain_variant_exists(c->max_depth, opt | iqpt::kOptCamAxis, c->chain_lanes)))
+        (!chain || iqpt::chain_variant_exists(c->max_depth, opt | iqpt::kOptCamAxis, c->chain_lanes)) &&
+        (!spec || iqpt::spec_variant_exists(c->max_depth, opt | iqpt::kOptCamAxis)))
         opt |= iqpt::kOptCamAxis;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
-    if (!ovl && !chain) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
+    if (!ovl && !chain && !fan && !spec) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
     hipEvent_t e0 = take_event(c), e1 = take_event(c);
     if (e0) (void)hipEventRecord(e0, ls);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
@@ -1417,11 +1530,15 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->ovl_epoch += 1;
         c->next_on_main = !c->next_on_main;
         if (le != 0) c->ovl_zero = true;     // a failed launch breaks the chain's counts: restart it
-    } else if (chain) {
-        // the split set's pixels on stream2 (iqpt_chain_kernel, pixels from queue[1]) beside the plain kernel
-        // over the anchored tiles on stream (queue[0]); stream waits for stream2 before the end event
-        const size_t ns = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
-        p.sp_pix = c->d_split + c->n_anchor + c->n_split_tiles;
+    } else if (chain || fan) {
+        // chain: the split set's pixels in iqpt_chain_kernel (pixels from queue[1]) on stream; fan: the split
+        // set's tiles in the plain kernel (queue[0]) on stream. Beside it on stream2 the anchored tiles, in
+        // iqpt_fan_kernel (one block per tile) or the plain kernel (queue[0]); stream waits for stream2
+        // before the end event.
+        // the chain kernel's pixels: every pixel of the split tiles, or (with the fan kernel beside it) those
+        // whose own bundle may reach a sphere
+        const size_t ns = fan_beside_chain ? c->n_chain_pix : (size_t)c->n_split_tiles * iqpt::kQueueChunk;
+        p.sp_pix = fan_beside_chain ? c->d_chain_pix : c->d_split + c->n_anchor + c->n_split_tiles;
         p.ns_cap = (uint32_t)ns;
         const uint32_t lanes = c->chain_lanes;
         const uint32_t lds_c = iqpt::chain_lds(p, lanes);
@@ -1441,13 +1558,30 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         p.queue = qset;
         IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
         IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
-        le = iqpt::launch_chain(c->stream, p, grid_c, opt, lanes);
-        if (le == 0 && c->n_anchor > 0) {
+        if (chain) {
+            if (ns > 0) le = iqpt::launch_chain(c->stream, p, grid_c, opt, lanes);
+        } else if (c->n_split_tiles > 0) {
+            iqpt::kparams ps = p;
+            ps.tile_order = c->d_split + c->n_anchor;
+            ps.nqueue = c->n_split_tiles;
+            const uint64_t want_s = ((uint64_t)c->n_split_tiles * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
+            const uint32_t grid_s = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_s, (uint64_t)c->num_cus * occ));
+            le = iqpt::launch_render(c->stream, ps, grid_s, lds, stream_batches, opt);
+        }
+        if (le == 0 && fan_beside_chain && c->n_fan_tiles > 0) {
+            p.tile_order = c->d_fan_tiles;
+            p.fan_lanes = c->d_fan_lanes;
+            le = iqpt::launch_fan(c->stream2, p, c->n_fan_tiles, opt);
+        } else if (le == 0 && c->n_anchor > 0) {
             p.tile_order = c->d_split;
             p.nqueue = c->n_anchor;
-            const uint64_t want_p = ((uint64_t)c->n_anchor * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
-            const uint32_t grid_p = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_p, (uint64_t)c->num_cus * occ));
-            le = iqpt::launch_render(c->stream2, p, grid_p, lds, stream_batches, opt);
+            if (fan) {
+                le = iqpt::launch_fan(c->stream2, p, c->n_anchor, opt);
+            } else {
+                const uint64_t want_p = ((uint64_t)c->n_anchor * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
+                const uint32_t grid_p = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_p, (uint64_t)c->num_cus * occ));
+                le = iqpt::launch_render(c->stream2, p, grid_p, lds, stream_batches, opt);
+            }
         }
         const uint32_t nxt = c->chain_par ^ 1u;
         IQPT_HIP(hipMemsetAsync(c->d_queue + 4 + nxt * (iqpt::kOverlapQueueWords / 2), 0, 4 * sizeof(uint32_t), c->stream2));
@@ -1456,9 +1590,82 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->chain_par = nxt;
         IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
         IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
+    } else if (spec) {
+        // every pixel without a sphere in reach in the fan kernel on stream2; on stream the sphere pixels:
+        // prep (windows, states, runs) -> slots -> stitch (walk, fold, finish, store)
+        iqpt::kspec ks2;
+        std::memset(&ks2, 0, sizeof ks2);
+        const uint32_t n = c->n_chain_pix;
+        const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
+        const uint32_t R = iqpt::kSpecRunLen;
+        const uint32_t runs_per = (m_cap + R - 1) / R;
+        if (n > 0 && (n > c->spec_n || m_cap > c->spec_mcap)) {
+            IQPT_HIP(hipStreamSynchronize(c->stream));
+            for (void* b : {(void*)c->d_spec, (void*)c->d_spec_st, (void*)c->d_spec_res, (void*)c->d_spec_nres})
+                if (b) (void)hipFree(b);
+            c->d_spec = nullptr;
+            c->d_spec_st = nullptr;
+            c->d_spec_res = nullptr;
+            c->d_spec_nres = nullptr;
+            c->spec_n = c->spec_mcap = 0;
+            const size_t slots = (size_t)n * m_cap;
+            if (slots * 17 + ((size_t)runs_per + 1) * 5 * n * 4 + 48 * (size_t)runs_per * n > iqpt::kSplitResBudget ||
+                hipMalloc(&c->d_spec, (2 * (size_t)n + 4 + 12 * (size_t)n * runs_per) * sizeof(uint32_t)) != hipSuccess ||
+                hipMalloc(&c->d_spec_st, ((size_t)runs_per + 1) * 5 * n * sizeof(uint32_t)) != hipSuccess ||
+                hipMalloc(&c->d_spec_res, slots * sizeof(float4_storage)) != hipSuccess ||
+                hipMalloc(&c->d_spec_nres, slots) != hipSuccess) {
+                (void)hipGetLastError();
+                return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec buffers");
+            }
+            c->spec_n = n;
+            c->spec_mcap = m_cap;
+            c->spec_rho_valid = false;
+        }
+        ks2.n = n;
+        ks2.m_cap = m_cap;
+        ks2.run_len = R;
+        ks2.g_max = runs_per;
+        ks2.rho0 = c->spec_rho0;
+        ks2.pix = c->d_chain_pix;
+        ks2.m = c->d_spec;
+        ks2.rho = c->d_spec + n;
+        ks2.run_count = c->d_spec + 2 * (size_t)n;
+        ks2.runs = c->d_spec + ((2 * (size_t)n + 2 + 3) & ~(size_t)3);   // 16-byte aligned records
+        ks2.st = c->d_spec_st;
+        ks2.res = c->d_spec_res;
+        ks2.nres = c->d_spec_nres;
+        IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
+        IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
+        if (c->n_fan_tiles > 0) {
+            iqpt::kparams pf = p;
+            pf.tile_order = c->d_fan_tiles;
+            pf.fan_lanes = c->d_fan_lanes;
+            le = iqpt::launch_fan(c->stream2, pf, c->n_fan_tiles, opt);
+        }
+        if (le == 0 && n > 0) {
+            if (!c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, (size_t)n * sizeof(uint32_t), c->stream));
+            c->spec_rho_valid = true;
+            IQPT_HIP(hipMemsetAsync(ks2.run_count, 0, 2 * sizeof(uint32_t), c->stream));
+            le = iqpt::launch_spec_prep(c->stream, p, ks2);
+            int occ_s = 0;
+            if (le == 0 && (iqpt::spec_occupancy(c->max_depth, opt, p, &occ_s) != 0 || occ_s < 1)) occ_s = 1;
+            if (le == 0) le = iqpt::launch_spec(c->stream, p, ks2, (uint32_t)c->num_cus * (uint32_t)occ_s, opt);
+            if (le == 0) le = iqpt::launch_spec_stitch(c->stream, p, ks2, opt);
+        }
+        IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
+        IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
     } else if (split) {
-        // prep -> round 1 (runs, anchored tiles, light split pixels) -> stitch -> round 2 (leftovers)
-        le = iqpt::launch_split_prep(c->stream, ks);
+        // prep -> round 1 (runs, anchored tiles, light split pixels) -> stitch -> round 2 (leftovers); with
+        // the fan kernel the anchored tiles leave round 1 for iqpt_fan_kernel on stream2
+        if (fan_split) {
+            iqpt::kparams pf = p;
+            pf.tile_order = c->d_split;
+            IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
+            IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
+            le = iqpt::launch_fan(c->stream2, pf, c->n_anchor, opt);
+            p.n_anchor = 0;
+        }
+        if (le == 0) le = iqpt::launch_split_prep(c->stream, ks);
         p.split_round = 1;
         p.queue = c->d_queue;
         if (le == 0) le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
@@ -1466,11 +1673,17 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         p.split_round = 2;
         p.queue = c->d_queue + 1;
         if (le == 0) le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
+        if (fan_split) {
+            IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
+            IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
+        }
     } else {
         le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
     }
     c->split_last = split;
     c->chain_last = chain;
+    c->fan_last = fan || fan_beside_chain || fan_split || spec;
+    c->spec_last = spec;
     c->last_ls = ls;
     c->last_ovl = ovl;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
@@ -1717,6 +1930,53 @@ int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
     return IQPT_OK;
 }
 
+/* Internal (tools): the per-pixel split of the last camera / packet — sphere pixels (the chain and spec
+ * kernels' list), fan tiles, anchored tiles, split tiles — and, after a spec launch, its run count and the
+ * sum of its windows. Synchronises. */
+int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
+    if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = enter(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < 8; ++i) out8[i] = 0;
+    out8[0] = c->n_chain_pix;
+    out8[1] = c->n_fan_tiles;
+    out8[2] = c->n_anchor;
+    out8[3] = c->n_split_tiles;
+    if (c->spec_last && c->d_spec && c->spec_n >= c->n_chain_pix) {
+        const uint32_t n = c->n_chain_pix;
+        std::vector<uint32_t> v(2 * (size_t)n + 2);
+        IQPT_HIP(hipMemcpy(v.data(), c->d_spec, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        out8[4] = v[2 * (size_t)n];
+        unsigned long long m = 0, rho = 0;
+        for (uint32_t q = 0; q < n; ++q) {
+            m += v[q];
+            rho += v[n + q];
+        }
+        out8[5] = m;
+        out8[6] = rho;
+    }
+    return IQPT_OK;
+}
+
+/* Internal (tests): the slots per sample (x 256) a spec window assumes for a pixel without history; a small
+ * value makes the chains of sphere pixels leave their first window (the stitch then finishes them).
+ * 0 restores the default; the history is dropped so that the next launch uses it. */
+int iqpt_debug_set_spec(iqpt_ctx* c, uint32_t rho0) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->spec_rho0 = rho0 ? rho0 : iqpt::kSpecRho0;
+    c->spec_rho_valid = false;
+    return IQPT_OK;
+}
+
+/* Internal (A/B): chain launches run the anchored tiles in iqpt_fan_kernel (1, the default) or in the
+ * plain kernel (0). */
+int iqpt_debug_set_fan(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->fan_anchored = on != 0;
+    return IQPT_OK;
+}
+
 /* Internal (tests): lower the kernels' forward-progress bounds (0 keeps a bound's default) and bias the
  * per-tile wait targets of overlapped launches, so that tests can force each error path. */
 int iqpt_debug_set_limits(iqpt_ctx* c, uint32_t spin_limit, uint32_t iter_limit, uint32_t wait_bias) {
@@ -1808,7 +2068,11 @@ int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
     out8[1] = c->n_anchor;
     const size_t ns = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
     out8[2] = ns;
-    out8[7] = c->split_last ? 1 : (c->chain_last ? 2 : 0);
+    // launch mode: 1 split, 2 chain (anchored tiles plain), 3 fan (split tiles plain), 4 chain + fan, 5 split + fan,
+    // 6 spec (sphere pixels slot-parallel, the rest fan)
+    out8[7] = c->spec_last ? 6
+                           : (c->split_last ? (c->fan_last ? 5 : 1)
+                                            : (c->chain_last ? (c->fan_last ? 4 : 2) : (c->fan_last ? 3 : 0)));
     if (!c->d_split || ns == 0) return IQPT_OK;
     uint32_t left = 0;
     IQPT_HIP(hipMemcpy(&left, c->d_queue + 2, sizeof left, hipMemcpyDeviceToHost));
@@ -1847,8 +2111,8 @@ int iqpt_debug_set_split_knobs(iqpt_ctx* c, uint32_t heavy_rho, uint32_t refill_
 int iqpt_debug_set_chain_waves(iqpt_ctx* c, uint32_t waves_per_cu) {
     const uint32_t lanes = (waves_per_cu >> 8) & 0xffu;
     waves_per_cu &= 0xffu;
-    if (!c || waves_per_cu > 64 || (lanes != 0 && lanes != 4 && lanes != 8))
-        return iqpt::fail(IQPT_ERR_INVALID_ARG, "waves_per_cu 0..64, lanes 0, 4 or 8");
+    if (!c || waves_per_cu > 64 || (lanes != 0 && lanes != 4 && lanes != 8 && lanes != 16))
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "waves_per_cu 0..64, lanes 0, 4, 8 or 16");
     c->chain_waves = waves_per_cu;
     if (lanes) c->chain_lanes = lanes;
     return IQPT_OK;
@@ -1870,8 +2134,9 @@ int iqpt_set_overlap(iqpt_ctx* c, int mode) {
 }
 int iqpt_set_split(iqpt_ctx* c, int mode) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    if (mode != IQPT_SPLIT_AUTO && mode != IQPT_SPLIT_OFF && mode != IQPT_SPLIT_ON && mode != IQPT_SPLIT_CHAIN)
-        return iqpt::fail(IQPT_ERR_INVALID_ARG, "split mode must be IQPT_SPLIT_AUTO, _OFF, _ON or _CHAIN");
+    if (mode != IQPT_SPLIT_AUTO && mode != IQPT_SPLIT_OFF && mode != IQPT_SPLIT_ON && mode != IQPT_SPLIT_CHAIN &&
+        mode != IQPT_SPLIT_FAN && mode != IQPT_SPLIT_SPEC)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "split mode must be IQPT_SPLIT_AUTO, _OFF, _ON, _CHAIN, _FAN or _SPEC");
     c->split_mode = mode;
     return IQPT_OK;
 }

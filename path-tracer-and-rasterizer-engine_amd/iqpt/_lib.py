@@ -20,7 +20,7 @@ MESH_TRIANGLES = 0
 MESH_SPHERES = 1
 DEFAULT_SEED = 1984
 DEFAULT_MAX_DEPTH = 5
-SPLIT_AUTO, SPLIT_OFF, SPLIT_ON, SPLIT_CHAIN = -1, 0, 1, 2     # IQPT_SPLIT_* (iqpt_set_split)
+SPLIT_AUTO, SPLIT_OFF, SPLIT_ON, SPLIT_CHAIN, SPLIT_FAN, SPLIT_SPEC = -1, 0, 1, 2, 3, 4   # IQPT_SPLIT_* (iqpt_set_split)
 OVERLAP_OFF, OVERLAP_AUTO = 0, 1               # IQPT_OVERLAP_* (iqpt_set_overlap)
 
 

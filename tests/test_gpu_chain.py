@@ -24,7 +24,7 @@ def ran_chain(pt) -> bool:
     lb.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
     info = (C.c_ulonglong * 8)()
     _lib.check(lb.iqpt_debug_split_info(pt._h, info), "iqpt_debug_split_info")
-    return info[7] == 2
+    return info[7] in (2, 4)     # chain (anchored tiles plain) or chain + fan
 
 
 def _check(pt, lin, bgra, fr):

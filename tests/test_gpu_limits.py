@@ -42,7 +42,7 @@ def expect_latched(pt, tmp_path, what):
 
 def test_overlap_wait_timeout_is_reported_and_latched(require_gpu, tmp_path):
     w, h = 256, 144                        # 144 blocks: overlapped launches run (>= 64 blocks, 8 XCDs)
-    _, pk = scene_for("cornell")
+    sc, pk = scene_for("cornell")          # the scene owns the packet's arrays: keep it alive
     cam = make_camera(w, h)
     pt = PathTracer(w, h, max_depth=8)
     pt.set_split(_lib.SPLIT_OFF)
@@ -75,7 +75,7 @@ def test_overlap_wait_timeout_is_reported_and_latched(require_gpu, tmp_path):
 
 def test_chain_iteration_bound_is_reported_and_latched(require_gpu, tmp_path):
     w, h = 480, 270
-    _, pk = scene_for("cornell")
+    sc, pk = scene_for("cornell")
     cam = make_camera(w, h)
     ps = pixel_set(w, h, 0, w, 0, 8, (h + 7) // 8)      # rank 0's rows of an 8-way split
     pt = PathTracer(w, h, pixels=ps, max_depth=8)
@@ -90,7 +90,8 @@ def test_chain_iteration_bound_is_reported_and_latched(require_gpu, tmp_path):
 
 
 def walls_packet():
-    """The Cornell box without its spheres: triangles only (every camera ray ends on its first hit)."""
+    """The Cornell box without its spheres: triangles only (every camera ray ends on its first hit).
+    Returns (scene, packet): the scene owns the packet's arrays."""
     sc = Scene()
     sc.add_mesh_quad("quad")
     wall = (2.0, 2.0, 1.0, 1.0)
@@ -99,7 +100,7 @@ def walls_packet():
     sc.add_model("ceiling", "quad", wall, (-1.5707963267948966, 0, 0), (0.0, 1.5, 0.0))
     sc.add_model("left", "quad", wall, (0, 1.5707963267948966, 0), (-1.0, 0.5, 0.0))
     sc.add_model("right", "quad", wall, (0, -1.5707963267948966, 0), (1.0, 0.5, 0.0))
-    return sc.build_packet()
+    return sc, sc.build_packet()
 
 
 def test_small_frames_do_not_overlap_and_stay_exact(require_gpu):
@@ -111,7 +112,7 @@ def test_small_frames_do_not_overlap_and_stay_exact(require_gpu):
     lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
     for preset in ("cornell_lit", "walls", "cornell"):
         w, h = 32, 32
-        pk = walls_packet() if preset == "walls" else scene_for(preset)[1]
+        sc, pk = walls_packet() if preset == "walls" else scene_for(preset)
         cam = make_camera(w, h)
         pt = PathTracer(w, h, max_depth=8)
         pt.set_split(_lib.SPLIT_OFF)

@@ -1,0 +1,142 @@
+"""Slot-parallel sphere pixels (IQPT_SPLIT_SPEC) vs the CPU oracle, bit for bit.
+
+Only the pixels whose own camera-ray bundle may reach a sphere can take more than two draws per sample.
+Every slot of their window (the sample that starts 2j draws into the pixel's XORWOW stream) is evaluated
+in parallel, the chain 0 -> j + n_j -> ... is walked afterwards and folded in sample order, and a chain
+that leaves its window is finished sequentially by the stitch thread; every other pixel runs in the fan
+kernel. The result must be the reference's sequential chain (path_tracer.cu:330-366, random.cu:66-107):
+accumulator, BGRA8, final RNG states, ray count. RMSE < 1e-5 stated.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import oracle
+from helpers import compare, gpu_render, oracle_render, pixel_set, scene_for
+
+pytestmark = pytest.mark.gpu
+RMSE_TOL = 1e-5
+SPLIT_OFF, SPLIT_SPEC = 0, 4
+
+
+def mode_of(pt) -> int:
+    from iqpt import _lib
+    lb = _lib.load()
+    lb.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    info = (C.c_ulonglong * 8)()
+    _lib.check(lb.iqpt_debug_split_info(pt._h, info), "iqpt_debug_split_info")
+    return int(info[7])
+
+
+def _check(pt, lin, bgra, fr):
+    c = compare(lin, fr.lin)
+    assert c["rmse"] < RMSE_TOL, c
+    assert c["bitexact"] == c["npix"], c
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    assert pt.rays() == int(fr.rays.sum())
+
+
+@pytest.mark.parametrize("launches", [[16], [8, 8, 8], [3, 1, 40], [64, 64], [300]])
+def test_cornell_crop_spec(require_gpu, launches):
+    """C2 crop through both spheres: long scatter chains, several launches (history-sized windows)."""
+    ps = pixel_set(1920, 1080, 880, 1000, 470, 1, 48)
+    pt, lin, bgra = gpu_render("cornell", 1920, 1080, 0, 8, pixels=ps, launches=launches, split=SPLIT_SPEC)
+    assert mode_of(pt) == 6
+    fr = oracle_render("cornell", 1920, 1080, 0, 8, pixels=ps, launches=launches)
+    _check(pt, lin, bgra, fr)
+
+
+@pytest.mark.parametrize("rank,world", [(0, 8), (5, 8), (1, 3), (0, 2), (3, 4)])
+def test_row_share_spec(require_gpu, rank, world):
+    """A rank's cyclic row share of a 484x270 Cornell frame (ragged tiles at the right edge)."""
+    w, h = 484, 270
+    n = len(range(rank, h, world))
+    ps = pixel_set(w, h, 0, w, rank, world, n)
+    pt, lin, bgra = gpu_render("cornell", w, h, 0, 8, pixels=ps, launches=[12, 12], split=SPLIT_SPEC)
+    assert mode_of(pt) == 6
+    fr = oracle_render("cornell", w, h, 0, 8, pixels=ps, launches=[12, 12])
+    _check(pt, lin, bgra, fr)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3, 16])
+def test_depths_spec(require_gpu, depth):
+    """max_depth 1 (every sphere hit ends on a scatter at max depth: two slots, one ray), 2, 3, 16."""
+    pt, lin, bgra = gpu_render("app_default", 160, 90, 0, depth, launches=[20, 7], split=SPLIT_SPEC)
+    assert mode_of(pt) == 6
+    fr = oracle_render("app_default", 160, 90, 0, depth, launches=[20, 7])
+    _check(pt, lin, bgra, fr)
+
+
+@pytest.mark.parametrize("spp", [1, 2, 5, 130])
+def test_launch_sizes_spec(require_gpu, spp):
+    pt, lin, bgra = gpu_render("cornell", 203, 117, 0, 8, launches=[spp, 7], split=SPLIT_SPEC)
+    assert mode_of(pt) == 6
+    fr = oracle_render("cornell", 203, 117, 0, 8, launches=[spp, 7])
+    _check(pt, lin, bgra, fr)
+
+
+def test_chains_leaving_their_window_spec(require_gpu):
+    """Windows sized for one slot per sample: the sphere pixels' chains leave them in the first launch and
+    the stitch finishes them sequentially; the second launch sizes the windows from that history."""
+    from iqpt import PathTracer, _lib, make_camera
+    w, h = 320, 180
+    sc, pk = scene_for("cornell")          # the scene owns the packet's arrays: keep it alive
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, max_depth=8)
+    pt.set_split(SPLIT_SPEC)
+    lib = _lib.load()
+    lib.iqpt_debug_set_spec.argtypes = [C.c_void_p, C.c_uint32]
+    _lib.check(lib.iqpt_debug_set_spec(pt._h, 256), "iqpt_debug_set_spec")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, max_depth=8)
+    for s in (24, 24):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    assert mode_of(pt) == 6
+    _check(pt, lin, bgra, fr)
+
+
+def test_large_frame_counter_spec(require_gpu):
+    from iqpt import PathTracer, _lib, make_camera
+    frame0 = (1 << 33) + 3
+    w, h = 96, 64
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, max_depth=8)
+    pt.set_split(SPLIT_SPEC)
+    lib = _lib.load()
+    lib.iqpt_debug_set_frame.argtypes = [C.c_void_p, C.c_uint64]
+    _lib.check(lib.iqpt_debug_set_frame(pt._h, frame0), "iqpt_debug_set_frame")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, max_depth=8)
+    fr.frame = frame0
+    for s in (4, 9):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    assert mode_of(pt) == 6
+    _check(pt, lin, bgra, fr)
+
+
+def test_c3_share8_spec_vs_plain(require_gpu):
+    """Rank 0's N = 8 row share of the full C3 frame (1920x1080, 64 spp, 8 bounces), three launches: the
+    spec launches equal the plain kernel bit for bit (the plain kernel equals the oracle on the whole
+    frame: test_gpu_fullframe)."""
+    w, h = 1920, 1080
+    n = len(range(0, h, 8))
+    ps = pixel_set(w, h, 0, w, 0, 8, n)
+    outs = []
+    for mode in (SPLIT_OFF, SPLIT_SPEC):
+        pt, lin, bgra = gpu_render("cornell", w, h, 0, 8, pixels=ps, launches=[64, 64, 64], split=mode)
+        outs.append((lin, bgra, pt.read_rng(), pt.rays(), mode_of(pt)))
+        pt.close()
+    assert [o[4] for o in outs] == [0, 6]
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]

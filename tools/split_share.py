@@ -27,7 +27,8 @@ from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
 OPT = 0
 
 
-def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain_waves: int = 0) -> dict:
+def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain_waves: int = 0,
+        fan: bool = True) -> dict:
     cfg = CONFIGS["c2"]
     sc = Scene()
     sc.add_preset(cfg.preset)
@@ -46,6 +47,11 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain
         lb = _lib.load()
         lb.iqpt_debug_set_split_knobs.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_split_knobs(pt._h, knobs[0], knobs[1]), "iqpt_debug_set_split_knobs")
+    if not fan:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_fan.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_fan(pt._h, 0), "iqpt_debug_set_fan")
     if chain_waves:
         import ctypes as C
         lb = _lib.load()
@@ -71,13 +77,19 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain
     lb.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
     _lib.check(lb.iqpt_debug_split_info(pt._h, info), "iqpt_debug_split_info")
     info = list(info)
+    spec = (C.c_ulonglong * 8)()
+    lb.iqpt_debug_spec_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    _lib.check(lb.iqpt_debug_spec_info(pt._h, spec), "iqpt_debug_spec_info")
+    spec = list(spec)
     lin, bgra = pt.read()
     st = pt.read_rng()
     pt.close()
     return {"ms": times, "rays": rays, "lin": lin, "bgra": bgra, "rng": st,
             "info": {"split_tiles": info[0], "anchor_tiles": info[1], "leftovers": info[3],
                      "split_pixels": info[6], "mean_window": info[4] / max(info[6], 1),
-                     "mean_slots_per_sample": info[5] / 256 / max(info[6], 1), "ran_split": info[7]}}
+                     "mean_slots_per_sample": info[5] / 256 / max(info[6], 1), "ran_split": info[7],
+                     "sphere_pixels": spec[0], "fan_tiles": spec[1], "spec_runs": spec[4], "spec_window_slots": spec[5],
+                     "spec_slots_per_sample": spec[6] / 256 / max(spec[0], 1)}}
 
 
 def wave_timeline(n: int, spp: int, warm: int, knobs=None) -> dict:
@@ -146,7 +158,8 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--ns", default="1,2,4,8")
     ap.add_argument("--out", default="")
-    ap.add_argument("--modes", default="plain,split", help="plain, split, chain (IQPT_SPLIT_CHAIN)")
+    ap.add_argument("--modes", default="plain,split", help="plain, split, chain (IQPT_SPLIT_CHAIN, anchored tiles in "
+                    "the fan kernel), chainplain (the same, anchored tiles in the plain kernel), fan (IQPT_SPLIT_FAN)")
     ap.add_argument("--chain-waves", default="", help="extra chain rows at these chain-kernel waves per CU")
     ap.add_argument("--knobs", default="", help="split knob sets heavy_rho:refill_min[,...] (extra split rows)")
     ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (instrumented library)")
@@ -176,7 +189,10 @@ def main():
         row = {"n": n}
         res = {}
         modes = [m for m in (("plain", _lib.SPLIT_OFF, 0), ("split", _lib.SPLIT_ON, 0),
-                             ("chain", _lib.SPLIT_CHAIN, 0)) if m[0] in args.modes.split(",")]
+                             ("chain", _lib.SPLIT_CHAIN, 0), ("chainplain", _lib.SPLIT_CHAIN, 0),
+                             ("fan", _lib.SPLIT_FAN, 0), ("splitplain", _lib.SPLIT_ON, 0),
+                             ("spec", _lib.SPLIT_SPEC, 0))
+                 if m[0] in args.modes.split(",")]
         # "16" = 16 chain-kernel waves per CU; "16a" = the same with every tile in the split set (all chains);
         # "16l4" = 4 lanes per pixel
         def cw(w):
@@ -185,15 +201,22 @@ def main():
         modes += [(f"chain_w{w}", _lib.SPLIT_CHAIN, cw(w)) for w in args.chain_waves.split(",") if w]
         for name, mode, cw in modes:
             kn = (0, 16 | (1 << 16)) if name.endswith("a") else None
-            r = run(n, mode, args.launches, args.warm, args.spp, knobs=kn, chain_waves=cw)
+            r = run(n, mode, args.launches, args.warm, args.spp, knobs=kn, chain_waves=cw, fan=name not in ("chainplain", "splitplain"))
             res[name] = r
             row[name + "_ms_median"] = float(np.median(r["ms"]))
             row[name + "_ms_min"] = float(np.min(r["ms"]))
             row[name + "_mrays_per_s"] = r["rays"] / (sum(r["ms"]) * 1e-3) / 1e6
             if name == "split":
                 row["split_info"] = r["info"]
-            if name.startswith("chain"):
-                row[name + "_ran"] = r["info"]["ran_split"] == 2
+            if name.startswith(("chain", "spec")):
+                row[name + "_sphere_pixels"] = r["info"]["sphere_pixels"]
+            if name.startswith("spec"):
+                row[name + "_runs"] = r["info"]["spec_runs"]
+                row[name + "_window_slots"] = r["info"]["spec_window_slots"]
+                row[name + "_slots_per_sample"] = round(r["info"]["spec_slots_per_sample"], 3)
+            if name.startswith(("chain", "fan", "split", "spec")):
+                row[name + "_ran"] = {0: "plain", 1: "split", 2: "chain", 3: "fan", 4: "chain+fan", 5: "split+fan", 6: "spec"}.get(
+                    int(r["info"]["ran_split"]), "?")
             if name != "plain" and "plain" in res:
                 a = res["plain"]
                 row[name + "_identical"] = bool(
@@ -204,6 +227,7 @@ def main():
             rl, rm = (int(x) for x in kn.split(":"))
             r = run(n, _lib.SPLIT_ON, args.launches, args.warm, args.spp, (rl, rm))
             row[f"split_h{rl}_m{rm}_ms_median"] = float(np.median(r["ms"]))
+            row[f"split_h{rl}_m{rm}_ran"] = int(r["info"]["ran_split"])
             if "plain" in res:
                 a = res["plain"]
                 row[f"split_h{rl}_m{rm}_identical"] = bool(
