@@ -73,7 +73,7 @@ struct kparams {
     float4_storage* lin;             // npix
     uint32_t* bgra;                  // npix
     uint32_t* rng;                   // 6 planes of npix words: v0..v4, d
-    unsigned long long* rays;        // closest-hit query counter
+    unsigned long long* rays;        // closest-hit query counters: kRaySlots slots, kRaySlotStride apart (summed on read)
     uint32_t* queue;                 // tile dequeue head (zeroed before every launch)
     unsigned long long* stats;       // kOptStats counters (8 x u64) or null
     // kOptCull: per screen tile of kCullTile x kCullTile owned pixels (columns x owned rows), one bit
@@ -165,6 +165,10 @@ struct kparams {
     // Chain launches give the plain kernel the anchored tiles only.
     uint32_t nqueue;
 };
+// The ray count is spread over kRaySlots counters 128 B apart: thousands of waves add their counts as
+// they end, and one counter would serialise those atomics at the end of every launch.
+constexpr uint32_t kRaySlots = 64;
+constexpr uint32_t kRaySlotStride = 16;      // unsigned long longs
 constexpr int kSphNodeFloat4 = 3;
 constexpr uint32_t kOverlapSpinLimit = 1u << 23;   // s_sleep(20) polls before a wait gives up (~seconds)
 constexpr uint32_t kChainIterLimit = 1u << 22;     // chain-kernel loop iterations before a wave gives up
@@ -173,29 +177,31 @@ constexpr uint32_t kOverlapQueueWords = 2 * 9 * 16;
 
 // Slot-parallel sphere pixels (IQPT_SPLIT_SPEC): the pixels whose own camera-ray bundle
 // may reach a sphere. Per launch a window of M slots per pixel (M from the pixel's last chain), every
-// slot j (the sample that starts 2j draws into the pixel's stream) evaluated in parallel by runs of
-// run_len consecutive slots, then the chain walked in order. Kernels: iqpt_spec_prep_kernel (windows,
-// states, run list), iqpt_spec_kernel (the slots), iqpt_spec_stitch_kernel (walk, fold, finish chains
-// that left their window, store the pixel).
+// slot j (the sample that starts 2j draws into the pixel's stream) evaluated in parallel, 16 lanes per
+// pixel, then the chain walked in order (iqpt_spec_kernel).
 struct kspec {
     uint32_t n;                      // sphere pixels q < n
     uint32_t m_cap;                  // window cap (a multiple of 16)
-    uint32_t run_len;                // R: slots per run
-    uint32_t g_max;                  // state plane of slot M (planes r < g_max: slot r R)
     uint32_t rho0;                   // slots per sample x 256 assumed for a pixel without history
+    uint32_t margin_div;             // spec_window's margin: 1 / margin_div of the extra slots
     const uint32_t* pix;             // tile-major storage index of sphere pixel q
-    uint32_t* m;                     // this launch's window of q
+    uint32_t* m;                     // the last launch's window of q (statistics)
     uint32_t* rho;                   // slots per sample x 256 of q's last chain (0: none)
-    uint32_t* st;                    // (g_max + 1) x 5 planes x n: v0..v4 at slots 0, R, 2R, ... and at M
-    // run list, 48 B per run, everything a lane needs to start it in one round of loads: (v0, v1, v2, v3),
-    // (v4, d, storage index, q), (first slot | end slot << 16, tile, tile mask words 0 of triangles, spheres)
-    uint32_t* runs;
-    uint32_t* run_count;             // runs in the list; run_count[1]: the spec kernel's dequeue head
-    float4_storage* res;             // res[q m_cap + j]: clamped colour of slot j (w unused)
-    uint8_t* nres;                   // nres[q m_cap + j]: slots slot j's sample consumed
+    uint32_t* run_count;             // [1]: chains finished past their window (statistics)
+    float4_storage* res;             // res[q m_cap + j]: clamped colour of slot j
 };
-constexpr uint32_t kSpecRunLen = 4;      // slots per run (a run starts on a state the prep kernel stored)
 constexpr uint32_t kSpecRho0 = 576;      // 2.25 slots per sample before a pixel has a history (sphere pixels take ~2)
+
+// The spec window of a sphere pixel whose last chain used rho256 / 256 slots per sample: that many slots
+// for spp samples plus a margin of 1 / margin_div of the extra slots (at least 4) and 4, within
+// [spp, m_cap]. A chain longer than its window is finished sequentially by the stitch.
+__host__ __device__ inline uint32_t spec_window(uint32_t rho256, uint32_t spp, uint32_t m_cap, uint32_t margin_div) {
+    const uint64_t m = ((uint64_t)spp * rho256 + 255u) / 256u;
+    const uint64_t extra = m > spp ? (m - spp) / (margin_div ? margin_div : 1u) : 0u;
+    uint64_t w = m + (extra > 4u ? extra : 4u) + 4u;
+    if (w < spp) w = spp;
+    return (uint32_t)(w > m_cap ? m_cap : w);
+}
 
 // iqpt_split_prep_kernel / iqpt_split_stitch_kernel (kOptSplit).
 struct ksplit {
@@ -341,13 +347,11 @@ bool chain_variant_exists(int max_depth, int opt, uint32_t lanes);
 uint32_t chain_lds(const kparams& p, uint32_t lanes);
 int chain_occupancy(int max_depth, int opt, uint32_t lanes, uint32_t lds, int* blocks_per_cu);
 int launch_chain(void* stream, const kparams& p, uint32_t grid_blocks, int opt, uint32_t lanes);
-// Slot-parallel sphere pixels: prep (zeroes nothing: run_count must be 0), slots, stitch.
-// The slot and stitch kernels need a resident scene, reference materials, max_depth <= 16, spp <= kAccTableMax.
-int launch_spec_prep(void* stream, const kparams& p, const kspec& s);
+// Slot-parallel sphere pixels: resident scene, reference materials, max_depth <= 16,
+// spp <= kAccTableMax.
 bool spec_variant_exists(int max_depth, int opt);
-int spec_occupancy(int max_depth, int opt, const kparams& p, int* blocks_per_cu);
-int launch_spec(void* stream, const kparams& p, const kspec& s, uint32_t grid_blocks, int opt);
-int launch_spec_stitch(void* stream, const kparams& p, const kspec& s, int opt);
+uint32_t spec_lds(const kparams& p, const kspec& s);
+int launch_spec(void* stream, const kparams& p, const kspec& s, int opt);
 // Sample-parallel anchored tiles (iqpt_fan_kernel): one block per tile of
 // p.tile_order[0 .. ntiles) — tiles without sphere candidates, reference materials, resident scene
 // (p.cull set, p.cull_wt <= 16), spp <= kAccTableMax.

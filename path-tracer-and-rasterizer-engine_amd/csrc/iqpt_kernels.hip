@@ -566,6 +566,11 @@ __device__ __forceinline__ void triangle_hit(const float4* __restrict__ tris, co
     }
 }
 
+// Adds a block's (or wave's) closest-hit queries to one of the kRaySlots spread counters.
+__device__ __forceinline__ void add_rays(unsigned long long* rays, unsigned long long v) {
+    atomicAdd(rays + (size_t)((blockIdx.x + threadIdx.x / 64u) % kRaySlots) * kRaySlotStride, v);
+}
+
 __device__ __forceinline__ uint32_t prefix_below(uint64_t mask) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
@@ -1924,7 +1929,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     }
 
     // closest-hit query count: one atomic per wave
-    if (lane == 0 && wave_rays) atomicAdd(p.rays, (unsigned long long)wave_rays);
+    if (lane == 0 && wave_rays) add_rays(p.rays, (unsigned long long)wave_rays);
     if (kOverlap && p.ovl_err) {
         // HIP promises no workgroup -> XCD placement: the last block to finish checks that every XCD's
         // tile list was taken to its end (a list no wave ran on would leave its tiles unrendered, silently)
@@ -2364,7 +2369,7 @@ __global__ __launch_bounds__(kStitchBlock) void iqpt_split_stitch_kernel(const k
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
-    if (__lane_id() == 0 && rays) atomicAdd(s.rays, rays);
+    if (__lane_id() == 0 && rays) add_rays(s.rays, rays);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2696,7 +2701,7 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
     }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) w_rays += __shfl_xor(w_rays, off);
-    if (lane == 0 && w_rays) atomicAdd(p.rays, w_rays);
+    if (lane == 0 && w_rays) add_rays(p.rays, w_rays);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2856,7 +2861,7 @@ __global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p)
         }
     }
     if (threadIdx.x == 0)   // one query per sample
-        atomicAdd(p.rays, (unsigned long long)__popcll(own & (npt == 64u ? ~0ull : ((1ull << npt) - 1ull))) * p.spp);
+        add_rays(p.rays, (unsigned long long)__popcll(own & (npt == 64u ? ~0ull : ((1ull << npt) - 1ull))) * p.spp);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -2864,362 +2869,289 @@ __global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p)
 // bundle may reach a sphere take more than one slot per sample, so only their chains need speculation.
 // Sample k of a pixel starts where sample k - 1's draws ended (path_tracer.cu:339): 2 draws for the
 // jitter (camera.cu:24-25) plus 2 per Oren-Nayar scatter (material.cu:10), and what a sample does from
-// stream offset 2j depends on j alone. So every slot j < M of a window is evaluated in parallel — runs of
-// R consecutive slots per lane, a run starting on a state the prep kernel stored, the next slot's state
-// being the one the camera draws of the current slot leave — and the stitch kernel then follows the chain
-// 0 -> j + n_j -> ... and folds its samples in order with the plain kernel's table values (the running
-// mean of path_tracer.cu:356-358). A chain that leaves its window is finished by the stitch thread itself.
-// Same bits as the plain kernel: the same per-sample code, the chain's own slots counted as rays.
-
-// Per sphere pixel: the window M (the last chain's slots per sample, split_window), the states at slots
-// 0, R, 2R, ... and at M, and the pixel's runs appended to the run list (one atomic per wave).
-__global__ __launch_bounds__(256) void iqpt_spec_prep_kernel(const kparams p, const kspec s) {
-    const uint32_t q = blockIdx.x * 256u + threadIdx.x, lane = __lane_id();
-    uint32_t nr = 0, M = 0, pix = 0;
-    if (q < s.n) {
-        pix = s.pix[q];
-        const uint32_t rho = s.rho[q];
-        M = split_window(rho ? rho : s.rho0, p.spp, s.m_cap);
-        s.m[q] = M;
-        nr = (M + s.run_len - 1u) / s.run_len;
-    }
-    uint32_t incl = nr;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t t = (uint32_t)__shfl_up((int)incl, off);
-        if ((int)lane >= off) incl += t;
-    }
-    const uint32_t total = (uint32_t)__shfl((int)incl, 63);
-    uint32_t base = 0;
-    if (lane == 0 && total) base = atomicAdd(s.run_count, total);
-    base = (uint32_t)__shfl((int)base, 0) + incl - nr;
-    if (q >= s.n) return;
-    // the states at slots 0, R, 2R, ... (each run's start) and at M; each run's record
-    const uint32_t R = s.run_len;
-    uint32_t v0 = p.rng[pix], v1 = p.rng[(size_t)p.npix + pix], v2 = p.rng[2 * (size_t)p.npix + pix],
-             v3 = p.rng[3 * (size_t)p.npix + pix], v4 = p.rng[4 * (size_t)p.npix + pix];
-    const uint32_t d0 = p.rng[5 * (size_t)p.npix + pix];
-    uint32_t col, row;
-    tile_decode(pix, p.ncols, p.nrows, &col, &row);
-    const uint32_t t = (row / kCullTile) * p.ntx + col / kCullTile;
-    const uint32_t cm0 = p.cull[(size_t)t * p.cull_stride], cm1 = p.cull[(size_t)t * p.cull_stride + p.cull_wt];
-    for (uint32_t r = 0; r < nr; ++r) {
-        const uint32_t j0 = r * R;
-        uint4* e = reinterpret_cast<uint4*>(s.runs) + 3 * (size_t)(base + r);
-        e[0] = make_uint4(v0, v1, v2, v3);
-        e[1] = make_uint4(v4, d0 + 2u * j0 * IQ_XORWOW_WEYL, pix, q);
-        e[2] = make_uint4(j0 | (min(j0 + R, M) << 16), t, cm0, cm1);
-        uint32_t* d = s.st + (size_t)r * 5u * s.n + q;
-        d[0] = v0;
-        d[s.n] = v1;
-        d[2 * (size_t)s.n] = v2;
-        d[3 * (size_t)s.n] = v3;
-        d[4 * (size_t)s.n] = v4;
-        xorwow_skip_v(v0, v1, v2, v3, v4, 2u * (min(j0 + R, M) - j0));
-    }
-    uint32_t* d = s.st + (size_t)s.g_max * 5u * s.n + q;
-    d[0] = v0;
-    d[s.n] = v1;
-    d[2 * (size_t)s.n] = v2;
-    d[3 * (size_t)s.n] = v3;
-    d[4 * (size_t)s.n] = v4;
-}
-
+// stream offset 2j ("slot" j) depends on j alone. One kernel, 16 lanes per sphere pixel:
+//  * slots: the pixel's window of M slots (its last chain's slots per sample, spec_window) is cut into 16
+//    ranges; each lane steps its state to its range's first slot and traces the range's slots back to
+//    back (the next slot's state is the one the current slot's camera draws leave), one ray per live lane
+//    per iteration; colours go to HBM, the slot counts to LDS;
+//  * walk: one lane per pixel follows the chain 0 -> j + n_j -> ... in LDS, the pixel's 16 lanes gather
+//    the colours of 64 chain samples at a time, and the walker folds them in sample order with the plain
+//    kernel's table values (path_tracer.cu:356-358), counting each sample's rays (its slots, or max_depth
+//    when it ended on a scatter at max_depth); a chain that leaves its window is finished by the walker.
+// Same bits as the plain kernel: the same per-sample code, the same mean terms, the chain's own slots as
+// rays, the state where the chain stops.
 constexpr uint32_t kSpecBlock = 256;
+constexpr uint32_t kSpecLanes = 16;                    // lanes per sphere pixel
+constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per block
 
-__host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth) {
+__host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth, uint32_t spp,
+                                                   uint32_t m_cap) {
+    const uint32_t sp4 = (spp + 3u) & ~3u;
     return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + kSpecBlock * 16u +
-           (uint32_t)(max_depth > 1 ? max_depth : 1) * kSpecBlock * 4u;
+           kSpecPix * 64u * 16u + sp4 * 12u + (uint32_t)(max_depth > 1 ? max_depth : 1) * kSpecBlock * 4u +
+           kSpecPix * kSpecLanes * 20u + kSpecPix * 64u + kSpecPix * 64u * 2u + kSpecPix * 8u + kSpecPix * m_cap;
 }
 
-// The slots: persistent waves, lane = one run at a time, one ray per live lane per iteration (a lane
-// whose slot ends starts its next one at once, its run's end takes a new run). Camera rays test their
-// tile's mask pairs, as in the plain kernel; a wave holding a secondary ray tests every pair.
 template <int MAXD, int OPT>
 __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams p, const kspec s) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    const uint32_t sp4 = (p.spp + 3u) & ~3u;
     float4* lds_tri = lds;
-    float4* lds_sph = lds + (size_t)p.ntri_pairs * kTriPairFloat4;
-    uint4* lds_cm = reinterpret_cast<uint4*>(lds_sph + (size_t)p.nsph_pairs * kSphPairFloat4);
-    float* lds_stk = reinterpret_cast<float*>(lds_cm + kSpecBlock);     // [depth][thread]
+    float4* lds_sph = lds_tri + (size_t)p.ntri_pairs * kTriPairFloat4;
+    uint4* lds_cm = reinterpret_cast<uint4*>(lds_sph + (size_t)p.nsph_pairs * kSphPairFloat4);    // [thread]
+    float4* lds_c = reinterpret_cast<float4*>(lds_cm + kSpecBlock);                               // [pixel][64]
+    float2* tab = reinterpret_cast<float2*>(lds_c + kSpecPix * 64u);
+    float* tab_n = reinterpret_cast<float*>(tab + sp4);
+    float* lds_stk = tab_n + sp4;                                                                  // [depth][thread]
+    uint32_t* lds_st = reinterpret_cast<uint32_t*>(lds_stk + (size_t)(p.max_depth > 1 ? p.max_depth : 1) * kSpecBlock);
+    // per pixel: 0 the round's first slot (absolute), 1 its window, 2..6 the state there (v0..v4), 7 done,
+    // and the walker's running mean (8..10), samples folded (11), rays (12), storage index (13) — kept in
+    // LDS across the slot loop, whose registers they would otherwise take
+    uint32_t* lds_rd = lds_st + kSpecPix * kSpecLanes * 5u;                                       // [pixel][16]
+    uint16_t* lds_pos = reinterpret_cast<uint16_t*>(lds_rd + kSpecPix * 16u);                      // [pixel][64]
+    uint32_t* lds_w = reinterpret_cast<uint32_t*>(lds_pos + kSpecPix * 64u);                       // [pixel][2]
+    uint8_t* lds_n = reinterpret_cast<uint8_t*>(lds_w + 2u * kSpecPix);                            // [pixel][slot]
     for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kSpecBlock)
         lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
     for (uint32_t i = threadIdx.x; i < p.nsph_pairs * kSphPairFloat4; i += kSpecBlock)
         lds_sph[i] = reinterpret_cast<const float4*>(p.sph_pairs)[i];
-    __syncthreads();
-    if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);   // these chains are the launch's longest
-
-    const uint32_t lane = __lane_id();
-    const uint32_t nruns = *s.run_count;                  // final: the prep kernel ran before this one
-    bool active = false, exhausted = false;
-    uint32_t q = 0, j = 0, jend = 0, px = 0, py = 0;
-    rng6 st = {0u, 0u, 0u, 0u, 0u, 0u}, base = {0u, 0u, 0u, 0u, 0u, 0u};
-    ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    int depth = 0;
-    // a slot's sample starts here: its camera ray, and the state its two draws leave (the next slot's)
-    auto start_slot = [&]() {
-        camera_ray<OPT>(p, px, py, st, ray);
-        base = st;
-        depth = 0;
-    };
-    auto refill = [&]() {
-        const uint64_t need = __ballot(!active);
-        if (need == 0ull || exhausted) return;
-        uint32_t b = 0;
-        if (lane == 0) b = atomicAdd(s.run_count + 1, (uint32_t)__popcll(need));
-        b = (uint32_t)__builtin_amdgcn_readfirstlane((int)b);
-        if (b + (uint32_t)__popcll(need) >= nruns) exhausted = true;
-        const uint32_t idx = b + prefix_below(need);
-        if (!active && idx < nruns) {
-            // the run's record: one round of three independent 16-byte loads
-            const uint4* e = reinterpret_cast<const uint4*>(s.runs) + 3 * (size_t)idx;
-            const uint4 e0 = e[0], e1 = e[1], e2 = e[2];
-            q = e1.w;
-            j = e2.x & 0xffffu;
-            jend = e2.x >> 16;
-            st = {e0.x, e0.y, e0.z, e0.w, e1.x, e1.y};
-            uint32_t col, row;
-            tile_decode(e1.z, p.ncols, p.nrows, &col, &row);
-            px = p.x0 + col;
-            py = p.y0 + row * p.ystep;
-            lds_cm[threadIdx.x] = make_uint4(e2.z, e2.w, e2.y, 0u);
-            start_slot();
-            active = true;
-        }
-    };
-    refill();
-    while (__any(active)) {
-        // closest hit (path_tracer.cu:253-295): camera rays over their tile's mask pairs in index order
-        float closest = kTMax;
-        int kind = kHitNone;
-        uint32_t hidx = 0;
-        {
-            const bool cull = !__any(active && depth != 0);
-            const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
-            uint4 cm = lds_cm[threadIdx.x];
-            const uint64_t act = __ballot(active);
-            const uint32_t first = (uint32_t)__builtin_ctzll(act);
-            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
-            const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
-            if (uni) {
-                cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
-                cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
-            }
-            const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
-            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray, closest,
-                                  kind, hidx, p.cull_wt, uni_mask);
-        }
-        if (active) {
-            // shade (path_tracer.cu:297-316) under the reference's materials
-            bool term = false;
-            uint32_t md_end = 0;
-            float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
-            if (kind == kHitSphere) {
-                const float* sq = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
-                const float sc = oren_nayar_scatter<OPT>(make_float4(sq[0], sq[2], sq[4], sq[6]), closest, ray, st);
-                if (depth + 1 >= p.max_depth) {
-                    term = true;                 // the last record is this scatter (biased, :252)
-                    md_end = 1;
-                    Lx = sc;
-                    Ly = sc;
-                    Lz = sc;
-                } else {
-                    lds_stk[(uint32_t)depth * kSpecBlock + threadIdx.x] = sc;
-                    ++depth;
-                }
-            } else if (kind == kHitTri) {
-                term = true;                     // emissive(1, 10)
-                Lx = 10.0f;
-                Ly = 10.0f;
-                Lz = 10.0f;
-            } else {
-                term = true;                     // sky gradient, :308-313
-                const float a = (ray.dy + 1.0f) * 0.5f;
-                const float one_a = 1.0f - a;
-                Lx = one_a + a * 0.5f;
-                Ly = one_a + a * 0.7f;
-                Lz = one_a + a * 1.0f;
-            }
-            if (term) {
-                // backward product (:321-324), clamp (:345-347), 0 + colour (:341, 348)
-                float cx = Lx, cy = Ly, cz = Lz;
-                for (int i = depth - 1; i >= 0; --i) {
-                    const float rr = lds_stk[(uint32_t)i * kSpecBlock + threadIdx.x];
-                    cx = cx * rr;
-                    cy = cy * rr;
-                    cz = cz * rr;
-                }
-                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                const size_t at = (size_t)q * s.m_cap + j;
-                reinterpret_cast<float4*>(s.res)[at] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
-                s.nres[at] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
-                if (++j == jend) {
-                    active = false;
-                } else {
-                    st = base;                   // slot j starts where slot j - 1's camera draws ended
-                    start_slot();
-                }
-            }
-        }
-        if (!exhausted && __ballot(!active) != 0ull) refill();
-    }
-}
-
-// The chain of one sphere pixel's slots, finished sequentially from slot j when it leaves the window:
-// one whole sample (camera ray, every bounce over every primitive from global memory, shading), its
-// clamped colour and the slots it consumed.
-template <int MAXD, int OPT>
-__device__ void spec_trace_one(const kparams& p, uint32_t px, uint32_t py, rng6& st, float& cx, float& cy,
-                               float& cz, uint32_t& nsl) {
-    float stk[MAXD];
-    ray3 ray;
-    camera_ray<OPT>(p, px, py, st, ray);
-    int depth = 0;
-    const float4* gtri = reinterpret_cast<const float4*>(p.tri_pairs);
-    const float4* gsph = reinterpret_cast<const float4*>(p.sph_pairs);
-    while (true) {
-        float closest = kTMax;
-        int kind = kHitNone;
-        uint32_t hidx = 0;
-        intersect_range<OPT>(gtri, 0, p.ntri, gsph, 0, p.nsph, ray, closest, kind, hidx);
-        uint32_t md_end = 0;
-        float Lx, Ly, Lz;
-        if (kind == kHitSphere) {
-            const float4_storage c = p.spheres[hidx];
-            const float sc = oren_nayar_scatter<OPT>(make_float4(c.x, c.y, c.z, c.w), closest, ray, st);
-            if (depth + 1 < p.max_depth) {
-                stk[depth++] = sc;
-                continue;
-            }
-            md_end = 1;
-            Lx = sc;
-            Ly = sc;
-            Lz = sc;
-        } else if (kind == kHitTri) {
-            Lx = 10.0f;
-            Ly = 10.0f;
-            Lz = 10.0f;
-        } else {
-            const float a = (ray.dy + 1.0f) * 0.5f;
-            const float one_a = 1.0f - a;
-            Lx = one_a + a * 0.5f;
-            Ly = one_a + a * 0.7f;
-            Lz = one_a + a * 1.0f;
-        }
-        for (int i = depth - 1; i >= 0; --i) {
-            Lx = Lx * stk[i];
-            Ly = Ly * stk[i];
-            Lz = Lz * stk[i];
-        }
-        cx = 0.0f + (Lx > 1.0f ? 1.0f : (Lx < 0.0f ? 0.0f : Lx));
-        cy = 0.0f + (Ly > 1.0f ? 1.0f : (Ly < 0.0f ? 0.0f : Ly));
-        cz = 0.0f + (Lz > 1.0f ? 1.0f : (Lz < 0.0f ? 0.0f : Lz));
-        nsl = (uint32_t)depth + 1u + md_end;
-        return;
-    }
-}
-
-// The walk (one thread per sphere pixel): slot counts 16 at a time, the colours of 8 chain samples in
-// flight at once, the running mean in sample order, the ray count (a sample's rays are its slots, or
-// max_depth when it ended on a scatter at max_depth), the state where the chain stops, the pixel.
-template <int MAXD, int OPT>
-__global__ __launch_bounds__(64) void iqpt_spec_stitch_kernel(const kparams p, const kspec s) {
-    __shared__ float2 tab[kAccTableMax];
-    __shared__ float tab_n[kAccTableMax];
-    for (uint32_t k = threadIdx.x; k < p.spp; k += 64u) {
+    for (uint32_t k = threadIdx.x; k < p.spp; k += kSpecBlock) {
         const uint64_t n = p.frame0 + k + 1;
         tab[k] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
         tab_n[k] = (float)n;
     }
+    if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);   // these chains are the launch's longest
+
+    const uint32_t g = threadIdx.x / kSpecLanes, l = threadIdx.x % kSpecLanes;
+    const uint32_t q = blockIdx.x * kSpecPix + g;
+    const bool valid = q < s.n, walker = valid && l == 0u;
+    const uint32_t pix = valid ? s.pix[q] : 0u;
+    uint8_t* ln = lds_n + (size_t)g * s.m_cap;
+    uint32_t* lst = lds_st + (size_t)g * kSpecLanes * 5u;
+    uint32_t* rd = lds_rd + g * 16u;
+    uint32_t col = 0, row = 0;
+    tile_decode(pix, p.ncols, p.nrows, &col, &row);
+    const uint32_t px = p.x0 + col, py = p.y0 + row * p.ystep;
+    {
+        const uint32_t t = (row / kCullTile) * p.ntx + col / kCullTile;
+        lds_cm[threadIdx.x] = make_uint4(p.cull[(size_t)t * p.cull_stride], p.cull[(size_t)t * p.cull_stride + p.cull_wt], t, 0u);
+    }
+    if (walker) {
+        // round 0: the launch's first slot, the window from the pixel's last chain, its state
+        rd[0] = 0u;
+        rd[1] = spec_window(s.rho[q] ? s.rho[q] : s.rho0, p.spp, s.m_cap, s.margin_div);
+        rd[2] = p.rng[pix];
+        rd[3] = p.rng[(size_t)p.npix + pix];
+        rd[4] = p.rng[2 * (size_t)p.npix + pix];
+        rd[5] = p.rng[3 * (size_t)p.npix + pix];
+        rd[6] = p.rng[4 * (size_t)p.npix + pix];
+        rd[7] = valid ? 0u : 1u;
+        s.m[q] = rd[1];
+        const uint32_t* a = reinterpret_cast<const uint32_t*>(p.lin + pix);
+        rd[8] = a[0];
+        rd[9] = a[1];
+        rd[10] = a[2];
+        rd[11] = 0u;
+        rd[12] = 0u;
+        rd[13] = pix;
+    } else if (!valid && l == 0u) {
+        // no pixel (the grid's last block): an empty, finished record (every field is read by the rounds)
+        for (uint32_t i = 0; i < 16u; ++i) rd[i] = 0u;
+        rd[7] = 1u;
+    }
+    float4* res = reinterpret_cast<float4*>(s.res) + (size_t)q * s.m_cap;
     __syncthreads();
-    const uint32_t q = blockIdx.x * 64u + threadIdx.x;
-    unsigned long long rays = 0;
-    if (q < s.n) {
-        const uint32_t pix = s.pix[q], M = s.m[q];
-        const float* a = reinterpret_cast<const float*>(p.lin + pix);
-        float ax = a[0], ay = a[1], az = a[2];
-        uint32_t k = 0, j = 0;
-        const float4* res = reinterpret_cast<const float4*>(s.res) + (size_t)q * s.m_cap;
-        const uint8_t* nr = s.nres + (size_t)q * s.m_cap;     // m_cap is a multiple of 16
-        uint32_t nbase = ~0u;
-        uint4 nb = make_uint4(0u, 0u, 0u, 0u);
-        auto fold = [&](float cx, float cy, float cz, uint32_t n) {
-            const float2 tv = tab[k];
-            float qx, qy, qz;
-            mean_terms<OPT>(cx, cy, cz, tab_n[k], tv.x, p.mean_tiny, qx, qy, qz);
-            ax = qx + ax * tv.y;
-            ay = qy + ay * tv.y;
-            az = qz + az * tv.y;
-            rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
-            ++k;
+
+    // Rounds: round 0 is the window; a chain that leaves it continues in a new window from its end
+    // (never expected with the margins; bounded by spp rounds since each folds at least one sample)
+    while (__syncthreads_or(rd[7] == 0u)) {
+        const bool live = rd[7] == 0u;
+        const uint32_t js = rd[0], M = rd[1];
+        // ---- slots [js + j0, js + j1) of this lane, relative slot indices j
+        const uint32_t j0 = M * l / kSpecLanes, j1 = M * (l + 1u) / kSpecLanes;
+        rng6 st = {rd[2], rd[3], rd[4], rd[5], rd[6], p.rng[5 * (size_t)p.npix + rd[13]] + 2u * (js + j0) * IQ_XORWOW_WEYL};
+        xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, live ? 2u * j0 : 0u);
+        lst[l * 5u] = st.v0;
+        lst[l * 5u + 1u] = st.v1;
+        lst[l * 5u + 2u] = st.v2;
+        lst[l * 5u + 3u] = st.v3;
+        lst[l * 5u + 4u] = st.v4;
+        uint32_t j = j0;
+        bool active = live && j0 < j1;
+        rng6 base = st;
+        ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+        int depth = 0;
+        // a slot's sample starts here: its camera ray, and the state its two draws leave (the next slot's)
+        auto start_slot = [&]() {
+            camera_ray<OPT>(p, px, py, st, ray);
+            base = st;
+            depth = 0;
         };
-        constexpr int kBatch = 8;
-        while (k < p.spp && j < M) {
-            uint32_t cj[kBatch], cn[kBatch];
-            int cnt = 0;
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b) {
-                cj[b] = 0u;
-                cn[b] = 0u;
-                if (k + (uint32_t)b < p.spp && j < M) {
-                    if ((j & ~15u) != nbase) {
-                        nbase = j & ~15u;
-                        nb = *reinterpret_cast<const uint4*>(nr + nbase);
+        if (active) start_slot();
+        while (__any(active)) {
+            // closest hit (path_tracer.cu:253-295): camera rays over their tile's mask pairs in index order
+            float closest = kTMax;
+            int kind = kHitNone;
+            uint32_t hidx = 0;
+            {
+                const bool cull = !__any(active && depth != 0);
+                const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
+                uint4 cm = lds_cm[threadIdx.x];
+                const uint64_t act = __ballot(active);
+                const uint32_t first = (uint32_t)__builtin_ctzll(act);
+                const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
+                const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
+                if (uni) {
+                    cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
+                    cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
+                }
+                const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
+                intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray,
+                                      closest, kind, hidx, p.cull_wt, uni_mask);
+            }
+            if (active) {
+                // shade (path_tracer.cu:297-316) under the reference's materials
+                bool term = false;
+                uint32_t md_end = 0;
+                float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
+                if (kind == kHitSphere) {
+                    const float* sq = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
+                    const float sc = oren_nayar_scatter<OPT>(make_float4(sq[0], sq[2], sq[4], sq[6]), closest, ray, st);
+                    if (depth + 1 >= p.max_depth) {
+                        term = true;                 // the last record is this scatter (biased, :252)
+                        md_end = 1;
+                        Lx = sc;
+                        Ly = sc;
+                        Lz = sc;
+                    } else {
+                        lds_stk[(uint32_t)depth * kSpecBlock + threadIdx.x] = sc;
+                        ++depth;
                     }
-                    const uint32_t o = j - nbase, w = o >> 2;
-                    const uint32_t word = w == 0u ? nb.x : (w == 1u ? nb.y : (w == 2u ? nb.z : nb.w));
-                    cj[b] = j;
-                    cn[b] = (word >> ((o & 3u) * 8u)) & 0xffu;
-                    j += cn[b];
-                    cnt = b + 1;
+                } else if (kind == kHitTri) {
+                    term = true;                     // emissive(1, 10)
+                    Lx = 10.0f;
+                    Ly = 10.0f;
+                    Lz = 10.0f;
+                } else {
+                    term = true;                     // sky gradient, :308-313
+                    const float a = (ray.dy + 1.0f) * 0.5f;
+                    const float one_a = 1.0f - a;
+                    Lx = one_a + a * 0.5f;
+                    Ly = one_a + a * 0.7f;
+                    Lz = one_a + a * 1.0f;
+                }
+                if (term) {
+                    // backward product (:321-324), clamp (:345-347), 0 + colour (:341, 348)
+                    float cx = Lx, cy = Ly, cz = Lz;
+                    for (int i = depth - 1; i >= 0; --i) {
+                        const float rr = lds_stk[(uint32_t)i * kSpecBlock + threadIdx.x];
+                        cx = cx * rr;
+                        cy = cy * rr;
+                        cz = cz * rr;
+                    }
+                    cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                    cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                    cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                    res[j] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                    ln[j] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
+                    if (++j == j1) {
+                        active = false;
+                    } else {
+                        st = base;                   // slot j starts where slot j - 1's camera draws ended
+                        start_slot();
+                    }
                 }
             }
-            float4 v[kBatch];
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b)
-                if (b < cnt) v[b] = res[cj[b]];
-#pragma unroll
-            for (int b = 0; b < kBatch; ++b)
-                if (b < cnt) fold(v[b].x, v[b].y, v[b].z, cn[b]);
         }
-        // the state at slot j: from the nearest stored state at or below it (slot M when past the window)
-        const uint32_t plane = j >= M ? s.g_max : j / s.run_len;
-        const uint32_t steps = j >= M ? j - M : j - plane * s.run_len;
-        const uint32_t* sv = s.st + (size_t)plane * 5u * s.n + q;
-        rng6 st = {sv[0], sv[s.n], sv[2 * (size_t)s.n], sv[3 * (size_t)s.n], sv[4 * (size_t)s.n],
-                   p.rng[5 * (size_t)p.npix + pix] + 2u * j * IQ_XORWOW_WEYL};
-        xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * steps);
-        if (k < p.spp) {
-            // the chain left its window: finish its samples here, in order
-            uint32_t col, row;
-            tile_decode(pix, p.ncols, p.nrows, &col, &row);
-            const uint32_t px = p.x0 + col, py = p.y0 + row * p.ystep;
-            while (k < p.spp) {
-                float cx, cy, cz;
-                uint32_t n;
-                spec_trace_one<MAXD, OPT>(p, px, py, st, cx, cy, cz, n);
-                fold(cx, cy, cz, n);
-                j += n;
+
+        // ---- walk: the colours are this block's own stores (complete: vmcnt 0), read back from L2
+        __builtin_amdgcn_s_waitcnt(0);
+        __syncthreads();
+        uint32_t jw = 0;                                 // walker: the chain's next relative slot
+        uint16_t* lp = lds_pos + g * 64u;
+        float ax = __uint_as_float(rd[8]), ay = __uint_as_float(rd[9]), az = __uint_as_float(rd[10]);
+        uint32_t k = rd[11], rays = rd[12];
+        for (uint32_t r0 = 0; r0 < p.spp; r0 += 64u) {
+            if (walker && live) {
+                uint32_t c = 0;
+                while (c < 64u && k + c < p.spp && jw < M) {
+                    lp[c++] = (uint16_t)jw;
+                    jw += ln[jw];
+                }
+                lds_w[2 * g] = c;
+            }
+            __syncthreads();
+            const uint32_t cnt = (valid && live) ? lds_w[2 * g] : 0u;
+            for (uint32_t i = l; i < cnt; i += kSpecLanes) {
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(res + lp[i]);
+                lds_c[g * 64u + i] = make_float4(
+                    __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                    __uint_as_float(__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
+                    __uint_as_float(__hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), 0.0f);
+            }
+            __syncthreads();
+            if (walker && live)
+                for (uint32_t i = 0; i < cnt; ++i) {
+                    const float4 c = lds_c[g * 64u + i];
+                    const float2 tv = tab[k];
+                    float qx, qy, qz;
+                    mean_terms<OPT>(c.x, c.y, c.z, tab_n[k], tv.x, p.mean_tiny, qx, qy, qz);
+                    ax = qx + ax * tv.y;
+                    ay = qy + ay * tv.y;
+                    az = qz + az * tv.y;
+                    const uint32_t n = ln[lp[i]];
+                    rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
+                    ++k;
+                }
+            __syncthreads();
+        }
+        if (walker && live) {
+            rd[8] = __float_as_uint(ax);
+            rd[9] = __float_as_uint(ay);
+            rd[10] = __float_as_uint(az);
+            rd[11] = k;
+            rd[12] = rays;
+            const uint32_t pix = rd[13];
+            // the state at the chain's end, slot js + jw: from the start of the last range at or below it
+            uint32_t kk = kSpecLanes - 1u;
+            while (kk > 0u && M * kk / kSpecLanes > jw) --kk;
+            const uint32_t jk = M * kk / kSpecLanes;
+            uint32_t v0 = lst[kk * 5u], v1 = lst[kk * 5u + 1u], v2 = lst[kk * 5u + 2u], v3 = lst[kk * 5u + 3u],
+                     v4 = lst[kk * 5u + 4u];
+            xorwow_skip_v(v0, v1, v2, v3, v4, 2u * (jw - jk));
+            rd[0] = js + jw;
+            rd[2] = v0;
+            rd[3] = v1;
+            rd[4] = v2;
+            rd[5] = v3;
+            rd[6] = v4;
+            if (k == p.spp) {
+                rd[7] = 1u;
+                const uint32_t jt = js + jw;
+                const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
+                const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
+                const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
+                p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+                reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
+                p.rng[pix] = v0;
+                p.rng[(size_t)p.npix + pix] = v1;
+                p.rng[2 * (size_t)p.npix + pix] = v2;
+                p.rng[3 * (size_t)p.npix + pix] = v3;
+                p.rng[4 * (size_t)p.npix + pix] = v4;
+                p.rng[5 * (size_t)p.npix + pix] = p.rng[5 * (size_t)p.npix + pix] + 2u * jt * IQ_XORWOW_WEYL;
+                s.rho[q] = (uint32_t)(((uint64_t)jt * 256u) / p.spp);
+            } else {
+                // the chain left its window: a new one from its end, sized for the remaining samples
+                atomicAdd(s.run_count + 1, 1u);
+                const uint32_t rem = p.spp - k;
+                rd[1] = min(s.m_cap, max(16u, 3u * rem + 4u));
             }
         }
-        const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
-        const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
-        const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
-        p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
-        reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
-        p.rng[pix] = st.v0;
-        p.rng[(size_t)p.npix + pix] = st.v1;
-        p.rng[2 * (size_t)p.npix + pix] = st.v2;
-        p.rng[3 * (size_t)p.npix + pix] = st.v3;
-        p.rng[4 * (size_t)p.npix + pix] = st.v4;
-        p.rng[5 * (size_t)p.npix + pix] = st.d;
-        s.rho[q] = (uint32_t)(((uint64_t)j * 256u) / p.spp);
     }
+    unsigned long long rays = (l == 0u) ? rd[12] : 0u;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
-    if (__lane_id() == 0 && rays) atomicAdd(p.rays, rays);
+    if (__lane_id() == 0 && rays) add_rays(p.rays, rays);
 }
 
 // LDS bytes of the chain kernel for a launch (scene pairs, mean table, mask slots, ring, group words,
@@ -3484,26 +3416,16 @@ int launch_fan(void* stream, const kparams& p, uint32_t ntiles, int opt) {
 // Slot-parallel sphere pixels (IQPT_SPLIT_SPEC): the resident production option sets, reference materials
 namespace {
 template <int MAXD, int OPT>
-int spec_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t grid, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_spec_kernel<MAXD, OPT>), dim3(grid), dim3(kSpecBlock), lds, stream, p, s);
-    return (int)hipGetLastError();
-}
-template <int MAXD, int OPT>
-int spec_occ_t(uint32_t lds, int* blocks) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_spec_kernel<MAXD, OPT>, kSpecBlock, lds);
-}
-template <int MAXD, int OPT>
-int spec_stitch_t(hipStream_t stream, const kparams& p, const kspec& s) {
-    hipLaunchKernelGGL((iqpt_spec_stitch_kernel<MAXD, OPT>), dim3((s.n + 63u) / 64u), dim3(64), 0, stream, p, s);
+int spec_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t lds) {
+    hipLaunchKernelGGL((iqpt_spec_kernel<MAXD, OPT>), dim3((s.n + kSpecPix - 1u) / kSpecPix), dim3(kSpecBlock), lds,
+                       stream, p, s);
     return (int)hipGetLastError();
 }
 struct spec_variant {
     int maxd, opt;
-    int (*launch)(hipStream_t, const kparams&, const kspec&, uint32_t, uint32_t);
-    int (*occ)(uint32_t, int*);
-    int (*stitch)(hipStream_t, const kparams&, const kspec&);
+    int (*launch)(hipStream_t, const kparams&, const kspec&, uint32_t);
 };
-#define IQPT_SV(M, O) {M, O, spec_launch_t<M, O>, spec_occ_t<M, O>, spec_stitch_t<M, O>}
+#define IQPT_SV(M, O) {M, O, spec_launch_t<M, O>}
 #define IQPT_SV2(O) IQPT_SV(8, O), IQPT_SV(16, O)
 const spec_variant kSpecVariants[] = {
     IQPT_SV2(kOptDefault | kOptPrio),
@@ -3520,32 +3442,18 @@ const spec_variant* find_spec(int max_depth, int opt) {
 }
 }  // namespace
 
-int launch_spec_prep(void* stream, const kparams& p, const kspec& s) {
-    if (s.n == 0) return 0;
-    hipLaunchKernelGGL(iqpt_spec_prep_kernel, dim3((s.n + 255u) / 256u), dim3(256), 0, (hipStream_t)stream, p, s);
-    return (int)hipGetLastError();
-}
-
 bool spec_variant_exists(int max_depth, int opt) { return max_depth <= 16 && find_spec(max_depth, opt) != nullptr; }
 
-int spec_occupancy(int max_depth, int opt, const kparams& p, int* blocks) {
-    const spec_variant* v = find_spec(max_depth, opt);
-    if (!v) return (int)hipErrorInvalidDeviceFunction;
-    return v->occ(spec_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.max_depth), blocks);
+uint32_t spec_lds(const kparams& p, const kspec& s) {
+    return spec_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.max_depth, p.spp, s.m_cap);
 }
 
-int launch_spec(void* stream, const kparams& p, const kspec& s, uint32_t grid, int opt) {
+int launch_spec(void* stream, const kparams& p, const kspec& s, int opt) {
     const spec_variant* v = find_spec(p.max_depth, opt);
-    if (!v || p.max_depth > 16 || p.cull == nullptr) return (int)hipErrorInvalidDeviceFunction;
-    if (s.n == 0 || grid == 0) return 0;
-    return v->launch((hipStream_t)stream, p, s, grid, spec_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.max_depth));
-}
-
-int launch_spec_stitch(void* stream, const kparams& p, const kspec& s, int opt) {
-    const spec_variant* v = find_spec(p.max_depth, opt);
-    if (!v || p.spp > kAccTableMax) return (int)hipErrorInvalidDeviceFunction;
+    if (!v || p.max_depth > 16 || p.cull == nullptr || p.spp > kAccTableMax || s.m_cap > 65535u)
+        return (int)hipErrorInvalidDeviceFunction;
     if (s.n == 0) return 0;
-    return v->stitch((hipStream_t)stream, p, s);
+    return v->launch((hipStream_t)stream, p, s, spec_lds(p, s));
 }
 
 bool chain_variant_exists(int max_depth, int opt, uint32_t lanes) {

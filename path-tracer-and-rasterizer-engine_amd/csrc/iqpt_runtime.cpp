@@ -40,6 +40,10 @@ constexpr double kSplitAutoPixelsPerLane = 1.2;
 // plain kernel (C3 shares: N = 4 has 1.6, N = 8 0.8; N = 2, 3.2, is faster plain); chain-kernel waves per
 // CU by default (profiles/r02/split_share_v12_lanes.json: 16 beats 8 at N <= 4, equal at N = 8)
 constexpr double kChainAutoPixelsPerLane = 2.0;
+// spec launches: AUTO takes them below this many owned pixels per resident lane of the
+// plain kernel (C3's N = 8 share has 0.8: spec 0.34 ms per launch against chain 0.39-0.44; N = 4, 1.6,
+// stays chain: 0.62 against 0.67-0.70; profiles/r03/share_modes.json)
+constexpr double kSpecAutoPixelsPerLane = 1.2;
 constexpr uint32_t kChainWavesPerCu = 16;
 constexpr size_t kSplitResBudget = size_t(8) << 30;   // speculative results (bytes)
 
@@ -173,17 +177,15 @@ struct iqpt_ctx {
     uint32_t* d_fan_tiles = nullptr;
     uint64_t* d_fan_lanes = nullptr;
     uint32_t n_fan_tiles = 0;
-    // spec launches: per sphere pixel (d_chain_pix) the window, the chain's slots per
-    // sample (history, zeroed when the pixel list changes), states every kSpecRunLen slots, the run list,
-    // the slot results; sized for (spec_n, spec_mcap)
-    uint32_t* d_spec = nullptr;         // m, rho (spec_n each), run_count (2), pad, runs (12 x spec_n x runs per pixel)
-    uint32_t* d_spec_st = nullptr;
+    // spec launches: per sphere pixel (d_chain_pix) the last window, the chain's slots per
+    // sample (history, zeroed when the pixel list changes), the slot colours; sized for (spec_n, spec_mcap)
+    uint32_t* d_spec = nullptr;         // m, rho (spec_n each), run_count (2)
     float4_storage* d_spec_res = nullptr;
-    uint8_t* d_spec_nres = nullptr;
     uint32_t spec_n = 0, spec_mcap = 0;
     bool spec_rho_valid = false;
     bool spec_last = false;
     uint32_t spec_rho0 = iqpt::kSpecRho0;   // window of a pixel without history (iqpt_debug_set_spec)
+    uint32_t spec_margin_div = 4;           // window margin: a quarter of the extra slots (iqpt_debug_set_spec)
     uint32_t chain_par = 0;             // the queue-counter set of the next chain launch
     bool chain_q_ready[2] = {false, false};   // that set is zeroed (in stream order)
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
@@ -790,6 +792,16 @@ int store_compact(iqpt_ctx* c, const void* host, uint32_t words, uint32_t planes
     return e == hipSuccess ? IQPT_OK : iqpt::hip_fail(e, "upload");
 }
 
+// The sum of the spread ray counters (iqpt_internal.hpp kRaySlots); the streams are synchronised.
+int read_rays(iqpt_ctx* c, unsigned long long* total) {
+    std::vector<unsigned long long> slots((size_t)iqpt::kRaySlots * iqpt::kRaySlotStride);
+    IQPT_HIP(hipMemcpy(slots.data(), c->d_rays, slots.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    unsigned long long v = 0;
+    for (uint32_t k = 0; k < iqpt::kRaySlots; ++k) v += slots[(size_t)k * iqpt::kRaySlotStride];
+    *total = v;
+    return IQPT_OK;
+}
+
 // After the context's streams are synchronised: read the kernels' error word and latch it (see
 // iqpt_ctx::dev_err). Returns IQPT_ERR_HIP while an error is latched.
 int check_dev_err(iqpt_ctx* c) {
@@ -885,14 +897,14 @@ int iqpt_create(int device, uint32_t width, uint32_t height, const iqpt_pixel_se
     if (hipMalloc(&c->d_lin, n * sizeof(float4_storage)) != hipSuccess ||
         hipMalloc(&c->d_bgra, n * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_rng, 6 * n * sizeof(uint32_t)) != hipSuccess ||
-        hipMalloc(&c->d_rays, sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_rays, iqpt::kRaySlots * iqpt::kRaySlotStride * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc(&c->d_queue, (4 + iqpt::kOverlapQueueWords) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_ovl_err, sizeof(uint32_t)) != hipSuccess)
         return cleanup(iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "device allocation of the frame state failed"));
     // path_tracer.cu:134-135: both buffers start at zero
     if (hipMemsetAsync(c->d_lin, 0, n * sizeof(float4_storage), c->stream) != hipSuccess ||
         hipMemsetAsync(c->d_bgra, 0, n * sizeof(uint32_t), c->stream) != hipSuccess ||
-        hipMemsetAsync(c->d_rays, 0, sizeof(unsigned long long), c->stream) != hipSuccess ||
+        hipMemsetAsync(c->d_rays, 0, iqpt::kRaySlots * iqpt::kRaySlotStride * sizeof(unsigned long long), c->stream) != hipSuccess ||
         hipMemsetAsync(c->d_ovl_err, 0, sizeof(uint32_t), c->stream) != hipSuccess)
         return cleanup(iqpt::fail(IQPT_ERR_HIP, "hipMemsetAsync"));
     // renderer_init_kernel (path_tracer.cu:139): curand_init(seed, pixelid, 0)
@@ -930,7 +942,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     free_split(c);
-    for (void* b : {(void*)c->d_spec, (void*)c->d_spec_st, (void*)c->d_spec_res, (void*)c->d_spec_nres})
+    for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res})
         if (b) (void)hipFree(b);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
@@ -1331,6 +1343,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // chain launches: the split set's pixels in iqpt_chain_kernel, the other tiles in the
     // plain kernel beside it (resident scenes, reference materials)
     bool chain = false;
+    bool auto_spec = false;             // AUTO: the share is small enough for spec launches (if they apply)
     if ((c->split_mode == IQPT_SPLIT_CHAIN || c->split_mode == IQPT_SPLIT_AUTO) && !stream_batches && p.cull &&
         c->n_split_tiles > 0 && tune_slot < 0 && !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax &&
         iqpt::chain_variant_exists(c->max_depth, opt, c->chain_lanes)) {
@@ -1338,6 +1351,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         if (iqpt::render_occupancy(c->max_depth, false, opt, lds, &occ_p) != 0) occ_p = 0;
         const double lanes = (double)c->num_cus * std::max(occ_p, 1) * iqpt::kRenderBlock;
         chain = c->split_mode == IQPT_SPLIT_CHAIN || (double)c->npix < iqpt::kChainAutoPixelsPerLane * lanes;
+        auto_spec = c->split_mode == IQPT_SPLIT_AUTO && (double)c->npix < iqpt::kSpecAutoPixelsPerLane * lanes;
     }
     // fan launches: the anchored tiles (no sphere candidate) in iqpt_fan_kernel, the split
     // set's tiles in the plain kernel beside it
@@ -1346,10 +1360,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
                         iqpt::fan_variant_exists(opt);
     const bool fan = !chain && fan_ok && c->split_mode == IQPT_SPLIT_FAN;
     // spec launches: sphere pixels slot-parallel, every other pixel in the fan kernel
-    const bool spec = !chain && fan_ok && c->split_mode == IQPT_SPLIT_SPEC && c->n_split_tiles > 0 &&
+    const bool spec = (!chain || auto_spec) && fan_ok && (c->split_mode == IQPT_SPLIT_SPEC || auto_spec) && c->n_split_tiles > 0 &&
                       iqpt::spec_variant_exists(c->max_depth, opt) &&
-                      (size_t)c->n_chain_pix * ((iqpt::kSplitMCapMul * spp + 15u) & ~15u) * 22u <= iqpt::kSplitResBudget;
-    const bool fan_beside_chain = chain && fan_ok && c->fan_anchored;
+                      (size_t)c->n_chain_pix * ((iqpt::kSplitMCapMul * spp + 15u) & ~15u) * 16u <= iqpt::kSplitResBudget;
+    bool fan_beside_chain = chain && fan_ok && c->fan_anchored;
+    if (spec) chain = fan_beside_chain = false;
     uint32_t lds_split = lds + iqpt::kRenderBlock * (16u + 24u);   // + lds_sp and the base states
     bool split = false;
     if (!chain && !fan && !spec && c->split_mode != IQPT_SPLIT_OFF && c->split_mode != IQPT_SPLIT_CHAIN &&
@@ -1591,29 +1606,23 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
         IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
     } else if (spec) {
-        // every pixel without a sphere in reach in the fan kernel on stream2; on stream the sphere pixels:
-        // prep (windows, states, runs) -> slots -> stitch (walk, fold, finish, store)
+        // every pixel without a sphere in reach in the fan kernel on stream2; the sphere pixels in
+        // iqpt_spec_kernel on stream (slots, then the walk)
         iqpt::kspec ks2;
         std::memset(&ks2, 0, sizeof ks2);
         const uint32_t n = c->n_chain_pix;
         const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
-        const uint32_t R = iqpt::kSpecRunLen;
-        const uint32_t runs_per = (m_cap + R - 1) / R;
         if (n > 0 && (n > c->spec_n || m_cap > c->spec_mcap)) {
             IQPT_HIP(hipStreamSynchronize(c->stream));
-            for (void* b : {(void*)c->d_spec, (void*)c->d_spec_st, (void*)c->d_spec_res, (void*)c->d_spec_nres})
+            for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res})
                 if (b) (void)hipFree(b);
             c->d_spec = nullptr;
-            c->d_spec_st = nullptr;
             c->d_spec_res = nullptr;
-            c->d_spec_nres = nullptr;
             c->spec_n = c->spec_mcap = 0;
             const size_t slots = (size_t)n * m_cap;
-            if (slots * 17 + ((size_t)runs_per + 1) * 5 * n * 4 + 48 * (size_t)runs_per * n > iqpt::kSplitResBudget ||
-                hipMalloc(&c->d_spec, (2 * (size_t)n + 4 + 12 * (size_t)n * runs_per) * sizeof(uint32_t)) != hipSuccess ||
-                hipMalloc(&c->d_spec_st, ((size_t)runs_per + 1) * 5 * n * sizeof(uint32_t)) != hipSuccess ||
-                hipMalloc(&c->d_spec_res, slots * sizeof(float4_storage)) != hipSuccess ||
-                hipMalloc(&c->d_spec_nres, slots) != hipSuccess) {
+            if (slots * 16 > iqpt::kSplitResBudget ||
+                hipMalloc(&c->d_spec, (2 * (size_t)n + 2) * sizeof(uint32_t)) != hipSuccess ||
+                hipMalloc(&c->d_spec_res, slots * sizeof(float4_storage)) != hipSuccess) {
                 (void)hipGetLastError();
                 return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec buffers");
             }
@@ -1623,34 +1632,26 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
         ks2.n = n;
         ks2.m_cap = m_cap;
-        ks2.run_len = R;
-        ks2.g_max = runs_per;
         ks2.rho0 = c->spec_rho0;
+        ks2.margin_div = c->spec_margin_div;
         ks2.pix = c->d_chain_pix;
         ks2.m = c->d_spec;
         ks2.rho = c->d_spec + n;
         ks2.run_count = c->d_spec + 2 * (size_t)n;
-        ks2.runs = c->d_spec + ((2 * (size_t)n + 2 + 3) & ~(size_t)3);   // 16-byte aligned records
-        ks2.st = c->d_spec_st;
         ks2.res = c->d_spec_res;
-        ks2.nres = c->d_spec_nres;
         IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
         IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
-        if (c->n_fan_tiles > 0) {
+        if (n > 0) {
+            if (!c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, (size_t)n * sizeof(uint32_t), c->stream));
+            c->spec_rho_valid = true;
+            IQPT_HIP(hipMemsetAsync(ks2.run_count, 0, 2 * sizeof(uint32_t), c->stream));
+            le = iqpt::launch_spec(c->stream, p, ks2, opt);
+        }
+        if (le == 0 && c->n_fan_tiles > 0) {
             iqpt::kparams pf = p;
             pf.tile_order = c->d_fan_tiles;
             pf.fan_lanes = c->d_fan_lanes;
             le = iqpt::launch_fan(c->stream2, pf, c->n_fan_tiles, opt);
-        }
-        if (le == 0 && n > 0) {
-            if (!c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, (size_t)n * sizeof(uint32_t), c->stream));
-            c->spec_rho_valid = true;
-            IQPT_HIP(hipMemsetAsync(ks2.run_count, 0, 2 * sizeof(uint32_t), c->stream));
-            le = iqpt::launch_spec_prep(c->stream, p, ks2);
-            int occ_s = 0;
-            if (le == 0 && (iqpt::spec_occupancy(c->max_depth, opt, p, &occ_s) != 0 || occ_s < 1)) occ_s = 1;
-            if (le == 0) le = iqpt::launch_spec(c->stream, p, ks2, (uint32_t)c->num_cus * (uint32_t)occ_s, opt);
-            if (le == 0) le = iqpt::launch_spec_stitch(c->stream, p, ks2, opt);
         }
         IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
         IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
@@ -1796,7 +1797,7 @@ int iqpt_checkpoint_save(iqpt_ctx* c, const char* path) {
         (st = fetch_compact(c, c->d_bgra, 1, 1, bgra.data())) != IQPT_OK ||
         (st = fetch_compact(c, c->d_rng, 1, 6, rng.data())) != IQPT_OK)
         return st;
-    IQPT_HIP(hipMemcpy(&rays, c->d_rays, sizeof rays, hipMemcpyDeviceToHost));
+    if ((st = read_rays(c, &rays)) != IQPT_OK) return st;
     ckpt_header h;
     std::memset(&h, 0, sizeof h);
     std::memcpy(h.magic, kCkptMagic, 8);
@@ -1876,7 +1877,11 @@ int iqpt_checkpoint_load(iqpt_ctx* c, const char* path) {
         (st = store_compact(c, bgra.data(), 1, 1, c->d_bgra)) != IQPT_OK ||
         (st = store_compact(c, rng.data(), 1, 6, c->d_rng)) != IQPT_OK)
         return st;
-    IQPT_HIP(hipMemcpy(c->d_rays, &rays, sizeof rays, hipMemcpyHostToDevice));
+    {
+        std::vector<unsigned long long> slots((size_t)iqpt::kRaySlots * iqpt::kRaySlotStride, 0ull);
+        slots[0] = rays;
+        IQPT_HIP(hipMemcpy(c->d_rays, slots.data(), slots.size() * sizeof(unsigned long long), hipMemcpyHostToDevice));
+    }
     c->frame = h.frame;
     // the whole pixel state is replaced: a latched kernel error no longer applies
     IQPT_HIP(hipMemset(c->d_ovl_err, 0, sizeof(uint32_t)));
@@ -1902,7 +1907,7 @@ int iqpt_rays_traced(iqpt_ctx* c, uint64_t* rays) {
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     unsigned long long v = 0;
-    IQPT_HIP(hipMemcpy(&v, c->d_rays, sizeof v, hipMemcpyDeviceToHost));
+    if ((st = read_rays(c, &v)) != IQPT_OK) return st;
     *rays = v;
     return IQPT_OK;
 }
@@ -1948,6 +1953,7 @@ int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
         std::vector<uint32_t> v(2 * (size_t)n + 2);
         IQPT_HIP(hipMemcpy(v.data(), c->d_spec, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
         out8[4] = v[2 * (size_t)n];
+        out8[7] = v[2 * (size_t)n + 1];
         unsigned long long m = 0, rho = 0;
         for (uint32_t q = 0; q < n; ++q) {
             m += v[q];
@@ -1959,11 +1965,12 @@ int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
     return IQPT_OK;
 }
 
-/* Internal (tests): the slots per sample (x 256) a spec window assumes for a pixel without history; a small
- * value makes the chains of sphere pixels leave their first window (the stitch then finishes them).
- * 0 restores the default; the history is dropped so that the next launch uses it. */
-int iqpt_debug_set_spec(iqpt_ctx* c, uint32_t rho0) {
+/* Internal (tests, A/B): the slots per sample (x 256) a spec window assumes for a pixel without history (a
+ * small value makes the chains of sphere pixels leave their first window: the walker then finishes them)
+ * and the window margin divisor. 0 restores a default; the history is dropped. */
+int iqpt_debug_set_spec(iqpt_ctx* c, uint32_t rho0, uint32_t margin_div) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->spec_margin_div = margin_div ? margin_div : 4u;
     c->spec_rho0 = rho0 ? rho0 : iqpt::kSpecRho0;
     c->spec_rho_valid = false;
     return IQPT_OK;

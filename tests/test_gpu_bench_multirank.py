@@ -40,7 +40,7 @@ def test_two_rank_strong_frame_equals_one_rank(require_gpu, tmp_path, gather):
     assert two["rays_per_sample"] == one["rays_per_sample"]
 
 
-@pytest.mark.parametrize("share,mode", [(2, "plain"), (8, "chain+fan")])
+@pytest.mark.parametrize("share,mode", [(2, "plain"), (4, "chain+fan"), (8, "spec")])
 def test_stream_ordered_gather_on_one_gpu(require_gpu, tmp_path, share, mode):
     """The RCCL path the driver's N-GPU runs take, on one GPU: a one-rank nccl process group, rank 0's
     rows of an N-way split, the stream-ordered frame copy + gather every step (copies that keep

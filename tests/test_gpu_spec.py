@@ -87,8 +87,8 @@ def test_chains_leaving_their_window_spec(require_gpu):
     pt = PathTracer(w, h, max_depth=8)
     pt.set_split(SPLIT_SPEC)
     lib = _lib.load()
-    lib.iqpt_debug_set_spec.argtypes = [C.c_void_p, C.c_uint32]
-    _lib.check(lib.iqpt_debug_set_spec(pt._h, 256), "iqpt_debug_set_spec")
+    lib.iqpt_debug_set_spec.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+    _lib.check(lib.iqpt_debug_set_spec(pt._h, 256, 0), "iqpt_debug_set_spec")
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, max_depth=8)
@@ -140,3 +140,26 @@ def test_c3_share8_spec_vs_plain(require_gpu):
     assert np.array_equal(outs[0][1], outs[1][1])
     assert np.array_equal(outs[0][2], outs[1][2])
     assert outs[0][3] == outs[1][3]
+
+
+@pytest.mark.parametrize("margin_div", [1, 16])
+def test_window_margins_spec(require_gpu, margin_div):
+    """Wide (margin = all the extra slots) and tight windows: the same bits."""
+    from iqpt import PathTracer, _lib, make_camera
+    w, h = 256, 144
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, max_depth=8)
+    pt.set_split(SPLIT_SPEC)
+    lib = _lib.load()
+    lib.iqpt_debug_set_spec.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+    _lib.check(lib.iqpt_debug_set_spec(pt._h, 0, margin_div), "iqpt_debug_set_spec")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, max_depth=8)
+    for s in (16, 40, 40):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    assert mode_of(pt) == 6
+    _check(pt, lin, bgra, fr)

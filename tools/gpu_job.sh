@@ -1,19 +1,12 @@
-# r03 run 10: spec with self-contained run records: exactness, statistics, kernel trace at N = 8
+# r03 run 17: the whole -m gpu suite, smoke, then share steps through the gather path and the default bench
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_spec.py tests/test_gpu_fan.py -x -q --timeout 200 --timeout-method thread > gpurun_out/r03_run10_tests.log 2>&1 || { tail -40 gpurun_out/r03_run10_tests.log; exit 1; }
-tail -2 gpurun_out/r03_run10_tests.log
-timeout -k 10 400 python -u tools/split_share.py --modes spec,chain,fan --ns 8,4,2,1 --launches 6 --out gpurun_out/r03_share_v6.json > gpurun_out/r03_run10_share.log 2>&1 || { tail -30 gpurun_out/r03_run10_share.log; exit 1; }
-python -c "
-import json; d=json.load(open('gpurun_out/r03_share_v6.json'))
-for r in d['rows']: print({k:(round(v,3) if isinstance(v,float) else v) for k,v in r.items() if k!='split_info' and 'min' not in k})"
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-timeout -k 10 180 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/r03_prof10_spec8 -o run -- python3 tools/split_share.py --modes spec --ns 8 --launches 4 --warm 2 > gpurun_out/r03_run10_prof.log 2>&1 || { tail -20 gpurun_out/r03_run10_prof.log; exit 1; }
-python3 - <<'PY'
-import csv
-rows=[r for r in csv.DictReader(open('gpurun_out/r03_prof10_spec8/run_kernel_trace.csv')) if 'iqpt_' in r['Kernel_Name'] or 'fill' in r['Kernel_Name']]
-rows.sort(key=lambda r:int(r['Start_Timestamp']))
-t0=int(rows[-8]['Start_Timestamp'])
-for r in rows[-8:]:
-    s=(int(r['Start_Timestamp'])-t0)/1e3; e=(int(r['End_Timestamp'])-t0)/1e3
-    print(r['Kernel_Name'][:50], round(s,1), round(e-s,1))
-PY
+timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 700 --timeout-method thread > gpurun_out/r03_run17_tests.log 2>&1 || { tail -60 gpurun_out/r03_run17_tests.log; exit 1; }
+tail -3 gpurun_out/r03_run17_tests.log
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_run17_smoke.log 2>&1 || { tail -20 gpurun_out/r03_run17_smoke.log; exit 1; }
+tail -1 gpurun_out/r03_run17_smoke.log
+for s in 8 4 2; do
+  timeout -k 10 180 python -u bench.py --self-gather --share-of $s --no-cpu-baseline --steps 30 > gpurun_out/r03_run17_share$s.json 2> gpurun_out/r03_run17_share$s.err || { tail -20 gpurun_out/r03_run17_share$s.err; exit 1; }
+  tail -1 gpurun_out/r03_run17_share$s.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print($s, d['ms_per_step'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'], d['roofline']['kernel_avg_ms'])"
+done
+timeout -k 10 300 python -u bench.py --cpu-seconds 10 > gpurun_out/r03_run17_default.json 2> gpurun_out/r03_run17_default.err || { tail -20 gpurun_out/r03_run17_default.err; exit 1; }
+tail -1 gpurun_out/r03_run17_default.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('default', d['value'], d['ms_per_step'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'])"

@@ -9,7 +9,10 @@ ACTIVE_INST_ANY ~= WAVE_CYCLES (MI355X_MICROARCH.md, rocprofv3 PMC slots). GRBM_
 over the 8 XCDs: kernel cycles = GRBM_GUI_ACTIVE / 8. valu_busy_frac = VALU-active cycles per SIMD
 over the kernel's cycles (1024 SIMDs).
 
-usage: pmc_mix.py <passA.csv> <passB.csv> <config> <wave_iterations_per_launch> <out.json> [label]
+usage: pmc_mix.py <passA.csv> <passB.csv> <config> <wave_iterations_per_launch> <out.json> [label] [kernel]
+
+kernel: a substring of the kernel name to select (default iqpt_render_kernel; e.g. iqpt_spec_kernel,
+iqpt_fan_kernel, iqpt_chain_kernel).
 """
 import csv
 import json
@@ -19,17 +22,20 @@ from collections import defaultdict
 SIMDS = 256 * 4
 
 
+KERNEL = "iqpt_render_kernel"
+
+
 def last_dispatch(path):
     agg = defaultdict(lambda: defaultdict(float))
     dur = {}
     with open(path) as f:
         for r in csv.DictReader(f):
-            if "iqpt_render_kernel" not in r.get("Kernel_Name", ""):
+            if KERNEL not in r.get("Kernel_Name", ""):
                 continue
             agg[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
             dur[r["Dispatch_Id"]] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
     if not agg:
-        raise SystemExit(f"no iqpt_render_kernel rows in {path}")
+        raise SystemExit(f"no {KERNEL} rows in {path}")
     d = sorted(agg, key=int)[-1]
     return dict(agg[d]), dur[d]
 
@@ -37,6 +43,9 @@ def last_dispatch(path):
 def main():
     a_csv, b_csv, config, iters, out = sys.argv[1:6]
     label = sys.argv[6] if len(sys.argv) > 6 else ""
+    global KERNEL
+    if len(sys.argv) > 7:
+        KERNEL = sys.argv[7]
     iters = float(iters)
     a, _ = last_dispatch(a_csv)
     b, dur = last_dispatch(b_csv)
@@ -44,7 +53,7 @@ def main():
     wave = b["SQ_WAVE_CYCLES"]
     res = {
         "config": config,
-        "kernel": label or "iqpt_render_kernel",
+        "kernel": label or KERNEL,
         "wave_iterations_per_launch": iters,
         "counters": {**a, **b},
         "per_iteration": {k: round(v / iters, 2) for k, v in a.items() if k.startswith("SQ_INSTS")},

@@ -28,7 +28,7 @@ OPT = 0
 
 
 def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain_waves: int = 0,
-        fan: bool = True) -> dict:
+        fan: bool = True, spec_run: int = 0) -> dict:
     cfg = CONFIGS["c2"]
     sc = Scene()
     sc.add_preset(cfg.preset)
@@ -47,6 +47,11 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain
         lb = _lib.load()
         lb.iqpt_debug_set_split_knobs.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_split_knobs(pt._h, knobs[0], knobs[1]), "iqpt_debug_set_split_knobs")
+    if spec_run:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_spec(pt._h, 0, spec_run), "iqpt_debug_set_spec")   # margin divisor
     if not fan:
         import ctypes as C
         lb = _lib.load()
@@ -89,7 +94,7 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain
                      "split_pixels": info[6], "mean_window": info[4] / max(info[6], 1),
                      "mean_slots_per_sample": info[5] / 256 / max(info[6], 1), "ran_split": info[7],
                      "sphere_pixels": spec[0], "fan_tiles": spec[1], "spec_runs": spec[4], "spec_window_slots": spec[5],
-                     "spec_slots_per_sample": spec[6] / 256 / max(spec[0], 1)}}
+                     "spec_slots_per_sample": spec[6] / 256 / max(spec[0], 1), "spec_leftovers": spec[7]}}
 
 
 def wave_timeline(n: int, spp: int, warm: int, knobs=None) -> dict:
@@ -161,6 +166,7 @@ def main():
     ap.add_argument("--modes", default="plain,split", help="plain, split, chain (IQPT_SPLIT_CHAIN, anchored tiles in "
                     "the fan kernel), chainplain (the same, anchored tiles in the plain kernel), fan (IQPT_SPLIT_FAN)")
     ap.add_argument("--chain-waves", default="", help="extra chain rows at these chain-kernel waves per CU")
+    ap.add_argument("--spec-runs", default="", help="extra spec rows at these window margin divisors")
     ap.add_argument("--knobs", default="", help="split knob sets heavy_rho:refill_min[,...] (extra split rows)")
     ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (instrumented library)")
     ap.add_argument("--opt", type=lambda v: int(v, 0), default=0, help="kernel option set (instrumented library; 0 = production)")
@@ -199,9 +205,11 @@ def main():
             v = w.rstrip("a")
             return int(v.split("l")[0]) | ((int(v.split("l")[1]) << 8) if "l" in v else 0)
         modes += [(f"chain_w{w}", _lib.SPLIT_CHAIN, cw(w)) for w in args.chain_waves.split(",") if w]
+        modes += [(f"spec_r{r}", _lib.SPLIT_SPEC, int(r)) for r in args.spec_runs.split(",") if r]
         for name, mode, cw in modes:
             kn = (0, 16 | (1 << 16)) if name.endswith("a") else None
-            r = run(n, mode, args.launches, args.warm, args.spp, knobs=kn, chain_waves=cw, fan=name not in ("chainplain", "splitplain"))
+            r = run(n, mode, args.launches, args.warm, args.spp, knobs=kn, chain_waves=0 if name.startswith("spec") else cw,
+                    fan=name not in ("chainplain", "splitplain"), spec_run=cw if name.startswith("spec_r") else 0)
             res[name] = r
             row[name + "_ms_median"] = float(np.median(r["ms"]))
             row[name + "_ms_min"] = float(np.min(r["ms"]))
@@ -213,6 +221,7 @@ def main():
             if name.startswith("spec"):
                 row[name + "_runs"] = r["info"]["spec_runs"]
                 row[name + "_window_slots"] = r["info"]["spec_window_slots"]
+                row[name + "_leftovers"] = r["info"]["spec_leftovers"]
                 row[name + "_slots_per_sample"] = round(r["info"]["spec_slots_per_sample"], 3)
             if name.startswith(("chain", "fan", "split", "spec")):
                 row[name + "_ran"] = {0: "plain", 1: "split", 2: "chain", 3: "fan", 4: "chain+fan", 5: "split+fan", 6: "spec"}.get(
