@@ -231,16 +231,17 @@ int iqpt_copy_accum_device(iqpt_ctx* ctx, void* dst_device, size_t bytes);
 int iqpt_copy_frame_device(iqpt_ctx* ctx, void* dst_device, size_t bytes);
 /* Stream-ordered form of iqpt_copy_frame_device for a pipelined gather: the copy is enqueued after
  * every render issued so far, on the stream iqpt_frame_stream names, and the call returns at once (no
- * host sync). It does not join overlapped launches: the next render still overlaps the last one (from
- * the first such copy on, overlapped launches write the frame into two buffers in turn).
- * The caller orders its own work against iqpt_frame_stream's stream, asked right before this call. */
+ * host sync). It does not join overlapped or pipelined launches: the next render still overlaps the last
+ * one (from the first such copy on, those launches write the frame into two buffers in turn, DESIGN.md §7,
+ * §3.11). The caller orders its own work against iqpt_frame_stream's stream, asked right before this call. */
 int iqpt_copy_frame_device_async(iqpt_ctx* ctx, void* dst_device, size_t bytes);
 /* The context's HIP stream (hipStream_t): renders, and every copy out, are ordered on it (overlapped
  * launches join it before any other call but iqpt_copy_frame_device_async). */
 int iqpt_stream(iqpt_ctx* ctx, void** stream);
 /* The stream iqpt_copy_frame_device_async enqueues on now: that of the last render launch while
- * overlapped launches are in flight, else the context's stream. Work enqueued there runs after that
- * launch, not after the ones issued later. */
+ * overlapped launches are in flight, a copy stream behind both kernels of the last launch while
+ * pipelined spec launches are (IQPT_SPLIT_SPEC), else the context's stream. Work enqueued there runs after
+ * that launch, not after the ones issued later. */
 int iqpt_frame_stream(iqpt_ctx* ctx, void** stream);
 
 int iqpt_num_pixels(const iqpt_ctx* ctx, uint64_t* npix);

@@ -189,7 +189,18 @@ struct kspec {
     uint32_t* rho;                   // slots per sample x 256 of q's last chain (0: none)
     uint32_t* run_count;             // [1]: chains finished past their window (statistics)
     float4_storage* res;             // res[q m_cap + j]: clamped colour of slot j
+    uint32_t fan_tiles;              // fused launches (iqpt_specfan_kernel): fan tiles in the same grid
+    uint32_t lead;                   // fused launches: spec blocks placed before every fan block
+    const uint32_t* order;           // a plan (else null): sphere pixel q at each position, heaviest first
+    const uint32_t* blocks;          // per plan block: first position, count | log2(lanes / 8) << 8
+    uint32_t nblocks;                // plan blocks (the spec part of the grid)
+    unsigned long long* tl;          // measurement (iqpt_debug_spec_timeline), else null: per spec block
+                                     // s_memrealtime at start, after round 0's slots and walk, at the end
+                                     // (| rounds << 48)
 };
+constexpr uint32_t kSpecReplan = 64;        // launches between two spec plans (the history read behind them)
+constexpr uint32_t kSpecPixPerBlock = 16;   // sphere pixels per iqpt_spec_kernel block without a plan (16 lanes each)
+constexpr uint32_t kSpecMaxPixPerBlock = 32;   // a plan's blocks: 256 / (8, 16, 32 or 64) pixels
 constexpr uint32_t kSpecRho0 = 576;      // 2.25 slots per sample before a pixel has a history (sphere pixels take ~2)
 
 // The spec window of a sphere pixel whose last chain used rho256 / 256 slots per sample: that many slots
@@ -352,6 +363,10 @@ int launch_chain(void* stream, const kparams& p, uint32_t grid_blocks, int opt, 
 bool spec_variant_exists(int max_depth, int opt);
 uint32_t spec_lds(const kparams& p, const kspec& s);
 int launch_spec(void* stream, const kparams& p, const kspec& s, int opt);
+// resident iqpt_spec_kernel blocks per CU for this launch
+int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks);
+// spec blocks and s.fan_tiles fan tiles (p.tile_order / p.fan_lanes) in one grid
+int launch_specfan(void* stream, const kparams& p, const kspec& s, int opt);
 // Sample-parallel anchored tiles (iqpt_fan_kernel): one block per tile of
 // p.tile_order[0 .. ntiles) — tiles without sphere candidates, reference materials, resident scene
 // (p.cull set, p.cull_wt <= 16), spp <= kAccTableMax.

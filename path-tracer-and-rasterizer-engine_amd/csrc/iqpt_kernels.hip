@@ -2736,7 +2736,7 @@ __host__ __device__ inline uint32_t fan_lds_bytes(uint32_t ntri_pairs, uint32_t 
 }
 
 template <int OPT>
-__global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p) {
+__device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     float4* lds_tri = lds;
     float2* lds_tab = reinterpret_cast<float2*>(lds_tri + (size_t)p.ntri_pairs * kTriPairFloat4);
@@ -2745,7 +2745,7 @@ __global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p)
     float* lds_sky = reinterpret_cast<float*>(lds_mask + 16);                             // [sample][lane]
     uint64_t* lds_hit = reinterpret_cast<uint64_t*>(lds_sky + kFanChunk * 64u);           // [sample]
 
-    const uint32_t t = p.tile_order[blockIdx.x];
+    const uint32_t t = p.tile_order[bid];
     for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kFanBlock)
         lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
     for (uint32_t s = threadIdx.x; s < p.spp; s += kFanBlock) {
@@ -2762,7 +2762,7 @@ __global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p)
     const uint32_t npt = tw * th;
     const bool inside = lane < npt;                     // partial tiles at the right / bottom edge
     // the pixels of this tile the fan kernel owns (chain launches: the others are the chain kernel's)
-    const uint64_t own = p.fan_lanes ? p.fan_lanes[blockIdx.x] : ~0ull;
+    const uint64_t own = p.fan_lanes ? p.fan_lanes[bid] : ~0ull;
     const bool has = inside && ((own >> lane) & 1ull);
     const uint32_t pix = ty * kCullTile * p.ncols + tx * kCullTile * th + (inside ? lane : 0u);
     const uint32_t px = p.x0 + tx * kCullTile + (inside ? lane % tw : 0u);
@@ -2869,48 +2869,53 @@ __global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p)
 // bundle may reach a sphere take more than one slot per sample, so only their chains need speculation.
 // Sample k of a pixel starts where sample k - 1's draws ended (path_tracer.cu:339): 2 draws for the
 // jitter (camera.cu:24-25) plus 2 per Oren-Nayar scatter (material.cu:10), and what a sample does from
-// stream offset 2j ("slot" j) depends on j alone. One kernel, 16 lanes per sphere pixel:
-//  * slots: the pixel's window of M slots (its last chain's slots per sample, spec_window) is cut into 16
+// stream offset 2j ("slot" j) depends on j alone. One kernel, L = 8, 16, 32 or 64 lanes per sphere pixel
+// (16 without a plan; a plan gives the pixels with the most work per lane more lanes, runtime):
+//  * slots: the pixel's window of M slots (its last chain's slots per sample, spec_window) is cut into L
 //    ranges; each lane steps its state to its range's first slot and traces the range's slots back to
 //    back (the next slot's state is the one the current slot's camera draws leave), one ray per live lane
 //    per iteration; colours go to HBM, the slot counts to LDS;
-//  * walk: one lane per pixel follows the chain 0 -> j + n_j -> ... in LDS, the pixel's 16 lanes gather
-//    the colours of 64 chain samples at a time, and the walker folds them in sample order with the plain
-//    kernel's table values (path_tracer.cu:356-358), counting each sample's rays (its slots, or max_depth
-//    when it ended on a scatter at max_depth); a chain that leaves its window is finished by the walker.
+//  * walk: one lane per pixel follows the chain 0 -> j + n_j -> ... in LDS, a batch of chain samples at a
+//    time; the pixel's lanes gather their colours, form the mean terms with the plain kernel's table
+//    values and count each sample's rays (its slots, or max_depth when it ended on a scatter at
+//    max_depth), and the walker folds the terms in sample order (path_tracer.cu:356-358); a chain that
+//    leaves its window continues in a new window (another round).
 // Same bits as the plain kernel: the same per-sample code, the same mean terms, the chain's own slots as
 // rays, the state where the chain stops.
 constexpr uint32_t kSpecBlock = 256;
-constexpr uint32_t kSpecLanes = 16;                    // lanes per sphere pixel
-constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per block
+constexpr uint32_t kSpecLanes = 16;                    // lanes per sphere pixel without a plan
+constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per block without a plan
+constexpr uint32_t kSpecMaxPix = 32;                   // pixels per block at 8 lanes each
+constexpr uint32_t kSpecBatch = 512;                   // walk: chain samples gathered per block and batch
+static_assert(kSpecPix == kSpecPixPerBlock && kSpecMaxPix == kSpecMaxPixPerBlock, "runtime and kernel agree on the spec block");
 
 __host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth, uint32_t spp,
                                                    uint32_t m_cap) {
     const uint32_t sp4 = (spp + 3u) & ~3u;
-    return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + kSpecBlock * 16u +
-           kSpecPix * 64u * 16u + sp4 * 12u + (uint32_t)(max_depth > 1 ? max_depth : 1) * kSpecBlock * 4u +
-           kSpecPix * kSpecLanes * 20u + kSpecPix * 64u + kSpecPix * 64u * 2u + kSpecPix * 8u + kSpecPix * m_cap;
+    return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + kSpecMaxPix * 16u +
+           kSpecBatch * 16u + sp4 * 12u + (uint32_t)(max_depth > 1 ? max_depth : 1) * kSpecBlock * 4u +
+           kSpecBlock * 20u + kSpecMaxPix * 64u + kSpecBatch * 2u + kSpecMaxPix * 8u + kSpecMaxPix * m_cap;
 }
 
 template <int MAXD, int OPT>
-__global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams p, const kspec s) {
+__device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint32_t bid) {
     extern __shared__ __attribute__((aligned(16))) float4 lds[];
     const uint32_t sp4 = (p.spp + 3u) & ~3u;
     float4* lds_tri = lds;
     float4* lds_sph = lds_tri + (size_t)p.ntri_pairs * kTriPairFloat4;
-    uint4* lds_cm = reinterpret_cast<uint4*>(lds_sph + (size_t)p.nsph_pairs * kSphPairFloat4);    // [thread]
-    float4* lds_c = reinterpret_cast<float4*>(lds_cm + kSpecBlock);                               // [pixel][64]
-    float2* tab = reinterpret_cast<float2*>(lds_c + kSpecPix * 64u);
+    uint4* lds_cm = reinterpret_cast<uint4*>(lds_sph + (size_t)p.nsph_pairs * kSphPairFloat4);    // [pixel]
+    float4* lds_c = reinterpret_cast<float4*>(lds_cm + kSpecMaxPix);                              // [pixel][batch]
+    float2* tab = reinterpret_cast<float2*>(lds_c + kSpecBatch);
     float* tab_n = reinterpret_cast<float*>(tab + sp4);
     float* lds_stk = tab_n + sp4;                                                                  // [depth][thread]
     uint32_t* lds_st = reinterpret_cast<uint32_t*>(lds_stk + (size_t)(p.max_depth > 1 ? p.max_depth : 1) * kSpecBlock);
     // per pixel: 0 the round's first slot (absolute), 1 its window, 2..6 the state there (v0..v4), 7 done,
-    // and the walker's running mean (8..10), samples folded (11), rays (12), storage index (13) — kept in
+    // and the walker's running mean (8..10), samples folded (11), storage index (13) — kept in
     // LDS across the slot loop, whose registers they would otherwise take
-    uint32_t* lds_rd = lds_st + kSpecPix * kSpecLanes * 5u;                                       // [pixel][16]
-    uint16_t* lds_pos = reinterpret_cast<uint16_t*>(lds_rd + kSpecPix * 16u);                      // [pixel][64]
-    uint32_t* lds_w = reinterpret_cast<uint32_t*>(lds_pos + kSpecPix * 64u);                       // [pixel][2]
-    uint8_t* lds_n = reinterpret_cast<uint8_t*>(lds_w + 2u * kSpecPix);                            // [pixel][slot]
+    uint32_t* lds_rd = lds_st + kSpecBlock * 5u;                                                    // [pixel][16]
+    uint16_t* lds_pos = reinterpret_cast<uint16_t*>(lds_rd + kSpecMaxPix * 16u);                   // [pixel][batch]
+    uint32_t* lds_w = reinterpret_cast<uint32_t*>(lds_pos + kSpecBatch);                           // [pixel][2]
+    uint8_t* lds_n = reinterpret_cast<uint8_t*>(lds_w + 2u * kSpecMaxPix);                         // [pixel][slot]
     for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kSpecBlock)
         lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
     for (uint32_t i = threadIdx.x; i < p.nsph_pairs * kSphPairFloat4; i += kSpecBlock)
@@ -2922,19 +2927,30 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams 
     }
     if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);   // these chains are the launch's longest
 
-    const uint32_t g = threadIdx.x / kSpecLanes, l = threadIdx.x % kSpecLanes;
-    const uint32_t q = blockIdx.x * kSpecPix + g;
-    const bool valid = q < s.n, walker = valid && l == 0u;
+    // the block's pixels: a plan's block (s.blocks: first position in s.order, count, 8 << lsh lanes per
+    // pixel) or the next 16 sphere pixels, 16 lanes each
+    uint32_t first = bid * kSpecPix, cnt = min(kSpecPix, s.n - min(s.n, bid * kSpecPix)), lsh = 1;
+    if (s.blocks) {
+        first = s.blocks[2 * bid];
+        const uint32_t w = s.blocks[2 * bid + 1];
+        cnt = w & 0xffu;
+        lsh = w >> 8;
+    }
+    const uint32_t L = 8u << lsh;                         // lanes per pixel: 8, 16, 32 or 64
+    const uint32_t batch = min(64u, 16u << lsh);          // walk: chain samples per pixel and batch
+    const uint32_t g = threadIdx.x >> (3u + lsh), l = threadIdx.x & (L - 1u);
+    const bool valid = g < cnt, walker = valid && l == 0u;
+    const uint32_t q = valid ? (s.order ? s.order[first + g] : first + g) : 0u;
     const uint32_t pix = valid ? s.pix[q] : 0u;
     uint8_t* ln = lds_n + (size_t)g * s.m_cap;
-    uint32_t* lst = lds_st + (size_t)g * kSpecLanes * 5u;
+    uint32_t* lst = lds_st + (size_t)g * L * 5u;
     uint32_t* rd = lds_rd + g * 16u;
     uint32_t col = 0, row = 0;
     tile_decode(pix, p.ncols, p.nrows, &col, &row);
     const uint32_t px = p.x0 + col, py = p.y0 + row * p.ystep;
-    {
+    if (l == 0u) {
         const uint32_t t = (row / kCullTile) * p.ntx + col / kCullTile;
-        lds_cm[threadIdx.x] = make_uint4(p.cull[(size_t)t * p.cull_stride], p.cull[(size_t)t * p.cull_stride + p.cull_wt], t, 0u);
+        lds_cm[g] = make_uint4(p.cull[(size_t)t * p.cull_stride], p.cull[(size_t)t * p.cull_stride + p.cull_wt], t, 0u);
     }
     if (walker) {
         // round 0: the launch's first slot, the window from the pixel's last chain, its state
@@ -2960,6 +2976,10 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams 
         rd[7] = 1u;
     }
     float4* res = reinterpret_cast<float4*>(s.res) + (size_t)q * s.m_cap;
+    const bool rec = s.tl != nullptr && threadIdx.x == 0;   // measurement only
+    uint64_t t_rec[3] = {rec ? __builtin_amdgcn_s_memrealtime() : 0ull, 0ull, 0ull};
+    uint32_t rounds = 0;
+    uint32_t lane_rays = 0;                                  // rays of the chain samples this lane gathered
     __syncthreads();
 
     // Rounds: round 0 is the window; a chain that leaves it continues in a new window from its end
@@ -2968,7 +2988,7 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams 
         const bool live = rd[7] == 0u;
         const uint32_t js = rd[0], M = rd[1];
         // ---- slots [js + j0, js + j1) of this lane, relative slot indices j
-        const uint32_t j0 = M * l / kSpecLanes, j1 = M * (l + 1u) / kSpecLanes;
+        const uint32_t j0 = M * l / L, j1 = M * (l + 1u) / L;
         rng6 st = {rd[2], rd[3], rd[4], rd[5], rd[6], p.rng[5 * (size_t)p.npix + rd[13]] + 2u * (js + j0) * IQ_XORWOW_WEYL};
         xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, live ? 2u * j0 : 0u);
         lst[l * 5u] = st.v0;
@@ -2995,8 +3015,8 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams 
             uint32_t hidx = 0;
             {
                 const bool cull = !__any(active && depth != 0);
-                const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
-                uint4 cm = lds_cm[threadIdx.x];
+                const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[g].z * p.cull_stride : nullptr;
+                uint4 cm = lds_cm[g];
                 const uint64_t act = __ballot(active);
                 const uint32_t first = (uint32_t)__builtin_ctzll(act);
                 const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
@@ -3067,42 +3087,47 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams 
         // ---- walk: the colours are this block's own stores (complete: vmcnt 0), read back from L2
         __builtin_amdgcn_s_waitcnt(0);
         __syncthreads();
+        if (rec && rounds == 0u) t_rec[1] = __builtin_amdgcn_s_memrealtime();
         uint32_t jw = 0;                                 // walker: the chain's next relative slot
-        uint16_t* lp = lds_pos + g * 64u;
+        uint16_t* lp = lds_pos + g * batch;
         float ax = __uint_as_float(rd[8]), ay = __uint_as_float(rd[9]), az = __uint_as_float(rd[10]);
-        uint32_t k = rd[11], rays = rd[12];
-        for (uint32_t r0 = 0; r0 < p.spp; r0 += 64u) {
+        uint32_t k = rd[11];
+        for (uint32_t r0 = 0; r0 < p.spp; r0 += batch) {
             if (walker && live) {
                 uint32_t c = 0;
-                while (c < 64u && k + c < p.spp && jw < M) {
+                while (c < batch && k + c < p.spp && jw < M) {
                     lp[c++] = (uint16_t)jw;
                     jw += ln[jw];
                 }
                 lds_w[2 * g] = c;
             }
             __syncthreads();
-            const uint32_t cnt = (valid && live) ? lds_w[2 * g] : 0u;
-            for (uint32_t i = l; i < cnt; i += kSpecLanes) {
+            const uint32_t cw = (valid && live) ? lds_w[2 * g] : 0u;
+            // the pixel's lanes gather the chain samples' colours and form their mean terms c / n and
+            // (n - 1) / n (sample k of the launch), and count their rays: the walker is left the
+            // multiply-add chain of the running mean alone
+            for (uint32_t i = l; i < cw; i += L) {
                 const uint32_t* src = reinterpret_cast<const uint32_t*>(res + lp[i]);
-                lds_c[g * 64u + i] = make_float4(
-                    __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                    __uint_as_float(__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)),
-                    __uint_as_float(__hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)), 0.0f);
+                const float cx = __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                const float cy = __uint_as_float(__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                const float cz = __uint_as_float(__hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                const float2 tv = tab[k + i];
+                float qx, qy, qz;
+                mean_terms<OPT>(cx, cy, cz, tab_n[k + i], tv.x, p.mean_tiny, qx, qy, qz);
+                lds_c[g * batch + i] = make_float4(qx, qy, qz, tv.y);
+                const uint32_t n = ln[lp[i]];
+                lane_rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
             }
             __syncthreads();
             if (walker && live)
-                for (uint32_t i = 0; i < cnt; ++i) {
-                    const float4 c = lds_c[g * 64u + i];
-                    const float2 tv = tab[k];
-                    float qx, qy, qz;
-                    mean_terms<OPT>(c.x, c.y, c.z, tab_n[k], tv.x, p.mean_tiny, qx, qy, qz);
-                    ax = qx + ax * tv.y;
-                    ay = qy + ay * tv.y;
-                    az = qz + az * tv.y;
-                    const uint32_t n = ln[lp[i]];
-                    rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
-                    ++k;
+#pragma unroll 4
+                for (uint32_t i = 0; i < cw; ++i) {
+                    const float4 v = lds_c[g * batch + i];
+                    ax = v.x + ax * v.w;
+                    ay = v.y + ay * v.w;
+                    az = v.z + az * v.w;
                 }
+            k += cw;
             __syncthreads();
         }
         if (walker && live) {
@@ -3110,12 +3135,11 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams 
             rd[9] = __float_as_uint(ay);
             rd[10] = __float_as_uint(az);
             rd[11] = k;
-            rd[12] = rays;
             const uint32_t pix = rd[13];
             // the state at the chain's end, slot js + jw: from the start of the last range at or below it
-            uint32_t kk = kSpecLanes - 1u;
-            while (kk > 0u && M * kk / kSpecLanes > jw) --kk;
-            const uint32_t jk = M * kk / kSpecLanes;
+            uint32_t kk = L - 1u;
+            while (kk > 0u && M * kk / L > jw) --kk;
+            const uint32_t jk = M * kk / L;
             uint32_t v0 = lst[kk * 5u], v1 = lst[kk * 5u + 1u], v2 = lst[kk * 5u + 2u], v3 = lst[kk * 5u + 3u],
                      v4 = lst[kk * 5u + 4u];
             xorwow_skip_v(v0, v1, v2, v3, v4, 2u * (jw - jk));
@@ -3147,11 +3171,52 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams 
                 rd[1] = min(s.m_cap, max(16u, 3u * rem + 4u));
             }
         }
+        if (rec && rounds == 0u) t_rec[2] = __builtin_amdgcn_s_memrealtime();
+        ++rounds;
     }
-    unsigned long long rays = (l == 0u) ? rd[12] : 0u;
+    if (rec) {
+        unsigned long long* o = s.tl + 4 * (size_t)bid;
+        o[0] = t_rec[0];
+        o[1] = t_rec[1];
+        o[2] = t_rec[2];
+        o[3] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) | ((unsigned long long)rounds << 48);
+    }
+    unsigned long long rays = lane_rays;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
     if (__lane_id() == 0 && rays) add_rays(p.rays, rays);
+}
+
+template <int OPT>
+__global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p) {
+    fan_body<OPT>(p, blockIdx.x);
+}
+
+template <int MAXD, int OPT>
+__global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams p, const kspec s) {
+    spec_body<MAXD, OPT>(p, s, blockIdx.x);
+}
+
+// Spec and fan blocks in one launch: the sphere pixels' blocks and the fan tiles share
+// one grid, so the launch needs no second stream and no cross-queue join (two event hops per launch).
+// The first s.lead blocks are spec blocks (the longest chains start first); the other spec blocks are
+// spread evenly among the fan blocks: of the positions b' = b - lead, a(b') = floor((b' + 1) R / (R + F))
+// of the first b' + 1 are spec blocks (R = spec blocks left, F = fan tiles).
+template <int MAXD, int OPT>
+__global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specfan_kernel(const kparams p, const kspec s) {
+    const uint32_t ns = s.blocks ? s.nblocks : (s.n + kSpecPix - 1u) / kSpecPix;
+    const uint32_t lead = min(s.lead, ns);
+    const uint32_t b = blockIdx.x;
+    if (b < lead) {
+        spec_body<MAXD, OPT>(p, s, b);
+        return;
+    }
+    const uint64_t r = ns - lead, tot = r + s.fan_tiles, bp = b - lead;
+    const uint32_t a1 = (uint32_t)(((bp + 1u) * r) / tot), a0 = (uint32_t)((bp * r) / tot);
+    if (a1 > a0)
+        spec_body<MAXD, OPT>(p, s, lead + a0);
+    else
+        fan_body<OPT>(p, (uint32_t)(bp - a1));
 }
 
 // LDS bytes of the chain kernel for a launch (scene pairs, mean table, mask slots, ring, group words,
@@ -3417,15 +3482,28 @@ int launch_fan(void* stream, const kparams& p, uint32_t ntiles, int opt) {
 namespace {
 template <int MAXD, int OPT>
 int spec_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_spec_kernel<MAXD, OPT>), dim3((s.n + kSpecPix - 1u) / kSpecPix), dim3(kSpecBlock), lds,
-                       stream, p, s);
+    hipLaunchKernelGGL((iqpt_spec_kernel<MAXD, OPT>), dim3(s.blocks ? s.nblocks : (s.n + kSpecPix - 1u) / kSpecPix),
+                       dim3(kSpecBlock), lds, stream, p, s);
     return (int)hipGetLastError();
+}
+template <int MAXD, int OPT>
+int specfan_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t lds) {
+    hipLaunchKernelGGL((iqpt_specfan_kernel<MAXD, OPT>),
+                       dim3((s.blocks ? s.nblocks : (s.n + kSpecPix - 1u) / kSpecPix) + s.fan_tiles),
+                       dim3(kSpecBlock), lds, stream, p, s);
+    return (int)hipGetLastError();
+}
+template <int MAXD, int OPT>
+int spec_occ_t(uint32_t lds, int* blocks) {
+    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_spec_kernel<MAXD, OPT>, kSpecBlock, lds);
 }
 struct spec_variant {
     int maxd, opt;
     int (*launch)(hipStream_t, const kparams&, const kspec&, uint32_t);
+    int (*launch_fused)(hipStream_t, const kparams&, const kspec&, uint32_t);
+    int (*occ)(uint32_t, int*);
 };
-#define IQPT_SV(M, O) {M, O, spec_launch_t<M, O>}
+#define IQPT_SV(M, O) {M, O, spec_launch_t<M, O>, specfan_launch_t<M, O>, spec_occ_t<M, O>}
 #define IQPT_SV2(O) IQPT_SV(8, O), IQPT_SV(16, O)
 const spec_variant kSpecVariants[] = {
     IQPT_SV2(kOptDefault | kOptPrio),
@@ -3454,6 +3532,22 @@ int launch_spec(void* stream, const kparams& p, const kspec& s, int opt) {
         return (int)hipErrorInvalidDeviceFunction;
     if (s.n == 0) return 0;
     return v->launch((hipStream_t)stream, p, s, spec_lds(p, s));
+}
+
+int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks) {
+    const spec_variant* v = find_spec(p.max_depth, opt);
+    if (!v) return (int)hipErrorInvalidDeviceFunction;
+    return v->occ(spec_lds(p, s), blocks);
+}
+
+int launch_specfan(void* stream, const kparams& p, const kspec& s, int opt) {
+    const spec_variant* v = find_spec(p.max_depth, opt);
+    if (!v || !find_fan(opt) || p.max_depth > 16 || p.cull == nullptr || p.cull_wt > 16u || p.spp > kAccTableMax ||
+        s.m_cap > 65535u || (s.fan_tiles > 0 && p.tile_order == nullptr))
+        return (int)hipErrorInvalidDeviceFunction;
+    if (p.spp == 0 || (s.n == 0 && s.fan_tiles == 0)) return 0;
+    const uint32_t ls = spec_lds(p, s), lf = fan_lds(p);
+    return v->launch_fused((hipStream_t)stream, p, s, ls > lf ? ls : lf);
 }
 
 bool chain_variant_exists(int max_depth, int opt, uint32_t lanes) {

@@ -135,7 +135,8 @@ struct iqpt_ctx {
     bool cull_valid = false;
     uint32_t cull_ntx = 0, cull_nty = 0, cull_wt = 0, cull_stride = 0;
     // timing
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> timed;
+    struct timed_launch { hipEvent_t e0, e1, e1b; };   // e1b: the second stream's end (pipelined spec), or null
+    std::vector<timed_launch> timed;
     std::vector<hipEvent_t> event_pool;
     // camera rays of a streamed scene with a BVH: tile masks or the BVH (kOptBvhPrimary), whichever
     // the first two launches after a packet upload time faster per sample (results are identical);
@@ -186,6 +187,38 @@ struct iqpt_ctx {
     bool spec_last = false;
     uint32_t spec_rho0 = iqpt::kSpecRho0;   // window of a pixel without history (iqpt_debug_set_spec)
     uint32_t spec_margin_div = 4;           // window margin: a quarter of the extra slots (iqpt_debug_set_spec)
+    // spec launches (iqpt_debug_set_specfan): 0 the two kernels on two streams, pipelined (the default), 1 one
+    // after the other on one stream (measurement), 2 spec + fan blocks in one grid (iqpt_specfan_kernel)
+    int specfan_mode = 0;
+    uint32_t spec_lead = 0xffffffffu;       // fused: spec blocks ahead of every fan block (all by default)
+    // spec plan: the sphere pixels ordered by their last chain's work, heaviest first, the
+    // heavy ones with 32 or 64 lanes; built on the host from an asynchronous read of the history (performance
+    // only: every plan gives the same bits). iqpt_debug_spec_plan: 0 off, 1 asynchronous (default), 2..5
+    // synchronous before every launch (tests; 3, 4: every pixel 32 / 64 lanes, 5: mixed)
+    int spec_plan_mode = 1;
+    uint32_t* h_spec_rho = nullptr;      // pinned: the history read back (spec_n)
+    uint32_t* h_spec_plan = nullptr;     // pinned: staging of the plan (3 spec_n)
+    hipEvent_t ev_spec_rho = nullptr, ev_spec_plan = nullptr;
+    bool spec_rho_pending = false;       // a history read in flight
+    bool spec_plan_up = false;           // a plan upload was enqueued (ev_spec_plan)
+    uint32_t* d_spec_plan = nullptr;     // order (spec_n words), then 2 words per block
+    uint32_t spec_plan_n = 0;            // pixels of the plan (0: none; must equal n_chain_pix to be used)
+    uint32_t spec_plan_blocks = 0;
+    uint32_t spec_plan_age = 0;          // launches since the plan was built
+    // Pipelined spec launches: the spec kernel on `stream`, the fan kernel on `stream2`, and
+    // no join at the end of a launch — launch k + 1's spec pixels follow launch k's on `stream`, its fan
+    // pixels launch k's on `stream2` (the two sets are disjoint), so the fan stream runs ahead into the spec
+    // kernel's tail. Every other entry point joins (join_streams). Frame copies (iqpt_copy_frame_device_async)
+    // go on `stream3` behind both kernels; from the first such copy on, launches write the two frame buffers
+    // in turn and a launch waits only for the copy that read its buffer two launches earlier.
+    bool spec_pipe = false;              // the last launch was pipelined and nothing has joined since
+    hipStream_t stream3 = nullptr;
+    hipEvent_t ev_spec_end = nullptr;    // on `stream`, after the last pipelined spec kernel
+    hipEvent_t ev_copy_cur = nullptr, ev_copy_alt = nullptr;   // on `stream3`, after the copy of d_bgra / d_bgra_alt
+    bool copy_pend_cur = false, copy_pend_alt = false;
+    unsigned long long* d_spec_tl = nullptr;   // iqpt_debug_spec_timeline: per spec block timestamps
+    size_t spec_tl_blocks = 0;
+    bool spec_tl_on = false;
     uint32_t chain_par = 0;             // the queue-counter set of the next chain launch
     bool chain_q_ready[2] = {false, false};   // that set is zeroed (in stream order)
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
@@ -238,6 +271,11 @@ int join_streams(iqpt_ctx* c) {
         IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
         c->s2_pending = false;
     }
+    // pipelined spec launches: `stream` also waits for the frame copies still reading a frame buffer
+    if (c->copy_pend_cur) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
+    if (c->copy_pend_alt) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_alt, 0));
+    c->copy_pend_cur = c->copy_pend_alt = false;
+    c->spec_pipe = false;
     c->next_on_main = true;
     c->ovl_zero = true;
     c->last_ovl = false;
@@ -290,7 +328,9 @@ void free_split(iqpt_ctx* c) {
     if (c->d_fan_lanes) (void)hipFree(c->d_fan_lanes);
     c->d_fan_lanes = nullptr;
     c->n_chain_pix = c->n_fan_tiles = 0;
-    c->spec_rho_valid = false;           // a new pixel list: no chain history
+    c->spec_rho_valid = false;           // a new pixel list: no chain history, no plan
+    c->spec_plan_n = 0;
+    c->spec_rho_pending = false;
     c->n_split_tiles = c->n_anchor = 0;
     c->res_slots = 0;
 }
@@ -356,6 +396,88 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
     c->n_chain_pix = (uint32_t)chain_pix.size();
     c->n_fan_tiles = (uint32_t)fan_tiles.size();
     return IQPT_OK;
+}
+
+// The spec plan from the history rho (n sphere pixels) into h: the order (n words: pixel q
+// at each position), then 2 words per block (first position, count | log2(lanes / 8) << 8); returns the
+// block count. Work of pixel q: the slots of its window (spec_window of its last chain's slots per sample)
+// times their mean length (those slots per sample again). Lanes per pixel (8, 16, 32 or 64) come from one
+// per-lane work target E, the smallest whose lanes all fit the resident blocks (one block-wave; if even 8
+// lanes each do not fit, E = total work / resident lanes): pixel q takes the fewest lanes with w_q / lanes
+// <= E. Each block holds one lane class (256 lanes), pixels sorted by work per lane, and the blocks run
+// heaviest per lane first, so the launch's longest block starts first and light blocks fill the tail.
+uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec& ks, int opt, const uint32_t* rho,
+                         uint32_t* h) {
+    const uint32_t n = ks.n;
+    std::vector<double> w(n);
+    double total = 0.0, wmax = 0.0;
+    for (uint32_t q = 0; q < n; ++q) {
+        const uint32_t r = rho[q] ? rho[q] : ks.rho0;
+        const uint32_t m = iqpt::spec_window(r, p.spp, ks.m_cap, ks.margin_div);
+        w[q] = (double)m * (double)std::max<uint32_t>(r, 256u) / 256.0;
+        total += w[q];
+        wmax = std::max(wmax, w[q]);
+    }
+    int occ = 0;
+    if (iqpt::spec_occupancy(p, ks, opt, &occ) != 0 || occ < 1) occ = 1;
+    const double cap = 0.97 * (double)c->num_cus * occ * 256.0;     // resident lanes, a little slack
+    auto lsh_of = [&](uint32_t q, double e) -> uint8_t {
+        uint8_t k = 0;
+        while (k < 3 && w[q] > e * (double)(8u << k)) ++k;
+        return k;
+    };
+    auto lanes_at = [&](double e) {
+        double sum = 0.0;
+        for (uint32_t q = 0; q < n; ++q) sum += (double)(8u << lsh_of(q, e));
+        return sum;
+    };
+    double e = total / cap;                      // several block-waves: balanced work per lane
+    if (lanes_at(wmax / 8.0) <= cap) {
+        double lo = 0.0, hi = wmax / 8.0;        // lanes_at(hi) fits; find the smallest E that fits
+        for (int it = 0; it < 40; ++it) {
+            const double mid = 0.5 * (lo + hi);
+            if (lanes_at(mid) <= cap) hi = mid;
+            else lo = mid;
+        }
+        e = hi;
+    }
+    std::vector<uint8_t> lsh(n);
+    double emax = 0.0;
+    for (uint32_t q = 0; q < n; ++q) {
+        uint8_t k = lsh_of(q, e);
+        if (c->spec_plan_mode == 3) k = 2;
+        if (c->spec_plan_mode == 4) k = 3;
+        if (c->spec_plan_mode == 5) k = (uint8_t)(q % 4u);
+        lsh[q] = k;
+        emax = std::max(emax, w[q] / (double)(8u << k));
+    }
+    // counting sort by (lane class, work per lane) descending
+    constexpr uint32_t kB = 1024;
+    std::vector<uint32_t> key(n), cnt(4 * kB + 1, 0);
+    for (uint32_t q = 0; q < n; ++q) {
+        const double pe = w[q] / (double)(8u << lsh[q]);
+        const uint32_t b = emax > 0.0 ? std::min<uint32_t>(kB - 1, (uint32_t)(pe / emax * (kB - 1))) : 0u;
+        key[q] = (3u - lsh[q]) * kB + (kB - 1 - b);       // ascending key: 64 lanes first, heaviest first
+        cnt[key[q] + 1]++;
+    }
+    for (uint32_t k = 0; k < 4 * kB; ++k) cnt[k + 1] += cnt[k];
+    for (uint32_t q = 0; q < n; ++q) h[cnt[key[q]]++] = q;
+    // blocks of one class, then ordered by their first (heaviest) pixel's work per lane
+    struct blk { double e; uint32_t first, word; };
+    std::vector<blk> blocks;
+    for (uint32_t i = 0; i < n;) {
+        const uint32_t k = lsh[h[i]], per = iqpt::kSpecMaxPixPerBlock >> k;
+        uint32_t m = 0;
+        while (m < per && i + m < n && lsh[h[i + m]] == k) ++m;
+        blocks.push_back({w[h[i]] / (double)(8u << k), i, m | (k << 8)});
+        i += m;
+    }
+    std::stable_sort(blocks.begin(), blocks.end(), [](const blk& a, const blk& b) { return a.e > b.e; });
+    for (size_t b = 0; b < blocks.size(); ++b) {
+        h[n + 2 * b] = blocks[b].first;
+        h[n + 2 * b + 1] = blocks[b].word;
+    }
+    return (uint32_t)blocks.size();
 }
 
 // The split set of kOptSplit: the tiles whose camera rays may scatter — a sphere
@@ -941,17 +1063,23 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
     if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
+    if (c->stream3) (void)hipStreamDestroy(c->stream3);
+    for (hipEvent_t e : {c->ev_spec_end, c->ev_copy_cur, c->ev_copy_alt})
+        if (e) (void)hipEventDestroy(e);
     free_split(c);
-    for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res})
+    for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_tl, (void*)c->d_spec_plan})
         if (b) (void)hipFree(b);
+    for (void* b : {(void*)c->h_spec_rho, (void*)c->h_spec_plan})
+        if (b) (void)hipHostFree(b);
+    for (hipEvent_t e : {c->ev_spec_rho, c->ev_spec_plan})
+        if (e) (void)hipEventDestroy(e);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
     if (c->d_tile_order) (void)hipFree(c->d_tile_order);
     if (c->d_list) (void)hipFree(c->d_list);
-    for (auto& pr : c->timed) {
-        (void)hipEventDestroy(pr.first);
-        (void)hipEventDestroy(pr.second);
-    }
+    for (auto& tl : c->timed)
+        for (hipEvent_t ev : {tl.e0, tl.e1, tl.e1b})
+            if (ev) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : c->event_pool) (void)hipEventDestroy(ev);
     for (hipEvent_t ev : c->tune_ev)
         if (ev) (void)hipEventDestroy(ev);
@@ -1376,7 +1504,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const double lanes = (double)c->num_cus * std::max(occ_s, 1) * iqpt::kRenderBlock;
         split = occ_s > 0 && (c->split_mode == IQPT_SPLIT_ON || (double)c->npix < iqpt::kSplitAutoPixelsPerLane * lanes);
     }
-    if ((split || chain || fan || spec) && (st = join_streams(c)) != IQPT_OK) return st;   // these never overlap
+    // pipelined spec launches continue without a join (the launch below orders itself); the others never overlap
+    const bool spec_pipe_next = spec && c->specfan_mode == 0 && c->spec_pipe;
+    if ((split || chain || fan || spec) && !spec_pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
     // split launches with the anchored tiles in the fan kernel beside the four split passes
     const bool fan_split = split && fan_ok && c->fan_anchored;
     const size_t ns_cap = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
@@ -1492,7 +1622,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             c->overlap_mode = IQPT_OVERLAP_OFF;
         }
     }
-    if (!ovl && (st = join_streams(c)) != IQPT_OK) return st;
+    if (!ovl && !spec_pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
     hipStream_t ls = c->stream;                       // the launch's stream
     if (ovl) {
         opt |= iqpt::kOptOverlap;
@@ -1536,7 +1666,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
     if (!ovl && !chain && !fan && !spec) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
-    hipEvent_t e0 = take_event(c), e1 = take_event(c);
+    hipEvent_t e0 = take_event(c), e1 = take_event(c), e1b = nullptr;
     if (e0) (void)hipEventRecord(e0, ls);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
     int le = 0;
@@ -1614,18 +1744,31 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
         if (n > 0 && (n > c->spec_n || m_cap > c->spec_mcap)) {
             IQPT_HIP(hipStreamSynchronize(c->stream));
-            for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res})
+            for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_plan})
                 if (b) (void)hipFree(b);
+            for (void* b : {(void*)c->h_spec_rho, (void*)c->h_spec_plan})
+                if (b) (void)hipHostFree(b);
             c->d_spec = nullptr;
             c->d_spec_res = nullptr;
+            c->d_spec_plan = nullptr;
+            c->h_spec_rho = c->h_spec_plan = nullptr;
             c->spec_n = c->spec_mcap = 0;
+            c->spec_plan_n = 0;
+            c->spec_rho_pending = c->spec_plan_up = false;
             const size_t slots = (size_t)n * m_cap;
-            if (slots * 16 > iqpt::kSplitResBudget ||
+            if ((!c->ev_spec_rho && hipEventCreateWithFlags(&c->ev_spec_rho, hipEventDisableTiming) != hipSuccess) ||
+                (!c->ev_spec_plan && hipEventCreateWithFlags(&c->ev_spec_plan, hipEventDisableTiming) != hipSuccess) ||
+                slots * 16 > iqpt::kSplitResBudget ||
                 hipMalloc(&c->d_spec, (2 * (size_t)n + 2) * sizeof(uint32_t)) != hipSuccess ||
-                hipMalloc(&c->d_spec_res, slots * sizeof(float4_storage)) != hipSuccess) {
+                hipMalloc(&c->d_spec_res, slots * sizeof(float4_storage)) != hipSuccess ||
+                hipMalloc(&c->d_spec_plan, 3 * (size_t)n * sizeof(uint32_t)) != hipSuccess ||
+                hipHostMalloc(&c->h_spec_rho, (size_t)n * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc(&c->h_spec_plan, 3 * (size_t)n * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
                 (void)hipGetLastError();
                 return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec buffers");
             }
+            // the statistics counters run from here (iqpt_debug_spec_info reads and clears them)
+            IQPT_HIP(hipMemsetAsync(c->d_spec + 2 * (size_t)n, 0, 2 * sizeof(uint32_t), c->stream));
             c->spec_n = n;
             c->spec_mcap = m_cap;
             c->spec_rho_valid = false;
@@ -1639,22 +1782,104 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.rho = c->d_spec + n;
         ks2.run_count = c->d_spec + 2 * (size_t)n;
         ks2.res = c->d_spec_res;
-        IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
-        IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
-        if (n > 0) {
-            if (!c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, (size_t)n * sizeof(uint32_t), c->stream));
-            c->spec_rho_valid = true;
-            IQPT_HIP(hipMemsetAsync(ks2.run_count, 0, 2 * sizeof(uint32_t), c->stream));
-            le = iqpt::launch_spec(c->stream, p, ks2, opt);
+        if (n > 0 && !c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, (size_t)n * sizeof(uint32_t), c->stream));
+        c->spec_rho_valid = c->spec_rho_valid || n > 0;
+        if (c->specfan_mode == 0) {
+            // pipelined: the frame buffer this launch writes (the other one once copies are asynchronous),
+            // after the copy that read it two launches ago; the fan stream after everything `stream` held
+            // unless it continues a pipeline
+            if (c->d_bgra_alt) {
+                std::swap(c->d_bgra, c->d_bgra_alt);
+                std::swap(c->ev_copy_cur, c->ev_copy_alt);
+                std::swap(c->copy_pend_cur, c->copy_pend_alt);
+                p.bgra = c->d_bgra;
+            }
+            if (c->copy_pend_cur) {
+                IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
+                IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_copy_cur, 0));
+                c->copy_pend_cur = false;
+            }
+            if (!c->spec_pipe) {
+                IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
+                IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
+            }
         }
-        if (le == 0 && c->n_fan_tiles > 0) {
-            iqpt::kparams pf = p;
-            pf.tile_order = c->d_fan_tiles;
-            pf.fan_lanes = c->d_fan_lanes;
-            le = iqpt::launch_fan(c->stream2, pf, c->n_fan_tiles, opt);
+        iqpt::kparams pf = p;
+        pf.tile_order = c->d_fan_tiles;
+        pf.fan_lanes = c->d_fan_lanes;
+        // the plan: built from the history read after an earlier launch (asynchronous), or, for tests,
+        // synchronously from the current history
+        if (n > 0 && c->spec_plan_mode >= 2) {
+            IQPT_HIP(hipStreamSynchronize(c->stream));
+            IQPT_HIP(hipMemcpy(c->h_spec_rho, ks2.rho, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            const uint32_t nb = spec_build_plan(c, p, ks2, opt, c->h_spec_rho, c->h_spec_plan);
+            IQPT_HIP(hipMemcpy(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
+                               hipMemcpyHostToDevice));
+            c->spec_plan_n = n;
+            c->spec_plan_blocks = nb;
+        } else if (n > 0 && c->spec_plan_mode == 1 && c->spec_rho_pending &&
+                   hipEventQuery(c->ev_spec_rho) == hipSuccess &&
+                   (!c->spec_plan_up || hipEventQuery(c->ev_spec_plan) == hipSuccess)) {
+            const uint32_t nb = spec_build_plan(c, p, ks2, opt, c->h_spec_rho, c->h_spec_plan);
+            IQPT_HIP(hipMemcpyAsync(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
+                                    hipMemcpyHostToDevice, c->stream));
+            IQPT_HIP(hipEventRecord(c->ev_spec_plan, c->stream));
+            c->spec_plan_up = true;
+            c->spec_rho_pending = false;
+            c->spec_plan_n = n;
+            c->spec_plan_blocks = nb;
+            c->spec_plan_age = 0;
         }
-        IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
-        IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
+        if (n > 0 && c->spec_plan_mode >= 1 && c->spec_plan_n == n) {
+            ks2.order = c->d_spec_plan;
+            ks2.blocks = c->d_spec_plan + n;
+            ks2.nblocks = c->spec_plan_blocks;
+        }
+        if (c->spec_tl_on && n > 0) {
+            const size_t nb = ks2.blocks ? ks2.nblocks : (n + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
+            if (nb > c->spec_tl_blocks) {
+                IQPT_HIP(hipStreamSynchronize(c->stream));
+                if (c->d_spec_tl) (void)hipFree(c->d_spec_tl);
+                c->d_spec_tl = nullptr;
+                c->spec_tl_blocks = 0;
+                if (hipMalloc(&c->d_spec_tl, nb * 4 * sizeof(unsigned long long)) != hipSuccess) {
+                    (void)hipGetLastError();
+                    return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec timeline");
+                }
+                c->spec_tl_blocks = nb;
+            }
+            IQPT_HIP(hipMemsetAsync(c->d_spec_tl, 0, nb * 4 * sizeof(unsigned long long), c->stream));
+            ks2.tl = c->d_spec_tl;
+        }
+        if (c->specfan_mode == 2) {
+            // one grid: no second stream, no join
+            ks2.fan_tiles = c->n_fan_tiles;
+            ks2.lead = c->spec_lead;
+            le = iqpt::launch_specfan(c->stream, pf, ks2, opt);
+        } else if (c->specfan_mode == 1) {
+            if (n > 0) le = iqpt::launch_spec(c->stream, p, ks2, opt);
+            if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream, pf, c->n_fan_tiles, opt);
+        } else {
+            if (n > 0) le = iqpt::launch_spec(c->stream, p, ks2, opt);
+            if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream2, pf, c->n_fan_tiles, opt);
+            IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
+            if (!c->ev_spec_end && hipEventCreateWithFlags(&c->ev_spec_end, hipEventDisableTiming) != hipSuccess) {
+                (void)hipGetLastError();
+                return iqpt::fail(IQPT_ERR_HIP, "pipelined spec events");
+            }
+            IQPT_HIP(hipEventRecord(c->ev_spec_end, c->stream));
+            e1b = take_event(c);
+            if (e1b) (void)hipEventRecord(e1b, c->stream2);
+            c->s2_pending = true;
+            c->spec_pipe = le == 0;
+        }
+        // read this launch's history for the next plan: before the first plan, then every kSpecReplan launches
+        if (n > 0 && c->spec_plan_mode == 1 && !c->spec_rho_pending && le == 0 &&
+            (c->spec_plan_n != n || ++c->spec_plan_age >= iqpt::kSpecReplan)) {
+            IQPT_HIP(hipMemcpyAsync(c->h_spec_rho, ks2.rho, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
+            IQPT_HIP(hipEventRecord(c->ev_spec_rho, c->stream));
+            c->spec_rho_pending = true;
+        }
     } else if (split) {
         // prep -> round 1 (runs, anchored tiles, light split pixels) -> stitch -> round 2 (leftovers); with
         // the fan kernel the anchored tiles leave round 1 for iqpt_fan_kernel on stream2
@@ -1689,7 +1914,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     c->last_ovl = ovl;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1) (void)hipEventRecord(e1, ls);
-    if (e0 && e1) c->timed.emplace_back(e0, e1);
+    if (e0 && e1) c->timed.push_back({e0, e1, e1b});
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "render kernel launch");
     c->last_opt = opt;
     if (tune_slot >= 0) {
@@ -1918,15 +2143,23 @@ int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     double sum = 0.0, span = 0.0;
-    for (auto& pr : c->timed) {
+    for (auto& tl : c->timed) {
         float ms = 0.0f, end = 0.0f;
-        IQPT_HIP(hipEventElapsedTime(&ms, pr.first, pr.second));
+        IQPT_HIP(hipEventElapsedTime(&ms, tl.e0, tl.e1));
         // span: from the first launch's start to the latest end (launches on two streams overlap)
-        IQPT_HIP(hipEventElapsedTime(&end, c->timed.front().first, pr.second));
+        IQPT_HIP(hipEventElapsedTime(&end, c->timed.front().e0, tl.e1));
+        if (tl.e1b) {
+            float ms2 = 0.0f, end2 = 0.0f;
+            IQPT_HIP(hipEventElapsedTime(&ms2, tl.e0, tl.e1b));
+            IQPT_HIP(hipEventElapsedTime(&end2, c->timed.front().e0, tl.e1b));
+            ms = std::max(ms, ms2);
+            end = std::max(end, end2);
+            c->event_pool.push_back(tl.e1b);
+        }
         sum += ms;
         span = std::max(span, (double)end);
-        c->event_pool.push_back(pr.first);
-        c->event_pool.push_back(pr.second);
+        c->event_pool.push_back(tl.e0);
+        c->event_pool.push_back(tl.e1);
     }
     c->last_span_ms = span;
     *total_ms = sum;
@@ -1936,8 +2169,9 @@ int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
 }
 
 /* Internal (tools): the per-pixel split of the last camera / packet — sphere pixels (the chain and spec
- * kernels' list), fan tiles, anchored tiles, split tiles — and, after a spec launch, its run count and the
- * sum of its windows. Synchronises. */
+ * kernels' list), fan tiles, anchored tiles, split tiles — and, after a spec launch, the sum of its
+ * windows and of its chains' slots per sample, and the chains finished past their window since the last
+ * call (out8[7]; the call clears it). Synchronises. */
 int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     int st = enter(c);
@@ -1952,7 +2186,7 @@ int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
         const uint32_t n = c->n_chain_pix;
         std::vector<uint32_t> v(2 * (size_t)n + 2);
         IQPT_HIP(hipMemcpy(v.data(), c->d_spec, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        out8[4] = v[2 * (size_t)n];
+        out8[4] = c->spec_plan_n == n && c->spec_plan_mode ? c->spec_plan_blocks : 0;   // plan blocks (0: none)
         out8[7] = v[2 * (size_t)n + 1];
         unsigned long long m = 0, rho = 0;
         for (uint32_t q = 0; q < n; ++q) {
@@ -1961,7 +2195,55 @@ int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
         }
         out8[5] = m;
         out8[6] = rho;
+        IQPT_HIP(hipMemset(c->d_spec + 2 * (size_t)n, 0, 2 * sizeof(uint32_t)));
     }
+    return IQPT_OK;
+}
+
+/* Internal (measurement): record per spec block s_memrealtime stamps (100 MHz) in later spec launches —
+ * start, after round 0's slots, after round 0's walk, end | rounds << 48 — and read the last launch's. */
+int iqpt_debug_spec_timeline(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->spec_tl_on = on != 0;
+    return IQPT_OK;
+}
+
+int iqpt_debug_read_spec_timeline(iqpt_ctx* c, unsigned long long* out, uint32_t cap_blocks, uint32_t* n) {
+    if (!c || !out || !n) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *n = 0;
+    int st = enter(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    if (!c->d_spec_tl || !c->spec_last) return IQPT_OK;
+    const size_t nspec = c->spec_plan_n == c->n_chain_pix && c->spec_plan_n && c->spec_plan_mode
+                             ? c->spec_plan_blocks
+                             : (c->n_chain_pix + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
+    const size_t nb = std::min<size_t>(nspec, std::min<size_t>(cap_blocks, c->spec_tl_blocks));
+    if (nb) IQPT_HIP(hipMemcpy(out, c->d_spec_tl, nb * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    *n = (uint32_t)nb;
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): the spec plan — 0 none (16 lanes per pixel, list order), 1 from an asynchronous
+ * read of the history (the default), 2 rebuilt synchronously before every launch, 3 / 4 the same with
+ * every pixel on 32 / 64 lanes, 5 the same with the lane count cycling over 8, 16, 32, 64. Drops the plan. */
+int iqpt_debug_spec_plan(iqpt_ctx* c, int mode) {
+    if (!c || mode < 0 || mode > 5) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or mode not 0..5");
+    c->spec_plan_mode = mode;
+    c->spec_plan_n = 0;
+    return IQPT_OK;
+}
+
+/* Internal (A/B): how spec launches run the fan tiles beside the sphere pixels — 0 two kernels on two
+ * streams, pipelined across launches (the default), 1 two kernels on one stream, 2 one grid
+ * (iqpt_specfan_kernel) — and, in one grid, how many spec blocks precede every fan block (0xffffffff: all;
+ * the rest are spread evenly). */
+int iqpt_debug_set_specfan(iqpt_ctx* c, int mode, uint32_t lead) {
+    if (!c || mode < 0 || mode > 2) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or mode not 0..2");
+    int st = enter(c);
+    if (st) return st;
+    c->specfan_mode = mode;
+    c->spec_lead = lead;
     return IQPT_OK;
 }
 
@@ -2017,6 +2299,29 @@ int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
     // synchronising call (iqpt_sync, iqpt_read, ...); one already latched fails the copy now
     if (c->dev_err) return check_dev_err(c);
     hipStream_t cs = c->stream;
+    if (c->spec_pipe) {
+        // pipelined spec launches: the copy on stream3 behind both kernels of the last launch; from here on
+        // the launches alternate two frame buffers
+        if (!c->d_bgra_alt && hipMalloc(&c->d_bgra_alt, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            c->d_bgra_alt = nullptr;
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "second frame buffer for pipelined copies");
+        }
+        if ((!c->stream3 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) ||
+            (!c->ev_copy_cur && hipEventCreateWithFlags(&c->ev_copy_cur, hipEventDisableTiming) != hipSuccess) ||
+            (!c->ev_copy_alt && hipEventCreateWithFlags(&c->ev_copy_alt, hipEventDisableTiming) != hipSuccess)) {
+            (void)hipGetLastError();
+            return iqpt::fail(IQPT_ERR_HIP, "frame copy stream");
+        }
+        IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_spec_end, 0));
+        IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_s2, 0));
+        const int le = iqpt::launch_relayout(c->stream3, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
+                                             c->set.nrows, 1, 1, true);
+        if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
+        IQPT_HIP(hipEventRecord(c->ev_copy_cur, c->stream3));
+        c->copy_pend_cur = true;
+        return IQPT_OK;
+    }
     if (c->last_ovl && c->last_ls) {
         // overlapped launches in flight: copy on the last launch's stream without joining, so the next
         // launch still overlaps this one (from here on overlapped launches alternate two frame buffers)
@@ -2038,7 +2343,7 @@ int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
 
 int iqpt_frame_stream(iqpt_ctx* c, void** stream) {
     if (!c || !stream) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    *stream = (void*)((c->last_ovl && c->last_ls) ? c->last_ls : c->stream);
+    *stream = (void*)(c->spec_pipe && c->stream3 ? c->stream3 : ((c->last_ovl && c->last_ls) ? c->last_ls : c->stream));
     return IQPT_OK;
 }
 

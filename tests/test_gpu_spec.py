@@ -3,8 +3,8 @@
 Only the pixels whose own camera-ray bundle may reach a sphere can take more than two draws per sample.
 Every slot of their window (the sample that starts 2j draws into the pixel's XORWOW stream) is evaluated
 in parallel, the chain 0 -> j + n_j -> ... is walked afterwards and folded in sample order, and a chain
-that leaves its window is finished sequentially by the stitch thread; every other pixel runs in the fan
-kernel. The result must be the reference's sequential chain (path_tracer.cu:330-366, random.cu:66-107):
+that leaves its window continues in a new window (another round of the same block); every other pixel
+runs in the fan kernel, in the same grid (iqpt_specfan_kernel) or beside it. The result must be the reference's sequential chain (path_tracer.cu:330-366, random.cu:66-107):
 accumulator, BGRA8, final RNG states, ray count. RMSE < 1e-5 stated.
 """
 import ctypes as C
@@ -79,7 +79,7 @@ def test_launch_sizes_spec(require_gpu, spp):
 
 def test_chains_leaving_their_window_spec(require_gpu):
     """Windows sized for one slot per sample: the sphere pixels' chains leave them in the first launch and
-    the stitch finishes them sequentially; the second launch sizes the windows from that history."""
+    further rounds finish them; the second launch sizes the windows from that history."""
     from iqpt import PathTracer, _lib, make_camera
     w, h = 320, 180
     sc, pk = scene_for("cornell")          # the scene owns the packet's arrays: keep it alive
@@ -162,4 +162,142 @@ def test_window_margins_spec(require_gpu, margin_div):
         fr.render(pk, cam, s)
     lin, bgra = pt.read()
     assert mode_of(pt) == 6
+    _check(pt, lin, bgra, fr)
+
+
+@pytest.mark.parametrize("specfan", [(0, 0), (1, 0), (2, 0), (2, 1), (2, 5), (2, 0xffffffff)])
+@pytest.mark.parametrize("rank,world", [(0, 8), (3, 4)])
+def test_specfan_layouts(require_gpu, specfan, rank, world):
+    """The fan tiles beside the sphere pixels on a second stream (0), after them on one stream (1), or in
+    one grid (2) with 0, 1, 5 or every spec block ahead of the fan blocks (the rest spread among them)."""
+    from iqpt import PathTracer, _lib, make_camera
+    w, h = 484, 270
+    n = len(range(rank, h, world))
+    ps = pixel_set(w, h, 0, w, rank, world, n)
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    pt.set_split(SPLIT_SPEC)
+    lib = _lib.load()
+    lib.iqpt_debug_set_specfan.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+    _lib.check(lib.iqpt_debug_set_specfan(pt._h, specfan[0], specfan[1]), "iqpt_debug_set_specfan")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    for s in (12, 20):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    assert mode_of(pt) == 6
+    _check(pt, lin, bgra, fr)
+
+
+@pytest.mark.parametrize("plan", [0, 2, 3, 4, 5])
+@pytest.mark.parametrize("specfan", [0, 2])
+def test_spec_plans(require_gpu, plan, specfan):
+    """Spec plans (the sphere pixels reordered by their last chain's work, 16 / 32 / 64 lanes per pixel):
+    none, rebuilt before every launch from the history, every pixel on 32 or on 64 lanes, mixed lane counts
+    in one grid. Four launches (the first without history), beside the fan tiles or in one grid."""
+    from iqpt import PathTracer, _lib, make_camera
+    w, h = 484, 270
+    n = len(range(1, h, 3))
+    ps = pixel_set(w, h, 0, w, 1, 3, n)
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    pt.set_split(SPLIT_SPEC)
+    lib = _lib.load()
+    lib.iqpt_debug_spec_plan.argtypes = [C.c_void_p, C.c_int]
+    _lib.check(lib.iqpt_debug_spec_plan(pt._h, plan), "iqpt_debug_spec_plan")
+    lib.iqpt_debug_set_specfan.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+    _lib.check(lib.iqpt_debug_set_specfan(pt._h, specfan, 0xffffffff), "iqpt_debug_set_specfan")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    for s in (10, 17, 3, 24):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    assert mode_of(pt) == 6
+    info = (C.c_ulonglong * 8)()
+    lib.iqpt_debug_spec_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    _lib.check(lib.iqpt_debug_spec_info(pt._h, info), "iqpt_debug_spec_info")
+    if plan >= 2:
+        assert info[4] > 0                   # the last launch ran a plan
+    _check(pt, lin, bgra, fr)
+
+
+def test_spec_plan_async_c3_share8(require_gpu):
+    """The default (asynchronous) plan on rank 0's N = 8 share of C3 over six launches (the history read
+    after a launch is used once it has arrived: a sync after each launch makes that the next launch) equals
+    the plain kernel bit for bit, and a plan is in use by the last launch."""
+    from iqpt import PathTracer, _lib, make_camera
+    w, h = 1920, 1080
+    n = len(range(0, h, 8))
+    ps = pixel_set(w, h, 0, w, 0, 8, n)
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    lib = _lib.load()
+    outs = []
+    for mode in (SPLIT_OFF, SPLIT_SPEC):
+        pt = PathTracer(w, h, pixels=ps, max_depth=8)
+        pt.set_split(mode)
+        pt.set_camera(cam)
+        pt.upload_packet(pk)
+        for _ in range(6):
+            pt.render(64)
+            pt.sync()
+        if mode == SPLIT_SPEC:
+            info = (C.c_ulonglong * 8)()
+            lib.iqpt_debug_spec_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+            _lib.check(lib.iqpt_debug_spec_info(pt._h, info), "iqpt_debug_spec_info")
+            assert info[4] > 0
+        lin, bgra = pt.read()
+        outs.append((lin, bgra, pt.read_rng(), pt.rays(), mode_of(pt)))
+        pt.close()
+    assert [o[4] for o in outs] == [0, 6]
+    assert np.array_equal(outs[0][0].view(np.uint32), outs[1][0].view(np.uint32))
+    assert np.array_equal(outs[0][1], outs[1][1])
+    assert np.array_equal(outs[0][2], outs[1][2])
+    assert outs[0][3] == outs[1][3]
+
+
+def test_pipelined_spec_async_copies(require_gpu):
+    """Pipelined spec launches (the fan stream runs ahead, no join per launch) with a stream-ordered frame copy
+    after every launch, as the multi-GPU gather issues them: copy k holds exactly launch k's frame (the launches
+    write two frame buffers in turn), a reset in the middle joins the streams, and the final state is the
+    oracle's bit for bit."""
+    import torch
+    from iqpt import PathTracer, _lib, make_camera
+    w, h = 484, 270
+    n = len(range(0, h, 4))
+    ps = pixel_set(w, h, 0, w, 0, 4, n)
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    pt.set_split(SPLIT_SPEC)
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    npix = w * n
+    bufs, want = [], []
+    for i, s in enumerate((6, 9, 4, 12, 7, 5)):
+        if i == 3:
+            pt.reset()
+            fr.reset()
+        pt.render(s)
+        fr.render(pk, cam, s)
+        b = torch.zeros(npix, dtype=torch.int32, device="cuda")
+        stream = torch.cuda.ExternalStream(pt.frame_stream_handle())
+        pt.copy_frame_device_async(b.data_ptr(), b.numel() * 4)
+        done = torch.cuda.Event()
+        done.record(stream)
+        torch.cuda.current_stream().wait_event(done)
+        bufs.append(b)
+        want.append(fr.bgra.copy())
+    torch.cuda.synchronize()
+    assert mode_of(pt) == 6
+    for b, wv in zip(bufs, want):
+        assert np.array_equal(b.cpu().numpy().view(np.uint8).reshape(-1, 4), wv)
+    lin, bgra = pt.read()
     _check(pt, lin, bgra, fr)

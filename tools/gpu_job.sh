@@ -1,12 +1,16 @@
-# r03 run 17: the whole -m gpu suite, smoke, then share steps through the gather path and the default bench
+# r03 run 25: pipelined spec launches (no per-launch join, async copies on a third stream)
 mkdir -p gpurun_out
-timeout -k 10 1500 python -u -m pytest tests -m gpu -x -q --timeout 700 --timeout-method thread > gpurun_out/r03_run17_tests.log 2>&1 || { tail -60 gpurun_out/r03_run17_tests.log; exit 1; }
-tail -3 gpurun_out/r03_run17_tests.log
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r03_run17_smoke.log 2>&1 || { tail -20 gpurun_out/r03_run17_smoke.log; exit 1; }
-tail -1 gpurun_out/r03_run17_smoke.log
+O=gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_spec.py tests/test_gpu_bench_multirank.py -x -q --timeout 300 --timeout-method thread > $O/r03_25_tests.log 2>&1 || { tail -40 $O/r03_25_tests.log; exit 1; }
+tail -1 $O/r03_25_tests.log
+timeout -k 10 600 python3 tools/split_share.py --ns 8,4,2 --modes spec --specfan 1,2 --launches 10 --warm 4 --out $O/r03_25_specfan.json > $O/r03_25_specfan.log 2>&1 || { tail -20 $O/r03_25_specfan.log; exit 1; }
+python3 -c "
+import json
+for r in json.load(open('$O/r03_25_specfan.json'))['rows']:
+    print(r['n'], {k: round(v, 4) for k, v in r.items() if k.endswith('ms_median')})
+"
 for s in 8 4 2; do
-  timeout -k 10 180 python -u bench.py --self-gather --share-of $s --no-cpu-baseline --steps 30 > gpurun_out/r03_run17_share$s.json 2> gpurun_out/r03_run17_share$s.err || { tail -20 gpurun_out/r03_run17_share$s.err; exit 1; }
-  tail -1 gpurun_out/r03_run17_share$s.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print($s, d['ms_per_step'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'], d['roofline']['kernel_avg_ms'])"
+  timeout -k 10 300 python3 bench.py --self-gather --share-of $s --split spec --steps 30 --warmup 8 --no-cpu-baseline --verify-rows 0 > $O/r03_25_share$s.json 2> $O/r03_25_share$s.err || { tail -20 $O/r03_25_share$s.err; exit 1; }
+  tail -1 $O/r03_25_share$s.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print($s, d['ms_per_step'], d['config']['launch_mode'], d['roofline']['kernel_avg_ms'])"
 done
-timeout -k 10 300 python -u bench.py --cpu-seconds 10 > gpurun_out/r03_run17_default.json 2> gpurun_out/r03_run17_default.err || { tail -20 gpurun_out/r03_run17_default.err; exit 1; }
-tail -1 gpurun_out/r03_run17_default.json | python -c "import json,sys; d=json.loads(sys.stdin.read()); print('default', d['value'], d['ms_per_step'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'])"
+timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $O/r03_25_trace_share8 -o run -- python3 bench.py --self-gather --share-of 8 --split spec --steps 20 --warmup 8 --no-cpu-baseline --verify-rows 0 > $O/r03_25_trace8.log 2>&1 || { tail -20 $O/r03_25_trace8.log; exit 1; }

@@ -8,7 +8,10 @@ read side is doubled; WRITE_SIZE is exact for 16-B-per-lane stores. The render k
 mostly 4-B-per-lane RNG planes + 16-B accumulators, so the x2 is an upper-bound correction; both
 the raw and corrected values are written.
 
-usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <config> <out.json> <spp_per_launch>
+usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <config> <out.json> <spp_per_launch> [last]
+
+last: average only the last `last` dispatches of each pass (the launches after the runtime's first-launch
+tuning, which alternates the masks and BVH-primary variants over its first launches on streamed scenes).
 
 bench.py uses a profile only for a run that launches the same spp (traffic per launch is matched on
 the launch shape, not the config name alone).
@@ -25,20 +28,23 @@ def per_kernel(path, counter):
         for row in csv.DictReader(f):
             if row.get("Counter_Name") == counter and "iqpt_render_kernel" in row.get("Kernel_Name", ""):
                 vals[row.get("Dispatch_Id")].append(float(row["Counter_Value"]))
-    per_dispatch = [sum(v) for v in vals.values()]
+    per_dispatch = [sum(vals[d]) for d in sorted(vals, key=int)]
     return per_dispatch
 
 
 def main():
     fetch_csv, write_csv, config, out, spp = sys.argv[1:6]
+    last = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     f = per_kernel(fetch_csv, "FETCH_SIZE")
     w = per_kernel(write_csv, "WRITE_SIZE")
+    if last:
+        f, w = f[-last:], w[-last:]
     if not f or not w:
         raise SystemExit("no iqpt_render_kernel rows found")
     f_avg = sum(f) / len(f) * 1024.0
     w_avg = sum(w) / len(w) * 1024.0
     res = {"config": config, "spp_per_launch": int(spp), "kernel": "iqpt_render_kernel",
-           "dispatches_fetch": len(f), "dispatches_write": len(w),
+           "dispatches_fetch": len(f), "dispatches_write": len(w), "last_dispatches_only": last or None,
            "fetch_bytes_raw": f_avg, "write_bytes": w_avg, "fetch_bytes_corrected": 2 * f_avg,
            "hbm_bytes_per_launch": 2 * f_avg + w_avg,
            "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B requests at 64 B)"}

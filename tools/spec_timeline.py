@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Per-block timeline of iqpt_spec_kernel on rank 0's row share of C2: for every spec
+block the s_memrealtime stamps (100 MHz) at its start, after round 0's slots, after round 0's walk and at
+its end (iqpt_debug_spec_timeline). Prints percentiles of the block start, the phases and the end, and
+the blocks that needed more than one round.
+
+    spec_timeline.py [--share 8] [--specfan 1] [--plan 1] [--out f.json]
+
+--specfan: 1 = the spec kernel alone on the stream (the fan kernel after it), 0 = beside the fan kernel
+on a second stream, 2 = one grid with the fan tiles."""
+import argparse
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "path-tracer-and-rasterizer-engine_amd"))
+import iqpt  # noqa: E402
+from iqpt import _lib  # noqa: E402
+from iqpt import dist as iqdist  # noqa: E402
+from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--share", type=int, default=8)
+ap.add_argument("--specfan", type=int, default=1)
+ap.add_argument("--warm", type=int, default=3)
+ap.add_argument("--plan", type=int, default=1, help="iqpt_debug_spec_plan mode (0 none, 1 asynchronous)")
+ap.add_argument("--out", default="")
+args = ap.parse_args()
+
+cfg = CONFIGS["c2"]
+sc = Scene()
+sc.add_preset(cfg.preset)
+pk = sc.build_packet()
+cam = make_camera(cfg.width, cfg.height)
+ps = iqdist.pixel_set_for_rank(cfg.width, cfg.height, 0, args.share)
+pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
+pt.set_split(_lib.SPLIT_SPEC)
+lb = _lib.load()
+lb.iqpt_debug_set_specfan.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+_lib.check(lb.iqpt_debug_set_specfan(pt._h, args.specfan, 0xffffffff), "iqpt_debug_set_specfan")
+lb.iqpt_debug_spec_plan.argtypes = [C.c_void_p, C.c_int]
+_lib.check(lb.iqpt_debug_spec_plan(pt._h, args.plan), "iqpt_debug_spec_plan")
+pt.set_camera(cam)
+pt.upload_packet(pk)
+for _ in range(args.warm):
+    pt.render(cfg.spp)
+pt.sync()
+lb.iqpt_debug_spec_timeline.argtypes = [C.c_void_p, C.c_int]
+_lib.check(lb.iqpt_debug_spec_timeline(pt._h, 1), "iqpt_debug_spec_timeline")
+pt.render(cfg.spp)
+pt.sync()
+cap = 1 << 16
+buf = (C.c_ulonglong * (4 * cap))()
+n = C.c_uint32(0)
+lb.iqpt_debug_read_spec_timeline.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32, C.POINTER(C.c_uint32)]
+_lib.check(lb.iqpt_debug_read_spec_timeline(pt._h, buf, cap, C.byref(n)), "iqpt_debug_read_spec_timeline")
+raw = np.array(buf[:4 * n.value], dtype=np.uint64).reshape(-1, 4)
+rounds = (raw[:, 3] >> np.uint64(48)).astype(np.int64)
+t = (raw & np.uint64(0xffffffffffff)).astype(np.float64)
+t0 = t[:, 0].min()
+us = (t - t0) / 100.0                     # 100 MHz ticks -> us
+start, slots_end, walk_end, end = us[:, 0], us[:, 1], us[:, 2], us[:, 3]
+
+
+def pct(a):
+    return {str(q): round(float(np.percentile(a, q)), 1) for q in (0, 10, 50, 90, 99, 100)}
+
+
+res = {"share": args.share, "specfan": args.specfan, "plan": args.plan, "blocks": int(n.value),
+       "kernel_us": round(float(end.max()), 1),
+       "start_us": pct(start), "slots_us": pct(slots_end - start), "walk_us": pct(walk_end - slots_end),
+       "later_rounds_us": pct(end - walk_end), "end_us": pct(end),
+       "rounds_hist": {str(int(k)): int(v) for k, v in zip(*np.unique(rounds, return_counts=True))},
+       "slowest": [[int(i), round(float(start[i]), 1), round(float(slots_end[i] - start[i]), 1),
+                    round(float(walk_end[i] - slots_end[i]), 1), round(float(end[i] - walk_end[i]), 1),
+                    int(rounds[i])] for i in np.argsort(-end)[:16]]}
+print(json.dumps(res), flush=True)
+if args.out:
+    Path(args.out).write_text(json.dumps(res, indent=1) + "\n")

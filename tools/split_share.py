@@ -28,7 +28,7 @@ OPT = 0
 
 
 def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain_waves: int = 0,
-        fan: bool = True, spec_run: int = 0) -> dict:
+        fan: bool = True, spec_run: int = 0, specfan=None) -> dict:
     cfg = CONFIGS["c2"]
     sc = Scene()
     sc.add_preset(cfg.preset)
@@ -52,6 +52,11 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain
         lb = _lib.load()
         lb.iqpt_debug_set_spec.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_spec(pt._h, 0, spec_run), "iqpt_debug_set_spec")   # margin divisor
+    if specfan is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_specfan.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_specfan(pt._h, specfan[0], specfan[1]), "iqpt_debug_set_specfan")
     if not fan:
         import ctypes as C
         lb = _lib.load()
@@ -167,6 +172,8 @@ def main():
                     "the fan kernel), chainplain (the same, anchored tiles in the plain kernel), fan (IQPT_SPLIT_FAN)")
     ap.add_argument("--chain-waves", default="", help="extra chain rows at these chain-kernel waves per CU")
     ap.add_argument("--spec-runs", default="", help="extra spec rows at these window margin divisors")
+    ap.add_argument("--specfan", default="", help="extra spec rows mode:lead[,...] (iqpt_debug_set_specfan: 0 two "
+                    "streams, 1 one stream, 2 one grid; lead 'all' or a block count)")
     ap.add_argument("--knobs", default="", help="split knob sets heavy_rho:refill_min[,...] (extra split rows)")
     ap.add_argument("--stats", action="store_true", help="wave timelines of the split variant (instrumented library)")
     ap.add_argument("--opt", type=lambda v: int(v, 0), default=0, help="kernel option set (instrumented library; 0 = production)")
@@ -206,10 +213,17 @@ def main():
             return int(v.split("l")[0]) | ((int(v.split("l")[1]) << 8) if "l" in v else 0)
         modes += [(f"chain_w{w}", _lib.SPLIT_CHAIN, cw(w)) for w in args.chain_waves.split(",") if w]
         modes += [(f"spec_r{r}", _lib.SPLIT_SPEC, int(r)) for r in args.spec_runs.split(",") if r]
+        sfs = {}
+        for v in args.specfan.split(","):
+            if v:
+                m, _, ld = v.partition(":")
+                sfs[f"spec_sf{m}_{ld or 'all'}"] = (int(m), 0xffffffff if ld in ("", "all") else int(ld))
+                modes.append((f"spec_sf{m}_{ld or 'all'}", _lib.SPLIT_SPEC, 0))
         for name, mode, cw in modes:
             kn = (0, 16 | (1 << 16)) if name.endswith("a") else None
             r = run(n, mode, args.launches, args.warm, args.spp, knobs=kn, chain_waves=0 if name.startswith("spec") else cw,
-                    fan=name not in ("chainplain", "splitplain"), spec_run=cw if name.startswith("spec_r") else 0)
+                    fan=name not in ("chainplain", "splitplain"), spec_run=cw if name.startswith("spec_r") else 0,
+                    specfan=sfs.get(name))
             res[name] = r
             row[name + "_ms_median"] = float(np.median(r["ms"]))
             row[name + "_ms_min"] = float(np.min(r["ms"]))
