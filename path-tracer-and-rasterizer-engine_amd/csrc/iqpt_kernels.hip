@@ -2391,9 +2391,24 @@ constexpr uint32_t kChainBlock = 64;                   // one wave per block
 constexpr int kChainWaves = 4;                         // __launch_bounds__ waves per SIMD
 constexpr uint32_t kChainRingMul = 2;                  // ring entries per lane
 
+// n XORWOW steps of the xorshift part (random.cu:66-107; the Weyl word d is the caller's, d += n WEYL).
+// Five steps at a time: each new word takes the slot of the word it retires (x_{k+5} = f(x_k, x_{k+4})),
+// so after five steps v0..v4 name the state again and no register moves are needed; the rest one by one.
+__device__ __forceinline__ uint32_t xorwow_next_word(uint32_t x, uint32_t y) {
+    const uint32_t t = x ^ (x >> 2);
+    return (y ^ (y << 4)) ^ (t ^ (t << 1));
+}
+
 __device__ __forceinline__ void xorwow_skip_v(uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& v3, uint32_t& v4,
                                               uint32_t n) {
-    for (uint32_t i = 0; i < n; ++i) {
+    for (uint32_t k = n / 5u; k; --k) {
+        v0 = xorwow_next_word(v0, v4);
+        v1 = xorwow_next_word(v1, v0);
+        v2 = xorwow_next_word(v2, v1);
+        v3 = xorwow_next_word(v3, v2);
+        v4 = xorwow_next_word(v4, v3);
+    }
+    for (uint32_t i = n % 5u; i; --i) {
         const uint32_t t = v0 ^ (v0 >> 2);
         v0 = v1;
         v1 = v2;
@@ -2723,11 +2738,11 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
 constexpr uint32_t kFanBlock = 256;                    // four waves, one tile
 constexpr uint32_t kFanChunk = 64;                     // samples per chunk (LDS: [chunk][pixel])
 
-// First sample of wave w's range in a chunk of cn samples: 0, 14 %, 44 %, 72 % of the chunk (wave 0 also
-// folds the chunk, about a sixth of a sample per fold; a later wave first steps 2 s draws, about 7 % of a
-// sample per sample skipped), so that the four ranges cost about the same.
+// First sample of wave w's range in a chunk of cn samples: 0, 20 %, 47 %, 73 % of the chunk (wave 0 also
+// folds the chunk, about a twentieth of a sample per fold of a triangle hit; a later wave first steps 2 s
+// draws, about 7 % of a sample per sample skipped), so that the four ranges cost about the same.
 __device__ __forceinline__ uint32_t fan_range(uint32_t cn, uint32_t w) {
-    return w == 0u ? 0u : (w == 1u ? (cn * 9u) / 64u : (w == 2u ? (cn * 28u) / 64u : (w == 3u ? (cn * 46u) / 64u : cn)));
+    return w == 0u ? 0u : (w == 1u ? (cn * 13u) / 64u : (w == 2u ? (cn * 30u) / 64u : (w == 3u ? (cn * 47u) / 64u : cn)));
 }
 
 __host__ __device__ inline uint32_t fan_lds_bytes(uint32_t ntri_pairs, uint32_t spp) {
@@ -2788,21 +2803,26 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
         for (uint32_t s = s0; s < s1; ++s) {
             ray3 ray;
             camera_ray<OPT>(p, px, py, st, ray);
-            // closest hit over the tile's candidate pairs, in index order (path_tracer.cu:257-275); the
-            // lane's pixel has no sphere candidate (its tile's mask, or its own bundle in chain launches), so no
-            // sphere test can accept (iq_interval.h)
+            // the tile's candidate pairs in index order (path_tracer.cu:257-275); the lane's pixel has no
+            // sphere candidate (its tile's mask, or its own bundle in chain launches), so no sphere test can
+            // accept (iq_interval.h). Every triangle is emissive, so the sample's colour depends only on whether
+            // some triangle is accepted, not on which (path_tracer.cu:278, material.cu:50-57): a lane stops at
+            // its first accepted triangle (accepted against the initial closest, as the first acceptance of the
+            // reference's loop is), the wave when every lane has one
             float closest = kTMax;
             int kind = kHitNone;
             uint32_t hidx = 0;
             for (uint32_t w = 0; w * 32u < tp; ++w) {
                 uint32_t m = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_mask[w]);
-                while (m) {
+                while (m && __any(kind != kHitTri)) {
                     const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(m);
                     m &= m - 1u;
                     if (j >= tp) break;
-                    const float4* q = lds_tri + (size_t)j * kTriPairFloat4;
-                    test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
-                                            2 * j + 1 < p.ntri);
+                    if (kind != kHitTri) {
+                        const float4* q = lds_tri + (size_t)j * kTriPairFloat4;
+                        test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
+                                                2 * j + 1 < p.ntri);
+                    }
                 }
             }
             const uint64_t hit = __ballot(kind == kHitTri);
@@ -2814,27 +2834,24 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
         if (wave == 0) {
             // the running mean in sample order (path_tracer.cu:341-358): an emissive hit is 10 clamped to 1
             for (uint32_t k = 0; k < cn; ++k) {
-                float cx, cy, cz;
+                const float2 tv = lds_tab[c0 + k];
+                float qx, qy, qz;
                 if ((lds_hit[k] >> lane) & 1ull) {
-                    cx = 1.0f;
-                    cy = 1.0f;
-                    cz = 1.0f;
+                    // c = (1, 1, 1): c / n = RN(1 / n), the table's rc, in every channel (mean_terms)
+                    qx = tv.x;
+                    qy = tv.x;
+                    qz = tv.x;
                 } else {
                     const float a = lds_sky[k * 64u + lane];
                     const float one_a = 1.0f - a;
-                    cx = one_a + a * 0.5f;
-                    cy = one_a + a * 0.7f;
-                    cz = one_a + a * 1.0f;
+                    float cx = one_a + a * 0.5f;
+                    float cy = one_a + a * 0.7f;
+                    float cz = one_a + a * 1.0f;
                     cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
                     cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
                     cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                    cx = 0.0f + cx;
-                    cy = 0.0f + cy;
-                    cz = 0.0f + cz;
+                    mean_terms<OPT>(0.0f + cx, 0.0f + cy, 0.0f + cz, lds_tab_n[c0 + k], tv.x, p.mean_tiny, qx, qy, qz);
                 }
-                const float2 tv = lds_tab[c0 + k];
-                float qx, qy, qz;
-                mean_terms<OPT>(cx, cy, cz, lds_tab_n[c0 + k], tv.x, p.mean_tiny, qx, qy, qz);
                 ax = qx + ax * tv.y;
                 ay = qy + ay * tv.y;
                 az = qz + az * tv.y;
@@ -2977,8 +2994,9 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     }
     float4* res = reinterpret_cast<float4*>(s.res) + (size_t)q * s.m_cap;
     const bool rec = s.tl != nullptr && threadIdx.x == 0;   // measurement only
+    const bool rec_w = s.tl != nullptr && (threadIdx.x & 63u) == 0u;
     uint64_t t_rec[3] = {rec ? __builtin_amdgcn_s_memrealtime() : 0ull, 0ull, 0ull};
-    uint32_t rounds = 0;
+    uint32_t rounds = 0, iters = 0;                          // measurement: this wave's slot-loop iterations
     uint32_t lane_rays = 0;                                  // rays of the chain samples this lane gathered
     __syncthreads();
 
@@ -3009,6 +3027,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         };
         if (active) start_slot();
         while (__any(active)) {
+            if (rec_w) ++iters;
             // closest hit (path_tracer.cu:253-295): camera rays over their tile's mask pairs in index order
             float closest = kTMax;
             int kind = kHitNone;
@@ -3175,12 +3194,13 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         ++rounds;
     }
     if (rec) {
-        unsigned long long* o = s.tl + 4 * (size_t)bid;
+        unsigned long long* o = s.tl + 8 * (size_t)bid;
         o[0] = t_rec[0];
         o[1] = t_rec[1];
         o[2] = t_rec[2];
         o[3] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) | ((unsigned long long)rounds << 48);
     }
+    if (rec_w) s.tl[8 * (size_t)bid + 4 + threadIdx.x / 64u] = iters;
     unsigned long long rays = lane_rays;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);

@@ -41,9 +41,9 @@ constexpr double kSplitAutoPixelsPerLane = 1.2;
 // CU by default (profiles/r02/split_share_v12_lanes.json: 16 beats 8 at N <= 4, equal at N = 8)
 constexpr double kChainAutoPixelsPerLane = 2.0;
 // spec launches: AUTO takes them below this many owned pixels per resident lane of the
-// plain kernel (C3's N = 8 share has 0.8: spec 0.34 ms per launch against chain 0.39-0.44; N = 4, 1.6,
-// stays chain: 0.62 against 0.67-0.70; profiles/r03/share_modes.json)
-constexpr double kSpecAutoPixelsPerLane = 1.2;
+// plain kernel (C3 shares: N = 8 has 0.8, N = 4 1.6; pipelined spec launches 0.29 / 0.51 ms per step through
+// the gather against chain 0.39 / 0.62; N = 2, 3.2, stays plain: 0.91 against 0.93; profiles/r03/share_modes.json)
+constexpr double kSpecAutoPixelsPerLane = 2.0;
 constexpr uint32_t kChainWavesPerCu = 16;
 constexpr size_t kSplitResBudget = size_t(8) << 30;   // speculative results (bytes)
 
@@ -1842,13 +1842,13 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
                 if (c->d_spec_tl) (void)hipFree(c->d_spec_tl);
                 c->d_spec_tl = nullptr;
                 c->spec_tl_blocks = 0;
-                if (hipMalloc(&c->d_spec_tl, nb * 4 * sizeof(unsigned long long)) != hipSuccess) {
+                if (hipMalloc(&c->d_spec_tl, nb * 8 * sizeof(unsigned long long)) != hipSuccess) {
                     (void)hipGetLastError();
                     return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec timeline");
                 }
                 c->spec_tl_blocks = nb;
             }
-            IQPT_HIP(hipMemsetAsync(c->d_spec_tl, 0, nb * 4 * sizeof(unsigned long long), c->stream));
+            IQPT_HIP(hipMemsetAsync(c->d_spec_tl, 0, nb * 8 * sizeof(unsigned long long), c->stream));
             ks2.tl = c->d_spec_tl;
         }
         if (c->specfan_mode == 2) {
@@ -2201,7 +2201,8 @@ int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
 }
 
 /* Internal (measurement): record per spec block s_memrealtime stamps (100 MHz) in later spec launches —
- * start, after round 0's slots, after round 0's walk, end | rounds << 48 — and read the last launch's. */
+ * start, after round 0's slots, after round 0's walk, end | rounds << 48, then the slot-loop iterations of
+ * its four waves (8 words per block) — and read the last launch's. */
 int iqpt_debug_spec_timeline(iqpt_ctx* c, int on) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     c->spec_tl_on = on != 0;
@@ -2219,8 +2220,29 @@ int iqpt_debug_read_spec_timeline(iqpt_ctx* c, unsigned long long* out, uint32_t
                              ? c->spec_plan_blocks
                              : (c->n_chain_pix + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
     const size_t nb = std::min<size_t>(nspec, std::min<size_t>(cap_blocks, c->spec_tl_blocks));
-    if (nb) IQPT_HIP(hipMemcpy(out, c->d_spec_tl, nb * 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (nb) IQPT_HIP(hipMemcpy(out, c->d_spec_tl, nb * 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     *n = (uint32_t)nb;
+    return IQPT_OK;
+}
+
+/* Internal (measurement): the spec plan in use and the history behind it — order (n words), blocks (2 words
+ * each, *nb of them) and the sphere pixels' slots per sample x 256 (n words); *n = sphere pixels (0: no plan).
+ * Synchronises. */
+int iqpt_debug_read_spec_plan(iqpt_ctx* c, uint32_t* order, uint32_t* blocks, uint32_t* rho, uint32_t cap,
+                              uint32_t* n, uint32_t* nb) {
+    if (!c || !order || !blocks || !rho || !n || !nb) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *n = *nb = 0;
+    int st = enter(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    const uint32_t np = c->n_chain_pix;
+    if (!c->spec_plan_n || c->spec_plan_n != np || np > cap || !c->d_spec_plan) return IQPT_OK;
+    IQPT_HIP(hipMemcpy(order, c->d_spec_plan, (size_t)np * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    IQPT_HIP(hipMemcpy(blocks, c->d_spec_plan + np, 2 * (size_t)c->spec_plan_blocks * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost));
+    IQPT_HIP(hipMemcpy(rho, c->d_spec + np, (size_t)np * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *n = np;
+    *nb = c->spec_plan_blocks;
     return IQPT_OK;
 }
 

@@ -54,12 +54,15 @@ _lib.check(lb.iqpt_debug_spec_timeline(pt._h, 1), "iqpt_debug_spec_timeline")
 pt.render(cfg.spp)
 pt.sync()
 cap = 1 << 16
-buf = (C.c_ulonglong * (4 * cap))()
+buf = (C.c_ulonglong * (8 * cap))()
 n = C.c_uint32(0)
 lb.iqpt_debug_read_spec_timeline.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32, C.POINTER(C.c_uint32)]
 _lib.check(lb.iqpt_debug_read_spec_timeline(pt._h, buf, cap, C.byref(n)), "iqpt_debug_read_spec_timeline")
-raw = np.array(buf[:4 * n.value], dtype=np.uint64).reshape(-1, 4)
+raw8 = np.array(buf[:8 * n.value], dtype=np.uint64).reshape(-1, 8)
+raw = raw8[:, :4]
+wave_iters = raw8[:, 4:].astype(np.int64)
 rounds = (raw[:, 3] >> np.uint64(48)).astype(np.int64)
+iters = wave_iters.max(axis=1)                            # the block's slowest wave's slot-loop iterations
 t = (raw & np.uint64(0xffffffffffff)).astype(np.float64)
 t0 = t[:, 0].min()
 us = (t - t0) / 100.0                     # 100 MHz ticks -> us
@@ -74,10 +77,49 @@ res = {"share": args.share, "specfan": args.specfan, "plan": args.plan, "blocks"
        "kernel_us": round(float(end.max()), 1),
        "start_us": pct(start), "slots_us": pct(slots_end - start), "walk_us": pct(walk_end - slots_end),
        "later_rounds_us": pct(end - walk_end), "end_us": pct(end),
+       "iters_max_wave": pct(iters), "iters_spread_in_block": pct(wave_iters.max(axis=1) - wave_iters.min(axis=1)),
        "rounds_hist": {str(int(k)): int(v) for k, v in zip(*np.unique(rounds, return_counts=True))},
        "slowest": [[int(i), round(float(start[i]), 1), round(float(slots_end[i] - start[i]), 1),
                     round(float(walk_end[i] - slots_end[i]), 1), round(float(end[i] - walk_end[i]), 1),
                     int(rounds[i])] for i in np.argsort(-end)[:16]]}
+# the plan behind the blocks and the history: per block its lanes per pixel, pixels, and its pixels' largest
+# work estimate (window x slots per sample) and window, to fit the slot phase against
+nb = C.c_uint32(0)
+npx = C.c_uint32(0)
+order = (C.c_uint32 * cap)()
+blk = (C.c_uint32 * (2 * cap))()
+rho = (C.c_uint32 * cap)()
+lb.iqpt_debug_read_spec_plan.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                         C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+_lib.check(lb.iqpt_debug_read_spec_plan(pt._h, order, blk, rho, cap, C.byref(npx), C.byref(nb)), "iqpt_debug_read_spec_plan")
+if npx.value and nb.value == n.value:
+    spp, mcap = cfg.spp, (3 * cfg.spp + 15) & ~15
+    rho_a = np.array(rho[:npx.value], dtype=np.float64)
+    r = np.where(rho_a > 0, rho_a, 576.0)
+    m = r * spp / 256.0
+    m = np.minimum(mcap, np.maximum(spp, m + np.maximum(4, (m - spp) / 4) + 4))   # spec_window (margin 4)
+    w = m * np.maximum(r, 256.0) / 256.0
+    rows = []
+    for b in range(nb.value):
+        first, word = blk[2 * b], blk[2 * b + 1]
+        cnt, lanes = word & 0xff, 8 << (word >> 8)
+        qs = [order[first + i] for i in range(cnt)]
+        rows.append([lanes, cnt, float(w[qs].max()), float(m[qs].max()), float(slots_end[b] - start[b]), float(iters[b])])
+    a = np.array(rows)
+    res["per_block"] = {"lanes_hist": {str(int(k)): int(v) for k, v in zip(*np.unique(a[:, 0], return_counts=True))}}
+    # slot phase ~ alpha * max w / lanes + beta * max window + gamma (least squares)
+    X = np.stack([a[:, 2] / a[:, 0], a[:, 3], np.ones(len(a))], axis=1)
+    coef, *_ = np.linalg.lstsq(X, a[:, 4], rcond=None)
+    pred = X @ coef
+    res["per_block"]["fit_us"] = {"per_work_per_lane": float(coef[0]), "per_window_slot": float(coef[1]),
+                                  "const": float(coef[2]),
+                                  "r2": float(1 - ((a[:, 4] - pred) ** 2).sum() / ((a[:, 4] - a[:, 4].mean()) ** 2).sum())}
+    for L in (8, 16, 32, 64):
+        sel = a[:, 0] == L
+        if sel.any():
+            res["per_block"][f"lanes{L}"] = {"blocks": int(sel.sum()), "slots_us": pct(a[sel, 4]), "iters_max_wave": pct(a[sel, 5]),
+                                             "us_per_iter": pct(a[sel, 4] / np.maximum(a[sel, 5], 1)),
+                                             "w_per_lane": pct(a[sel, 2] / L), "window": pct(a[sel, 3])}
 print(json.dumps(res), flush=True)
 if args.out:
     Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
