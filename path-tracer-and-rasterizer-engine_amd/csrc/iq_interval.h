@@ -1,4 +1,5 @@
-// iq_interval.h — exact conservative culling of primitives for bundles of camera rays.
+// iq_interval.h — exact conservative culling of primitives for bundles of camera rays, and the
+// converse: triangles every ray of a bundle is certain to hit.
 //
 // The kernel's closest-hit loop must return exactly what the reference's brute-force loop over
 // every primitive returns (path_tracer.cu:257-295). A primitive may therefore be skipped for a ray
@@ -185,6 +186,39 @@ IQ_HD inline bool tri_culled(const bundle& b, const float v0[3], const float e1[
     const ivl t = mul(add(add(mul(pt(e2[0]), qx), mul(pt(e2[1]), qy)), mul(pt(e2[2]), qz)), inv);
     if (!finite(t)) return false;
     return t.hi < kTMinIv;
+}
+
+constexpr float kTMaxIv = 999.99f;     // the kernel's kTMax: the closest hit a ray starts with
+
+// true if the Möller–Trumbore test (shape.cu:62-103 as the kernel evaluates it) accepts triangle
+// (v0, e1, e2) for every ray of the bundle as a first hit: |det| >= 1e-6 with one sign, u in [0, 1],
+// v >= 0, u + v <= 1 and t in [t_min, kTMax] on every lane — each of the reference's reject tests
+// fails for the whole bundle. Used for tiles without a sphere candidate under the reference's
+// materials, where every camera ray then ends on an emissive triangle (path_tracer.cu:278).
+IQ_HD inline bool tri_certain(const bundle& b, const float v0[3], const float e1[3], const float e2[3]) {
+    if (!b.ok) return false;
+    const ivl* d = b.d;
+    const ivl px = sub(mul(d[1], pt(e2[2])), mul(d[2], pt(e2[1])));
+    const ivl py = sub(mul(d[2], pt(e2[0])), mul(d[0], pt(e2[2])));
+    const ivl pz = sub(mul(d[0], pt(e2[1])), mul(d[1], pt(e2[0])));
+    const ivl det = add(add(mul(pt(e1[0]), px), mul(pt(e1[1]), py)), mul(pt(e1[2]), pz));
+    if (!finite(det)) return false;
+    const float eps = 0.000001f;
+    if (!(det.lo >= eps || det.hi <= -eps)) return false;   // every lane |det| >= 1e-6, one sign
+    const ivl inv = rcp(det);
+    const ivl tx = sub(b.o[0], pt(v0[0])), ty = sub(b.o[1], pt(v0[1])), tz = sub(b.o[2], pt(v0[2]));
+    const ivl u = mul(add(add(mul(tx, px), mul(ty, py)), mul(tz, pz)), inv);
+    if (!finite(u) || !(u.lo >= 0.0f && u.hi <= 1.0f)) return false;
+    const ivl qx = sub(mul(ty, pt(e1[2])), mul(tz, pt(e1[1])));
+    const ivl qy = sub(mul(tz, pt(e1[0])), mul(tx, pt(e1[2])));
+    const ivl qz = sub(mul(tx, pt(e1[1])), mul(ty, pt(e1[0])));
+    const ivl v = mul(add(add(mul(d[0], qx), mul(d[1], qy)), mul(d[2], qz)), inv);
+    if (!finite(v) || !(v.lo >= 0.0f)) return false;
+    const ivl uv = add(u, v);
+    if (!finite(uv) || !(uv.hi <= 1.0f)) return false;
+    const ivl t = mul(add(add(mul(pt(e2[0]), qx), mul(pt(e2[1]), qy)), mul(pt(e2[2]), qz)), inv);
+    if (!finite(t)) return false;
+    return t.lo >= kTMinIv && t.hi <= kTMaxIv;
 }
 
 // true if sphere::intersect (shape.cu:13-46 as the kernel evaluates it) rejects sphere (c, r)

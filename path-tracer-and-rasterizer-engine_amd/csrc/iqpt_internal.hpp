@@ -81,6 +81,10 @@ struct kparams {
     // camera rays of the tile may hit (iq_interval.h); null = no culling for this launch
     const uint32_t* cull;
     uint32_t cull_ntx, cull_wt, cull_stride;
+    // per tile: 1 if every camera ray of the tile is certain to end on an emissive triangle (no sphere
+    // candidate, a candidate triangle every ray of the tile's bundle hits: iq_interval.h tri_certain; the
+    // reference's materials only); null = none. Such a tile's samples are (1, 1, 1) folds and two draws.
+    const uint32_t* certain;
     // work queue over tiles: queue position q -> tile tile_order[q] (null = identity); built with the
     // masks, most expensive tiles first (longest-processing-time order: a shorter launch tail)
     const uint32_t* tile_order;
@@ -331,6 +335,8 @@ int launch_relayout(void* stream, const uint32_t* src, uint32_t* dst, uint32_t n
 // Tile masks for kOptCull (one thread per tile word).
 int launch_bin(void* stream, const kbin& b);
 // Per-tile candidate counts from the masks (triangle pairs, sphere pairs), and the candidate lists.
+// per tile of the masks: the certain flags of kparams::certain (one thread per tile)
+int launch_certain(void* stream, const kbin& b, uint32_t* certain);
 int launch_tile_count(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
                       uint32_t* cnt_tri, uint32_t* cnt_sph);
 int launch_tile_list(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,

@@ -238,6 +238,33 @@ __device__ __forceinline__ void camera_ray(const kparams& p, uint32_t x, uint32_
     else camera_ndc<OPT>(p, x_ndc, y_ndc, r);
 }
 
+// n XORWOW steps of the xorshift part (random.cu:66-107; the Weyl word d is the caller's, d += n WEYL).
+// Five steps at a time: each new word takes the slot of the word it retires (x_{k+5} = f(x_k, x_{k+4})),
+// so after five steps v0..v4 name the state again and no register moves are needed; the rest one by one.
+__device__ __forceinline__ uint32_t xorwow_next_word(uint32_t x, uint32_t y) {
+    const uint32_t t = x ^ (x >> 2);
+    return (y ^ (y << 4)) ^ (t ^ (t << 1));
+}
+
+__device__ __forceinline__ void xorwow_skip_v(uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& v3, uint32_t& v4,
+                                              uint32_t n) {
+    for (uint32_t k = n / 5u; k; --k) {
+        v0 = xorwow_next_word(v0, v4);
+        v1 = xorwow_next_word(v1, v0);
+        v2 = xorwow_next_word(v2, v1);
+        v3 = xorwow_next_word(v3, v2);
+        v4 = xorwow_next_word(v4, v3);
+    }
+    for (uint32_t i = n % 5u; i; --i) {
+        const uint32_t t = v0 ^ (v0 >> 2);
+        v0 = v1;
+        v1 = v2;
+        v2 = v3;
+        v3 = v4;
+        v4 = (v4 ^ (v4 << 4)) ^ (t ^ (t << 1));
+    }
+}
+
 // CUDA float -> uint8_t: NaN -> 0, saturating, truncating (path_tracer.cu:361-363).
 __device__ __forceinline__ uint32_t to_u8(float f) {
     if (!(f > 0.0f)) return 0u;
@@ -1188,6 +1215,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // tile, 2 leftovers [chunk_next, chunk_end) of the leftover list, 3 the light pixels of a split tile
     // (anchored) — and the split tile's first slot and storage index
     uint32_t chunk_kind = 0, chunk_sp0 = 0, chunk_first = 0, chunk_r = 0;
+    // the chunk's tile is certain (kparams::certain): its pixels take the whole launch at once (refill)
+    constexpr bool kCertain = !kSplit && (OPT & kOptAccTable) && !(OPT & kOptMaterials) && !(OPT & kOptStats);
+    bool chunk_certain = false;
     uint32_t queue_total = kOverlap ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : (p.nqueue ? p.nqueue : p.ntiles), n_runs = 0;
     if (kSplit) {
         // round 1, longest tasks first: the split tiles' light pixels (anchored chains with scatters, in
@@ -1295,6 +1325,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         t = p.tile_order ? p.tile_order[q] : q;
                     }
                     chunk_tile = t;
+                    chunk_certain = kCertain && p.certain != nullptr && p.certain[t] != 0u;
                     const uint32_t tx = t % p.ntx, ty = t / p.ntx;
                     const uint32_t th = min(kCullTile, p.nrows - ty * kCullTile);
                     const uint32_t tw = min(kCullTile, p.ncols - tx * kCullTile);
@@ -1387,15 +1418,44 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         if (kSplit && chunk_kind == 0) lds_sp[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
                     }
                     depth = 0;
-                    if (kSplit) need_cam = true;   // one camera_ray call site per iteration (loop top)
-                    else camera_ray<OPT>(p, px, py, st, ray);
-                    if (kCull && p.cull) {
-                        // the tile and word 0 of its triangle / sphere masks, kept in this lane's LDS slot for
-                        // the pixel's lifetime (the global load latency is paid once per pixel, not per ray)
-                        lds_cm[threadIdx.x] = make_uint4(p.cull[(size_t)tile * p.cull_stride],
-                                                         p.cull[(size_t)tile * p.cull_stride + p.cull_wt], tile, 0u);
+                    if (kCertain && chunk_certain) {
+                        // a certain tile (kparams::certain): every sample takes the camera's two draws and
+                        // ends on an emissive triangle, clamped colour (1, 1, 1), whose mean term c / n is the
+                        // table's RN(1 / n) (mean_terms): the launch's samples fold at once, in order
+                        xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * p.spp);
+                        st.d += 2u * p.spp * IQ_XORWOW_WEYL;
+                        for (uint32_t k = 0; k < p.spp; ++k) {
+                            const float2 tv = lds_tab[k];
+                            acc.x = tv.x + acc.x * tv.y;
+                            acc.y = tv.x + acc.y * tv.y;
+                            acc.z = tv.x + acc.z * tv.y;
+                        }
+                        store_pixel();
+                        go = false;
+                    } else if (kSplit) {
+                        need_cam = true;           // one camera_ray call site per iteration (loop top)
+                    } else {
+                        camera_ray<OPT>(p, px, py, st, ray);
                     }
-                    active = true;
+                }
+                if (go && kCull && p.cull) {
+                    // the tile and word 0 of its triangle / sphere masks, kept in this lane's LDS slot for
+                    // the pixel's lifetime (the global load latency is paid once per pixel, not per ray)
+                    lds_cm[threadIdx.x] = make_uint4(p.cull[(size_t)tile * p.cull_stride],
+                                                     p.cull[(size_t)tile * p.cull_stride + p.cull_wt], tile, 0u);
+                }
+                if (go) active = true;
+            }
+            if (kCertain && chunk_certain) {
+                // the certain pixels of this pass are complete: their rays, and (overlapped launches) their
+                // tile's completion count once their stores are done
+                const uint32_t nfin = min((uint32_t)__popcll(need), avail);
+                if (nfin) {
+                    wave_rays += (uint64_t)nfin * p.spp;
+                    if (kOverlap && p.tile_done) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        if (lane == 0) atomicAdd(p.tile_done + chunk_tile, nfin);
+                    }
                 }
             }
             if (OPT & kOptStats) {
@@ -2116,6 +2176,53 @@ __global__ __launch_bounds__(256) void iqpt_bin_kernel(const kbin b) {
     b.cull[gid] = bits;
 }
 
+// Per tile: 1 if the tile has no sphere candidate and one of its candidate triangles is accepted by every
+// camera ray of the tile's bundle (iq_interval.h tri_certain). Under the reference's materials (the runtime
+// launches this only without a material table) every sample of such a tile ends on its first ray with
+// the emissive colour, clamped to (1, 1, 1), after the two jitter draws (path_tracer.cu:278, 341-358;
+// camera.cu:24-25). Run after iqpt_bin_kernel on the same stream.
+__global__ __launch_bounds__(256) void iqpt_certain_kernel(const kbin b, uint32_t* certain) {
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    if (t >= b.ntx * b.nty) return;
+    const uint32_t* m = b.cull + (size_t)t * b.stride;
+    uint32_t ok = 0u;
+    bool sph = false;
+    for (uint32_t w = b.wt; w < b.stride; ++w) sph = sph || m[w] != 0u;
+    if (!sph) {
+        const uint32_t tx = t % b.ntx, ty = t / b.ntx;
+        const uint32_t c0 = tx * kCullTile, c1 = min(c0 + kCullTile, b.ncols) - 1u;
+        const uint32_t k0 = ty * kCullTile, k1 = min(k0 + kCullTile, b.nrows) - 1u;
+        iqiv::camera_in ci;
+        ci.width = b.width;
+        ci.height = b.height;
+        ci.rcp_width = 0.0f;
+        ci.rcp_height = 0.0f;
+        ci.inv_proj = b.inv_proj;
+        ci.inv_view = b.inv_view;
+        ci.cam_const = (int)b.cam_const;
+        ci.near_rw = b.cam_near_rw;
+        ci.far_rw = b.cam_far_rw;
+        const iqiv::bundle bd = iqiv::camera_bundle(ci, b.x0 + c0, b.x0 + c1, b.y0 + k0 * b.ystep, b.y0 + k1 * b.ystep);
+        for (uint32_t w = 0; w < b.wt && bd.ok && !ok; ++w) {
+            uint32_t bits = m[w];
+            while (bits && !ok) {
+                const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(bits);
+                bits &= bits - 1u;
+                for (uint32_t e = 0; e < 2u && !ok; ++e) {
+                    const uint32_t k = 2u * j + e;
+                    if (k >= b.ntri) break;
+                    const float4_storage* tr = b.tris + (size_t)k * kTriFloat4;
+                    const float v0[3] = {tr[0].x, tr[0].y, tr[0].z};
+                    const float e1[3] = {tr[0].w, tr[1].x, tr[1].y};
+                    const float e2[3] = {tr[1].z, tr[1].w, tr[2].x};
+                    ok = iqiv::tri_certain(bd, v0, e1, e2) ? 1u : 0u;
+                }
+            }
+        }
+    }
+    certain[t] = ok;
+}
+
 // Per tile: candidate triangle pairs and sphere pairs of its masks (the queue-order cost and the
 // sizes of the candidate lists).
 __global__ __launch_bounds__(256) void iqpt_tile_count_kernel(const uint32_t* cull, uint32_t ntiles, uint32_t wt,
@@ -2390,33 +2497,6 @@ __global__ __launch_bounds__(kStitchBlock) void iqpt_split_stitch_kernel(const k
 constexpr uint32_t kChainBlock = 64;                   // one wave per block
 constexpr int kChainWaves = 4;                         // __launch_bounds__ waves per SIMD
 constexpr uint32_t kChainRingMul = 2;                  // ring entries per lane
-
-// n XORWOW steps of the xorshift part (random.cu:66-107; the Weyl word d is the caller's, d += n WEYL).
-// Five steps at a time: each new word takes the slot of the word it retires (x_{k+5} = f(x_k, x_{k+4})),
-// so after five steps v0..v4 name the state again and no register moves are needed; the rest one by one.
-__device__ __forceinline__ uint32_t xorwow_next_word(uint32_t x, uint32_t y) {
-    const uint32_t t = x ^ (x >> 2);
-    return (y ^ (y << 4)) ^ (t ^ (t << 1));
-}
-
-__device__ __forceinline__ void xorwow_skip_v(uint32_t& v0, uint32_t& v1, uint32_t& v2, uint32_t& v3, uint32_t& v4,
-                                              uint32_t n) {
-    for (uint32_t k = n / 5u; k; --k) {
-        v0 = xorwow_next_word(v0, v4);
-        v1 = xorwow_next_word(v1, v0);
-        v2 = xorwow_next_word(v2, v1);
-        v3 = xorwow_next_word(v3, v2);
-        v4 = xorwow_next_word(v4, v3);
-    }
-    for (uint32_t i = n % 5u; i; --i) {
-        const uint32_t t = v0 ^ (v0 >> 2);
-        v0 = v1;
-        v1 = v2;
-        v2 = v3;
-        v3 = v4;
-        v4 = (v4 ^ (v4 << 4)) ^ (t ^ (t << 1));
-    }
-}
 
 template <int MAXD, int OPT, int LANES>
 __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(const kparams p) {
@@ -2790,6 +2870,35 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
         ax = a[0];
         ay = a[1];
         az = a[2];
+    }
+    if (p.certain != nullptr && p.certain[t] != 0u) {
+        // a certain tile (kparams::certain): every sample takes the camera's two draws and ends on an emissive
+        // triangle, clamped colour (1, 1, 1), whose mean term c / n is the table's RN(1 / n); wave 0 folds
+        // the launch's samples in order, the other waves have nothing to do
+        if (wave == 0 && has) {
+            xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * p.spp);
+            st.d += 2u * p.spp * IQ_XORWOW_WEYL;
+            for (uint32_t k = 0; k < p.spp; ++k) {
+                const float2 tv = lds_tab[k];
+                ax = tv.x + ax * tv.y;
+                ay = tv.x + ay * tv.y;
+                az = tv.x + az * tv.y;
+            }
+            p.rng[pix] = st.v0;
+            p.rng[(size_t)p.npix + pix] = st.v1;
+            p.rng[2 * (size_t)p.npix + pix] = st.v2;
+            p.rng[3 * (size_t)p.npix + pix] = st.v3;
+            p.rng[4 * (size_t)p.npix + pix] = st.v4;
+            p.rng[5 * (size_t)p.npix + pix] = st.d;
+            const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
+            const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
+            const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
+            p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+            reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
+        }
+        if (threadIdx.x == 0)
+            add_rays(p.rays, (unsigned long long)__popcll(own & (npt == 64u ? ~0ull : ((1ull << npt) - 1ull))) * p.spp);
+        return;
     }
     const uint32_t tp = (p.ntri + 1) / 2;
     uint32_t pos = 0;                                   // samples whose draws this lane's state has passed
@@ -3367,6 +3476,13 @@ int launch_bin(void* stream, const kbin& b) {
     if (n == 0) return 0;
     if (n > 0xffffffffull * 256ull) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(iqpt_bin_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, b);
+    return (int)hipGetLastError();
+}
+
+int launch_certain(void* stream, const kbin& b, uint32_t* certain) {
+    const uint32_t ntiles = b.ntx * b.nty;
+    if (ntiles == 0) return 0;
+    hipLaunchKernelGGL(iqpt_certain_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, b, certain);
     return (int)hipGetLastError();
 }
 

@@ -41,9 +41,9 @@ constexpr double kSplitAutoPixelsPerLane = 1.2;
 // CU by default (profiles/r02/split_share_v12_lanes.json: 16 beats 8 at N <= 4, equal at N = 8)
 constexpr double kChainAutoPixelsPerLane = 2.0;
 // spec launches: AUTO takes them below this many owned pixels per resident lane of the
-// plain kernel (C3 shares: N = 8 has 0.8, N = 4 1.6; pipelined spec launches 0.29 / 0.51 ms per step through
-// the gather against chain 0.39 / 0.62; N = 2, 3.2, stays plain: 0.91 against 0.93; profiles/r03/share_modes.json)
-constexpr double kSpecAutoPixelsPerLane = 2.0;
+// plain kernel (C3 shares: N = 8 has 0.8, N = 4 1.6, N = 2 3.2; pipelined spec launches 0.27 / 0.47 / 0.87 ms
+// per step through the gather against plain 0.95 / 1.0 / 0.91; N = 1, 6.3, stays plain; profiles/r03/share_modes.json)
+constexpr double kSpecAutoPixelsPerLane = 4.0;
 constexpr uint32_t kChainWavesPerCu = 16;
 constexpr size_t kSplitResBudget = size_t(8) << 30;   // speculative results (bytes)
 
@@ -128,6 +128,9 @@ struct iqpt_ctx {
     bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
     // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
     uint32_t* d_cull = nullptr;
+    uint32_t* d_certain = nullptr;      // per tile: every camera ray certain to end on an emissive triangle
+    bool certain_valid = false;         // d_certain holds the current masks' flags (no material table)
+    bool certain_on = true;             // iqpt_debug_set_certain (A/B: 0 renders certain tiles normally)
     uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
     uint32_t* d_list = nullptr;         // candidate lists of the masks, then their offsets (tri, sph)
     uint64_t list_total = 0;
@@ -186,10 +189,13 @@ struct iqpt_ctx {
     bool spec_rho_valid = false;
     bool spec_last = false;
     uint32_t spec_rho0 = iqpt::kSpecRho0;   // window of a pixel without history (iqpt_debug_set_spec)
-    uint32_t spec_margin_div = 4;           // window margin: a quarter of the extra slots (iqpt_debug_set_spec)
+    uint32_t spec_margin_div = 16;          // window margin: 1/16 of the extra slots, at least 4 (iqpt_debug_set_spec;
+                                            // against 1/4, 5 % of the chains take a second round instead of 0.6 %,
+                                            // yet -4 % per launch at N = 2 / 4 / 8, profiles/r03/spec_margins.json)
     // spec launches (iqpt_debug_set_specfan): 0 the two kernels on two streams, pipelined (the default), 1 one
     // after the other on one stream (measurement), 2 spec + fan blocks in one grid (iqpt_specfan_kernel)
     int specfan_mode = 0;
+    bool fan_pipe = true;                // FAN launches pipelined (iqpt_debug_set_pipe)
     uint32_t spec_lead = 0xffffffffu;       // fused: spec blocks ahead of every fan block (all by default)
     // spec plan: the sphere pixels ordered by their last chain's work, heaviest first, the
     // heavy ones with 32 or 64 lanes; built on the host from an asynchronous read of the history (performance
@@ -205,15 +211,16 @@ struct iqpt_ctx {
     uint32_t spec_plan_n = 0;            // pixels of the plan (0: none; must equal n_chain_pix to be used)
     uint32_t spec_plan_blocks = 0;
     uint32_t spec_plan_age = 0;          // launches since the plan was built
-    // Pipelined spec launches: the spec kernel on `stream`, the fan kernel on `stream2`, and
-    // no join at the end of a launch — launch k + 1's spec pixels follow launch k's on `stream`, its fan
-    // pixels launch k's on `stream2` (the two sets are disjoint), so the fan stream runs ahead into the spec
-    // kernel's tail. Every other entry point joins (join_streams). Frame copies (iqpt_copy_frame_device_async)
+    // Pipelined spec and fan launches: the spec kernel (or, FAN, the plain kernel over the
+    // split tiles) on `stream`, the fan kernel on `stream2`, and no join at the end of a launch — launch
+    // k + 1's pixels on `stream` follow launch k's there, its fan pixels launch k's on `stream2` (the two sets
+    // are disjoint and the same for launches of one kind), so the fan stream runs ahead into the other's tail. Every other entry point joins (join_streams). Frame copies (iqpt_copy_frame_device_async)
     // go on `stream3` behind both kernels; from the first such copy on, launches write the two frame buffers
     // in turn and a launch waits only for the copy that read its buffer two launches earlier.
-    bool spec_pipe = false;              // the last launch was pipelined and nothing has joined since
+    bool pipe = false;                   // the last launch was pipelined and nothing has joined since
+    int pipe_kind = 0;                   // ... a spec launch (1) or a fan launch (2)
     hipStream_t stream3 = nullptr;
-    hipEvent_t ev_spec_end = nullptr;    // on `stream`, after the last pipelined spec kernel
+    hipEvent_t ev_pipe_end = nullptr;    // on `stream`, after the last pipelined launch's first kernel
     hipEvent_t ev_copy_cur = nullptr, ev_copy_alt = nullptr;   // on `stream3`, after the copy of d_bgra / d_bgra_alt
     bool copy_pend_cur = false, copy_pend_alt = false;
     unsigned long long* d_spec_tl = nullptr;   // iqpt_debug_spec_timeline: per spec block timestamps
@@ -275,7 +282,7 @@ int join_streams(iqpt_ctx* c) {
     if (c->copy_pend_cur) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
     if (c->copy_pend_alt) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_alt, 0));
     c->copy_pend_cur = c->copy_pend_alt = false;
-    c->spec_pipe = false;
+    c->pipe = false;
     c->next_on_main = true;
     c->ovl_zero = true;
     c->last_ovl = false;
@@ -570,10 +577,25 @@ int build_cull(iqpt_ctx* c) {
     b.cull = c->d_cull;
     const int le = iqpt::launch_bin(c->stream, b);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "cull binning kernel");
+    const uint32_t ntiles = c->cull_ntx * c->cull_nty;
+    // certain tiles (iq_interval.h tri_certain): only under the reference's materials (every triangle emissive)
+    c->certain_valid = false;
+    if (c->d_certain) (void)hipFree(c->d_certain);
+    c->d_certain = nullptr;
+    std::vector<uint32_t> certain;
+    if (!c->d_mats && ntiles > 0) {
+        if (hipMalloc(&c->d_certain, (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "certain tile flags");
+        const int lc = iqpt::launch_certain(c->stream, b, c->d_certain);
+        if (lc != 0) return iqpt::hip_fail((hipError_t)lc, "certain tile kernel");
+        certain.resize(ntiles);
+        IQPT_HIP(hipMemcpyAsync(certain.data(), c->d_certain, (size_t)ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                c->stream));
+        c->certain_valid = true;
+    }
     // queue order over tiles (a queue chunk is one tile): most expensive first, so the pixels that set
     // the end of the launch are cheap ones. Cost = candidate triangle pairs + 8 x candidate sphere pairs
     // (a camera ray that can hit a sphere starts an Oren-Nayar path: more rays and the scatter shading).
-    const uint32_t ntiles = c->cull_ntx * c->cull_nty;
     uint32_t* d_cnt = nullptr;
     IQPT_HIP(hipMalloc(&d_cnt, 2 * (size_t)ntiles * sizeof(uint32_t)));
     std::vector<uint32_t> cnt(2 * (size_t)ntiles);
@@ -588,6 +610,10 @@ int build_cull(iqpt_ctx* c) {
     }
     std::vector<uint32_t> cost(ntiles);
     for (uint32_t t = 0; t < ntiles; ++t) cost[t] = cnt[t] + 8u * cnt[ntiles + t];
+    // a certain tile costs a fold of its samples: last in the order
+    if (c->certain_valid && c->certain_on)
+        for (uint32_t t = 0; t < ntiles; ++t)
+            if (certain[t]) cost[t] = 0u;
     // candidate lists for the streamed kernel (pairs of a tile without scanning its mask words): only
     // worth building where the masks are long; skipped when they would exceed the list budget
     if (c->d_list) (void)hipFree(c->d_list);
@@ -1064,7 +1090,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream3) (void)hipStreamDestroy(c->stream3);
-    for (hipEvent_t e : {c->ev_spec_end, c->ev_copy_cur, c->ev_copy_alt})
+    for (hipEvent_t e : {c->ev_pipe_end, c->ev_copy_cur, c->ev_copy_alt})
         if (e) (void)hipEventDestroy(e);
     free_split(c);
     for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_tl, (void*)c->d_spec_plan})
@@ -1075,6 +1101,7 @@ int iqpt_destroy(iqpt_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
+    if (c->d_certain) (void)hipFree(c->d_certain);
     if (c->d_tile_order) (void)hipFree(c->d_tile_order);
     if (c->d_list) (void)hipFree(c->d_list);
     for (auto& tl : c->timed)
@@ -1413,6 +1440,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             if ((st = build_cull(c)) != IQPT_OK) return st;
         }
         p.cull = c->d_cull;
+        p.certain = c->certain_valid && c->certain_on ? c->d_certain : nullptr;
         p.tile_order = c->d_tile_order;
         p.cull_ntx = c->cull_ntx;
         p.cull_wt = c->cull_wt;
@@ -1505,8 +1533,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         split = occ_s > 0 && (c->split_mode == IQPT_SPLIT_ON || (double)c->npix < iqpt::kSplitAutoPixelsPerLane * lanes);
     }
     // pipelined spec launches continue without a join (the launch below orders itself); the others never overlap
-    const bool spec_pipe_next = spec && c->specfan_mode == 0 && c->spec_pipe;
-    if ((split || chain || fan || spec) && !spec_pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
+    const bool fan_pipe = fan && !chain && !spec && c->fan_pipe;   // pipelined FAN launch
+    const bool pipe_next = c->pipe && ((spec && c->specfan_mode == 0 && c->pipe_kind == 1) || (fan_pipe && c->pipe_kind == 2));
+    if ((split || chain || fan || spec) && !pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
     // split launches with the anchored tiles in the fan kernel beside the four split passes
     const bool fan_split = split && fan_ok && c->fan_anchored;
     const size_t ns_cap = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
@@ -1622,7 +1651,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             c->overlap_mode = IQPT_OVERLAP_OFF;
         }
     }
-    if (!ovl && !spec_pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
+    if (!ovl && !pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
     hipStream_t ls = c->stream;                       // the launch's stream
     if (ovl) {
         opt |= iqpt::kOptOverlap;
@@ -1670,11 +1699,68 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     if (e0) (void)hipEventRecord(e0, ls);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
     int le = 0;
+    // pipelined launches (spec, FAN): the frame buffer this launch writes (the other one once copies are
+    // asynchronous), after the copy that read it two launches ago; the second stream after everything
+    // `stream` held unless the launch continues a pipeline
+    auto pipe_begin = [&]() -> int {
+        if (c->d_bgra_alt) {
+            std::swap(c->d_bgra, c->d_bgra_alt);
+            std::swap(c->ev_copy_cur, c->ev_copy_alt);
+            std::swap(c->copy_pend_cur, c->copy_pend_alt);
+            p.bgra = c->d_bgra;
+        }
+        if (c->copy_pend_cur) {
+            IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
+            IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_copy_cur, 0));
+            c->copy_pend_cur = false;
+        }
+        if (!pipe_next) {
+            IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
+            IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
+        }
+        return IQPT_OK;
+    };
+    // ... and its end: no join; the copy stream and every other entry point wait for both streams
+    auto pipe_end = [&](int kind) -> int {
+        IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
+        if (!c->ev_pipe_end && hipEventCreateWithFlags(&c->ev_pipe_end, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            return iqpt::fail(IQPT_ERR_HIP, "pipelined launch events");
+        }
+        IQPT_HIP(hipEventRecord(c->ev_pipe_end, c->stream));
+        e1b = take_event(c);
+        if (e1b) (void)hipEventRecord(e1b, c->stream2);
+        c->s2_pending = true;
+        c->pipe = le == 0;
+        c->pipe_kind = kind;
+        return IQPT_OK;
+    };
     if (ovl) {
         le = iqpt::launch_render(ls, p, grid, lds, stream_batches, opt);
         c->ovl_epoch += 1;
         c->next_on_main = !c->next_on_main;
         if (le != 0) c->ovl_zero = true;     // a failed launch breaks the chain's counts: restart it
+    } else if (fan_pipe) {
+        // pipelined FAN launch: the split tiles in the plain kernel on stream (queue[0], zeroed there), the
+        // anchored tiles in the fan kernel on stream2
+        if ((st = pipe_begin()) != IQPT_OK) return st;
+        IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
+        p.queue = c->d_queue;
+        p.ovl_err = c->d_ovl_err;
+        if (c->n_split_tiles > 0) {
+            iqpt::kparams ps = p;
+            ps.tile_order = c->d_split + c->n_anchor;
+            ps.nqueue = c->n_split_tiles;
+            const uint64_t want_s = ((uint64_t)c->n_split_tiles * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
+            const uint32_t grid_s = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_s, (uint64_t)c->num_cus * occ));
+            le = iqpt::launch_render(c->stream, ps, grid_s, lds, stream_batches, opt);
+        }
+        if (le == 0 && c->n_anchor > 0) {
+            p.tile_order = c->d_split;
+            p.nqueue = c->n_anchor;
+            le = iqpt::launch_fan(c->stream2, p, c->n_anchor, opt);
+        }
+        if ((st = pipe_end(2)) != IQPT_OK) return st;
     } else if (chain || fan) {
         // chain: the split set's pixels in iqpt_chain_kernel (pixels from queue[1]) on stream; fan: the split
         // set's tiles in the plain kernel (queue[0]) on stream. Beside it on stream2 the anchored tiles, in
@@ -1784,26 +1870,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.res = c->d_spec_res;
         if (n > 0 && !c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, (size_t)n * sizeof(uint32_t), c->stream));
         c->spec_rho_valid = c->spec_rho_valid || n > 0;
-        if (c->specfan_mode == 0) {
-            // pipelined: the frame buffer this launch writes (the other one once copies are asynchronous),
-            // after the copy that read it two launches ago; the fan stream after everything `stream` held
-            // unless it continues a pipeline
-            if (c->d_bgra_alt) {
-                std::swap(c->d_bgra, c->d_bgra_alt);
-                std::swap(c->ev_copy_cur, c->ev_copy_alt);
-                std::swap(c->copy_pend_cur, c->copy_pend_alt);
-                p.bgra = c->d_bgra;
-            }
-            if (c->copy_pend_cur) {
-                IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
-                IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_copy_cur, 0));
-                c->copy_pend_cur = false;
-            }
-            if (!c->spec_pipe) {
-                IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
-                IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
-            }
-        }
+        if (c->specfan_mode == 0 && (st = pipe_begin()) != IQPT_OK) return st;
         iqpt::kparams pf = p;
         pf.tile_order = c->d_fan_tiles;
         pf.fan_lanes = c->d_fan_lanes;
@@ -1862,16 +1929,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         } else {
             if (n > 0) le = iqpt::launch_spec(c->stream, p, ks2, opt);
             if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream2, pf, c->n_fan_tiles, opt);
-            IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
-            if (!c->ev_spec_end && hipEventCreateWithFlags(&c->ev_spec_end, hipEventDisableTiming) != hipSuccess) {
-                (void)hipGetLastError();
-                return iqpt::fail(IQPT_ERR_HIP, "pipelined spec events");
-            }
-            IQPT_HIP(hipEventRecord(c->ev_spec_end, c->stream));
-            e1b = take_event(c);
-            if (e1b) (void)hipEventRecord(e1b, c->stream2);
-            c->s2_pending = true;
-            c->spec_pipe = le == 0;
+            if ((st = pipe_end(1)) != IQPT_OK) return st;
         }
         // read this launch's history for the next plan: before the first plan, then every kSpecReplan launches
         if (n > 0 && c->spec_plan_mode == 1 && !c->spec_rho_pending && le == 0 &&
@@ -2256,6 +2314,44 @@ int iqpt_debug_spec_plan(iqpt_ctx* c, int mode) {
     return IQPT_OK;
 }
 
+/* Internal (A/B, tests): certain tiles (kparams::certain) folded at once (1, the default) or rendered like
+ * every other tile (0). Rebuilds the masks at the next launch. */
+int iqpt_debug_set_certain(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->certain_on = on != 0;
+    c->cull_valid = false;
+    return IQPT_OK;
+}
+
+/* Internal (tools, tests): certain tiles of the current masks (*n; 0 without masks or flags), the tile
+ * grid's width in tiles (*ntx) and, if flags is not NULL, up to cap per-tile flags. Synchronises. */
+int iqpt_debug_certain_tiles(iqpt_ctx* c, uint32_t* n, uint32_t* ntiles, uint32_t* ntx, uint32_t* flags, uint32_t cap) {
+    if (!c || !n || !ntiles || !ntx) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *ntx = c->cull_ntx;
+    *n = *ntiles = 0;
+    int st = enter(c);
+    if (st) return st;
+    if (!c->certain_valid || !c->d_certain) return IQPT_OK;
+    const uint32_t nt = c->cull_ntx * c->cull_nty;
+    std::vector<uint32_t> v(nt);
+    IQPT_HIP(hipMemcpy(v.data(), c->d_certain, (size_t)nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (uint32_t t = 0; t < nt; ++t) *n += v[t] ? 1u : 0u;
+    *ntiles = nt;
+    if (flags) std::memcpy(flags, v.data(), std::min(nt, cap) * sizeof(uint32_t));
+    return IQPT_OK;
+}
+
+/* Internal (A/B): FAN launches pipelined (1, the default) or joined after every launch (0). */
+int iqpt_debug_set_pipe(iqpt_ctx* c, int fan_pipe) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->fan_pipe = fan_pipe != 0;
+    return IQPT_OK;
+}
+
 /* Internal (A/B): how spec launches run the fan tiles beside the sphere pixels — 0 two kernels on two
  * streams, pipelined across launches (the default), 1 two kernels on one stream, 2 one grid
  * (iqpt_specfan_kernel) — and, in one grid, how many spec blocks precede every fan block (0xffffffff: all;
@@ -2274,7 +2370,7 @@ int iqpt_debug_set_specfan(iqpt_ctx* c, int mode, uint32_t lead) {
  * and the window margin divisor. 0 restores a default; the history is dropped. */
 int iqpt_debug_set_spec(iqpt_ctx* c, uint32_t rho0, uint32_t margin_div) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    c->spec_margin_div = margin_div ? margin_div : 4u;
+    c->spec_margin_div = margin_div ? margin_div : 16u;
     c->spec_rho0 = rho0 ? rho0 : iqpt::kSpecRho0;
     c->spec_rho_valid = false;
     return IQPT_OK;
@@ -2321,7 +2417,7 @@ int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
     // synchronising call (iqpt_sync, iqpt_read, ...); one already latched fails the copy now
     if (c->dev_err) return check_dev_err(c);
     hipStream_t cs = c->stream;
-    if (c->spec_pipe) {
+    if (c->pipe) {
         // pipelined spec launches: the copy on stream3 behind both kernels of the last launch; from here on
         // the launches alternate two frame buffers
         if (!c->d_bgra_alt && hipMalloc(&c->d_bgra_alt, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) {
@@ -2335,7 +2431,7 @@ int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
             (void)hipGetLastError();
             return iqpt::fail(IQPT_ERR_HIP, "frame copy stream");
         }
-        IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_spec_end, 0));
+        IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_pipe_end, 0));
         IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_s2, 0));
         const int le = iqpt::launch_relayout(c->stream3, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
                                              c->set.nrows, 1, 1, true);
@@ -2365,7 +2461,7 @@ int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
 
 int iqpt_frame_stream(iqpt_ctx* c, void** stream) {
     if (!c || !stream) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    *stream = (void*)(c->spec_pipe && c->stream3 ? c->stream3 : ((c->last_ovl && c->last_ls) ? c->last_ls : c->stream));
+    *stream = (void*)(c->pipe && c->stream3 ? c->stream3 : ((c->last_ovl && c->last_ls) ? c->last_ls : c->stream));
     return IQPT_OK;
 }
 

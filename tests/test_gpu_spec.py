@@ -262,11 +262,12 @@ def test_spec_plan_async_c3_share8(require_gpu):
     assert outs[0][3] == outs[1][3]
 
 
-def test_pipelined_spec_async_copies(require_gpu):
-    """Pipelined spec launches (the fan stream runs ahead, no join per launch) with a stream-ordered frame copy
-    after every launch, as the multi-GPU gather issues them: copy k holds exactly launch k's frame (the launches
-    write two frame buffers in turn), a reset in the middle joins the streams, and the final state is the
-    oracle's bit for bit."""
+@pytest.mark.parametrize("split,expect", [(SPLIT_SPEC, 6), (3, 3)])
+def test_pipelined_async_copies(require_gpu, split, expect):
+    """Pipelined spec and FAN launches (the fan stream runs ahead, no join per launch) with a stream-ordered
+    frame copy after every launch, as the multi-GPU gather issues them: copy k holds exactly launch k's frame
+    (the launches write two frame buffers in turn), a reset in the middle joins the streams, and the final
+    state is the oracle's bit for bit."""
     import torch
     from iqpt import PathTracer, _lib, make_camera
     w, h = 484, 270
@@ -275,7 +276,7 @@ def test_pipelined_spec_async_copies(require_gpu):
     sc, pk = scene_for("cornell")
     cam = make_camera(w, h)
     pt = PathTracer(w, h, pixels=ps, max_depth=8)
-    pt.set_split(SPLIT_SPEC)
+    pt.set_split(split)
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
@@ -296,7 +297,7 @@ def test_pipelined_spec_async_copies(require_gpu):
         bufs.append(b)
         want.append(fr.bgra.copy())
     torch.cuda.synchronize()
-    assert mode_of(pt) == 6
+    assert mode_of(pt) == expect
     for b, wv in zip(bufs, want):
         assert np.array_equal(b.cpu().numpy().view(np.uint8).reshape(-1, 4), wv)
     lin, bgra = pt.read()

@@ -97,7 +97,7 @@ if npx.value and nb.value == n.value:
     rho_a = np.array(rho[:npx.value], dtype=np.float64)
     r = np.where(rho_a > 0, rho_a, 576.0)
     m = r * spp / 256.0
-    m = np.minimum(mcap, np.maximum(spp, m + np.maximum(4, (m - spp) / 4) + 4))   # spec_window (margin 4)
+    m = np.minimum(mcap, np.maximum(spp, m + np.maximum(4, (m - spp) / 16) + 4))   # spec_window (margin 1/16)
     w = m * np.maximum(r, 256.0) / 256.0
     rows = []
     for b in range(nb.value):
