@@ -81,9 +81,10 @@ struct kparams {
     // camera rays of the tile may hit (iq_interval.h); null = no culling for this launch
     const uint32_t* cull;
     uint32_t cull_ntx, cull_wt, cull_stride;
-    // per tile: 1 if every camera ray of the tile is certain to end on an emissive triangle (no sphere
-    // candidate, a candidate triangle every ray of the tile's bundle hits: iq_interval.h tri_certain; the
-    // reference's materials only); null = none. Such a tile's samples are (1, 1, 1) folds and two draws.
+    // per tile, two words: the 64-bit mask of its pixels (storage order inside the tile) whose every camera
+    // ray is certain to end on an emissive triangle (no sphere candidate in the tile, a candidate triangle
+    // every ray of the pixel's bundle hits: iq_interval.h tri_certain; the reference's materials only);
+    // null = none. Such a pixel's samples are (1, 1, 1) folds and two draws each.
     const uint32_t* certain;
     // work queue over tiles: queue position q -> tile tile_order[q] (null = identity); built with the
     // masks, most expensive tiles first (longest-processing-time order: a shorter launch tail)

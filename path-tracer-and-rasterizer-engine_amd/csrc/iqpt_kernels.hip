@@ -1215,9 +1215,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // tile, 2 leftovers [chunk_next, chunk_end) of the leftover list, 3 the light pixels of a split tile
     // (anchored) — and the split tile's first slot and storage index
     uint32_t chunk_kind = 0, chunk_sp0 = 0, chunk_first = 0, chunk_r = 0;
-    // the chunk's tile is certain (kparams::certain): its pixels take the whole launch at once (refill)
+    // the chunk's tile's certain pixels (kparams::certain): they take the whole launch at once (refill)
     constexpr bool kCertain = !kSplit && (OPT & kOptAccTable) && !(OPT & kOptMaterials) && !(OPT & kOptStats);
-    bool chunk_certain = false;
+    uint64_t chunk_certain = 0;
     uint32_t queue_total = kOverlap ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : (p.nqueue ? p.nqueue : p.ntiles), n_runs = 0;
     if (kSplit) {
         // round 1, longest tasks first: the split tiles' light pixels (anchored chains with scatters, in
@@ -1325,7 +1325,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         t = p.tile_order ? p.tile_order[q] : q;
                     }
                     chunk_tile = t;
-                    chunk_certain = kCertain && p.certain != nullptr && p.certain[t] != 0u;
+                    chunk_certain = (kCertain && p.certain != nullptr)
+                                        ? ((uint64_t)p.certain[2 * (size_t)t] | ((uint64_t)p.certain[2 * (size_t)t + 1] << 32))
+                                        : 0ull;
                     const uint32_t tx = t % p.ntx, ty = t / p.ntx;
                     const uint32_t th = min(kCullTile, p.nrows - ty * kCullTile);
                     const uint32_t tw = min(kCullTile, p.ncols - tx * kCullTile);
@@ -1418,7 +1420,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         if (kSplit && chunk_kind == 0) lds_sp[threadIdx.x] = make_uint4(0u, 0u, 0u, 0u);
                     }
                     depth = 0;
-                    if (kCertain && chunk_certain) {
+                    if (kCertain && ((chunk_certain >> (pix - chunk_first)) & 1ull)) {
                         // a certain tile (kparams::certain): every sample takes the camera's two draws and
                         // ends on an emissive triangle, clamped colour (1, 1, 1), whose mean term c / n is the
                         // table's RN(1 / n) (mean_terms): the launch's samples fold at once, in order
@@ -1449,7 +1451,8 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             if (kCertain && chunk_certain) {
                 // the certain pixels of this pass are complete: their rays, and (overlapped launches) their
                 // tile's completion count once their stores are done
-                const uint32_t nfin = min((uint32_t)__popcll(need), avail);
+                const uint32_t took = prefix_below(need) < avail && ((need >> lane) & 1ull) ? 1u : 0u;
+                const uint32_t nfin = (uint32_t)__popcll(__ballot(took && !active));
                 if (nfin) {
                     wave_rays += (uint64_t)nfin * p.spp;
                     if (kOverlap && p.tile_done) {
@@ -2176,22 +2179,23 @@ __global__ __launch_bounds__(256) void iqpt_bin_kernel(const kbin b) {
     b.cull[gid] = bits;
 }
 
-// Per tile: 1 if the tile has no sphere candidate and one of its candidate triangles is accepted by every
-// camera ray of the tile's bundle (iq_interval.h tri_certain). Under the reference's materials (the runtime
-// launches this only without a material table) every sample of such a tile ends on its first ray with
-// the emissive colour, clamped to (1, 1, 1), after the two jitter draws (path_tracer.cu:278, 341-358;
-// camera.cu:24-25). Run after iqpt_bin_kernel on the same stream.
-__global__ __launch_bounds__(256) void iqpt_certain_kernel(const kbin b, uint32_t* certain) {
-    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-    if (t >= b.ntx * b.nty) return;
+// Per pixel: certain if its tile has no sphere candidate and one of the tile's candidate triangles is
+// accepted by every camera ray of the pixel's own bundle (its jitter square; iq_interval.h tri_certain).
+// Under the reference's materials (the runtime launches this only without a material table) every
+// sample of such a pixel ends on its first ray with the emissive colour, clamped to (1, 1, 1), after the
+// two jitter draws (path_tracer.cu:278, 341-358; camera.cu:24-25). One wave per tile, lane = pixel in the
+// tile's storage order (row-major inside the tile); certain[2 t], certain[2 t + 1] = the tile's 64-bit
+// mask. Run after iqpt_bin_kernel on the same stream.
+__global__ __launch_bounds__(64) void iqpt_certain_kernel(const kbin b, uint32_t* certain) {
+    const uint32_t t = blockIdx.x, lane = threadIdx.x;
     const uint32_t* m = b.cull + (size_t)t * b.stride;
-    uint32_t ok = 0u;
     bool sph = false;
     for (uint32_t w = b.wt; w < b.stride; ++w) sph = sph || m[w] != 0u;
-    if (!sph) {
-        const uint32_t tx = t % b.ntx, ty = t / b.ntx;
-        const uint32_t c0 = tx * kCullTile, c1 = min(c0 + kCullTile, b.ncols) - 1u;
-        const uint32_t k0 = ty * kCullTile, k1 = min(k0 + kCullTile, b.nrows) - 1u;
+    const uint32_t tx = t % b.ntx, ty = t / b.ntx;
+    const uint32_t tw = min(kCullTile, b.ncols - tx * kCullTile), th = min(kCullTile, b.nrows - ty * kCullTile);
+    bool ok = false;
+    if (!sph && lane < tw * th) {
+        const uint32_t col = tx * kCullTile + lane % tw, row = ty * kCullTile + lane / tw;
         iqiv::camera_in ci;
         ci.width = b.width;
         ci.height = b.height;
@@ -2202,7 +2206,8 @@ __global__ __launch_bounds__(256) void iqpt_certain_kernel(const kbin b, uint32_
         ci.cam_const = (int)b.cam_const;
         ci.near_rw = b.cam_near_rw;
         ci.far_rw = b.cam_far_rw;
-        const iqiv::bundle bd = iqiv::camera_bundle(ci, b.x0 + c0, b.x0 + c1, b.y0 + k0 * b.ystep, b.y0 + k1 * b.ystep);
+        const uint32_t x = b.x0 + col, y = b.y0 + row * b.ystep;
+        const iqiv::bundle bd = iqiv::camera_bundle(ci, x, x, y, y);
         for (uint32_t w = 0; w < b.wt && bd.ok && !ok; ++w) {
             uint32_t bits = m[w];
             while (bits && !ok) {
@@ -2215,12 +2220,16 @@ __global__ __launch_bounds__(256) void iqpt_certain_kernel(const kbin b, uint32_
                     const float v0[3] = {tr[0].x, tr[0].y, tr[0].z};
                     const float e1[3] = {tr[0].w, tr[1].x, tr[1].y};
                     const float e2[3] = {tr[1].z, tr[1].w, tr[2].x};
-                    ok = iqiv::tri_certain(bd, v0, e1, e2) ? 1u : 0u;
+                    ok = iqiv::tri_certain(bd, v0, e1, e2);
                 }
             }
         }
     }
-    certain[t] = ok;
+    const uint64_t mask = __ballot(ok);
+    if (lane == 0) {
+        certain[2 * (size_t)t] = (uint32_t)mask;
+        certain[2 * (size_t)t + 1] = (uint32_t)(mask >> 32);
+    }
 }
 
 // Per tile: candidate triangle pairs and sphere pairs of its masks (the queue-order cost and the
@@ -2871,7 +2880,11 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
         ay = a[1];
         az = a[2];
     }
-    if (p.certain != nullptr && p.certain[t] != 0u) {
+    const uint64_t valid = npt == 64u ? ~0ull : ((1ull << npt) - 1ull);
+    const uint64_t cmask = p.certain != nullptr
+                               ? ((uint64_t)p.certain[2 * (size_t)t] | ((uint64_t)p.certain[2 * (size_t)t + 1] << 32))
+                               : 0ull;
+    if ((cmask & valid) == valid) {
         // a certain tile (kparams::certain): every sample takes the camera's two draws and ends on an emissive
         // triangle, clamped colour (1, 1, 1), whose mean term c / n is the table's RN(1 / n); wave 0 folds
         // the launch's samples in order, the other waves have nothing to do
@@ -3482,7 +3495,7 @@ int launch_bin(void* stream, const kbin& b) {
 int launch_certain(void* stream, const kbin& b, uint32_t* certain) {
     const uint32_t ntiles = b.ntx * b.nty;
     if (ntiles == 0) return 0;
-    hipLaunchKernelGGL(iqpt_certain_kernel, dim3((ntiles + 255) / 256), dim3(256), 0, (hipStream_t)stream, b, certain);
+    hipLaunchKernelGGL(iqpt_certain_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, b, certain);
     return (int)hipGetLastError();
 }
 

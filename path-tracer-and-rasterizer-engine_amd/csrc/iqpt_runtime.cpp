@@ -128,7 +128,7 @@ struct iqpt_ctx {
     bool fast_rcp_ok = true;   // packet within the range of the kOptFastDiv reciprocals (upload)
     // kOptCull tile masks (iq_interval.h), rebuilt on the stream after a camera or packet change
     uint32_t* d_cull = nullptr;
-    uint32_t* d_certain = nullptr;      // per tile: every camera ray certain to end on an emissive triangle
+    uint32_t* d_certain = nullptr;      // per tile: 64-bit mask of pixels certain to end on an emissive triangle
     bool certain_valid = false;         // d_certain holds the current masks' flags (no material table)
     bool certain_on = true;             // iqpt_debug_set_certain (A/B: 0 renders certain tiles normally)
     uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
@@ -584,12 +584,12 @@ int build_cull(iqpt_ctx* c) {
     c->d_certain = nullptr;
     std::vector<uint32_t> certain;
     if (!c->d_mats && ntiles > 0) {
-        if (hipMalloc(&c->d_certain, (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
-            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "certain tile flags");
+        if (hipMalloc(&c->d_certain, 2 * (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "certain pixel masks");
         const int lc = iqpt::launch_certain(c->stream, b, c->d_certain);
-        if (lc != 0) return iqpt::hip_fail((hipError_t)lc, "certain tile kernel");
-        certain.resize(ntiles);
-        IQPT_HIP(hipMemcpyAsync(certain.data(), c->d_certain, (size_t)ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+        if (lc != 0) return iqpt::hip_fail((hipError_t)lc, "certain pixel kernel");
+        certain.resize(2 * (size_t)ntiles);
+        IQPT_HIP(hipMemcpyAsync(certain.data(), c->d_certain, 2 * (size_t)ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                 c->stream));
         c->certain_valid = true;
     }
@@ -610,10 +610,17 @@ int build_cull(iqpt_ctx* c) {
     }
     std::vector<uint32_t> cost(ntiles);
     for (uint32_t t = 0; t < ntiles; ++t) cost[t] = cnt[t] + 8u * cnt[ntiles + t];
-    // a certain tile costs a fold of its samples: last in the order
+    // a certain pixel costs a fold of its samples: a tile's cost scales with its uncertain pixels (fully
+    // certain tiles last in the order)
     if (c->certain_valid && c->certain_on)
-        for (uint32_t t = 0; t < ntiles; ++t)
-            if (certain[t]) cost[t] = 0u;
+        for (uint32_t t = 0; t < ntiles; ++t) {
+            const uint32_t tx = t % c->cull_ntx, ty = t / c->cull_ntx;
+            const uint32_t npt = std::min(iqpt::kCullTile, c->ncols - tx * iqpt::kCullTile) *
+                                 std::min(iqpt::kCullTile, c->set.nrows - ty * iqpt::kCullTile);
+            const uint32_t nc = (uint32_t)__builtin_popcountll((uint64_t)certain[2 * (size_t)t] |
+                                                               ((uint64_t)certain[2 * (size_t)t + 1] << 32));
+            cost[t] = (uint32_t)(((uint64_t)cost[t] * (npt - std::min(nc, npt)) + npt - 1) / npt);
+        }
     // candidate lists for the streamed kernel (pairs of a tile without scanning its mask words): only
     // worth building where the masks are long; skipped when they would exceed the list budget
     if (c->d_list) (void)hipFree(c->d_list);
@@ -2325,9 +2332,10 @@ int iqpt_debug_set_certain(iqpt_ctx* c, int on) {
     return IQPT_OK;
 }
 
-/* Internal (tools, tests): certain tiles of the current masks (*n; 0 without masks or flags), the tile
- * grid's width in tiles (*ntx) and, if flags is not NULL, up to cap per-tile flags. Synchronises. */
-int iqpt_debug_certain_tiles(iqpt_ctx* c, uint32_t* n, uint32_t* ntiles, uint32_t* ntx, uint32_t* flags, uint32_t cap) {
+/* Internal (tools, tests): certain pixels of the current masks (*n; 0 without masks or flags), the tile
+ * count and the tile grid's width in tiles (*ntx) and, if masks is not NULL, up to cap tiles' 64-bit
+ * masks (two words per tile). Synchronises. */
+int iqpt_debug_certain_tiles(iqpt_ctx* c, uint32_t* n, uint32_t* ntiles, uint32_t* ntx, uint32_t* masks, uint32_t cap) {
     if (!c || !n || !ntiles || !ntx) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     *ntx = c->cull_ntx;
     *n = *ntiles = 0;
@@ -2335,11 +2343,11 @@ int iqpt_debug_certain_tiles(iqpt_ctx* c, uint32_t* n, uint32_t* ntiles, uint32_
     if (st) return st;
     if (!c->certain_valid || !c->d_certain) return IQPT_OK;
     const uint32_t nt = c->cull_ntx * c->cull_nty;
-    std::vector<uint32_t> v(nt);
-    IQPT_HIP(hipMemcpy(v.data(), c->d_certain, (size_t)nt * sizeof(uint32_t), hipMemcpyDeviceToHost));
-    for (uint32_t t = 0; t < nt; ++t) *n += v[t] ? 1u : 0u;
+    std::vector<uint32_t> v(2 * (size_t)nt);
+    IQPT_HIP(hipMemcpy(v.data(), c->d_certain, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < v.size(); ++i) *n += (uint32_t)__builtin_popcount(v[i]);
     *ntiles = nt;
-    if (flags) std::memcpy(flags, v.data(), std::min(nt, cap) * sizeof(uint32_t));
+    if (masks) std::memcpy(masks, v.data(), std::min<size_t>(v.size(), 2 * (size_t)cap) * sizeof(uint32_t));
     return IQPT_OK;
 }
 

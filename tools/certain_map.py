@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Map of the certain tiles (kparams::certain, iq_interval.h tri_certain) of a config's frame: per 8x8 tile
-'#' certain, '.' anchored (no sphere candidate) but not certain, 'S' a sphere candidate. Prints the counts
+'#' every pixel certain, '+' at least half, '-' some, '.' none. Prints the counts
 and a character map, and writes them to --out.
 
     certain_map.py [--config c2] [--share 1] [--out f.json]"""
@@ -36,15 +36,29 @@ lb.iqpt_debug_certain_tiles.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POI
                                         C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint32]
 n, nt, ntx = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
 _lib.check(lb.iqpt_debug_certain_tiles(pt._h, C.byref(n), C.byref(nt), C.byref(ntx), None, 0), "certain")
-flags = (C.c_uint32 * nt.value)()
+flags = (C.c_uint32 * (2 * nt.value))()
 _lib.check(lb.iqpt_debug_certain_tiles(pt._h, C.byref(n), C.byref(nt), C.byref(ntx), flags, nt.value), "certain")
 info = (C.c_ulonglong * 8)()
 lb.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
-res = {"config": cfg.name, "share": args.share, "tiles": nt.value, "certain": n.value, "tiles_x": ntx.value}
+res = {"config": cfg.name, "share": args.share, "tiles": nt.value, "certain_pixels": n.value,
+       "pixels": ps.nrows * (ps.x1 - ps.x0), "tiles_x": ntx.value}
 rows = []
 w = ntx.value
+full = 0
+
+
+def cnt(t):
+    return bin(flags[2 * t]).count("1") + bin(flags[2 * t + 1]).count("1")
+
+
 for r in range(nt.value // w):
-    rows.append("".join("#" if flags[r * w + x] else "." for x in range(w)))
+    line = ""
+    for x in range(w):
+        k = cnt(r * w + x)
+        full += k == 64
+        line += "#" if k == 64 else ("+" if k >= 32 else ("-" if k > 0 else "."))
+    rows.append(line)
+res["full_tiles"] = full
 res["map"] = rows
 print(json.dumps({k: v for k, v in res.items() if k != "map"}))
 for line in rows[:: max(1, len(rows) // 40)]:

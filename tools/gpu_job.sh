@@ -1,19 +1,19 @@
-# r03 run 37: certain tiles (proven emissive first hits fold at once): parity, default bench, shares
+# r03 run 38: per-pixel certain masks: parity, default bench, shares
 mkdir -p gpurun_out
 O=gpurun_out
-timeout -k 10 120 python3 tools/certain_map.py --out $O/r03_37_certain_map.json && timeout -k 10 900 python -u -m pytest tests/test_gpu_certain.py tests/test_gpu_fullframe.py tests/test_gpu_parity.py tests/test_gpu_fan.py tests/test_gpu_overlap.py -x -q --timeout 600 --timeout-method thread > $O/r03_37_tests.log 2>&1 || { tail -40 $O/r03_37_tests.log; exit 1; }
-tail -1 $O/r03_37_tests.log
+timeout -k 10 120 python3 tools/certain_map.py --out $O/r03_38_certain_map.json && timeout -k 10 900 python -u -m pytest tests/test_gpu_certain.py tests/test_gpu_fullframe.py tests/test_gpu_parity.py tests/test_gpu_fan.py tests/test_gpu_overlap.py -x -q --timeout 600 --timeout-method thread > $O/r03_38_tests.log 2>&1 || { tail -40 $O/r03_38_tests.log; exit 1; }
+tail -1 $O/r03_38_tests.log
 for r in 1 2; do
-timeout -k 10 300 python3 bench.py --steps 30 --warmup 8 --no-cpu-baseline --verify-rows 8 > $O/r03_37_default_$r.json 2> $O/r03_37_default_$r.err || { tail -20 $O/r03_37_default_$r.err; exit 1; }
-tail -1 $O/r03_37_default_$r.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('default', d['value'], d['ms_per_step'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'], d['roofline']['kernel_avg_ms'])"
+timeout -k 10 300 python3 bench.py --steps 30 --warmup 8 --no-cpu-baseline --verify-rows 8 > $O/r03_38_default_$r.json 2> $O/r03_38_default_$r.err || { tail -20 $O/r03_38_default_$r.err; exit 1; }
+tail -1 $O/r03_38_default_$r.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('default', d['value'], d['ms_per_step'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'], d['roofline']['kernel_avg_ms'])"
 done
 for s in 8 4 2; do
-  timeout -k 10 300 python3 bench.py --self-gather --share-of $s --steps 30 --warmup 8 --no-cpu-baseline --verify-rows 0 > $O/r03_37_share$s.json 2> $O/r03_37_share$s.err || { tail -20 $O/r03_37_share$s.err; exit 1; }
-  tail -1 $O/r03_37_share$s.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print($s, d['ms_per_step'], d['config']['launch_mode'], d['roofline']['kernel_avg_ms'])"
+  timeout -k 10 300 python3 bench.py --self-gather --share-of $s --steps 30 --warmup 8 --no-cpu-baseline --verify-rows 0 > $O/r03_38_share$s.json 2> $O/r03_38_share$s.err || { tail -20 $O/r03_38_share$s.err; exit 1; }
+  tail -1 $O/r03_38_share$s.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print($s, d['ms_per_step'], d['config']['launch_mode'], d['roofline']['kernel_avg_ms'])"
 done
-timeout -k 10 300 python3 tools/split_share.py --ns 8,4,2,1 --modes plain,spec --launches 10 --warm 4 --out $O/r03_37_modes.json > $O/r03_37_modes.log 2>&1 || { tail -20 $O/r03_37_modes.log; exit 1; }
+timeout -k 10 300 python3 tools/split_share.py --ns 8,4,2,1 --modes plain,spec --launches 10 --warm 4 --out $O/r03_38_modes.json > $O/r03_38_modes.log 2>&1 || { tail -20 $O/r03_38_modes.log; exit 1; }
 python3 -c "
 import json
-for r in json.load(open('$O/r03_37_modes.json'))['rows']:
+for r in json.load(open('$O/r03_38_modes.json'))['rows']:
     print(r['n'], {k: round(v, 4) for k, v in r.items() if k.endswith('ms_median')}, {k: v for k, v in r.items() if k.endswith('identical')})
 "
