@@ -75,6 +75,8 @@ def parse():
                     help="what the strong-scaling step gathers to rank 0: the BGRA8 frame or the float accumulators")
     ap.add_argument("--overlap", default="auto", choices=["auto", "off"],
                     help="overlapped launches on two streams (iqpt_set_overlap, DESIGN.md §3.8)")
+    ap.add_argument("--certain", default="on", choices=["on", "off"],
+                    help="A/B: certain pixels folded at once (iqpt_debug_set_certain, DESIGN.md §3.3)")
     ap.add_argument("--kernel-options", type=lambda v: int(v, 0), default=0,
                     help="A/B: render-kernel option mask (iqpt_debug_set_kernel_options; 0 = production)")
     ap.add_argument("--gather-sync", action="store_true",
@@ -363,6 +365,11 @@ def main():
         _lib.check(_lib.load().iqpt_debug_set_kernel_options(pt.handle, args.kernel_options),
                    "iqpt_debug_set_kernel_options")
     pt.set_overlap(_lib.OVERLAP_AUTO if args.overlap == "auto" else _lib.OVERLAP_OFF)
+    if args.certain == "off":
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_certain.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_certain(pt._h, 0), "iqpt_debug_set_certain")
     pt.set_camera(cam)
     t0 = time.perf_counter()
     pt.upload_packet(pk)
@@ -534,7 +541,7 @@ def main():
                                       ("none in the timed region; one reduce of the accumulators after it"
                                        if weak else f"gather of the {gathered} to rank 0 every step")
                                       + (" (rccl)" if on_gpu else " (gloo via host, rehearsal)")),
-                       "split": args.split, "overlap": args.overlap, "launch_mode": launch_mode,
+                       "split": args.split, "overlap": args.overlap, "certain": args.certain, "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {})},
             "n_ranks_seen": n_ranks_seen,
             "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),

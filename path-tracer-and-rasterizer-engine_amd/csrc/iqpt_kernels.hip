@@ -1216,7 +1216,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // (anchored) — and the split tile's first slot and storage index
     uint32_t chunk_kind = 0, chunk_sp0 = 0, chunk_first = 0, chunk_r = 0;
     // the chunk's tile's certain pixels (kparams::certain): they take the whole launch at once (refill)
-    constexpr bool kCertain = !kSplit && (OPT & kOptAccTable) && !(OPT & kOptMaterials) && !(OPT & kOptStats);
+    constexpr bool kCertain = !kSplit && !STREAM && (OPT & kOptAccTable) && !(OPT & kOptMaterials) && !(OPT & kOptStats);
     uint64_t chunk_certain = 0;
     uint32_t queue_total = kOverlap ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : (p.nqueue ? p.nqueue : p.ntiles), n_runs = 0;
     if (kSplit) {

@@ -578,12 +578,15 @@ int build_cull(iqpt_ctx* c) {
     const int le = iqpt::launch_bin(c->stream, b);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "cull binning kernel");
     const uint32_t ntiles = c->cull_ntx * c->cull_nty;
-    // certain tiles (iq_interval.h tri_certain): only under the reference's materials (every triangle emissive)
+    // certain pixels (iq_interval.h tri_certain): only under the reference's materials (every triangle
+    // emissive) and for scenes resident in LDS (streamed scenes run LDS batches with workgroup barriers, where
+    // a wave folding a certain pixel's launch holds the others: C4 +66 % per launch, profiles/r03/ab_certain.json)
     c->certain_valid = false;
     if (c->d_certain) (void)hipFree(c->d_certain);
     c->d_certain = nullptr;
     std::vector<uint32_t> certain;
-    if (!c->d_mats && ntiles > 0) {
+    const uint64_t resident_bytes = (uint64_t)ntp * iqpt::kTriPairFloat4 * 16u + (uint64_t)nsp * iqpt::kSphPairFloat4 * 16u;
+    if (!c->d_mats && ntiles > 0 && resident_bytes <= iqpt::kLdsResidentBytes) {
         if (hipMalloc(&c->d_certain, 2 * (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "certain pixel masks");
         const int lc = iqpt::launch_certain(c->stream, b, c->d_certain);
