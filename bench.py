@@ -59,8 +59,9 @@ def parse():
     ap.add_argument("--pmc-json", default="",
                     help="PMC traffic of the config's launch (tools/pmc_traffic.py; default: the newest "
                          "profiles/r0*/pmc_traffic_<config>*.json whose spp_per_launch equals this run's)")
-    ap.add_argument("--pmc-mix-json", default=str(REPO / "profiles" / "r02" / "c2_pmc_mix_v5.json"),
-                    help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy)")
+    ap.add_argument("--pmc-mix-json", default="",
+                    help="rocprofv3 instruction-mix counters of the same kernel (VALU pipe occupancy; default: the "
+                         "newest profiles/r0*/<config>_pmc_mix*.json)")
     ap.add_argument("--work-json", default="",
                     help="executed-work counters of the config (tools/work_counters.py; default "
                          "profiles/r02/work_<config>.json): prices C4/C5, reported beside C2's algorithmic price")
@@ -218,6 +219,31 @@ def find_pmc(cfg_name: str, spp: int, explicit: str):
     return None, why
 
 
+def find_mix(cfg_name: str, explicit: str):
+    """The PMC instruction-mix profile (tools/pmc_mix.py) of this config's current kernel: the explicit
+    file, else the newest round's profiles/r0*/<config>_pmc_mix*.json. Returns (profile, path)."""
+    cands = [Path(explicit)] if explicit else sorted(
+        (REPO / "profiles").glob(f"r0*/{cfg_name}_pmc_mix*.json"), key=lambda q: (q.parent.name, q.name), reverse=True)
+    for c in cands:
+        d = load_json(str(c), cfg_name)
+        if d:
+            return d, str(c.resolve().relative_to(REPO)) if c.resolve().is_relative_to(REPO) else str(c)
+    return None, None
+
+
+def certain_pixels(pt, _lib) -> int:
+    """Pixels of this context whose camera rays the certain-pixel proof resolves (0 when the path is off or
+    the scene is streamed)."""
+    import ctypes as C
+    lb = _lib.load()
+    lb.iqpt_debug_certain_tiles.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32),
+                                            C.POINTER(C.c_uint32), C.POINTER(C.c_uint32), C.c_uint32]
+    n, nt, ntx = C.c_uint32(0), C.c_uint32(0), C.c_uint32(0)
+    _lib.check(lb.iqpt_debug_certain_tiles(pt.handle, C.byref(n), C.byref(nt), C.byref(ntx), None, 0),
+               "iqpt_debug_certain_tiles")
+    return int(n.value)
+
+
 def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name, spp: int, npix_owned: int) -> dict:
     """The dominant kernel against the FP32 vector (VALU) peak.
 
@@ -233,13 +259,14 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name, spp: i
     # algorithmic bytes (84 B per owned pixel per launch) for every line, rank 0's share at N > 1
     pmc, pmc_src = find_pmc(cfg.name, spp, args.pmc_json) if world == 1 and not args.share_of else (None, "N > 1: per-rank PMC not collected")
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    mix = load_json(args.pmc_mix_json, cfg.name)
+    mix, mix_src = find_mix(cfg.name, args.pmc_mix_json)
     work_path = args.work_json or str(REPO / "profiles" / "r02" / f"work_{cfg.name}.json")
     work = load_json(work_path, cfg.name)
     out = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "kernel": kernel_name,
            "kernel_avg_ms": round(kern_avg_ms, 4), "traffic": traffic,
            "valu_busy_frac": (mix or {}).get("valu_busy_frac") if world == 1 else None,
-           "wave_time_split": (mix or {}).get("wave_time_split") if world == 1 else None}
+           "wave_time_split": (mix or {}).get("wave_time_split") if world == 1 else None,
+           "mix_source": mix_src if world == 1 else None}
     ex = work["flops_per_ray"] * rays_per_launch / t / 1e12 if (work and work.get("flops_per_ray") and t > 0) else None
     if ex is not None and ref_tflops > FP32_PEAK_TFLOPS:
         out.update(achieved=round(ex, 4), frac=round(ex / FP32_PEAK_TFLOPS, 5),
@@ -468,6 +495,7 @@ def main():
     # number is the kernel time per launch that the throughput sees; each launch's own duration is longer
     kern_span_ms = pt.kernel_span()
     launch_mode = pt.launch_mode()
+    certain_px = certain_pixels(pt, _lib) if args.certain != "off" else 0
 
     # the last step's gathered frame: rank 0's own rows of it must be its BGRA frame (checks the gather path)
     gather_check = None
@@ -509,6 +537,7 @@ def main():
         total_rays, kern_avg_ms = float(rays), kern_span_ms / max(1, launches)
         rmse_v, bitexact = (verify["rmse"], verify["bitexact_frac"]) if verify else (None, None)
 
+    npix_owned = (ps.x1 - ps.x0) * ps.nrows
     if rank == 0:
         mrays = total_rays / elapsed / 1e6
         rays_per_launch = float(rays) / max(1, args.steps)           # rank 0's kernel
@@ -549,6 +578,15 @@ def main():
                if strong_multi else {}),
             "msamples_per_s": round(samples / elapsed / 1e6, 3),
             "rays_per_sample": round(total_rays / samples, 5),
+            # value counts the closest-hit queries the reference performs for the same image; the camera rays
+            # of certain pixels are among them but resolved by one interval proof per pixel
+            # (every ray of the pixel's jitter square hits an emissive triangle first) instead of per-ray tests
+            "certain_pixels": {"pixels": certain_px, "frac_of_owned_pixels": round(certain_px / max(1, npix_owned), 5),
+                               "frac_of_rays_counted": round(certain_px * spp_step * args.steps / max(1.0, float(rays)), 5),
+                               "note": "rank 0's pixels whose camera rays are proven (iq_interval.h tri_certain) to end "
+                                       "on an emissive triangle: their samples take the two camera draws and fold "
+                                       "the clamped (1, 1, 1) without a per-ray intersection test; bit-identical "
+                                       "results (tests/test_gpu_certain.py)"},
             "rmse_vs_oracle": rmse_v,
             "bitexact_frac_vs_oracle": bitexact,
             "setup_ms": {k: round(v, 2) for k, v in setup.items()},
@@ -557,7 +595,7 @@ def main():
                              "reference binary, which cannot be built here"),
             "fma_flavour_rmse_c2": fma_flavour_rmse(),
             "roofline": roofline(cfg, args, world, rays_per_launch, kern_avg_ms, iqpt.kernel_name(), spp_step,
-                                 (ps.x1 - ps.x0) * ps.nrows),
+                                 npix_owned),
         }
         out["roofline"]["launch_duration_ms"] = round(kern_ms / max(1, launches), 4)
         out["roofline"]["overlapped_launches"] = bool(kern_span_ms < 0.98 * kern_ms)

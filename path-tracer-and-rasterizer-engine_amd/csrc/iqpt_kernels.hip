@@ -821,8 +821,11 @@ __device__ __forceinline__ bool bvh_node_test(const kparams& p, const float4* __
     const float slack = 8.0f * 0x1p-24f, up = 1.0f + 0x1p-20f, up16 = 1.0f + 0x1p-16f;
     const float4* nd = nodes + (size_t)kBvhNodeFloat4 * i;
     const float4 lo = nd[0], hi = nd[1], ax = nd[2], co = nd[3];
-    const float sx = fmaxf(iq_fabsf(r.ox - lo.x), iq_fabsf(r.ox - hi.x));
-    const float sy = fmaxf(iq_fabsf(r.oy - lo.y), iq_fabsf(r.oy - hi.y));
+    // x and y in packed pairs (v_pk_add / v_pk_mul: the same IEEE operations, two per instruction)
+    const f2 oxy = {r.ox, r.oy}, loxy = {lo.x, lo.y}, hixy = {hi.x, hi.y};
+    const f2 dlo = oxy - loxy, dhi = oxy - hixy;
+    const float sx = fmaxf(iq_fabsf(dlo.x), iq_fabsf(dhi.x));
+    const float sy = fmaxf(iq_fabsf(dlo.y), iq_fabsf(dhi.y));
     const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
     const float S = fmaxf(fmaxf(sx, sy), sz) * up;
     // lambda = 1e-6 / D, D a lower bound of |det^| over the node's triangles for this ray
@@ -843,8 +846,10 @@ __device__ __forceinline__ bool bvh_node_test(const kparams& p, const float4* __
     const float g = (lambda * (co.x + co.y * S)) * up + p.bvh_gulp;   // gulp includes gC
     // per axis [t0, t1] of the slab; a NaN (0 * inf: origin on a slab plane of an axis-parallel
     // ray) widens that axis to everything
-    float t0x = ((lo.x - g) - r.ox) * br.ix, t1x = ((hi.x + g) - r.ox) * br.ix;
-    float t0y = ((lo.y - g) - r.oy) * br.iy, t1y = ((hi.y + g) - r.oy) * br.iy;
+    const f2 gg = {g, g}, ixy = {br.ix, br.iy};
+    const f2 t0xy = ((loxy - gg) - oxy) * ixy, t1xy = ((hixy + gg) - oxy) * ixy;
+    float t0x = t0xy.x, t1x = t1xy.x;
+    float t0y = t0xy.y, t1y = t1xy.y;
     float t0z = ((lo.z - g) - r.oz) * br.iz, t1z = ((hi.z + g) - r.oz) * br.iz;
     float ax0 = fminf(t0x, t1x), ax1 = fmaxf(t0x, t1x);
     float ay0 = fminf(t0y, t1y), ay1 = fmaxf(t0y, t1y);
@@ -973,8 +978,10 @@ __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const 
         const float4 lo = nd[0], hi = nd[1], rr = nd[2];
         const uint32_t skip = __float_as_uint(lo.w), fc = __float_as_uint(hi.w);
         // S >= |c - o| for every centre of the node (box corners), rounded up
-        const float sx = fmaxf(iq_fabsf(r.ox - lo.x), iq_fabsf(r.ox - hi.x));
-        const float sy = fmaxf(iq_fabsf(r.oy - lo.y), iq_fabsf(r.oy - hi.y));
+        const f2 oxy = {r.ox, r.oy}, loxy = {lo.x, lo.y}, hixy = {hi.x, hi.y};   // packed x, y (bvh_node_test)
+        const f2 dlo = oxy - loxy, dhi = oxy - hixy;
+        const float sx = fmaxf(iq_fabsf(dlo.x), iq_fabsf(dhi.x));
+        const float sy = fmaxf(iq_fabsf(dlo.y), iq_fabsf(dhi.y));
         const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
         const float S2 = ((sx * sx + sy * sy) + sz * sz) * up;
         const float S = __builtin_sqrtf(S2) * up;
@@ -984,8 +991,10 @@ __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const 
         const float g = (K * __builtin_amdgcn_rcpf(__builtin_sqrtf(rr.x * rr.x + K) + rr.x) * (1.0f + 0x1p-12f) +
                          (4.0f * u) * S + (8.0f * u) * rr.y) * up + p.sbvh_gulp;
         const float dts = ((20.0f * u + 4.0f * eps) * S) * up + 1e-30f;
-        float t0x = ((lo.x - g) - r.ox) * br.ix, t1x = ((hi.x + g) - r.ox) * br.ix;
-        float t0y = ((lo.y - g) - r.oy) * br.iy, t1y = ((hi.y + g) - r.oy) * br.iy;
+        const f2 gg = {g, g}, ixy = {br.ix, br.iy};
+        const f2 t0xy = ((loxy - gg) - oxy) * ixy, t1xy = ((hixy + gg) - oxy) * ixy;
+        float t0x = t0xy.x, t1x = t1xy.x;
+        float t0y = t0xy.y, t1y = t1xy.y;
         float t0z = ((lo.z - g) - r.oz) * br.iz, t1z = ((hi.z + g) - r.oz) * br.iz;
         float ax0 = fminf(t0x, t1x), ax1 = fmaxf(t0x, t1x);
         float ay0 = fminf(t0y, t1y), ay1 = fmaxf(t0y, t1y);
@@ -1509,6 +1518,28 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
         const bool cull = kCull && p.cull != nullptr && !__any(active && depth != 0);
         const uint32_t* lane_mask =
             (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;   // null: 0
+        // kBvhPrimary: the path state the traversals never read (RNG state, accumulator, pixel, sample
+        // count, depth: 13 words) waits in this thread's slots of the unused scene-batch region of LDS
+        // (>= 13 x kRenderBlock words, checked by the runtime), so the traversals' live ranges fit the
+        // 5-wave register budget instead of spilling to scratch. The empty asm keeps the
+        // compiler from forwarding the stores into registers across the traversal.
+        uint32_t* const park = reinterpret_cast<uint32_t*>(lds_tri) + threadIdx.x;
+        if (kBvhPrimary) {
+            park[0 * kRenderBlock] = st.v0;
+            park[1 * kRenderBlock] = st.v1;
+            park[2 * kRenderBlock] = st.v2;
+            park[3 * kRenderBlock] = st.v3;
+            park[4 * kRenderBlock] = st.v4;
+            park[5 * kRenderBlock] = st.d;
+            park[6 * kRenderBlock] = __float_as_uint(acc.x);
+            park[7 * kRenderBlock] = __float_as_uint(acc.y);
+            park[8 * kRenderBlock] = __float_as_uint(acc.z);
+            park[9 * kRenderBlock] = px;
+            park[10 * kRenderBlock] = py;
+            park[11 * kRenderBlock] = done;
+            park[12 * kRenderBlock] = (uint32_t)depth;
+            asm volatile("" ::: "memory");
+        }
         if (kBvhPrimary) {
             // Triangles through the exact BVH, spheres through the exact sphere BVH (each falls back to
             // the brute-force fold from global memory where its BVH is absent or the ray is outside
@@ -1750,6 +1781,22 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             if (OPT & kOptStats) s_full += cull ? 0ull : 1ull;
         } else if (active) {
             intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
+        }
+        if (kBvhPrimary) {
+            asm volatile("" ::: "memory");
+            st.v0 = park[0 * kRenderBlock];
+            st.v1 = park[1 * kRenderBlock];
+            st.v2 = park[2 * kRenderBlock];
+            st.v3 = park[3 * kRenderBlock];
+            st.v4 = park[4 * kRenderBlock];
+            st.d = park[5 * kRenderBlock];
+            acc.x = __uint_as_float(park[6 * kRenderBlock]);
+            acc.y = __uint_as_float(park[7 * kRenderBlock]);
+            acc.z = __uint_as_float(park[8 * kRenderBlock]);
+            px = park[9 * kRenderBlock];
+            py = park[10 * kRenderBlock];
+            done = park[11 * kRenderBlock];
+            depth = (int)park[12 * kRenderBlock];
         }
 
         // ------------------------------------------------ shade (path_tracer.cu:297-316)

@@ -33,6 +33,9 @@ constexpr uint32_t kLdsResidentBytes = 32 * 1024;
 // slots and scatter stack a block stays under 32 KB, so 5 blocks fit a CU).
 constexpr uint32_t kTriBatch = 256;   // primitives per LDS batch (128 pairs = 10 KB)
 constexpr uint32_t kSphBatch = 256;
+// kOptBvhPrimary launches leave the batch region unused and park 13 words of path state per thread there
+static_assert((kTriBatch / 2) * kTriPairFloat4 * 16 + (kSphBatch / 2) * kSphPairFloat4 * 16 >= 13 * kRenderBlock * 4,
+              "the BVH-primary path-state slots must fit the scene-batch region");
 constexpr int kTuneLaunches = 4;     // timed launches before the camera-ray path is chosen (A, B, A, B)
 // kOptSplit auto mode: split when the owned pixels are fewer than this many per resident lane
 constexpr double kSplitAutoPixelsPerLane = 1.2;
