@@ -797,6 +797,7 @@ __device__ __forceinline__ bool bvh_ray_ok(const kparams& p, const ray3& r) {
 struct bvh_ray {
     float ix, iy, iz;    // 1 / d (IEEE)
     float dd, dl;        // |d|^2 and |d|, rounded up (normal cones)
+    bool inf_dir;        // some 1 / d_i is infinite: a slab parameter can be 0 * inf (NaN)
 };
 
 __device__ __forceinline__ bvh_ray bvh_ray_setup(const ray3 r) {
@@ -807,7 +808,19 @@ __device__ __forceinline__ bvh_ray bvh_ray_setup(const ray3 r) {
     b.iz = 1.0f / r.dz;
     b.dd = ((r.dx * r.dx + r.dy * r.dy) + r.dz * r.dz) * up16;
     b.dl = __builtin_sqrtf(b.dd) * up16;
+    b.inf_dir = !(iq_fabsf(b.ix) < INFINITY && iq_fabsf(b.iy) < INFINITY && iq_fabsf(b.iz) < INFINITY);
     return b;
+}
+
+// Bounds of sqrt(x), x >= 0, for the node tests only (conservative box growths, not the reference's
+// rounding): v_sqrt_f32 is within 1 ulp for x >= 2^-96 (iq_fastdiv.h); below that the upper bound's
+// absolute 2^-47 covers sqrt(x) < 2^-48 and the lower bound is 0. One instruction instead of the
+// correctly rounded expansion (about 17).
+__device__ __forceinline__ float sqrt_up(float x) {
+    return __builtin_amdgcn_sqrtf(x) * (1.0f + 0x1p-20f) + 0x1p-47f;
+}
+__device__ __forceinline__ float sqrt_dn(float x) {
+    return x >= 0x1p-96f ? __builtin_amdgcn_sqrtf(x) * (1.0f - 0x1p-20f) : 0.0f;
 }
 
 // Box test of node i (iq_bvh.hpp): the segment t in [t_min - dt, closest + dt] against the node's box
@@ -838,7 +851,7 @@ __device__ __forceinline__ bool bvh_node_test(const kparams& p, const float4* __
         const float c_lo = fmaxf(0.0f, c * (1.0f - 0x1p-16f) - 0x1p-20f * br.dl);
         // |d| sin(theta) <= sqrt(dd - c_lo^2); the subtraction's rounding (<= 2u dd) is covered by
         // adding 2^-20 dd before the root
-        const float s_hi = __builtin_sqrtf(fmaxf(0.0f, br.dd - c_lo * c_lo) + 0x1p-20f * br.dd) * up16;
+        const float s_hi = sqrt_up(fmaxf(0.0f, br.dd - c_lo * c_lo) + 0x1p-20f * br.dd) * up16;
         const float nc = ((c_lo * co.z) * (1.0f - 0x1p-16f) - (s_hi * co.w) * up16) * (1.0f - 0x1p-16f);
         const float D = nc - ax.w * up16;
         if (D > 1e-6f) lambda = fminf(1.0f, (1e-6f * __builtin_amdgcn_rcpf(D)) * up16);
@@ -854,9 +867,14 @@ __device__ __forceinline__ bool bvh_node_test(const kparams& p, const float4* __
     float ax0 = fminf(t0x, t1x), ax1 = fmaxf(t0x, t1x);
     float ay0 = fminf(t0y, t1y), ay1 = fmaxf(t0y, t1y);
     float az0 = fminf(t0z, t1z), az1 = fmaxf(t0z, t1z);
-    if (t0x != t0x || t1x != t1x) { ax0 = -INFINITY; ax1 = INFINITY; }
-    if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
-    if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
+    if (__builtin_expect(br.inf_dir || g != g, 0)) {
+        // only an infinite 1 / d_i (or a NaN g) makes a NaN (the other factors are finite); rare, so kept off the
+        // common path (the empty asm stops the compiler from if-converting it)
+        asm volatile("");
+        if (t0x != t0x || t1x != t1x) { ax0 = -INFINITY; ax1 = INFINITY; }
+        if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
+        if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
+    }
     // computed slab bounds are within 3 ulp (relative) of the exact ones: widen by 8 ulp
     const uint32_t tab = __float_as_uint(hi.w);                        // tA | tB, bf16 rounded up
     const float tA = __uint_as_float(tab & 0xffff0000u), tB = __uint_as_float(tab << 16);
@@ -984,11 +1002,12 @@ __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const 
         const float sy = fmaxf(iq_fabsf(dlo.y), iq_fabsf(dhi.y));
         const float sz = fmaxf(iq_fabsf(r.oz - lo.z), iq_fabsf(r.oz - hi.z));
         const float S2 = ((sx * sx + sy * sy) + sz * sz) * up;
-        const float S = __builtin_sqrtf(S2) * up;
-        // growth(S) of iq_bvh.hpp with the ray's |d|^2 deviation eps folded in (rounded up)
+        const float S = sqrt_up(S2) * up;
+        // growth(S) of iq_bvh.hpp with the ray's |d|^2 deviation eps folded in (rounded up; the root in
+        // the denominator rounded down)
         const float K = ((24.0f * u) * (rr.y * rr.y) + (86.0f * u + 2.01f * eps) * S2) * (1.0f + 0x1p-8f) +
                         (2.01f * eps) * (rr.y * rr.y);
-        const float g = (K * __builtin_amdgcn_rcpf(__builtin_sqrtf(rr.x * rr.x + K) + rr.x) * (1.0f + 0x1p-12f) +
+        const float g = (K * __builtin_amdgcn_rcpf(sqrt_dn(rr.x * rr.x + K) + rr.x) * (1.0f + 0x1p-12f) +
                          (4.0f * u) * S + (8.0f * u) * rr.y) * up + p.sbvh_gulp;
         const float dts = ((20.0f * u + 4.0f * eps) * S) * up + 1e-30f;
         const f2 gg = {g, g}, ixy = {br.ix, br.iy};
@@ -999,9 +1018,13 @@ __device__ __forceinline__ void sbvh_pass(const kparams& p, const ray3 r, const 
         float ax0 = fminf(t0x, t1x), ax1 = fmaxf(t0x, t1x);
         float ay0 = fminf(t0y, t1y), ay1 = fmaxf(t0y, t1y);
         float az0 = fminf(t0z, t1z), az1 = fmaxf(t0z, t1z);
-        if (t0x != t0x || t1x != t1x) { ax0 = -INFINITY; ax1 = INFINITY; }
-        if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
-        if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
+        if (__builtin_expect(br.inf_dir || g != g, 0)) {
+            // a NaN needs an infinite 1 / d_i or g = 0 * inf (K = 0 over a zero denominator): rare
+            asm volatile("");
+            if (t0x != t0x || t1x != t1x) { ax0 = -INFINITY; ax1 = INFINITY; }
+            if (t0y != t0y || t1y != t1y) { ay0 = -INFINITY; ay1 = INFINITY; }
+            if (t0z != t0z || t1z != t1z) { az0 = -INFINITY; az1 = INFINITY; }
+        }
         float enter = fmaxf(fmaxf(ax0, ay0), az0), exit = fminf(fminf(ax1, ay1), az1);
         enter = enter - iq_fabsf(enter) * slack;
         exit = exit + iq_fabsf(exit) * slack;
