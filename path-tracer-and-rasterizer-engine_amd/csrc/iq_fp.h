@@ -107,9 +107,17 @@ IQ_INLINE float iq_fminf(float a, float b) {
 IQ_INLINE float iq__sin_poly(float r, float z) {
     return ((-1.9515295891e-4f * z + 8.3321608736e-3f) * z - 1.6666654611e-1f) * z * r + r;
 }
+/* 0.5 z, exact scaling with one rounding either way. On the device as v_ldexp_f32: as a multiply the
+ * SLP vectorizer pairs it with the polynomial's last multiply into a v_pk_mul_f32 whose constant half
+ * (0.5) then lives in a VGPR pair that the register-bound render kernels spill to scratch. */
+#if defined(__HIP_DEVICE_COMPILE__)
+IQ_INLINE float iq__half(float z) { return __builtin_ldexpf(z, -1); }
+#else
+IQ_INLINE float iq__half(float z) { return 0.5f * z; }
+#endif
 IQ_INLINE float iq__cos_poly(float z) {
     float y = ((2.443315711809948e-5f * z - 1.388731625493765e-3f) * z + 4.166664568298827e-2f) * z * z;
-    y = y - 0.5f * z;
+    y = y - iq__half(z);
     return y + 1.0f;
 }
 
