@@ -206,7 +206,7 @@ def find_pmc(cfg_name: str, spp: int, explicit: str):
     per launch grows with spp only through the kernel's own re-reads, but a 1-spp profile divided by a
     16-spp kernel time is meaningless). Returns (profile, path) or (None, why)."""
     cands = [Path(explicit)] if explicit else sorted(
-        (REPO / "profiles").glob(f"r0*/pmc_traffic_{cfg_name}*.json"), key=lambda q: q.parent.name, reverse=True)
+        (REPO / "profiles").glob(f"r0*/pmc_traffic_{cfg_name}*.json"), key=lambda q: (q.parent.name, q.name), reverse=True)
     why = "no PMC profile of this config"
     for c in cands:
         d = load_json(str(c), cfg_name)
