@@ -582,8 +582,10 @@ int build_cull(iqpt_ctx* c) {
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "cull binning kernel");
     const uint32_t ntiles = c->cull_ntx * c->cull_nty;
     // certain pixels (iq_interval.h tri_certain): only under the reference's materials (every triangle
-    // emissive) and for scenes resident in LDS (streamed scenes run LDS batches with workgroup barriers, where
-    // a wave folding a certain pixel's launch holds the others: C4 +66 % per launch, profiles/r03/ab_certain.json)
+    // emissive) and for scenes resident in LDS. In a streamed scene a lane that leaves a certain pixel takes
+    // a pixel of the next tile, so waves hold two tiles and their LDS batches test the union of both tiles'
+    // candidates: C4 +66 % per launch whether the pixels are folded in the refill or by a kernel of their own
+    // (profiles/r03/ab_certain.json, ab_streamed_certain_fold_rejected.json)
     c->certain_valid = false;
     if (c->d_certain) (void)hipFree(c->d_certain);
     c->d_certain = nullptr;

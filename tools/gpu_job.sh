@@ -1,16 +1,18 @@
-# r03 run 49: the tree after the C5 register diet: default bench (CPU baseline), C3 share steps N = 8 / 4 / 2
-# through the gather path, C4 / C5 lines
+# r03 run 50: certain pixels of streamed scenes folded by iqpt_certain_fold_kernel (the render kernel skips
+# them): certain / BVH / full-frame parity, C4 / C5 / C2 lines against run 47's library (A/B)
 mkdir -p gpurun_out
 O=gpurun_out
-timeout -k 10 300 python3 bench.py --cpu-seconds 20 > $O/r03_49_default.json 2> $O/r03_49_default.err || { tail -20 $O/r03_49_default.err; exit 1; }
-tail -1 $O/r03_49_default.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('default', d['value'], d['ms_per_step'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'], d['roofline']['kernel_avg_ms'], d['cpu_baseline']['value'])"
+L=path-tracer-and-rasterizer-engine_amd/iqpt
+timeout -k 10 900 python -u -m pytest tests/test_gpu_certain.py tests/test_gpu_bvh.py tests/test_gpu_sphere_bvh.py tests/test_gpu_fullframe.py -x -q --timeout 600 --timeout-method thread > $O/r03_50_tests.log 2>&1 || { tail -40 $O/r03_50_tests.log; exit 1; }
+tail -1 $O/r03_50_tests.log
 for r in 1 2; do
-for s in 8 4 2; do
-  timeout -k 10 300 python3 bench.py --self-gather --share-of $s --steps 30 --warmup 8 --no-cpu-baseline --verify-rows 0 > $O/r03_49_share${s}_$r.json 2> $O/r03_49_share${s}_$r.err || { tail -20 $O/r03_49_share${s}_$r.err; exit 1; }
-  tail -1 $O/r03_49_share${s}_$r.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('share', $s, d['ms_per_step'], d['config']['launch_mode'], d['roofline']['kernel_avg_ms'], d.get('gather_check'))"
+for v in base new; do
+  lib=$L/libiqpt_ab_base.so; [ $v = new ] && lib=$L/libiqpt.so
+  timeout -k 10 300 python3 bench.py --lib $lib --config c4 --steps 3 --warmup 5 --no-cpu-baseline --verify-rows 4 > $O/r03_50_c4_${v}_$r.json 2> $O/r03_50_c4_${v}_$r.err || { tail -20 $O/r03_50_c4_${v}_$r.err; exit 1; }
+  tail -1 $O/r03_50_c4_${v}_$r.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c4', '$v', d['value'], d['ms_per_step'], d['bitexact_frac_vs_oracle'], d['certain_pixels']['frac_of_rays_counted'])"
+  timeout -k 10 300 python3 bench.py --lib $lib --config c5 --spp 16 --steps 5 --warmup 5 --no-cpu-baseline --verify-rows 2 > $O/r03_50_c5_${v}_$r.json 2> $O/r03_50_c5_${v}_$r.err || { tail -20 $O/r03_50_c5_${v}_$r.err; exit 1; }
+  tail -1 $O/r03_50_c5_${v}_$r.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c5', '$v', d['value'], d['ms_per_step'], d['bitexact_frac_vs_oracle'], d['certain_pixels']['frac_of_rays_counted'])"
 done
 done
-timeout -k 10 300 python3 bench.py --config c5 --spp 16 --steps 5 --warmup 5 --no-cpu-baseline --verify-rows 4 > $O/r03_49_c5.json 2> $O/r03_49_c5.err || { tail -20 $O/r03_49_c5.err; exit 1; }
-tail -1 $O/r03_49_c5.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c5', d['value'], d['ms_per_step'], d['bitexact_frac_vs_oracle'], d['roofline']['hbm'])"
-timeout -k 10 300 python3 bench.py --config c4 --steps 3 --warmup 5 --no-cpu-baseline --verify-rows 4 > $O/r03_49_c4.json 2> $O/r03_49_c4.err || { tail -20 $O/r03_49_c4.err; exit 1; }
-tail -1 $O/r03_49_c4.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c4', d['value'], d['ms_per_step'], d['bitexact_frac_vs_oracle'])"
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 8 --no-cpu-baseline --verify-rows 4 > $O/r03_50_c2.json 2> $O/r03_50_c2.err || { tail -20 $O/r03_50_c2.err; exit 1; }
+tail -1 $O/r03_50_c2.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c2', d['value'], d['ms_per_step'], d['bitexact_frac_vs_oracle'])"
