@@ -1427,9 +1427,8 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     if (stream_batches && !iqpt::render_variant_exists(c->max_depth, true, opt) &&
         iqpt::render_variant_exists(c->max_depth, true, opt & ~iqpt::kOptLB5))
         opt &= ~iqpt::kOptLB5;
-    // kOptCamAxis (opt-in through iqpt_debug_set_kernel_options): the short camera transform, kept
-    // only where the camera qualifies. Not selected by default: 10 % fewer VALU instructions per
-    // wave-iteration on C2 but no shorter launch
+    // kOptCamAxis: the short camera transform, kept only where the camera qualifies (a caller's option
+    // mask may ask for it; production launches add it below, where a variant exists: DESIGN.md §3.8)
     if (!cam_axis) opt &= ~iqpt::kOptCamAxis;
     // resident production variants carry kOptPrio (VALU priority for scatter-heavy waves; same bits)
     if (!stream_batches && !iqpt::render_variant_exists(c->max_depth, false, opt) &&
