@@ -1,18 +1,12 @@
-# r03 run 50: certain pixels of streamed scenes folded by iqpt_certain_fold_kernel (the render kernel skips
-# them): certain / BVH / full-frame parity, C4 / C5 / C2 lines against run 47's library (A/B)
+# r03 run 51: final check of the tree: -m gpu suite, smoke, default bench as the driver runs it (60-s CPU
+# baseline), rocprofv3 kernel trace + stats of the default bench
 mkdir -p gpurun_out
 O=gpurun_out
-L=path-tracer-and-rasterizer-engine_amd/iqpt
-timeout -k 10 900 python -u -m pytest tests/test_gpu_certain.py tests/test_gpu_bvh.py tests/test_gpu_sphere_bvh.py tests/test_gpu_fullframe.py -x -q --timeout 600 --timeout-method thread > $O/r03_50_tests.log 2>&1 || { tail -40 $O/r03_50_tests.log; exit 1; }
-tail -1 $O/r03_50_tests.log
-for r in 1 2; do
-for v in base new; do
-  lib=$L/libiqpt_ab_base.so; [ $v = new ] && lib=$L/libiqpt.so
-  timeout -k 10 300 python3 bench.py --lib $lib --config c4 --steps 3 --warmup 5 --no-cpu-baseline --verify-rows 4 > $O/r03_50_c4_${v}_$r.json 2> $O/r03_50_c4_${v}_$r.err || { tail -20 $O/r03_50_c4_${v}_$r.err; exit 1; }
-  tail -1 $O/r03_50_c4_${v}_$r.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c4', '$v', d['value'], d['ms_per_step'], d['bitexact_frac_vs_oracle'], d['certain_pixels']['frac_of_rays_counted'])"
-  timeout -k 10 300 python3 bench.py --lib $lib --config c5 --spp 16 --steps 5 --warmup 5 --no-cpu-baseline --verify-rows 2 > $O/r03_50_c5_${v}_$r.json 2> $O/r03_50_c5_${v}_$r.err || { tail -20 $O/r03_50_c5_${v}_$r.err; exit 1; }
-  tail -1 $O/r03_50_c5_${v}_$r.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c5', '$v', d['value'], d['ms_per_step'], d['bitexact_frac_vs_oracle'], d['certain_pixels']['frac_of_rays_counted'])"
-done
-done
-timeout -k 10 300 python3 bench.py --steps 20 --warmup 8 --no-cpu-baseline --verify-rows 4 > $O/r03_50_c2.json 2> $O/r03_50_c2.err || { tail -20 $O/r03_50_c2.err; exit 1; }
-tail -1 $O/r03_50_c2.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('c2', d['value'], d['ms_per_step'], d['bitexact_frac_vs_oracle'])"
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread > $O/r03_51_tests.log 2>&1 || { tail -40 $O/r03_51_tests.log; exit 1; }
+tail -1 $O/r03_51_tests.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/r03_51_smoke.log 2>&1 || { tail -20 $O/r03_51_smoke.log; exit 1; }
+tail -1 $O/r03_51_smoke.log
+timeout -k 10 400 python3 bench.py > $O/r03_51_bench.json 2> $O/r03_51_bench.err || { tail -20 $O/r03_51_bench.err; exit 1; }
+tail -1 $O/r03_51_bench.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('default', d['value'], d['ms_per_step'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'], d['roofline']['kernel_avg_ms'], d['roofline']['frac'], d['cpu_baseline']['value'])"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/r03_51_stats -o run -- python3 bench.py --steps 20 --warmup 3 --no-cpu-baseline --verify-rows 0 > $O/r03_51_stats.log 2>&1 || { tail -20 $O/r03_51_stats.log; exit 1; }
+tail -1 $O/r03_51_stats.log | cut -c1-300
