@@ -205,6 +205,7 @@ struct iqpt_ctx {
     // only: every plan gives the same bits). iqpt_debug_spec_plan: 0 off, 1 asynchronous (default), 2..5
     // synchronous before every launch (tests; 3, 4: every pixel 32 / 64 lanes, 5: mixed)
     int spec_plan_mode = 1;
+    double spec_cap = 0.97;                 // a plan's lanes: this fraction of the resident lanes (iqpt_debug_set_spec_cap)
     uint32_t* h_spec_rho = nullptr;      // pinned: the history read back (spec_n)
     uint32_t* h_spec_plan = nullptr;     // pinned: staging of the plan (3 spec_n)
     hipEvent_t ev_spec_rho = nullptr, ev_spec_plan = nullptr;
@@ -430,7 +431,7 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     }
     int occ = 0;
     if (iqpt::spec_occupancy(p, ks, opt, &occ) != 0 || occ < 1) occ = 1;
-    const double cap = 0.97 * (double)c->num_cus * occ * 256.0;     // resident lanes, a little slack
+    const double cap = c->spec_cap * (double)c->num_cus * occ * 256.0;     // resident lanes, a little slack
     auto lsh_of = [&](uint32_t q, double e) -> uint8_t {
         uint8_t k = 0;
         while (k < 3 && w[q] > e * (double)(8u << k)) ++k;
@@ -2388,6 +2389,15 @@ int iqpt_debug_set_spec(iqpt_ctx* c, uint32_t rho0, uint32_t margin_div) {
     c->spec_margin_div = margin_div ? margin_div : 16u;
     c->spec_rho0 = rho0 ? rho0 : iqpt::kSpecRho0;
     c->spec_rho_valid = false;
+    return IQPT_OK;
+}
+
+/* Internal (A/B): the fraction of the spec kernel's resident lanes a plan may fill in one block-wave
+ * (0.97 by default; a plan only orders work: same bits). The next plan uses it. */
+int iqpt_debug_set_spec_cap(iqpt_ctx* c, double frac) {
+    if (!c || !(frac > 0.0 && frac <= 64.0)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or fraction not in (0, 64]");
+    c->spec_cap = frac;
+    c->spec_plan_n = 0;
     return IQPT_OK;
 }
 
