@@ -88,6 +88,8 @@ def parse():
                          "with --self-gather the per-step gather path too)")
     ap.add_argument("--self-gather", action="store_true",
                     help="test: run the per-step gather path at N = 1 (a one-rank process group)")
+    ap.add_argument("--spec-cap", type=float, default=0.0,
+                    help="A/B: a spec plan's lanes as a fraction of the resident lanes (iqpt_debug_set_spec_cap; 0 = default)")
     ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain", "fan", "spec"],
                     help="sample-parallel chains (iqpt_set_split, DESIGN.md §3.7)")
     return ap.parse_args()
@@ -397,6 +399,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_certain.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_certain(pt._h, 0), "iqpt_debug_set_certain")
+    if args.spec_cap:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec_cap.argtypes = [C.c_void_p, C.c_double]
+        _lib.check(lb.iqpt_debug_set_spec_cap(pt._h, args.spec_cap), "iqpt_debug_set_spec_cap")
     pt.set_camera(cam)
     t0 = time.perf_counter()
     pt.upload_packet(pk)
@@ -578,7 +585,8 @@ def main():
                                        if weak else f"gather of the {gathered} to rank 0 every step")
                                       + (" (rccl)" if on_gpu else " (gloo via host, rehearsal)")),
                        "split": args.split, "overlap": args.overlap, "certain": args.certain, "launch_mode": launch_mode,
-                       **({"kernel_options": args.kernel_options} if args.kernel_options else {})},
+                       **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
+                       **({"spec_cap": args.spec_cap} if args.spec_cap else {})},
             "n_ranks_seen": n_ranks_seen,
             "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             **({"gather": "stream-ordered" if stream_gather else "blocking", "gather_check": gather_check}
