@@ -246,7 +246,39 @@ def certain_pixels(pt, _lib) -> int:
     return int(n.value)
 
 
-def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name, spp: int, npix_owned: int) -> dict:
+# the kernels a launch mode runs (iqpt_debug_split_info's launch mode)
+LAUNCH_KERNELS = {"plain": "iqpt_render_kernel", "spec": "iqpt_spec_kernel + iqpt_fan_kernel",
+                  "fan": "iqpt_render_kernel + iqpt_fan_kernel", "chain": "iqpt_chain_kernel + iqpt_render_kernel",
+                  "chain+fan": "iqpt_chain_kernel + iqpt_fan_kernel", "split": "iqpt_render_kernel (split rounds)",
+                  "split+fan": "iqpt_render_kernel (split rounds) + iqpt_fan_kernel"}
+
+
+def mix_for_launch(cfg_name: str, launch_mode: str, split_ways: int, explicit: str):
+    """The instruction-mix profile of the kernels this launch mode ran: the plain kernel's for a full-frame
+    plain line; for a spec line the spec and fan kernels' own at this share (profiles/r0*/pmc_mix_{spec,fan}_n<N>.json,
+    taken at the same C3 share); else none (no profile of those kernels). Returns (busy, split, source)."""
+    if explicit or (launch_mode == "plain" and split_ways == 1):
+        mix, src = find_mix(cfg_name, explicit)
+        return ((mix or {}).get("valu_busy_frac"), (mix or {}).get("wave_time_split"), src)
+    if launch_mode == "spec":
+        name = f"c3_share{split_ways}"
+        got = {}
+        for k in ("spec", "fan"):
+            cands = sorted((REPO / "profiles").glob(f"r0*/pmc_mix_{k}_n{split_ways}*.json"),
+                           key=lambda q: (q.parent.name, q.name), reverse=True)
+            for c in cands:
+                d = load_json(str(c), name)
+                if d:
+                    got[k] = (d.get("valu_busy_frac"), d.get("wave_time_split"), str(c.relative_to(REPO)))
+                    break
+        if len(got) == 2:
+            return ({k: v[0] for k, v in got.items()}, {k: v[1] for k, v in got.items()},
+                    {k: v[2] for k, v in got.items()})
+    return None, None, None
+
+
+def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode: str, split_ways: int, spp: int,
+             npix_owned: int, certain_ray_frac: float) -> dict:
     """The dominant kernel against the FP32 vector (VALU) peak.
 
     C1/C2/C3: algorithmic FLOPs F_ray = 52 T + 19 S per ray (the reference's brute-force
@@ -261,14 +293,13 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name, spp: i
     # algorithmic bytes (84 B per owned pixel per launch) for every line, rank 0's share at N > 1
     pmc, pmc_src = find_pmc(cfg.name, spp, args.pmc_json) if world == 1 and not args.share_of else (None, "N > 1: per-rank PMC not collected")
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    mix, mix_src = find_mix(cfg.name, args.pmc_mix_json)
-    work_path = args.work_json or str(REPO / "profiles" / "r02" / f"work_{cfg.name}.json")
+    busy, wsplit, mix_src = mix_for_launch(cfg.name, launch_mode, split_ways, args.pmc_mix_json)
+    work_path = args.work_json or newest_work(cfg.name)
     work = load_json(work_path, cfg.name)
-    out = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS, "kernel": kernel_name,
+    out = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS,
+           "kernel": LAUNCH_KERNELS.get(launch_mode, launch_mode), "launch_mode": launch_mode,
            "kernel_avg_ms": round(kern_avg_ms, 4), "traffic": traffic,
-           "valu_busy_frac": (mix or {}).get("valu_busy_frac") if world == 1 else None,
-           "wave_time_split": (mix or {}).get("wave_time_split") if world == 1 else None,
-           "mix_source": mix_src if world == 1 else None}
+           "valu_busy_frac": busy, "wave_time_split": wsplit, "mix_source": mix_src}
     ex = work["flops_per_ray"] * rays_per_launch / t / 1e12 if (work and work.get("flops_per_ray") and t > 0) else None
     if ex is not None and ref_tflops > FP32_PEAK_TFLOPS:
         out.update(achieved=round(ex, 4), frac=round(ex / FP32_PEAK_TFLOPS, 5),
@@ -281,7 +312,13 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name, spp: i
         if ex is not None:
             # the tests the kernel actually executes (the tile masks skip most of the brute-force ones)
             out["executed_work"] = {"achieved": round(ex, 4), "frac": round(ex / FP32_PEAK_TFLOPS, 5),
-                                    "flops_per_ray": work["flops_per_ray"], "per_ray": work.get("per_ray")}
+                                    "flops_per_ray": work["flops_per_ray"], "per_ray": work.get("per_ray"),
+                                    "source": str(Path(work_path).resolve().relative_to(REPO))}
+    # the counted rays include the camera rays of certain pixels, resolved by a per-pixel proof instead of
+    # per-ray tests: the rate of rays that ran a per-ray closest-hit test
+    if t > 0:
+        out["traced_rays_per_launch"] = round(rays_per_launch * (1.0 - certain_ray_frac))
+        out["traced_rays_per_s"] = round(rays_per_launch * (1.0 - certain_ray_frac) / t, 1)
     else:
         # the brute-force price exceeds the peak: the kernel skips that work, so it is no roofline
         out.update(achieved=None, frac=None, flops_per_ray=None,
@@ -304,6 +341,13 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, kernel_name, spp: i
                    "PMC HBM bytes per launch (tools/pmc_traffic.py); valu_busy_frac / wave_time_split: PMC "
                    "instruction-mix pass (tools/pmc_mix.py), profiles/.")
     return out
+
+
+def newest_work(cfg_name: str) -> str:
+    """The newest executed-work profile of the config (tools/work_counters.py: profiles/r0*/work_<config>*.json)."""
+    cands = sorted((REPO / "profiles").glob(f"r0*/work_{cfg_name}*.json"), key=lambda q: (q.parent.name, q.name),
+                   reverse=True)
+    return str(cands[0]) if cands else str(REPO / "profiles" / "r02" / f"work_{cfg_name}.json")
 
 
 def fma_flavour_rmse():
@@ -355,10 +399,11 @@ def main():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", str(_free_port()))
             os.environ.setdefault("RANK", "0")
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", device), world_size=world, rank=rank)
-        else:
-            dist.init_process_group("gloo", world_size=world, rank=rank)
+        # torch.distributed only for the rendezvous, the barriers and the post-timing reductions (host, gloo);
+        # the data path's collective — the per-step frame gather over RCCL / xGMI — is libiqpt's own
+        # communicator (iqpt_comm_init / iqpt_gather_frame_async). --backend gloo keeps a host
+        # gather through torch for the one-device multi-rank rehearsal (RCCL refuses two ranks on one GPU).
+        dist.init_process_group("gloo", world_size=world, rank=rank)
     n_ranks_seen = dist.get_world_size() if use_pg else 1
 
     def barrier():
@@ -418,8 +463,18 @@ def main():
     strong_multi = (world > 1 or args.self_gather) and not weak
     words = 4 if args.gather == "accum" else 1
     dtype = torch.float32 if args.gather == "accum" else torch.int32
-    buf = torch.zeros((max_px, words), dtype=dtype, device=tdev) if strong_multi else None
-    gather_list = [torch.empty_like(buf) for _ in range(world)] if (strong_multi and rank == 0) else None
+    # nccl: libiqpt's RCCL communicator gathers the BGRA8 frame (or the accumulators) to rank 0 and assembles
+    # it there on the device (W x H, row-major); gloo: the host gather below
+    lib_gather = strong_multi and on_gpu
+    if lib_gather:
+        uid = [iqpt.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        pt.comm_init(rank, world, uid[0])
+    frame_dev = (torch.zeros((cfg.width * cfg.height, words), dtype=dtype, device="cuda")
+                 if lib_gather and rank == 0 else None)
+    buf = torch.zeros((max_px, words), dtype=dtype, device=tdev) if strong_multi and not lib_gather else None
+    gather_list = ([torch.empty_like(buf) for _ in range(world)]
+                   if (strong_multi and not lib_gather and rank == 0) else None)
     assembled = None
 
     def fetch(dst, what):
@@ -436,38 +491,28 @@ def main():
         st = torch.stack(parts).view(world, -1, cfg.width, channels)
         return st.transpose(0, 1).reshape(-1, cfg.width, channels)[: cfg.height]
 
-    # Stream-ordered gather (nccl, BGRA frame): the frame copy is enqueued on the context's stream after the
-    # step's render, the gather on torch's stream waits for it with an event, and the next step's copy
-    # into the same buffer waits for that gather: no host synchronisation inside the timed steps, and
-    # the gather of step k runs while step k + 1 renders.
-    stream_gather = strong_multi and on_gpu and args.gather == "frame" and not args.gather_sync
-    # With overlapped launches (N = 2 plain shares) the copy goes on the last launch's stream, so the next
-    # render keeps overlapping it (iqpt_frame_stream; the launches write two frame buffers in turn).
-    ext_streams = {}
-    gathered = None                                   # torch-stream event after the last gather
-
-    def frame_stream():
-        h = pt.frame_stream_handle()
-        if h not in ext_streams:
-            ext_streams[h] = torch.cuda.ExternalStream(h)
-        return ext_streams[h]
+    # Stream-ordered gather (nccl, BGRA frame, libiqpt): the copy of the step's frame is enqueued behind its
+    # render (on the launch's own stream: overlapped and pipelined launches keep overlapping), the RCCL
+    # gather and rank 0's assembly on the communicator's stream behind the copy; no host synchronisation
+    # inside the timed steps, and the gather of step k runs while step k + 1 renders.
+    stream_gather = lib_gather and args.gather == "frame" and not args.gather_sync
 
     def step():
-        nonlocal assembled, gathered
+        nonlocal assembled
         pt.render(spp_step)
-        if strong_multi and stream_gather:
-            fs = frame_stream()
-            if gathered is not None:
-                fs.wait_event(gathered)               # buf is read by the previous gather
-            pt.copy_frame_device_async(buf.data_ptr(), buf.numel() * 4)
-            copied = torch.cuda.Event()
-            copied.record(fs)
-            torch.cuda.current_stream().wait_event(copied)
-            dist.gather(buf, gather_list, dst=0)
-            if rank == 0:
-                assembled = deinterleave(gather_list, words)
-            gathered = torch.cuda.Event()
-            gathered.record(torch.cuda.current_stream())
+        if stream_gather:
+            pt.gather_frame_async(0, frame_dev.data_ptr() if rank == 0 else 0,
+                                  frame_dev.numel() * 4 if rank == 0 else 0)
+            assembled = frame_dev
+        elif lib_gather:
+            # --gather-sync / --gather accum: the blocking form
+            if args.gather == "accum":
+                pt.gather_accum(0, frame_dev.data_ptr() if rank == 0 else 0, frame_dev.numel() * 4 if rank == 0 else 0)
+            else:
+                pt.gather_frame_async(0, frame_dev.data_ptr() if rank == 0 else 0,
+                                      frame_dev.numel() * 4 if rank == 0 else 0)
+                pt.sync()
+            assembled = frame_dev
         elif strong_multi:
             fetch(buf, args.gather)
             dist.gather(buf, gather_list, dst=0)
@@ -503,21 +548,29 @@ def main():
     # overlapped launches run two at a time: the event span of the timed launches / their
     # number is the kernel time per launch that the throughput sees; each launch's own duration is longer
     kern_span_ms = pt.kernel_span()
+    gather_ms, gathers = pt.comm_time() if lib_gather else (0.0, 0)
     launch_mode = pt.launch_mode()
     certain_px = certain_pixels(pt, _lib) if args.certain != "off" else 0
 
-    # the last step's gathered frame: rank 0's own rows of it must be its BGRA frame (checks the gather path)
+    # the last step's gathered frame: rank 0's own rows of it must be its own frame (checks the gather path;
+    # libiqpt's assembly puts them at rows 0, S, 2S, ... of the W x H frame, S = the split's ways)
     gather_check = None
     if strong_multi and rank == 0 and assembled is not None:
         torch.cuda.synchronize()
-        own = pt.read()[1].view(np.int32).reshape(-1, cfg.width)
-        got = assembled.reshape(-1, cfg.width)[0::world].cpu().numpy().view(np.int32)
+        lin_own, bgra_own = pt.read()
+        own = (lin_own.view(np.int32) if words == 4 else bgra_own.view(np.int32)).reshape(-1, cfg.width * words)
+        step_rows = part_world if lib_gather else world
+        got = assembled.reshape(-1, cfg.width * words)[0::step_rows][: own.shape[0]].cpu().numpy().view(np.int32)
         gather_check = bool(own.shape == got.shape and np.array_equal(own, got))
 
-    # after timing: the float frame on rank 0 (strong: the gathered accumulators de-interleaved, bit-
-    # identical to one GPU's frame; weak: the N independent estimates averaged)
+    # after timing: the float frame on rank 0 (strong: the gathered accumulators assembled, bit-identical to
+    # one GPU's frame; weak: the N independent estimates averaged)
     frame = None
-    if world > 1:
+    if world > 1 and lib_gather:
+        acc = torch.zeros((cfg.width * cfg.height, 4), dtype=torch.float32, device="cuda") if rank == 0 else None
+        pt.gather_accum(0, acc.data_ptr() if rank == 0 else 0, acc.numel() * 4 if rank == 0 else 0)
+        frame = acc
+    elif world > 1:
         acc = torch.zeros((max_px, 4), dtype=torch.float32, device=tdev)
         fetch(acc, "accum")
         if weak:
@@ -535,9 +588,17 @@ def main():
                                   seed=seed, spp=spp_step)
         first_lin = None
 
-    dev = "cuda" if on_gpu else "cpu"
     vals = torch.tensor([elapsed, float(rays), kern_span_ms / max(1, launches), verify["rmse"] if verify else 0.0,
-                         verify["bitexact_frac"] if verify else 1.0], dtype=torch.float64, device=dev)
+                         verify["bitexact_frac"] if verify else 1.0], dtype=torch.float64)
+    # per rank (N > 1 lines): the render span per launch, the step, the gathers' own time per step on the
+    # communicator stream (transfer + waiting for slower ranks), and the step time outside the render span
+    mine = {"rank": rank, "render_span_ms": round(kern_span_ms / max(1, launches), 4),
+            "step_ms": round(elapsed / args.steps * 1e3, 4),
+            "gather_ms": round(gather_ms / gathers, 4) if gathers else None,
+            "outside_render_ms": round(elapsed / args.steps * 1e3 - kern_span_ms / max(1, launches), 4)}
+    per_rank = [None] * world if world > 1 else [mine]
+    if world > 1:
+        dist.all_gather_object(per_rank, mine)
     if world > 1:
         mx = vals[[0, 2, 3]].clone()
         dist.all_reduce(mx, op=dist.ReduceOp.MAX)
@@ -580,10 +641,11 @@ def main():
                                      else (f"cyclic rows x{world}" if world > 1 else
                                            (f"rank 0's rows of a cyclic x{args.share_of} split (one-GPU share "
                                             "rehearsal)" if args.share_of else "full frame"))),
-                       "collective": ("none" if world == 1 else
+                       "collective": ("none" if not (strong_multi or world > 1) else
                                       ("none in the timed region; one reduce of the accumulators after it"
                                        if weak else f"gather of the {gathered} to rank 0 every step")
-                                      + (" (rccl)" if on_gpu else " (gloo via host, rehearsal)")),
+                                      + (" (RCCL ncclGather inside libiqpt: iqpt_gather_frame_async)" if lib_gather
+                                         else " (gloo via host, rehearsal)")),
                        "split": args.split, "overlap": args.overlap, "certain": args.certain, "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
                        **({"spec_cap": args.spec_cap} if args.spec_cap else {})},
@@ -609,9 +671,11 @@ def main():
                              "FMA contraction off and shared iq_fp.h transcendentals); unpinned vs the nvcc/cuRAND "
                              "reference binary, which cannot be built here"),
             "fma_flavour_rmse_c2": fma_flavour_rmse(),
-            "roofline": roofline(cfg, args, world, rays_per_launch, kern_avg_ms, iqpt.kernel_name(), spp_step,
-                                 npix_owned),
+            "roofline": roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode, part_world, spp_step,
+                                 npix_owned, certain_px * spp_step * args.steps / max(1.0, float(rays))),
         }
+        if strong_multi or world > 1:
+            out["per_rank"] = per_rank
         out["roofline"]["launch_duration_ms"] = round(kern_ms / max(1, launches), 4)
         out["roofline"]["overlapped_launches"] = bool(kern_span_ms < 0.98 * kern_ms)
         if world == 1 and not args.no_cpu_baseline:

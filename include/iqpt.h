@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define IQPT_ABI_VERSION 3
+#define IQPT_ABI_VERSION 4
 
 typedef enum iqpt_status {
     IQPT_OK = 0,
@@ -244,6 +244,42 @@ int iqpt_stream(iqpt_ctx* ctx, void** stream);
  * pipelined spec launches are (IQPT_SPLIT_SPEC), else the context's stream. Work enqueued there runs after
  * that launch, not after the ones issued later. */
 int iqpt_frame_stream(iqpt_ctx* ctx, void** stream);
+
+/* ---------------------------------------------------------------- multi-GPU frame delivery
+ * One process per GPU, one ctx per process, each owning its rank's cyclic rows of ONE frame: pixel set
+ * {0, W, rank, world, ceil((H - rank) / world)} (row y -> rank y mod world; the RNG stream and camera ray of a
+ * pixel are keyed by its global id, path_tracer.cu:36-46 and :336-339, so the assembled frame is bit-identical
+ * to one GPU's). The frame the reference copies back after every launch (path_tracer.cu:385, the D3D present
+ * of :171-210) is gathered to a root rank over RCCL (ncclGather over xGMI) and assembled there
+ * in row-major order. The reference is single-GPU; these calls are the library's multi-GPU extension of
+ * that readback. RCCL is loaded at the first call (librccl.so.1; a process that already holds one, e.g.
+ * PyTorch-ROCm's, shares it).
+ *
+ * iqpt_comm_unique_id: on one rank, then handed to every rank out of band (MPI, a TCP store, a file).
+ * iqpt_comm_init: collective over the world ranks (each blocks until all have called it); fails with
+ *   IQPT_ERR_INVALID_ARG unless the ctx owns exactly its rank's cyclic rows {0, W, rank, S, ceil((H - rank) / S)}
+ *   with S >= world (S = world on a node; S > world is a rehearsal of an S-way share on fewer GPUs, in which
+ *   the root places the rows of the communicator's ranks only).
+ * iqpt_gather_frame_async: collective; enqueues a copy of the BGRA8 frame behind every render issued so far
+ *   (it does not end overlapped or pipelined launches, like iqpt_copy_frame_device_async), the gather and,
+ *   on the root, the assembly of the W x H frame into dst_device (W*H*4 bytes; ignored elsewhere) on the
+ *   communicator's stream (iqpt_comm_stream), and returns. The caller orders its reads of dst_device on that
+ *   stream; every other entry point waits for the gathers in flight.
+ * iqpt_gather_accum: collective, synchronous; the float4 accumulators (W*H*16 bytes of device memory) on the root.
+ * iqpt_gather_read: collective, synchronous; the whole frame's accumulator (W*H*4 floats) and BGRA8 (W*H*4
+ *   bytes) into the root's host buffers (either may be NULL; other ranks' pointers are ignored) — the
+ *   multi-GPU iqpt_read. */
+#define IQPT_COMM_ID_BYTES 128
+int iqpt_comm_unique_id(void* id, size_t bytes);
+int iqpt_comm_init(iqpt_ctx* ctx, int rank, int world, const void* id, size_t bytes);
+int iqpt_gather_frame_async(iqpt_ctx* ctx, int root, void* dst_device, size_t bytes);
+int iqpt_gather_accum(iqpt_ctx* ctx, int root, void* dst_device, size_t bytes);
+int iqpt_gather_read(iqpt_ctx* ctx, int root, float* lin_rgba, uint8_t* bgra);
+int iqpt_comm_stream(iqpt_ctx* ctx, void** stream);
+/* Sum of the gathers' durations on the communicator's stream (from the rank's copy being done to the end
+ * of the gather and, on the root, of the assembly: the transfer plus any wait for slower ranks) and their
+ * count, since the last call (then cleared). Synchronises the communicator's stream. */
+int iqpt_comm_time(iqpt_ctx* ctx, double* total_ms, uint64_t* gathers);
 
 int iqpt_num_pixels(const iqpt_ctx* ctx, uint64_t* npix);
 int iqpt_frame_count(const iqpt_ctx* ctx, uint64_t* frames);

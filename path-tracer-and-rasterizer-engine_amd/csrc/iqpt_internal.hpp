@@ -86,6 +86,10 @@ struct kparams {
     // every ray of the pixel's bundle hits: iq_interval.h tri_certain; the reference's materials only);
     // null = none. Such a pixel's samples are (1, 1, 1) folds and two draws each.
     const uint32_t* certain;
+    // per tile, two words: the 64-bit mask of its pixels whose every camera ray is certain to miss every
+    // primitive (the pixel's own bundle culls each candidate, iq_interval.h): their samples are the sky
+    // gradient of the camera ray, rendered by iqpt_sky_kernel; the plain kernel skips them. null = none.
+    const uint32_t* miss;
     // work queue over tiles: queue position q -> tile tile_order[q] (null = identity); built with the
     // masks, most expensive tiles first (longest-processing-time order: a shorter launch tail)
     const uint32_t* tile_order;
@@ -333,6 +337,10 @@ int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, u
 // element width in 32-bit words (4 for the accumulator), the planes are npix * words apart.
 int launch_relayout(void* stream, const uint32_t* src, uint32_t* dst, uint32_t ncols, uint32_t nrows,
                     uint32_t words, uint32_t planes, bool to_compact);
+// Frame assembly after the multi-GPU gather: src = world blocks of `stride` pixels (rank r's rows base + r + k split
+// in compact row-major order), dst = the W x H frame; `words` 32-bit words per pixel (1 BGRA8, 4 accumulator).
+int launch_assemble_rows(void* stream, const uint32_t* src, uint32_t* dst, uint32_t width, uint32_t height,
+                         uint32_t world, uint32_t split, uint32_t base, uint64_t stride, uint32_t words);
 // Tile masks for kOptCull (one thread per tile word).
 int launch_bin(void* stream, const kbin& b);
 // Per-tile candidate counts from the masks (triangle pairs, sphere pairs), and the candidate lists.
@@ -374,6 +382,10 @@ int launch_spec(void* stream, const kparams& p, const kspec& s, int opt);
 int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks);
 // spec blocks and s.fan_tiles fan tiles (p.tile_order / p.fan_lanes) in one grid
 int launch_specfan(void* stream, const kparams& p, const kspec& s, int opt);
+// Certain-miss pixels (iqpt_sky_kernel): the p.miss pixels of `ntiles` tiles (tiles[i]),
+// lane = pixel, one wave per tile; resident scenes, reference materials, spp <= kAccTableMax.
+bool sky_variant_exists(int opt);
+int launch_sky(void* stream, const kparams& p, const uint32_t* tiles, uint32_t ntiles, int opt);
 // Sample-parallel anchored tiles (iqpt_fan_kernel): one block per tile of
 // p.tile_order[0 .. ntiles) — tiles without sphere candidates, reference materials, resident scene
 // (p.cull set, p.cull_wt <= 16), spp <= kAccTableMax.

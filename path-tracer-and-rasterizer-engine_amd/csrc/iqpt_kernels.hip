@@ -1250,6 +1250,8 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // the chunk's tile's certain pixels (kparams::certain): they take the whole launch at once (refill)
     constexpr bool kCertain = !kSplit && !STREAM && (OPT & kOptAccTable) && !(OPT & kOptMaterials) && !(OPT & kOptStats);
     uint64_t chunk_certain = 0;
+    // ... and its certain-miss pixels (kparams::miss): iqpt_sky_kernel renders them, this kernel skips them
+    uint64_t chunk_miss = 0;
     uint32_t queue_total = kOverlap ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : (p.nqueue ? p.nqueue : p.ntiles), n_runs = 0;
     if (kSplit) {
         // round 1, longest tasks first: the split tiles' light pixels (anchored chains with scatters, in
@@ -1360,6 +1362,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     chunk_certain = (kCertain && p.certain != nullptr)
                                         ? ((uint64_t)p.certain[2 * (size_t)t] | ((uint64_t)p.certain[2 * (size_t)t + 1] << 32))
                                         : 0ull;
+                    chunk_miss = (kCertain && p.miss != nullptr)
+                                     ? ((uint64_t)p.miss[2 * (size_t)t] | ((uint64_t)p.miss[2 * (size_t)t + 1] << 32))
+                                     : 0ull;
                     const uint32_t tx = t % p.ntx, ty = t / p.ntx;
                     const uint32_t th = min(kCullTile, p.nrows - ty * kCullTile);
                     const uint32_t tw = min(kCullTile, p.ncols - tx * kCullTile);
@@ -1374,7 +1379,8 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             if (!active && rank < avail) {
                 uint32_t pix = chunk_next + rank;                  // tile-major storage index
                 uint32_t tile = chunk_tile;
-                bool go = true, spec = false;
+                // a certain-miss pixel is iqpt_sky_kernel's: skipped (no state touched, no ray counted here)
+                bool go = !(kCertain && ((chunk_miss >> (pix - chunk_first)) & 1ull)), spec = false;
                 uint32_t sp = 0;
                 if (kSplit && (chunk_kind == 1 || chunk_kind == 3)) {
                     sp = chunk_sp0 + (pix - chunk_first);
@@ -1480,13 +1486,16 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 }
                 if (go) active = true;
             }
-            if (kCertain && chunk_certain) {
+            if (kCertain && (chunk_certain | chunk_miss)) {
                 // the certain pixels of this pass are complete: their rays, and (overlapped launches) their
-                // tile's completion count once their stores are done
+                // tile's completion count once their stores are done; the skipped certain misses count
+                // toward the tile's completion only (the sky kernel renders them and counts their rays)
                 const uint32_t took = prefix_below(need) < avail && ((need >> lane) & 1ull) ? 1u : 0u;
                 const uint32_t nfin = (uint32_t)__popcll(__ballot(took && !active));
+                const uint32_t nmiss = (uint32_t)__popcll(
+                    __ballot(took && ((chunk_miss >> ((chunk_next + prefix_below(need) - chunk_first) & 63u)) & 1ull)));
                 if (nfin) {
-                    wave_rays += (uint64_t)nfin * p.spp;
+                    wave_rays += (uint64_t)(nfin - nmiss) * p.spp;
                     if (kOverlap && p.tile_done) {
                         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                         if (lane == 0) atomicAdd(p.tile_done + chunk_tile, nfin);
@@ -2256,6 +2265,10 @@ __global__ __launch_bounds__(256) void iqpt_bin_kernel(const kbin b) {
 // two jitter draws (path_tracer.cu:278, 341-358; camera.cu:24-25). One wave per tile, lane = pixel in the
 // tile's storage order (row-major inside the tile); certain[2 t], certain[2 t + 1] = the tile's 64-bit
 // mask. Run after iqpt_bin_kernel on the same stream.
+// Round 4: also the converse per pixel, certain misses — the pixel's own bundle culls every candidate triangle
+// and sphere of its tile (iq_interval.h tri_culled / sphere_culled, the tests the tile masks are built with), so
+// every camera ray of the pixel misses everything and ends on the sky gradient (path_tracer.cu:307-316) —
+// into certain[2 ntiles + 2 t], certain[2 ntiles + 2 t + 1] (iqpt_sky_kernel's pixels).
 __global__ __launch_bounds__(64) void iqpt_certain_kernel(const kbin b, uint32_t* certain) {
     const uint32_t t = blockIdx.x, lane = threadIdx.x;
     const uint32_t* m = b.cull + (size_t)t * b.stride;
@@ -2263,8 +2276,8 @@ __global__ __launch_bounds__(64) void iqpt_certain_kernel(const kbin b, uint32_t
     for (uint32_t w = b.wt; w < b.stride; ++w) sph = sph || m[w] != 0u;
     const uint32_t tx = t % b.ntx, ty = t / b.ntx;
     const uint32_t tw = min(kCullTile, b.ncols - tx * kCullTile), th = min(kCullTile, b.nrows - ty * kCullTile);
-    bool ok = false;
-    if (!sph && lane < tw * th) {
+    bool ok = false, miss = false;
+    if (lane < tw * th) {
         const uint32_t col = tx * kCullTile + lane % tw, row = ty * kCullTile + lane / tw;
         iqiv::camera_in ci;
         ci.width = b.width;
@@ -2278,7 +2291,8 @@ __global__ __launch_bounds__(64) void iqpt_certain_kernel(const kbin b, uint32_t
         ci.far_rw = b.cam_far_rw;
         const uint32_t x = b.x0 + col, y = b.y0 + row * b.ystep;
         const iqiv::bundle bd = iqiv::camera_bundle(ci, x, x, y, y);
-        for (uint32_t w = 0; w < b.wt && bd.ok && !ok; ++w) {
+        // certain hit: no sphere candidate in the tile, some candidate triangle accepts every ray
+        for (uint32_t w = 0; !sph && w < b.wt && bd.ok && !ok; ++w) {
             uint32_t bits = m[w];
             while (bits && !ok) {
                 const uint32_t j = w * 32u + (uint32_t)__builtin_ctz(bits);
@@ -2294,11 +2308,39 @@ __global__ __launch_bounds__(64) void iqpt_certain_kernel(const kbin b, uint32_t
                 }
             }
         }
+        // certain miss: every candidate triangle and sphere of the tile culled for the pixel's own bundle
+        miss = bd.ok && !ok;
+        for (uint32_t w = 0; w < b.stride && miss; ++w) {
+            uint32_t bits = m[w];
+            while (bits && miss) {
+                const uint32_t j = (w < b.wt ? w : w - b.wt) * 32u + (uint32_t)__builtin_ctz(bits);
+                bits &= bits - 1u;
+                for (uint32_t e = 0; e < 2u && miss; ++e) {
+                    const uint32_t k = 2u * j + e;
+                    if (w < b.wt) {
+                        if (k >= b.ntri) break;
+                        const float4_storage* tr = b.tris + (size_t)k * kTriFloat4;
+                        const float v0[3] = {tr[0].x, tr[0].y, tr[0].z};
+                        const float e1[3] = {tr[0].w, tr[1].x, tr[1].y};
+                        const float e2[3] = {tr[1].z, tr[1].w, tr[2].x};
+                        miss = iqiv::tri_culled(bd, v0, e1, e2);
+                    } else {
+                        if (k >= b.nsph) break;
+                        const float4_storage sp = b.spheres[k];
+                        const float c[3] = {sp.x, sp.y, sp.z};
+                        miss = iqiv::sphere_culled(bd, c, sp.w);
+                    }
+                }
+            }
+        }
     }
-    const uint64_t mask = __ballot(ok);
+    const uint64_t mask = __ballot(ok), miss_mask = __ballot(miss);
     if (lane == 0) {
+        const size_t nt = (size_t)b.ntx * b.nty;
         certain[2 * (size_t)t] = (uint32_t)mask;
         certain[2 * (size_t)t + 1] = (uint32_t)(mask >> 32);
+        certain[2 * nt + 2 * (size_t)t] = (uint32_t)miss_mask;
+        certain[2 * nt + 2 * (size_t)t + 1] = (uint32_t)(miss_mask >> 32);
     }
 }
 
@@ -2349,6 +2391,27 @@ __global__ __launch_bounds__(256) void iqpt_relayout_kernel(const uint32_t* __re
     const uint64_t si = plane * npix * words + (uint64_t)s * words + k;
     if (to_compact) dst[ci] = src[si];
     else dst[si] = src[ci];
+}
+
+// Multi-GPU frame assembly on the gather's root: the gathered buffer holds, per rank r <
+// world, `stride` pixels of `words` words — rank r's rows b + r, b + r + S, ... of an S-way cyclic split in
+// compact row-major order — and row k of rank r is row b + r + k S of the W x H frame (S = world and b = 0
+// on a real node; a one-rank rehearsal of an S-way share, rank 0 owning rows b + k S, writes those rows
+// only). One thread per gathered word.
+__global__ __launch_bounds__(256) void iqpt_assemble_rows_kernel(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                                 uint32_t width, uint32_t height, uint32_t world,
+                                                                 uint32_t split, uint32_t base, uint64_t stride,
+                                                                 uint32_t words) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+    if (i >= (uint64_t)world * stride * words) return;
+    const uint64_t blk = stride * words;
+    const uint32_t r = (uint32_t)(i / blk);
+    const uint64_t e = i - (uint64_t)r * blk;
+    const uint64_t px = e / words;
+    const uint32_t row = (uint32_t)(px / width), x = (uint32_t)(px - (uint64_t)row * width);
+    const uint64_t y = (uint64_t)base + r + (uint64_t)row * split;
+    if (y >= height) return;                          // padding past this rank's last row
+    dst[(y * width + x) * words + (e - px * words)] = src[i];
 }
 
 // curand_init(seed, global pixel id, 0) per owned pixel (renderer_init_kernel, path_tracer.cu:36-46).
@@ -3080,10 +3143,15 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
 // jitter (camera.cu:24-25) plus 2 per Oren-Nayar scatter (material.cu:10), and what a sample does from
 // stream offset 2j ("slot" j) depends on j alone. One kernel, L = 8, 16, 32 or 64 lanes per sphere pixel
 // (16 without a plan; a plan gives the pixels with the most work per lane more lanes, runtime):
-//  * slots: the pixel's window of M slots (its last chain's slots per sample, spec_window) is cut into L
-//    ranges; each lane steps its state to its range's first slot and traces the range's slots back to
-//    back (the next slot's state is the one the current slot's camera draws leave), one ray per live lane
-//    per iteration; colours go to HBM, the slot counts to LDS;
+//  * slots (round 4: coalescing chains): the pixel's window of M slots (its last chain's slots per sample,
+//    spec_window) gets L starting points j0 = M l / L; lane l steps its state to its start and FOLLOWS THE
+//    CHAIN from there — a sample that used n slots leaves exactly the state slot j + n starts from — taking
+//    each slot it traces in an LDS mark, until the window's end or a slot another lane has taken: from that
+//    slot on, the chain is the other lane's (chains from different starts meet and then coincide), so the
+//    lane stops. Slot 0 is on the true chain, hence by induction every slot of the true chain is traced by
+//    some lane; the waste is only each lane's prefix before it meets the true chain (one or two samples)
+//    instead of every dead slot of the window (the earlier form traced all M slots: rho x the chain's work
+//    at rho slots per sample). One ray per live lane per iteration; colours go to HBM, slot counts to LDS;
 //  * walk: one lane per pixel follows the chain 0 -> j + n_j -> ... in LDS, a batch of chain samples at a
 //    time; the pixel's lanes gather their colours, form the mean terms with the plain kernel's table
 //    values and count each sample's rays (its slots, or max_depth when it ended on a scatter at
@@ -3096,6 +3164,7 @@ constexpr uint32_t kSpecLanes = 16;                    // lanes per sphere pixel
 constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per block without a plan
 constexpr uint32_t kSpecMaxPix = 32;                   // pixels per block at 8 lanes each
 constexpr uint32_t kSpecBatch = 512;                   // walk: chain samples gathered per block and batch
+constexpr uint8_t kSpecTaken = 0xffu;                  // slot mark: a lane is tracing it (slot counts are <= 17)
 static_assert(kSpecPix == kSpecPixPerBlock && kSpecMaxPix == kSpecMaxPixPerBlock, "runtime and kernel agree on the spec block");
 
 __host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth, uint32_t spp,
@@ -3197,8 +3266,11 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     while (__syncthreads_or(rd[7] == 0u)) {
         const bool live = rd[7] == 0u;
         const uint32_t js = rd[0], M = rd[1];
-        // ---- slots [js + j0, js + j1) of this lane, relative slot indices j
-        const uint32_t j0 = M * l / L, j1 = M * (l + 1u) / L;
+        // ---- the window's slot marks: 0 not taken, kSpecTaken taken by a lane, else the slots its sample used
+        for (uint32_t i = l; i < M; i += L) ln[i] = 0u;
+        // ---- this lane's chain starts at slot j0 = M l / L (relative to js), with the state 2 j0 draws in
+        const uint32_t j0 = M * l / L;
+        const bool first_ok = live && j0 < M && (l == 0u || M * (l - 1u) / L < j0);
         rng6 st = {rd[2], rd[3], rd[4], rd[5], rd[6], p.rng[5 * (size_t)p.npix + rd[13]] + 2u * (js + j0) * IQ_XORWOW_WEYL};
         xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, live ? 2u * j0 : 0u);
         lst[l * 5u] = st.v0;
@@ -3206,15 +3278,16 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         lst[l * 5u + 2u] = st.v2;
         lst[l * 5u + 3u] = st.v3;
         lst[l * 5u + 4u] = st.v4;
+        __syncthreads();                                 // the marks are clear before any lane takes a slot
+        if (first_ok) ln[j0] = kSpecTaken;
         uint32_t j = j0;
-        bool active = live && j0 < j1;
-        rng6 base = st;
+        bool active = first_ok;
         ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         int depth = 0;
-        // a slot's sample starts here: its camera ray, and the state its two draws leave (the next slot's)
+        // a slot's sample starts here: its camera ray (two draws); its scatters draw two more each, so when it
+        // ends having used n slots the state is the one slot j + n starts from
         auto start_slot = [&]() {
             camera_ray<OPT>(p, px, py, st, ray);
-            base = st;
             depth = 0;
         };
         if (active) start_slot();
@@ -3284,11 +3357,16 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                     cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
                     cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
                     res[j] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
-                    ln[j] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
-                    if (++j == j1) {
+                    const uint32_t n = (uint32_t)depth + 1u + md_end;  // slots: 1 + its scatters
+                    ln[j] = (uint8_t)n;
+                    // follow the chain: the next sample starts at slot j + n from the state this one left.
+                    // A slot another lane has taken is on a chain that lane follows to the window's end
+                    // (or to a slot taken before it), so this lane's chain has merged into it and stops.
+                    j += n;
+                    if (j >= M || *reinterpret_cast<volatile uint8_t*>(ln + j) != 0u) {
                         active = false;
                     } else {
-                        st = base;                   // slot j starts where slot j - 1's camera draws ended
+                        ln[j] = kSpecTaken;
                         start_slot();
                     }
                 }
@@ -3307,8 +3385,16 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             if (walker && live) {
                 uint32_t c = 0;
                 while (c < batch && k + c < p.spp && jw < M) {
+                    const uint32_t nj = ln[jw];
+                    if (nj - 1u >= (uint32_t)kSpecTaken - 1u) {
+                        // a chain slot no lane traced: impossible by construction (every taken slot's chain
+                        // is followed to the window's end); report it instead of folding garbage
+                        atomicOr(p.ovl_err, 8u);
+                        jw = M;
+                        break;
+                    }
                     lp[c++] = (uint16_t)jw;
-                    jw += ln[jw];
+                    jw += nj;
                 }
                 lds_w[2 * g] = c;
             }
@@ -3397,6 +3483,82 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
     if (__lane_id() == 0 && rays) add_rays(p.rays, rays);
+}
+
+// ------------------------------------------------------------------------------------------------
+// Certain-miss pixels. A pixel whose own camera-ray bundle (its jitter square, iq_interval.h)
+// is proven to miss every primitive ends every sample on its camera ray with the sky gradient
+// (path_tracer.cu:307-316), after exactly the camera's two jitter draws (camera.cu:24-25): one ray per sample,
+// no intersection test, no scatter. Lane = pixel, one wave per tile of such pixels (kparams::miss), four tiles
+// per block; each lane runs its samples in order — camera ray, sky colour, clamp, running mean with the plain
+// kernel's table values and mean terms — the plain kernel's own operations for that path, so the same bits,
+// at a fraction of its per-iteration cost (no mask, no closest-hit loop, no refill or path bookkeeping).
+constexpr uint32_t kSkyBlock = 256;
+
+template <int OPT>
+__global__ __launch_bounds__(kSkyBlock) void iqpt_sky_kernel(const kparams p, const uint32_t* __restrict__ tiles,
+                                                             uint32_t ntiles) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    float2* tab = reinterpret_cast<float2*>(lds);
+    float* tab_n = reinterpret_cast<float*>(tab + ((p.spp + 1u) & ~1u));
+    for (uint32_t k = threadIdx.x; k < p.spp; k += kSkyBlock) {
+        const uint64_t n = p.frame0 + k + 1;
+        tab[k] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
+        tab_n[k] = (float)n;
+    }
+    __syncthreads();
+    const uint32_t w = blockIdx.x * (kSkyBlock / 64u) + threadIdx.x / 64u;
+    if (w >= ntiles) return;
+    const uint32_t lane = __lane_id();
+    const uint32_t t = tiles[w];
+    const uint64_t miss = (uint64_t)p.miss[2 * (size_t)t] | ((uint64_t)p.miss[2 * (size_t)t + 1] << 32);
+    if ((miss >> lane) & 1ull) {
+        const uint32_t tx = t % p.ntx, ty = t / p.ntx;
+        const uint32_t th = min(kCullTile, p.nrows - ty * kCullTile);
+        const uint32_t pix = ty * kCullTile * p.ncols + tx * kCullTile * th + lane;   // tile-major storage
+        uint32_t col, row;
+        tile_decode(pix, p.ncols, p.nrows, &col, &row);
+        const uint32_t px = p.x0 + col, py = p.y0 + row * p.ystep;
+        rng6 st = {p.rng[pix], p.rng[(size_t)p.npix + pix], p.rng[2 * (size_t)p.npix + pix],
+                   p.rng[3 * (size_t)p.npix + pix], p.rng[4 * (size_t)p.npix + pix], p.rng[5 * (size_t)p.npix + pix]};
+        const float4 a0 = reinterpret_cast<const float4*>(p.lin)[pix];
+        float ax = a0.x, ay = a0.y, az = a0.z;
+        for (uint32_t k = 0; k < p.spp; ++k) {
+            ray3 ray;
+            camera_ray<OPT>(p, px, py, st, ray);
+            // sky gradient (:308-313), no records: the colour itself, clamped (:345-347), 0 + colour (:341, 348)
+            const float a = (ray.dy + 1.0f) * 0.5f;
+            const float one_a = 1.0f - a;
+            float cx = one_a + a * 0.5f, cy = one_a + a * 0.7f, cz = one_a + a * 1.0f;
+            cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+            cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+            cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+            cx = 0.0f + cx;
+            cy = 0.0f + cy;
+            cz = 0.0f + cz;
+            // running mean (:356-358) with the launch table's RN(1 / n), (n - 1) / n and (float) n
+            const float2 tv = tab[k];
+            float qx, qy, qz;
+            mean_terms<OPT>(cx, cy, cz, tab_n[k], tv.x, p.mean_tiny, qx, qy, qz);
+            ax = qx + ax * tv.y;
+            ay = qy + ay * tv.y;
+            az = qz + az * tv.y;
+        }
+        const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
+        const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
+        const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
+        p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+        reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
+        p.rng[pix] = st.v0;
+        p.rng[(size_t)p.npix + pix] = st.v1;
+        p.rng[2 * (size_t)p.npix + pix] = st.v2;
+        p.rng[3 * (size_t)p.npix + pix] = st.v3;
+        p.rng[4 * (size_t)p.npix + pix] = st.v4;
+        p.rng[5 * (size_t)p.npix + pix] = st.d;
+    }
+    // one closest-hit query per sample (path_tracer.cu:252-318: the miss ends the loop at crt_depth 1)
+    const uint32_t nm = (uint32_t)__popcll(miss);
+    if (lane == 0 && nm) add_rays(p.rays, (unsigned long long)nm * p.spp);
 }
 
 template <int OPT>
@@ -3537,6 +3699,15 @@ int launch_relayout(void* stream, const uint32_t* src, uint32_t* dst, uint32_t n
     if (n == 0) return 0;
     hipLaunchKernelGGL(iqpt_relayout_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        src, dst, ncols, nrows, words, planes, to_compact ? 1 : 0);
+    return (int)hipGetLastError();
+}
+
+int launch_assemble_rows(void* stream, const uint32_t* src, uint32_t* dst, uint32_t width, uint32_t height,
+                         uint32_t world, uint32_t split, uint32_t base, uint64_t stride, uint32_t words) {
+    const uint64_t n = (uint64_t)world * stride * words;
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(iqpt_assemble_rows_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       src, dst, width, height, world, split, base, stride, words);
     return (int)hipGetLastError();
 }
 
@@ -3686,6 +3857,41 @@ const fan_variant* find_fan(int opt) {
 }  // namespace
 
 bool fan_variant_exists(int opt) { return find_fan(opt) != nullptr; }
+
+// iqpt_sky_kernel launches: keyed like the fan kernel (camera form, division forms)
+namespace {
+template <int OPT>
+int sky_launch_t(hipStream_t stream, const kparams& p, const uint32_t* tiles, uint32_t ntiles, uint32_t lds) {
+    hipLaunchKernelGGL((iqpt_sky_kernel<OPT>), dim3((ntiles + kSkyBlock / 64u - 1u) / (kSkyBlock / 64u)),
+                       dim3(kSkyBlock), lds, stream, p, tiles, ntiles);
+    return (int)hipGetLastError();
+}
+struct sky_variant {
+    int key;
+    int (*launch)(hipStream_t, const kparams&, const uint32_t*, uint32_t, uint32_t);
+};
+const sky_variant kSkyVariants[] = {
+    {kOptFastDiv, sky_launch_t<kOptDefault>},
+    {0, sky_launch_t<kOptDefault & ~kOptFastDiv>},
+    {kOptFastDiv | kOptCamAxis, sky_launch_t<kOptDefault | kOptCamAxis>},
+};
+const sky_variant* find_sky(int opt) {
+    if ((opt & (kOptAccTable | kOptCamConst)) != (kOptAccTable | kOptCamConst) || (opt & (kOptMaterials | kOptStats)))
+        return nullptr;
+    for (const sky_variant& v : kSkyVariants)
+        if (v.key == (opt & kFanKeyBits)) return &v;
+    return nullptr;
+}
+}  // namespace
+
+bool sky_variant_exists(int opt) { return find_sky(opt) != nullptr; }
+
+int launch_sky(void* stream, const kparams& p, const uint32_t* tiles, uint32_t ntiles, int opt) {
+    const sky_variant* v = find_sky(opt);
+    if (!v || p.spp > kAccTableMax || p.miss == nullptr || tiles == nullptr) return (int)hipErrorInvalidDeviceFunction;
+    if (ntiles == 0 || p.spp == 0) return 0;
+    return v->launch((hipStream_t)stream, p, tiles, ntiles, ((p.spp + 1u) & ~1u) * 8u + ((p.spp + 3u) & ~3u) * 4u);
+}
 
 uint32_t fan_lds(const kparams& p) { return fan_lds_bytes(p.ntri_pairs, p.spp); }
 

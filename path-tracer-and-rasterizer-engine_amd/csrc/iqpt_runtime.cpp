@@ -3,7 +3,9 @@
 //
 // Replaces the CUDA side of path_tracer (IoniqRE/path_tracer.cu:48-164, 368-404) and the upload
 // half of scene::build_packet / free_packet (IoniqRE/scene.cu:183-264).
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -45,7 +47,8 @@ constexpr double kSplitAutoPixelsPerLane = 1.2;
 constexpr double kChainAutoPixelsPerLane = 2.0;
 // spec launches: AUTO takes them below this many owned pixels per resident lane of the
 // plain kernel (C3 shares: N = 8 has 0.8, N = 4 1.6, N = 2 3.2; pipelined spec launches 0.27 / 0.47 / 0.87 ms
-// per step through the gather against plain 0.95 / 1.0 / 0.91; N = 1, 6.3, stays plain; profiles/r03/share_modes.json)
+// per step through the gather against plain 0.95 / 1.0 / 0.91; N = 1, 6.3, stays plain; profiles/r03/
+// split_share_run37.json, r03_share_v11.json, run49_share{2,4,8}_2.json)
 constexpr double kSpecAutoPixelsPerLane = 4.0;
 constexpr uint32_t kChainWavesPerCu = 16;
 constexpr size_t kSplitResBudget = size_t(8) << 30;   // speculative results (bytes)
@@ -93,6 +96,7 @@ struct iqpt_ctx {
     uint64_t frame = 0;
     int num_cus = 0;
     int num_xcc = 0;              // XCDs of the device (overlapped launches bind tiles to the 8 XCDs)
+    uint32_t lds_per_block = 0;   // the device's LDS limit per workgroup (bytes)
     int opt = iqpt::kOptDefault;
     bool have_camera = false, have_packet = false;
     iqpt_camera cam{};
@@ -134,6 +138,13 @@ struct iqpt_ctx {
     uint32_t* d_certain = nullptr;      // per tile: 64-bit mask of pixels certain to end on an emissive triangle
     bool certain_valid = false;         // d_certain holds the current masks' flags (no material table)
     bool certain_on = true;             // iqpt_debug_set_certain (A/B: 0 renders certain tiles normally)
+    // certain-miss pixels: the tiles holding some (d_certain + 2 ntiles has their masks), the
+    // pixel count; plain launches hand them to iqpt_sky_kernel (iqpt_debug_set_sky: 0 traces them as before)
+    uint32_t* d_sky_tiles = nullptr;
+    uint32_t n_sky_tiles = 0, n_sky_pixels = 0;
+    bool sky_on = true;
+    hipEvent_t ev_sky = nullptr;        // after the last sky kernel (the next one, maybe on the other stream, waits)
+    hipStream_t sky_last = nullptr;     // the stream of the last sky kernel since the streams were joined
     uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
     uint32_t* d_list = nullptr;         // candidate lists of the masks, then their offsets (tri, sph)
     uint64_t list_total = 0;
@@ -265,6 +276,24 @@ struct iqpt_ctx {
     // gave up or a chain wave past its bound the pixel state is undefined, so every later call that
     // returns or persists pixel state fails until iqpt_checkpoint_load replaces the whole state
     uint32_t dev_err = 0;
+    // multi-GPU frame delivery (iqpt_comm_init): an RCCL communicator over the ranks of one
+    // frame's cyclic row split and its own stream. A gather copies the rank's pixels (compact order, padded
+    // to comm_stride pixels) into one of two send buffers in turn — the copy of gather g waits only for
+    // gather g - 2 — then ncclGather to the root, which assembles the frame from the rank blocks.
+    void* comm = nullptr;                // ncclComm_t
+    int comm_rank = 0, comm_world = 0;
+    uint64_t comm_stride = 0;            // pixels per rank block: the most rows any rank owns x W
+    hipStream_t cstream = nullptr;
+    uint32_t* d_gsend[2] = {nullptr, nullptr};   // comm_stride x 4 words each
+    hipEvent_t ev_gdone[2] = {nullptr, nullptr}; // on cstream, after the gather that read d_gsend[i]
+    bool gdone_pend[2] = {false, false};
+    uint32_t gpar = 0;                   // the send buffer of the next gather
+    hipEvent_t ev_gcopy = nullptr;       // after the copy into the send buffer (cstream waits for it)
+    hipEvent_t ev_gend = nullptr;        // on cstream, after the last gather (every other entry point joins it)
+    bool comm_pend = false;
+    uint32_t* d_grecv = nullptr;         // root: comm_world x comm_stride x 4 words
+    uint32_t* d_gframe = nullptr;        // root: the assembled W x H x 4 words of iqpt_gather_read
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> gtimed;   // per gather: cstream events around it (iqpt_comm_time)
 };
 
 namespace {
@@ -290,13 +319,32 @@ int join_streams(iqpt_ctx* c) {
     c->next_on_main = true;
     c->ovl_zero = true;
     c->last_ovl = false;
+    c->sky_last = nullptr;             // everything before is ordered on `stream` now
     return IQPT_OK;
 }
 
-// Every entry point but iqpt_render: the device, then the streams joined.
+// Pipelined launches: the frame-copy stream and its two events, created when the first pipelined launch
+// ends, so that iqpt_frame_stream names the stream the next copy goes on before any copy was asked for.
+int ensure_copy_stream(iqpt_ctx* c) {
+    if ((!c->stream3 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) ||
+        (!c->ev_copy_cur && hipEventCreateWithFlags(&c->ev_copy_cur, hipEventDisableTiming) != hipSuccess) ||
+        (!c->ev_copy_alt && hipEventCreateWithFlags(&c->ev_copy_alt, hipEventDisableTiming) != hipSuccess)) {
+        (void)hipGetLastError();
+        return iqpt::fail(IQPT_ERR_HIP, "frame copy stream");
+    }
+    return IQPT_OK;
+}
+
+// Every entry point but iqpt_render: the device, then the streams joined — the gathers in flight too
+// (they read the send buffers and write the caller's frame; a render never waits for them: the copy
+// into a send buffer is ordered behind the launch that wrote the frame, on the launch's own stream).
 int enter(iqpt_ctx* c) {
     int st = use_device(c);
     if (st) return st;
+    if (c->comm_pend) {
+        IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_gend, 0));
+        c->comm_pend = false;
+    }
     return join_streams(c);
 }
 
@@ -425,7 +473,8 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     for (uint32_t q = 0; q < n; ++q) {
         const uint32_t r = rho[q] ? rho[q] : ks.rho0;
         const uint32_t m = iqpt::spec_window(r, p.spp, ks.m_cap, ks.margin_div);
-        w[q] = (double)m * (double)std::max<uint32_t>(r, 256u) / 256.0;
+        // lanes follow the chain (round 4): each window slot is traced about once, as one ray
+        w[q] = (double)m;
         total += w[q];
         wmax = std::max(wmax, w[q]);
     }
@@ -592,15 +641,37 @@ int build_cull(iqpt_ctx* c) {
     c->d_certain = nullptr;
     std::vector<uint32_t> certain;
     const uint64_t resident_bytes = (uint64_t)ntp * iqpt::kTriPairFloat4 * 16u + (uint64_t)nsp * iqpt::kSphPairFloat4 * 16u;
+    if (c->d_sky_tiles) (void)hipFree(c->d_sky_tiles);
+    c->d_sky_tiles = nullptr;
+    c->n_sky_tiles = 0;
+    c->n_sky_pixels = 0;
     if (!c->d_mats && ntiles > 0 && resident_bytes <= iqpt::kLdsResidentBytes) {
-        if (hipMalloc(&c->d_certain, 2 * (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
+        // per tile: the certain-hit mask (2 words), then after all tiles the certain-miss masks (2 words each)
+        if (hipMalloc(&c->d_certain, 4 * (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "certain pixel masks");
         const int lc = iqpt::launch_certain(c->stream, b, c->d_certain);
         if (lc != 0) return iqpt::hip_fail((hipError_t)lc, "certain pixel kernel");
-        certain.resize(2 * (size_t)ntiles);
-        IQPT_HIP(hipMemcpyAsync(certain.data(), c->d_certain, 2 * (size_t)ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
+        certain.resize(4 * (size_t)ntiles);
+        IQPT_HIP(hipMemcpyAsync(certain.data(), c->d_certain, 4 * (size_t)ntiles * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                 c->stream));
+        IQPT_HIP(hipStreamSynchronize(c->stream));
         c->certain_valid = true;
+        // the tiles holding certain-miss pixels: iqpt_sky_kernel's work list (one wave each)
+        std::vector<uint32_t> sky;
+        for (uint32_t t = 0; t < ntiles; ++t) {
+            const uint64_t m = (uint64_t)certain[2 * (size_t)ntiles + 2 * (size_t)t] |
+                               ((uint64_t)certain[2 * (size_t)ntiles + 2 * (size_t)t + 1] << 32);
+            if (m) {
+                sky.push_back(t);
+                c->n_sky_pixels += (uint32_t)__builtin_popcountll(m);
+            }
+        }
+        if (!sky.empty()) {
+            if (hipMalloc(&c->d_sky_tiles, sky.size() * sizeof(uint32_t)) != hipSuccess)
+                return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "sky tile list");
+            IQPT_HIP(hipMemcpy(c->d_sky_tiles, sky.data(), sky.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+            c->n_sky_tiles = (uint32_t)sky.size();
+        }
     }
     // queue order over tiles (a queue chunk is one tile): most expensive first, so the pixels that set
     // the end of the launch are cheap ones. Cost = candidate triangle pairs + 8 x candidate sphere pairs
@@ -626,8 +697,12 @@ int build_cull(iqpt_ctx* c) {
             const uint32_t tx = t % c->cull_ntx, ty = t / c->cull_ntx;
             const uint32_t npt = std::min(iqpt::kCullTile, c->ncols - tx * iqpt::kCullTile) *
                                  std::min(iqpt::kCullTile, c->set.nrows - ty * iqpt::kCullTile);
-            const uint32_t nc = (uint32_t)__builtin_popcountll((uint64_t)certain[2 * (size_t)t] |
-                                                               ((uint64_t)certain[2 * (size_t)t + 1] << 32));
+            uint32_t nc = (uint32_t)__builtin_popcountll((uint64_t)certain[2 * (size_t)t] |
+                                                         ((uint64_t)certain[2 * (size_t)t + 1] << 32));
+            // certain misses leave the plain kernel's work too when the sky kernel takes them
+            if (c->sky_on)
+                nc += (uint32_t)__builtin_popcountll((uint64_t)certain[2 * (size_t)ntiles + 2 * (size_t)t] |
+                                                     ((uint64_t)certain[2 * (size_t)ntiles + 2 * (size_t)t + 1] << 32));
             cost[t] = (uint32_t)(((uint64_t)cost[t] * (npt - std::min(nc, npt)) + npt - 1) / npt);
         }
     // candidate lists for the streamed kernel (pairs of a tile without scanning its mask words): only
@@ -977,6 +1052,7 @@ int check_dev_err(iqpt_ctx* c) {
     if (!c->dev_err) return IQPT_OK;
     return iqpt::fail(IQPT_ERR_HIP, std::string((c->dev_err & 2u)   ? "chain launch: a wave exceeded its iteration bound"
                                                 : (c->dev_err & 4u) ? "overlapped launch: an XCD's tiles were never taken"
+                                                : (c->dev_err & 8u) ? "spec launch: a chain slot was never traced"
                                                                     : "overlapped launch: a per-tile wait timed out") +
                                         " (pixel state undefined until iqpt_checkpoint_load)");
 }
@@ -990,6 +1066,71 @@ hipEvent_t take_event(iqpt_ctx* c) {
     hipEvent_t e = nullptr;
     if (hipEventCreate(&e) != hipSuccess) return nullptr;
     return e;
+}
+
+// RCCL, bound at the first iqpt_comm_* call (dlopen by SONAME): a process that already holds an RCCL — the
+// one PyTorch-ROCm ships, also librccl.so.1 — shares it instead of loading a second copy, and a single-GPU
+// user of libiqpt never needs it. The entry points are RCCL's C API (/opt/rocm/include/rccl/rccl.h).
+struct rccl_api {
+    ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
+    const char* (*error_string)(ncclResult_t) = nullptr;
+    std::string why;
+};
+
+const rccl_api& rccl() {
+    static rccl_api api;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = nullptr;
+        for (const char* name : {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"})
+            if ((h = dlopen(name, RTLD_NOW | RTLD_GLOBAL)) != nullptr) break;
+        if (!h) {
+            const char* e = dlerror();
+            api.why = std::string("RCCL not loadable: ") + (e ? e : "librccl.so.1");
+            return;
+        }
+        api.get_unique_id = reinterpret_cast<decltype(api.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
+        api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
+        api.gather = reinterpret_cast<decltype(api.gather)>(dlsym(h, "ncclGather"));
+        api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(h, "ncclGetErrorString"));
+        if (!api.get_unique_id || !api.comm_init_rank || !api.comm_destroy || !api.gather || !api.error_string) {
+            api.get_unique_id = nullptr;
+            api.why = "RCCL lacks ncclGetUniqueId / ncclCommInitRank / ncclCommDestroy / ncclGather";
+        }
+    });
+    return api;
+}
+
+int rccl_fail(ncclResult_t r, const char* what) {
+    return iqpt::fail(IQPT_ERR_HIP, std::string(what) + ": " + (rccl().error_string ? rccl().error_string(r) : "?"));
+}
+
+void free_comm(iqpt_ctx* c) {
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    if (c->comm && rccl().comm_destroy) (void)rccl().comm_destroy(static_cast<ncclComm_t>(c->comm));
+    c->comm = nullptr;
+    for (uint32_t** b : {&c->d_gsend[0], &c->d_gsend[1], &c->d_grecv, &c->d_gframe}) {
+        if (*b) (void)hipFree(*b);
+        *b = nullptr;
+    }
+    for (hipEvent_t* e : {&c->ev_gdone[0], &c->ev_gdone[1], &c->ev_gcopy, &c->ev_gend}) {
+        if (*e) (void)hipEventDestroy(*e);
+        *e = nullptr;
+    }
+    for (auto& g : c->gtimed) {
+        c->event_pool.push_back(g.first);
+        c->event_pool.push_back(g.second);
+    }
+    c->gtimed.clear();
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    c->cstream = nullptr;
+    c->gdone_pend[0] = c->gdone_pend[1] = false;
+    c->comm_pend = false;
+    c->comm_world = 0;
 }
 
 }  // namespace
@@ -1051,6 +1192,7 @@ int iqpt_create(int device, uint32_t width, uint32_t height, const iqpt_pixel_se
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return cleanup(iqpt::fail(IQPT_ERR_HIP, "hipGetDeviceProperties"));
     c->num_cus = prop.multiProcessorCount;
+    c->lds_per_block = (uint32_t)prop.sharedMemPerBlock;
     if (hipDeviceGetAttribute(&c->num_xcc, hipDeviceAttributeNumberOfXccs, device) != hipSuccess) {
         (void)hipGetLastError();
         c->num_xcc = 0;
@@ -1093,6 +1235,8 @@ int iqpt_destroy(iqpt_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
+    if (c->stream3) (void)hipStreamSynchronize(c->stream3);
+    free_comm(c);
     free_scene(c);
     if (c->d_lin) (void)hipFree(c->d_lin);
     if (c->d_bgra) (void)hipFree(c->d_bgra);
@@ -1118,6 +1262,8 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->d_stats) (void)hipFree(c->d_stats);
     if (c->d_cull) (void)hipFree(c->d_cull);
     if (c->d_certain) (void)hipFree(c->d_certain);
+    if (c->d_sky_tiles) (void)hipFree(c->d_sky_tiles);
+    if (c->ev_sky) (void)hipEventDestroy(c->ev_sky);
     if (c->d_tile_order) (void)hipFree(c->d_tile_order);
     if (c->d_list) (void)hipFree(c->d_list);
     for (auto& tl : c->timed)
@@ -1531,9 +1677,21 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
                         iqpt::fan_variant_exists(opt);
     const bool fan = !chain && fan_ok && c->split_mode == IQPT_SPLIT_FAN;
     // spec launches: sphere pixels slot-parallel, every other pixel in the fan kernel
-    const bool spec = (!chain || auto_spec) && fan_ok && (c->split_mode == IQPT_SPLIT_SPEC || auto_spec) && c->n_split_tiles > 0 &&
-                      iqpt::spec_variant_exists(c->max_depth, opt) &&
-                      (size_t)c->n_chain_pix * ((iqpt::kSplitMCapMul * spp + 15u) & ~15u) * 16u <= iqpt::kSplitResBudget;
+    bool spec = (!chain || auto_spec) && fan_ok && (c->split_mode == IQPT_SPLIT_SPEC || auto_spec) && c->n_split_tiles > 0 &&
+                iqpt::spec_variant_exists(c->max_depth, opt) &&
+                (size_t)c->n_chain_pix * ((iqpt::kSplitMCapMul * spp + 15u) & ~15u) * 16u <= iqpt::kSplitResBudget;
+    if (spec) {
+        // the block's LDS (scene, tables, slot marks: 32 pixels x the window cap) must fit the device's per-block
+        // limit with at least one resident block, else the plain path (same bits; ADVICE r3: a 1,024-spp launch
+        // with a scene near the resident limit needs ~170 KB)
+        iqpt::kspec probe;
+        std::memset(&probe, 0, sizeof probe);
+        probe.m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
+        int occ_s = 0;
+        spec = iqpt::spec_lds(p, probe) <= c->lds_per_block && probe.m_cap <= 65535u &&
+               iqpt::spec_occupancy(p, probe, opt, &occ_s) == 0 && occ_s >= 1;
+        (void)hipGetLastError();
+    }
     bool fan_beside_chain = chain && fan_ok && c->fan_anchored;
     if (spec) chain = fan_beside_chain = false;
     uint32_t lds_split = lds + iqpt::kRenderBlock * (16u + 24u);   // + lds_sp and the base states
@@ -1743,6 +1901,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             return iqpt::fail(IQPT_ERR_HIP, "pipelined launch events");
         }
         IQPT_HIP(hipEventRecord(c->ev_pipe_end, c->stream));
+        if (int s = ensure_copy_stream(c)) return s;
         e1b = take_event(c);
         if (e1b) (void)hipEventRecord(e1b, c->stream2);
         c->s2_pending = true;
@@ -1750,6 +1909,25 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->pipe_kind = kind;
         return IQPT_OK;
     };
+    // certain-miss pixels: plain launches hand them to iqpt_sky_kernel, ahead of the plain
+    // kernel on the launch's stream; the plain kernel skips them. Consecutive sky kernels order themselves
+    // through ev_sky (overlapped launches alternate streams); their pixels are disjoint from the plain kernel's.
+    const bool sky = c->sky_on && c->certain_on && c->certain_valid && c->n_sky_tiles > 0 && p.certain != nullptr &&
+                     !stream_batches && !split && !chain && !fan && !spec && tune_slot < 0 &&
+                     !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax && iqpt::sky_variant_exists(opt);
+    if (sky) {
+        p.miss = c->d_certain + 2 * (size_t)c->cull_ntx * c->cull_nty;
+        if (!c->ev_sky && hipEventCreateWithFlags(&c->ev_sky, hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            return iqpt::fail(IQPT_ERR_HIP, "sky kernel event");
+        }
+        const hipStream_t ss = ovl ? ls : c->stream;
+        if (c->sky_last && c->sky_last != ss) IQPT_HIP(hipStreamWaitEvent(ss, c->ev_sky, 0));
+        le = iqpt::launch_sky(ss, p, c->d_sky_tiles, c->n_sky_tiles, opt);
+        if (le != 0) return iqpt::hip_fail((hipError_t)le, "sky kernel launch");
+        IQPT_HIP(hipEventRecord(c->ev_sky, ss));
+        c->sky_last = ss;
+    }
     if (ovl) {
         le = iqpt::launch_render(ls, p, grid, lds, stream_batches, opt);
         c->ovl_epoch += 1;
@@ -1874,6 +2052,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             c->spec_mcap = m_cap;
             c->spec_rho_valid = false;
         }
+        p.ovl_err = c->d_ovl_err;          // bit 3: a chain slot no lane traced (never expected)
         ks2.n = n;
         ks2.m_cap = m_cap;
         ks2.rho0 = c->spec_rho0;
@@ -1883,7 +2062,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.rho = c->d_spec + n;
         ks2.run_count = c->d_spec + 2 * (size_t)n;
         ks2.res = c->d_spec_res;
-        if (n > 0 && !c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, (size_t)n * sizeof(uint32_t), c->stream));
+        // a new pixel list: no history, and the statistics counters behind it (d_spec + 2 n) restart too
+        // (after a list that shrank n they pointed into the old history)
+        if (n > 0 && !c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, ((size_t)n + 2) * sizeof(uint32_t), c->stream));
         c->spec_rho_valid = c->spec_rho_valid || n > 0;
         if (c->specfan_mode == 0 && (st = pipe_begin()) != IQPT_OK) return st;
         iqpt::kparams pf = p;
@@ -2340,6 +2521,25 @@ int iqpt_debug_set_certain(iqpt_ctx* c, int on) {
     return IQPT_OK;
 }
 
+/* Internal (A/B, tests): certain-miss pixels rendered by iqpt_sky_kernel beside plain launches (1, the default)
+ * or traced by the plain kernel like every other pixel (0). Rebuilds the masks at the next launch. */
+int iqpt_debug_set_sky(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->sky_on = on != 0;
+    c->cull_valid = false;
+    return IQPT_OK;
+}
+
+/* Internal (tools): the certain-miss pixels of the current masks and the tiles holding them. */
+int iqpt_debug_sky_info(iqpt_ctx* c, uint32_t* pixels, uint32_t* tiles) {
+    if (!c || !pixels || !tiles) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *pixels = c->certain_valid ? c->n_sky_pixels : 0u;
+    *tiles = c->certain_valid ? c->n_sky_tiles : 0u;
+    return IQPT_OK;
+}
+
 /* Internal (tools, tests): certain pixels of the current masks (*n; 0 without masks or flags), the tile
  * count and the tile grid's width in tiles (*ntx) and, if masks is not NULL, up to cap tiles' 64-bit
  * masks (two words per tile). Synchronises. */
@@ -2433,14 +2633,15 @@ int iqpt_copy_frame_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
     return check_dev_err(c);
 }
 
-int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
-    if (!c || !dst_device) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    if (bytes < (size_t)c->npix * sizeof(uint32_t)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
-    int st = use_device(c);
-    if (st) return st;
+namespace {
+// The stream-ordered frame copy (iqpt_copy_frame_device_async, the gather's send copy): the BGRA8 frame in
+// compact order into dst, behind every render issued so far; `wait` (if not null) is waited for on the copy's
+// stream first; *used = that stream.
+int copy_frame_async(iqpt_ctx* c, uint32_t* dst, hipEvent_t wait, hipStream_t* used) {
     // no synchronisation here: an error the kernels raise for this launch is reported by the next
     // synchronising call (iqpt_sync, iqpt_read, ...); one already latched fails the copy now
     if (c->dev_err) return check_dev_err(c);
+    int st = IQPT_OK;
     hipStream_t cs = c->stream;
     if (c->pipe) {
         // pipelined spec launches: the copy on stream3 behind both kernels of the last launch; from here on
@@ -2450,19 +2651,15 @@ int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
             c->d_bgra_alt = nullptr;
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "second frame buffer for pipelined copies");
         }
-        if ((!c->stream3 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) ||
-            (!c->ev_copy_cur && hipEventCreateWithFlags(&c->ev_copy_cur, hipEventDisableTiming) != hipSuccess) ||
-            (!c->ev_copy_alt && hipEventCreateWithFlags(&c->ev_copy_alt, hipEventDisableTiming) != hipSuccess)) {
-            (void)hipGetLastError();
-            return iqpt::fail(IQPT_ERR_HIP, "frame copy stream");
-        }
+        if ((st = ensure_copy_stream(c)) != IQPT_OK) return st;
         IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_pipe_end, 0));
         IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_s2, 0));
-        const int le = iqpt::launch_relayout(c->stream3, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
-                                             c->set.nrows, 1, 1, true);
+        if (wait) IQPT_HIP(hipStreamWaitEvent(c->stream3, wait, 0));
+        const int le = iqpt::launch_relayout(c->stream3, c->d_bgra, dst, c->ncols, c->set.nrows, 1, 1, true);
         if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
         IQPT_HIP(hipEventRecord(c->ev_copy_cur, c->stream3));
         c->copy_pend_cur = true;
+        *used = c->stream3;
         return IQPT_OK;
     }
     if (c->last_ovl && c->last_ls) {
@@ -2478,15 +2675,240 @@ int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
     } else if ((st = join_streams(c)) != IQPT_OK) {
         return st;
     }
-    const int le = iqpt::launch_relayout(cs, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
-                                         c->set.nrows, 1, 1, true);
+    if (wait) IQPT_HIP(hipStreamWaitEvent(cs, wait, 0));
+    const int le = iqpt::launch_relayout(cs, c->d_bgra, dst, c->ncols, c->set.nrows, 1, 1, true);
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
+    *used = cs;
     return IQPT_OK;
+}
+}  // namespace
+
+int iqpt_copy_frame_device_async(iqpt_ctx* c, void* dst_device, size_t bytes) {
+    if (!c || !dst_device) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (bytes < (size_t)c->npix * sizeof(uint32_t)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
+    int st = use_device(c);
+    if (st) return st;
+    hipStream_t used = nullptr;
+    return copy_frame_async(c, static_cast<uint32_t*>(dst_device), nullptr, &used);
 }
 
 int iqpt_frame_stream(iqpt_ctx* c, void** stream) {
     if (!c || !stream) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    *stream = (void*)(c->pipe && c->stream3 ? c->stream3 : ((c->last_ovl && c->last_ls) ? c->last_ls : c->stream));
+    // pipelined launches: the copy stream exists from the launch's end on (pipe_end), so the stream named
+    // here is the one the next copy goes on (it used to appear only at the first copy)
+    if (c->pipe) {
+        int st = use_device(c);
+        if (st) return st;
+        if ((st = ensure_copy_stream(c)) != IQPT_OK) return st;
+    }
+    *stream = (void*)(c->pipe ? c->stream3 : ((c->last_ovl && c->last_ls) ? c->last_ls : c->stream));
+    return IQPT_OK;
+}
+
+// ---- multi-GPU frame delivery over RCCL ----------------------------------
+
+int iqpt_comm_unique_id(void* id, size_t bytes) {
+    if (!id || bytes < IQPT_COMM_ID_BYTES) return iqpt::fail(IQPT_ERR_INVALID_ARG, "id NULL or shorter than IQPT_COMM_ID_BYTES");
+    if (!rccl().get_unique_id) return iqpt::fail(IQPT_ERR_UNSUPPORTED, rccl().why);
+    static_assert(sizeof(ncclUniqueId) == IQPT_COMM_ID_BYTES, "RCCL's unique id size");
+    ncclUniqueId u;
+    const ncclResult_t r = rccl().get_unique_id(&u);
+    if (r != ncclSuccess) return rccl_fail(r, "ncclGetUniqueId");
+    std::memcpy(id, &u, sizeof u);
+    return IQPT_OK;
+}
+
+int iqpt_comm_init(iqpt_ctx* c, int rank, int world, const void* id, size_t bytes) {
+    if (!c || !id || bytes < IQPT_COMM_ID_BYTES) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument or short id");
+    if (world < 1 || rank < 0 || rank >= world || (uint32_t)world > c->height)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "rank / world out of range");
+    // the frame's cyclic row split (rank r owns rows r, r + S, ... of every column, S = the set's ystep), which
+    // the root's assembly inverts: S = world on a node; S > world only for a one-GPU rehearsal of an S-way
+    // share (the root then places the rows the communicator's ranks own)
+    // (base = y0 - rank, the same on every rank: 0 on a node, rank 0's row offset in a rehearsal)
+    const uint32_t split = c->set.ystep;
+    const uint32_t nrows = (c->height - c->set.y0 + split - 1u) / split;
+    if (c->set.x0 != 0 || c->set.x1 != c->width || c->set.y0 < (uint32_t)rank ||
+        c->set.y0 - (uint32_t)rank + (uint32_t)world > split || c->set.nrows != nrows)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "the context's pixel set is not rank's cyclic rows of a world-way split "
+                                                "(iqpt_pixel_set {0, W, rank, world, ceil((H - rank) / world)})");
+    if (!rccl().comm_init_rank) return iqpt::fail(IQPT_ERR_UNSUPPORTED, rccl().why);
+    int st = enter(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    free_comm(c);
+    const uint64_t stride = (uint64_t)((c->height + split - 1u) / split) * c->width;
+    if (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gdone[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gdone[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gcopy, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gend, hipEventDisableTiming) != hipSuccess) {
+        (void)hipGetLastError();
+        free_comm(c);
+        return iqpt::fail(IQPT_ERR_HIP, "communicator stream / events");
+    }
+    if (hipMalloc(&c->d_gsend[0], stride * 16) != hipSuccess || hipMalloc(&c->d_gsend[1], stride * 16) != hipSuccess) {
+        (void)hipGetLastError();
+        free_comm(c);
+        return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "gather send buffers");
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclComm_t comm = nullptr;
+    const ncclResult_t r = rccl().comm_init_rank(&comm, world, u, rank);    // collective over the ranks
+    if (r != ncclSuccess) {
+        free_comm(c);
+        return rccl_fail(r, "ncclCommInitRank");
+    }
+    c->comm = comm;
+    c->comm_rank = rank;
+    c->comm_world = world;
+    c->comm_stride = stride;
+    c->gpar = 0;
+    return IQPT_OK;
+}
+
+namespace {
+// One gather of `words` words per pixel from d_gsend[b] (filled on stream `from`) to the root, assembled
+// there into dst (W x H pixels) — on cstream, behind the copy and nothing else.
+int gather_enqueue(iqpt_ctx* c, uint32_t b, hipStream_t from, int root, uint32_t* dst, uint32_t words) {
+    IQPT_HIP(hipEventRecord(c->ev_gcopy, from));
+    IQPT_HIP(hipStreamWaitEvent(c->cstream, c->ev_gcopy, 0));
+    // timing (iqpt_comm_time): from the moment the copy is done to the end of the root's assembly — the
+    // transfer plus any wait for slower ranks inside the collective
+    hipEvent_t t0 = take_event(c), t1 = take_event(c);
+    if (t0) (void)hipEventRecord(t0, c->cstream);
+    const bool is_root = root == c->comm_rank;
+    if (is_root && !c->d_grecv) {
+        if (hipMalloc(&c->d_grecv, (size_t)c->comm_world * c->comm_stride * 16) != hipSuccess) {
+            (void)hipGetLastError();
+            c->d_grecv = nullptr;
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "gather receive buffer");
+        }
+    }
+    const ncclResult_t r = rccl().gather(c->d_gsend[b], is_root ? c->d_grecv : nullptr, (size_t)c->comm_stride * words,
+                                         ncclUint32, root, static_cast<ncclComm_t>(c->comm), c->cstream);
+    if (r != ncclSuccess) return rccl_fail(r, "ncclGather");
+    if (is_root) {
+        const int le = iqpt::launch_assemble_rows(c->cstream, c->d_grecv, dst, c->width, c->height,
+                                                  (uint32_t)c->comm_world, c->set.ystep,
+                                                  c->set.y0 - (uint32_t)c->comm_rank, c->comm_stride, words);
+        if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame assembly");
+    }
+    if (t1) (void)hipEventRecord(t1, c->cstream);
+    if (t0 && t1) c->gtimed.emplace_back(t0, t1);
+    IQPT_HIP(hipEventRecord(c->ev_gdone[b], c->cstream));
+    IQPT_HIP(hipEventRecord(c->ev_gend, c->cstream));
+    c->gdone_pend[b] = true;
+    c->comm_pend = true;
+    c->gpar = b ^ 1u;
+    return IQPT_OK;
+}
+
+int comm_check(iqpt_ctx* c, int root) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    if (!c->comm) return iqpt::fail(IQPT_ERR_NOT_READY, "no communicator: call iqpt_comm_init first");
+    if (root < 0 || root >= c->comm_world) return iqpt::fail(IQPT_ERR_INVALID_ARG, "root out of range");
+    return use_device(c);
+}
+
+// Synchronous gather of the accumulators (what & 1) and / or the BGRA8 frame (what & 2) into d_gframe on the
+// root (W x H x 4 words, reused for each); `out_lin` / `out_bgra` (root, host) receive them.
+int gather_sync(iqpt_ctx* c, int root, int what, float* out_lin, uint8_t* out_bgra) {
+    int st = enter(c);
+    if (st) return st;
+    const bool is_root = root == c->comm_rank;
+    const size_t frame_px = (size_t)c->width * c->height;
+    if (is_root && !c->d_gframe && hipMalloc(&c->d_gframe, frame_px * 16) != hipSuccess) {
+        (void)hipGetLastError();
+        c->d_gframe = nullptr;
+        return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "assembled frame");
+    }
+    for (int k = 0; k < 2; ++k) {
+        if (!(what & (1 << k))) continue;
+        const uint32_t words = k == 0 ? 4u : 1u;
+        const uint32_t b = c->gpar;
+        if (c->gdone_pend[b]) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_gdone[b], 0));
+        const int le = iqpt::launch_relayout(c->stream, k == 0 ? reinterpret_cast<const uint32_t*>(c->d_lin) : c->d_bgra,
+                                             c->d_gsend[b], c->ncols, c->set.nrows, words, 1, true);
+        if (le != 0) return iqpt::hip_fail((hipError_t)le, "gather copy");
+        if ((st = gather_enqueue(c, b, c->stream, root, c->d_gframe, words)) != IQPT_OK) return st;
+        IQPT_HIP(hipStreamSynchronize(c->cstream));
+        c->comm_pend = false;
+        if (is_root && (k == 0 ? (void*)out_lin : (void*)out_bgra))
+            IQPT_HIP(hipMemcpy(k == 0 ? (void*)out_lin : (void*)out_bgra, c->d_gframe, frame_px * words * 4,
+                               hipMemcpyDeviceToHost));
+    }
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    return check_dev_err(c);
+}
+}  // namespace
+
+int iqpt_gather_frame_async(iqpt_ctx* c, int root, void* dst_device, size_t bytes) {
+    int st = comm_check(c, root);
+    if (st) return st;
+    if (root == c->comm_rank && (!dst_device || bytes < (size_t)c->width * c->height * 4))
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "root: destination NULL or smaller than W x H x 4 bytes");
+    const uint32_t b = c->gpar;
+    hipStream_t used = nullptr;
+    // the copy into send buffer b waits for the gather that read it two gathers ago (long done)
+    if ((st = copy_frame_async(c, c->d_gsend[b], c->gdone_pend[b] ? c->ev_gdone[b] : nullptr, &used)) != IQPT_OK)
+        return st;
+    return gather_enqueue(c, b, used, root, static_cast<uint32_t*>(dst_device), 1u);
+}
+
+int iqpt_gather_accum(iqpt_ctx* c, int root, void* dst_device, size_t bytes) {
+    int st = comm_check(c, root);
+    if (st) return st;
+    const size_t need = (size_t)c->width * c->height * 16;
+    if (root == c->comm_rank && (!dst_device || bytes < need))
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "root: destination NULL or smaller than W x H x 16 bytes");
+    if ((st = enter(c)) != IQPT_OK) return st;
+    const uint32_t b = c->gpar;
+    if (c->gdone_pend[b]) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_gdone[b], 0));
+    const int le = iqpt::launch_relayout(c->stream, reinterpret_cast<const uint32_t*>(c->d_lin), c->d_gsend[b], c->ncols,
+                                         c->set.nrows, 4, 1, true);
+    if (le != 0) return iqpt::hip_fail((hipError_t)le, "gather copy");
+    if ((st = gather_enqueue(c, b, c->stream, root, static_cast<uint32_t*>(dst_device), 4u)) != IQPT_OK) return st;
+    IQPT_HIP(hipStreamSynchronize(c->cstream));
+    c->comm_pend = false;
+    return check_dev_err(c);
+}
+
+int iqpt_gather_read(iqpt_ctx* c, int root, float* lin_rgba, uint8_t* bgra) {
+    int st = comm_check(c, root);
+    if (st) return st;
+    // every rank takes part in the same gathers; the root's pointers choose what is read back (the others'
+    // are ignored): both are gathered unless the root asked for neither
+    return gather_sync(c, root, 3, lin_rgba, bgra);
+}
+
+int iqpt_comm_time(iqpt_ctx* c, double* total_ms, uint64_t* gathers) {
+    if (!c || !total_ms || !gathers) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *total_ms = 0.0;
+    *gathers = 0;
+    if (!c->comm) return IQPT_OK;
+    int st = use_device(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->cstream));
+    double sum = 0.0;
+    for (auto& g : c->gtimed) {
+        float ms = 0.0f;
+        IQPT_HIP(hipEventElapsedTime(&ms, g.first, g.second));
+        sum += ms;
+        c->event_pool.push_back(g.first);
+        c->event_pool.push_back(g.second);
+    }
+    *total_ms = sum;
+    *gathers = c->gtimed.size();
+    c->gtimed.clear();
+    return IQPT_OK;
+}
+
+int iqpt_comm_stream(iqpt_ctx* c, void** stream) {
+    if (!c || !stream) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    if (!c->comm) return iqpt::fail(IQPT_ERR_NOT_READY, "no communicator: call iqpt_comm_init first");
+    *stream = (void*)c->cstream;
     return IQPT_OK;
 }
 

@@ -61,9 +61,24 @@ void path_tracer::shutdown() {                                             // pa
 }
 path_tracer* path_tracer::get() { return g_path_tracer; }
 
+std::vector<uint8_t> path_tracer::comm_unique_id() {
+    std::vector<uint8_t> id(IQPT_COMM_ID_BYTES);
+    IQPT_THROW_FAILED(iqpt_comm_unique_id(id.data(), id.size()));
+    return id;
+}
+
 path_tracer::path_tracer(camera* cam, const path_tracer_options& opt) : m_camera(cam), m_opt(opt) {
     const uint32_t w = cam->get_width(), h = cam->get_height();
-    IQPT_THROW_FAILED(iqpt_create(opt.device, w, h, nullptr, opt.seed, opt.max_depth, &m_ctx));
+    if (opt.comm_id.empty()) {
+        IQPT_THROW_FAILED(iqpt_create(opt.device, w, h, nullptr, opt.seed, opt.max_depth, &m_ctx));
+    } else {
+        // rank's cyclic rows of the frame (row y -> rank y mod world), then the communicator (collective)
+        const uint32_t r = (uint32_t)opt.rank, n = (uint32_t)opt.world;
+        const iqpt_pixel_set rows{0, w, r, n, n && r < h ? (h - r + n - 1) / n : 0};
+        IQPT_THROW_FAILED(iqpt_create(opt.device, w, h, &rows, opt.seed, opt.max_depth, &m_ctx));
+        IQPT_THROW_FAILED(iqpt_comm_init(m_ctx, opt.rank, opt.world, opt.comm_id.data(), opt.comm_id.size()));
+        m_comm = true;
+    }
     IQPT_THROW_FAILED(iqpt_set_camera(m_ctx, &cam->raw()));
     m_host_pixels.assign((size_t)w * h, pixel{0, 0, 0, 0});              // path_tracer.cu:130-131
 }
@@ -73,7 +88,7 @@ path_tracer::~path_tracer() { iqpt_destroy(m_ctx); }
 void path_tracer::begin_frame() {}
 
 void path_tracer::end_frame() {                                            // path_tracer.cu:171-210
-    if (m_image_updated && !m_opt.ppm_path.empty()) {
+    if (m_image_updated && !m_opt.ppm_path.empty() && m_opt.rank == 0) {
         IQPT_THROW_FAILED(iqpt_write_ppm(m_opt.ppm_path.c_str(), m_camera->get_width(), m_camera->get_height(),
                                          reinterpret_cast<const uint8_t*>(m_host_pixels.data())));
     }
@@ -84,8 +99,10 @@ void path_tracer::draw_scene(const scene& scn, std::vector<shader>& /*shaders*/,
     m_time += dt;
     if (!(m_time > m_opt.launch_interval)) return;
     m_time = 0.0f;
-    // sync with the previous launch and fetch its frame (:382-386)
-    IQPT_THROW_FAILED(iqpt_read(m_ctx, nullptr, reinterpret_cast<uint8_t*>(m_host_pixels.data())));
+    // sync with the previous launch and fetch its frame (:382-386); sharded: the whole frame on rank 0
+    uint8_t* host = reinterpret_cast<uint8_t*>(m_host_pixels.data());
+    if (m_comm) IQPT_THROW_FAILED(iqpt_gather_read(m_ctx, 0, nullptr, host));
+    else IQPT_THROW_FAILED(iqpt_read(m_ctx, nullptr, host));
     m_image_updated = true;
     if (scn.modified() || !m_have_packet) {                                // :389-392
         const iqpt_packet_desc pk = scn.build_packet();
@@ -112,6 +129,11 @@ uint64_t path_tracer::rays_traced() const {
 }
 
 void path_tracer::read_linear(std::vector<float>& rgba) const {
+    if (m_comm) {                 // collective: the whole frame's accumulator on rank 0
+        rgba.resize((size_t)m_camera->get_width() * m_camera->get_height() * 4);
+        IQPT_THROW_FAILED(iqpt_gather_read(m_ctx, 0, rgba.data(), nullptr));
+        return;
+    }
     uint64_t n = 0;
     IQPT_THROW_FAILED(iqpt_num_pixels(m_ctx, &n));
     rgba.resize((size_t)n * 4);

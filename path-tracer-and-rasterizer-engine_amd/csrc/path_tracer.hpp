@@ -92,6 +92,12 @@ struct path_tracer_options {
     float launch_interval = 0.1f;                // path_tracer.cu:378
     uint32_t spp_per_launch = 1;                 // one sample per reference launch
     std::string ppm_path;                        // headless present target ("" = none)
+    // multi-GPU (one process per GPU): this process renders rank's cyclic rows of the frame and the present
+    // path gathers the frame to rank 0 over RCCL (iqpt_comm_init / iqpt_gather_read). comm_id: the bytes of
+    // path_tracer::comm_unique_id() from one rank, shared out of band; empty = single GPU.
+    int rank = 0;
+    int world = 1;
+    std::vector<uint8_t> comm_id;
 };
 
 class path_tracer : public renderer_template {
@@ -101,6 +107,8 @@ public:
     };
 
     static void init(camera* cam, const path_tracer_options& opt = path_tracer_options());
+    // an RCCL unique id for path_tracer_options::comm_id (made on one rank)
+    static std::vector<uint8_t> comm_unique_id();
     static void shutdown();
     static path_tracer* get();
 
@@ -109,7 +117,7 @@ public:
     void draw_scene(const scene& scene, std::vector<shader>& shaders, float dt) override;
     void reset() { m_pending_reset = true; }                              // path_tracer.h:35
 
-    // headless extensions
+    // headless extensions; with a communicator the host frame is the whole gathered frame on rank 0
     const std::vector<pixel>& host_pixels() const { return m_host_pixels; }
     uint64_t frames() const;
     uint64_t rays_traced() const;
@@ -131,6 +139,7 @@ private:
     bool m_have_packet = false;
     bool m_image_updated = false;
     bool m_pending_reset = false;
+    bool m_comm = false;          // rank's rows of a sharded frame (path_tracer_options::comm_id)
 };
 
 }  // namespace iqpt

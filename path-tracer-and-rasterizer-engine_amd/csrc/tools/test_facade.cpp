@@ -2,6 +2,7 @@
 // reference engine (application.cu:66-99, renderer.cu:45-68): cadence, deferred reset, present.
 // Prints one JSON line that tests/test_gpu_facade.py checks against the C-ABI path.
 #include <cmath>
+#include <cstring>
 #include <cstdio>
 #include <string>
 #include <vector>
@@ -75,10 +76,41 @@ int main(int argc, char** argv) {
         FILE* f = std::fopen(ppm.c_str(), "rb");
         CHECK(f != nullptr);
         std::fclose(f);
-        std::printf("{\"ok\": true, \"sum_after_4\": %.9g, \"sum_after_reset\": %.9g, \"rays\": %llu}\n", s4, s5,
-                    (unsigned long long)pt->rays_traced());
+        const unsigned long long rays = (unsigned long long)pt->rays_traced();
         iqpt::path_tracer::shutdown();
         CHECK(iqpt::path_tracer::get() == nullptr);
+
+        // the sharded present path (one process per GPU; here a one-rank communicator): the frame comes back
+        // through the RCCL gather and rank 0's assembly, and must equal the single-GPU facade's bit for bit
+        auto run4 = [&](const iqpt::path_tracer_options& o, std::vector<float>& lin, std::vector<iqpt::path_tracer::pixel>& px) {
+            iqpt::scene s;
+            s.add_preset("cornell");
+            iqpt::path_tracer::init(&cam, o);
+            iqpt::path_tracer* p = iqpt::path_tracer::get();
+            for (int i = 0; i < 5; ++i) {            // 4 launches; the 5th tick fetches the 4th launch's frame
+                p->begin_frame();
+                p->draw_scene(s, shaders, 0.2f);
+                p->end_frame();
+            }
+            p->read_linear(lin);
+            px = p->host_pixels();
+            iqpt::path_tracer::shutdown();
+        };
+        iqpt::path_tracer_options single = opt;
+        single.ppm_path.clear();
+        iqpt::path_tracer_options sharded = single;
+        sharded.rank = 0;
+        sharded.world = 1;
+        sharded.comm_id = iqpt::path_tracer::comm_unique_id();
+        std::vector<float> lin_a, lin_b;
+        std::vector<iqpt::path_tracer::pixel> px_a, px_b;
+        run4(single, lin_a, px_a);
+        run4(sharded, lin_b, px_b);
+        CHECK(lin_a.size() == lin_b.size() && px_a.size() == px_b.size());
+        CHECK(std::memcmp(lin_a.data(), lin_b.data(), lin_a.size() * sizeof(float)) == 0);
+        CHECK(std::memcmp(px_a.data(), px_b.data(), px_a.size() * sizeof(px_a[0])) == 0);
+        std::printf("{\"ok\": true, \"sum_after_4\": %.9g, \"sum_after_reset\": %.9g, \"rays\": %llu, \"sharded_equal\": true}\n",
+                    s4, s5, rays);
     } catch (const std::exception& e) {
         std::fprintf(stderr, "%s\n", e.what());
         return 1;

@@ -22,6 +22,7 @@ DEFAULT_SEED = 1984
 DEFAULT_MAX_DEPTH = 5
 SPLIT_AUTO, SPLIT_OFF, SPLIT_ON, SPLIT_CHAIN, SPLIT_FAN, SPLIT_SPEC = -1, 0, 1, 2, 3, 4   # IQPT_SPLIT_* (iqpt_set_split)
 OVERLAP_OFF, OVERLAP_AUTO = 0, 1               # IQPT_OVERLAP_* (iqpt_set_overlap)
+COMM_ID_BYTES = 128                            # IQPT_COMM_ID_BYTES (iqpt_comm_unique_id)
 
 
 class IqptError(RuntimeError):
@@ -114,6 +115,13 @@ SIGNATURES = [
     ("iqpt_error_string", C.c_char_p, [C.c_int]),
     ("iqpt_last_error", C.c_char_p, []),
     ("iqpt_abi_version", C.c_int, []),
+    ("iqpt_comm_unique_id", C.c_int, [_P, C.c_size_t]),
+    ("iqpt_comm_init", C.c_int, [_P, C.c_int, C.c_int, _P, C.c_size_t]),
+    ("iqpt_gather_frame_async", C.c_int, [_P, C.c_int, _P, C.c_size_t]),
+    ("iqpt_gather_accum", C.c_int, [_P, C.c_int, _P, C.c_size_t]),
+    ("iqpt_gather_read", C.c_int, [_P, C.c_int, _FP, C.POINTER(C.c_uint8)]),
+    ("iqpt_comm_stream", C.c_int, [_P, C.POINTER(C.c_void_p)]),
+    ("iqpt_comm_time", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     ("iqpt_scene_create", C.c_int, [C.POINTER(_P)]),
     ("iqpt_scene_destroy", C.c_int, [_P]),
     ("iqpt_scene_add_mesh_tri", C.c_int, [_P, C.c_char_p]),
@@ -133,7 +141,7 @@ SIGNATURES = [
 _lib = None
 
 
-ABI_VERSION = 3      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
+ABI_VERSION = 4      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
 
 
 def load() -> C.CDLL:

@@ -117,6 +117,47 @@ class PathTracer:
         check(self._lib.iqpt_frame_stream(self._h, C.byref(s)), "iqpt_frame_stream")
         return int(s.value or 0)
 
+    # ---- multi-GPU frame delivery over RCCL, inside libiqpt (iqpt_comm_*, iqpt_gather_*)
+
+    def comm_init(self, rank: int, world: int, uid: bytes):
+        """Join the ranks of one frame's cyclic row split (collective; this context must own rank's rows,
+        dist.pixel_set_for_rank). `uid` from comm_unique_id() on one rank, shared out of band."""
+        b = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(bytes(uid))
+        check(self._lib.iqpt_comm_init(self._h, rank, world, b, _lib.COMM_ID_BYTES), "iqpt_comm_init")
+
+    def gather_frame_async(self, root: int, dst_ptr: int, nbytes: int):
+        """Collective: the BGRA8 frame gathered to `root` and assembled there (W x H uint32 into dst_ptr, a
+        device buffer; ignored on other ranks), stream-ordered behind the renders issued so far
+        (iqpt_gather_frame_async). Order reads of dst on comm_stream_handle()."""
+        check(self._lib.iqpt_gather_frame_async(self._h, root, C.c_void_p(dst_ptr or None), nbytes),
+              "iqpt_gather_frame_async")
+
+    def gather_accum(self, root: int, dst_ptr: int, nbytes: int):
+        """Collective, synchronous: the float4 accumulators of the whole frame on `root` (device buffer)."""
+        check(self._lib.iqpt_gather_accum(self._h, root, C.c_void_p(dst_ptr or None), nbytes), "iqpt_gather_accum")
+
+    def gather_read(self, root: int):
+        """Collective, synchronous: (lin [W*H,4] float32, bgra [W*H,4] uint8) of the whole frame on `root`
+        (row-major), None elsewhere (iqpt_gather_read)."""
+        lin = np.empty((self.width * self.height, 4), dtype=np.float32)
+        bgra = np.empty((self.width * self.height, 4), dtype=np.uint8)
+        check(self._lib.iqpt_gather_read(self._h, root, lin.ctypes.data_as(C.POINTER(C.c_float)),
+                                         bgra.ctypes.data_as(C.POINTER(C.c_uint8))), "iqpt_gather_read")
+        return lin, bgra
+
+    def comm_time(self) -> tuple[float, int]:
+        """(ms, gathers): the gathers' summed durations on the communicator stream since the last call."""
+        ms = C.c_double()
+        n = C.c_uint64()
+        check(self._lib.iqpt_comm_time(self._h, C.byref(ms), C.byref(n)), "iqpt_comm_time")
+        return ms.value, n.value
+
+    def comm_stream_handle(self) -> int:
+        """The communicator's hipStream_t (iqpt_comm_stream): the gathers and the root's assembly run on it."""
+        s = C.c_void_p()
+        check(self._lib.iqpt_comm_stream(self._h, C.byref(s)), "iqpt_comm_stream")
+        return int(s.value or 0)
+
     def set_split(self, mode: int):
         """Sample-parallel launches: _lib.SPLIT_AUTO (default), SPLIT_OFF, SPLIT_ON, SPLIT_CHAIN or SPLIT_FAN
         (iqpt_set_split)."""
@@ -161,6 +202,13 @@ class PathTracer:
         n = C.c_uint64()
         check(self._lib.iqpt_kernel_time(self._h, C.byref(ms), C.byref(n)), "iqpt_kernel_time")
         return ms.value, n.value
+
+
+def comm_unique_id() -> bytes:
+    """An RCCL unique id for comm_init (iqpt_comm_unique_id): made on one rank, shared with the others."""
+    b = (C.c_uint8 * _lib.COMM_ID_BYTES)()
+    check(_lib.load().iqpt_comm_unique_id(b, _lib.COMM_ID_BYTES), "iqpt_comm_unique_id")
+    return bytes(b)
 
 
 def kernel_name() -> str:

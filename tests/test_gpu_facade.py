@@ -21,6 +21,7 @@ def test_facade_program(require_gpu, tmp_path):
     assert res.returncode == 0, res.stderr
     out = json.loads(res.stdout.strip().splitlines()[-1])
     assert out["ok"] is True
+    assert out["sharded_equal"] is True          # the facade's sharded present path (RCCL gather, world 1)
     # the same four 1-spp launches through the Python C-ABI binding, then oracle
     import oracle
     from helpers import scene_for
