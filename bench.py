@@ -78,6 +78,11 @@ def parse():
                     help="overlapped launches on two streams (iqpt_set_overlap, DESIGN.md §3.8)")
     ap.add_argument("--certain", default="on", choices=["on", "off"],
                     help="A/B: certain pixels folded at once (iqpt_debug_set_certain, DESIGN.md §3.3)")
+    ap.add_argument("--hybrid", default="off", choices=["on", "off"],
+                    help="A/B: hybrid launches, the sphere pixels in the spec kernel beside overlapped plain launches "
+                         "(iqpt_debug_set_hybrid, DESIGN.md §3.13)")
+    ap.add_argument("--sky", default="on", choices=["on", "off"],
+                    help="A/B: certain-miss pixels in iqpt_sky_kernel (iqpt_debug_set_sky, DESIGN.md §3.12)")
     ap.add_argument("--kernel-options", type=lambda v: int(v, 0), default=0,
                     help="A/B: render-kernel option mask (iqpt_debug_set_kernel_options; 0 = production)")
     ap.add_argument("--gather-sync", action="store_true",
@@ -250,7 +255,8 @@ def certain_pixels(pt, _lib) -> int:
 LAUNCH_KERNELS = {"plain": "iqpt_render_kernel", "spec": "iqpt_spec_kernel + iqpt_fan_kernel",
                   "fan": "iqpt_render_kernel + iqpt_fan_kernel", "chain": "iqpt_chain_kernel + iqpt_render_kernel",
                   "chain+fan": "iqpt_chain_kernel + iqpt_fan_kernel", "split": "iqpt_render_kernel (split rounds)",
-                  "split+fan": "iqpt_render_kernel (split rounds) + iqpt_fan_kernel"}
+                  "split+fan": "iqpt_render_kernel (split rounds) + iqpt_fan_kernel",
+                  "hybrid": "iqpt_render_kernel + iqpt_spec_kernel + iqpt_sky_kernel"}
 
 
 def mix_for_launch(cfg_name: str, launch_mode: str, split_ways: int, explicit: str):
@@ -275,6 +281,16 @@ def mix_for_launch(cfg_name: str, launch_mode: str, split_ways: int, explicit: s
             return ({k: v[0] for k, v in got.items()}, {k: v[1] for k, v in got.items()},
                     {k: v[2] for k, v in got.items()})
     return None, None, None
+
+
+def sky_pixels(pt, _lib) -> int:
+    """Pixels of this context proven to miss every primitive (iqpt_sky_kernel's; 0 when the path is off)."""
+    import ctypes as C
+    lb = _lib.load()
+    lb.iqpt_debug_sky_info.argtypes = [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]
+    n, t = C.c_uint32(0), C.c_uint32(0)
+    _lib.check(lb.iqpt_debug_sky_info(pt.handle, C.byref(n), C.byref(t)), "iqpt_debug_sky_info")
+    return int(n.value)
 
 
 def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode: str, split_ways: int, spp: int,
@@ -314,8 +330,8 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode: str, s
             out["executed_work"] = {"achieved": round(ex, 4), "frac": round(ex / FP32_PEAK_TFLOPS, 5),
                                     "flops_per_ray": work["flops_per_ray"], "per_ray": work.get("per_ray"),
                                     "source": str(Path(work_path).resolve().relative_to(REPO))}
-    # the counted rays include the camera rays of certain pixels, resolved by a per-pixel proof instead of
-    # per-ray tests: the rate of rays that ran a per-ray closest-hit test
+    # the counted rays include the camera rays of certain-hit and certain-miss (sky) pixels, resolved by a
+    # per-pixel proof instead of per-ray tests: the rate of rays that ran a per-ray closest-hit test
     if t > 0:
         out["traced_rays_per_launch"] = round(rays_per_launch * (1.0 - certain_ray_frac))
         out["traced_rays_per_s"] = round(rays_per_launch * (1.0 - certain_ray_frac) / t, 1)
@@ -444,6 +460,16 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_certain.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_certain(pt._h, 0), "iqpt_debug_set_certain")
+    if args.hybrid == "on":
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_hybrid.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_hybrid(pt._h, 1), "iqpt_debug_set_hybrid")
+    if args.sky == "off":
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_sky.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_sky(pt._h, 0), "iqpt_debug_set_sky")
     if args.spec_cap:
         import ctypes as C
         lb = _lib.load()
@@ -551,6 +577,7 @@ def main():
     gather_ms, gathers = pt.comm_time() if lib_gather else (0.0, 0)
     launch_mode = pt.launch_mode()
     certain_px = certain_pixels(pt, _lib) if args.certain != "off" else 0
+    sky_px = sky_pixels(pt, _lib) if (args.certain != "off" and args.sky != "off") else 0
 
     # the last step's gathered frame: rank 0's own rows of it must be its own frame (checks the gather path;
     # libiqpt's assembly puts them at rows 0, S, 2S, ... of the W x H frame, S = the split's ways)
@@ -646,7 +673,9 @@ def main():
                                        if weak else f"gather of the {gathered} to rank 0 every step")
                                       + (" (RCCL ncclGather inside libiqpt: iqpt_gather_frame_async)" if lib_gather
                                          else " (gloo via host, rehearsal)")),
-                       "split": args.split, "overlap": args.overlap, "certain": args.certain, "launch_mode": launch_mode,
+                       "split": args.split, "overlap": args.overlap, "certain": args.certain, "sky": args.sky,
+                       "hybrid": args.hybrid,
+                       "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
                        **({"spec_cap": args.spec_cap} if args.spec_cap else {})},
             "n_ranks_seen": n_ranks_seen,
@@ -664,6 +693,10 @@ def main():
                                        "on an emissive triangle: their samples take the two camera draws and fold "
                                        "the clamped (1, 1, 1) without a per-ray intersection test; bit-identical "
                                        "results (tests/test_gpu_certain.py)"},
+            # pixels proven (iq_interval.h) to miss every primitive: their samples are one camera ray each, the sky
+            # gradient, rendered by iqpt_sky_kernel without an intersection test
+            "sky_pixels": {"pixels": sky_px, "frac_of_owned_pixels": round(sky_px / max(1, npix_owned), 5),
+                           "frac_of_rays_counted": round(sky_px * spp_step * args.steps / max(1.0, float(rays)), 5)},
             "rmse_vs_oracle": rmse_v,
             "bitexact_frac_vs_oracle": bitexact,
             "setup_ms": {k: round(v, 2) for k, v in setup.items()},
@@ -672,7 +705,7 @@ def main():
                              "reference binary, which cannot be built here"),
             "fma_flavour_rmse_c2": fma_flavour_rmse(),
             "roofline": roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode, part_world, spp_step,
-                                 npix_owned, certain_px * spp_step * args.steps / max(1.0, float(rays))),
+                                 npix_owned, (certain_px + sky_px) * spp_step * args.steps / max(1.0, float(rays))),
         }
         if strong_multi or world > 1:
             out["per_rank"] = per_rank

@@ -3013,14 +3013,15 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
         ay = a[1];
         az = a[2];
     }
-    const uint64_t valid = npt == 64u ? ~0ull : ((1ull << npt) - 1ull);
+    const uint64_t valid = (npt == 64u ? ~0ull : ((1ull << npt) - 1ull)) & own;
     const uint64_t cmask = p.certain != nullptr
                                ? ((uint64_t)p.certain[2 * (size_t)t] | ((uint64_t)p.certain[2 * (size_t)t + 1] << 32))
                                : 0ull;
     if ((cmask & valid) == valid) {
-        // a certain tile (kparams::certain): every sample takes the camera's two draws and ends on an emissive
-        // triangle, clamped colour (1, 1, 1), whose mean term c / n is the table's RN(1 / n); wave 0 folds
-        // the launch's samples in order, the other waves have nothing to do
+        // a certain tile (kparams::certain) — every pixel of it this kernel owns is certain (the others are the
+        // sky kernel's): every sample takes the camera's two draws and ends on an emissive triangle, clamped
+        // colour (1, 1, 1), whose mean term c / n is the table's RN(1 / n); wave 0 folds the launch's samples
+        // in order, the other waves have nothing to do
         if (wave == 0 && has) {
             xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * p.spp);
             st.d += 2u * p.spp * IQ_XORWOW_WEYL;
@@ -3165,6 +3166,7 @@ constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per bloc
 constexpr uint32_t kSpecMaxPix = 32;                   // pixels per block at 8 lanes each
 constexpr uint32_t kSpecBatch = 512;                   // walk: chain samples gathered per block and batch
 constexpr uint8_t kSpecTaken = 0xffu;                  // slot mark: a lane is tracing it (slot counts are <= 17)
+constexpr uint32_t kSpecOvershoot = 24u;               // slots a lane may follow past the next lane's start
 static_assert(kSpecPix == kSpecPixPerBlock && kSpecMaxPix == kSpecMaxPixPerBlock, "runtime and kernel agree on the spec block");
 
 __host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth, uint32_t spp,
@@ -3268,9 +3270,15 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         const uint32_t js = rd[0], M = rd[1];
         // ---- the window's slot marks: 0 not taken, kSpecTaken taken by a lane, else the slots its sample used
         for (uint32_t i = l; i < M; i += L) ln[i] = 0u;
-        // ---- this lane's chain starts at slot j0 = M l / L (relative to js), with the state 2 j0 draws in
-        const uint32_t j0 = M * l / L;
-        const bool first_ok = live && j0 < M && (l == 0u || M * (l - 1u) / L < j0);
+        // ---- this lane's chain starts at slot j0 = M l / L rounded down to even (relative to js), with the state
+        // 2 j0 draws in. Even: a pixel whose samples all take an even number of slots (camera ray -> sphere ->
+        // wall: 2) has its chain on even slots only, and a chain from an odd slot would never meet it.
+        const uint32_t j0 = (M * l / L) & ~1u;
+        const bool first_ok = live && j0 < M && (l == 0u || ((M * (l - 1u) / L) & ~1u) < j0);
+        // a lane that has not met another chain this far past the next lane's start gives up: the walker then
+        // continues from the first slot no lane traced in a new round (rare; bounds the cost of chains that
+        // do not meet)
+        const uint32_t j_stop = l + 1u < L ? min(M, ((M * (l + 1u) / L) & ~1u) + kSpecOvershoot) : M;
         rng6 st = {rd[2], rd[3], rd[4], rd[5], rd[6], p.rng[5 * (size_t)p.npix + rd[13]] + 2u * (js + j0) * IQ_XORWOW_WEYL};
         xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, live ? 2u * j0 : 0u);
         lst[l * 5u] = st.v0;
@@ -3363,7 +3371,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                     // A slot another lane has taken is on a chain that lane follows to the window's end
                     // (or to a slot taken before it), so this lane's chain has merged into it and stops.
                     j += n;
-                    if (j >= M || *reinterpret_cast<volatile uint8_t*>(ln + j) != 0u) {
+                    if (j >= j_stop || *reinterpret_cast<volatile uint8_t*>(ln + j) != 0u) {
                         active = false;
                     } else {
                         ln[j] = kSpecTaken;
@@ -3386,13 +3394,9 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                 uint32_t c = 0;
                 while (c < batch && k + c < p.spp && jw < M) {
                     const uint32_t nj = ln[jw];
-                    if (nj - 1u >= (uint32_t)kSpecTaken - 1u) {
-                        // a chain slot no lane traced: impossible by construction (every taken slot's chain
-                        // is followed to the window's end); report it instead of folding garbage
-                        atomicOr(p.ovl_err, 8u);
-                        jw = M;
-                        break;
-                    }
+                    // a chain slot no lane traced (a lane gave up before meeting another chain): the round ends
+                    // here and the next one starts a window at this slot, like a chain that left its window
+                    if (nj == 0u) break;
                     lp[c++] = (uint16_t)jw;
                     jw += nj;
                 }

@@ -143,6 +143,8 @@ struct iqpt_ctx {
     uint32_t* d_sky_tiles = nullptr;
     uint32_t n_sky_tiles = 0, n_sky_pixels = 0;
     bool sky_on = true;
+    bool sky_active = false;            // the masks' miss pixels are the sky kernel's: the fan lists exclude them
+    std::vector<uint64_t> h_miss;       // per tile: the certain-miss mask (host copy, for the fan lists)
     hipEvent_t ev_sky = nullptr;        // after the last sky kernel (the next one, maybe on the other stream, waits)
     hipStream_t sky_last = nullptr;     // the stream of the last sky kernel since the streams were joined
     uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
@@ -235,6 +237,16 @@ struct iqpt_ctx {
     bool pipe = false;                   // the last launch was pipelined and nothing has joined since
     int pipe_kind = 0;                   // ... a spec launch (1) or a fan launch (2)
     hipStream_t stream3 = nullptr;
+    // hybrid launches: the spec kernel over the sphere pixels on `stream4`, pipelined across
+    // launches, beside the overlapped plain kernel (which skips those pixels, d_skip) and the sky kernel
+    hipStream_t stream4 = nullptr;
+    int hybrid_mode = 0;                // iqpt_debug_set_hybrid: 0 off, 1 on (overlapped plain launches only)
+    bool hyb_pend = false;              // a hybrid spec kernel is in flight on stream4 (joined by join_streams)
+    bool hybrid_last = false;           // the last launch was hybrid
+    hipEvent_t ev_h0 = nullptr, ev_spec4 = nullptr;
+    uint32_t* d_skip = nullptr;         // per tile (2 words): pixels the plain kernel skips in hybrid launches —
+                                        // the sphere pixels (the spec kernel's) and, with the sky kernel, the misses
+    std::vector<uint64_t> h_specmask;   // per tile: its sphere pixels (build_pixel_split)
     hipEvent_t ev_pipe_end = nullptr;    // on `stream`, after the last pipelined launch's first kernel
     hipEvent_t ev_copy_cur = nullptr, ev_copy_alt = nullptr;   // on `stream3`, after the copy of d_bgra / d_bgra_alt
     bool copy_pend_cur = false, copy_pend_alt = false;
@@ -320,6 +332,10 @@ int join_streams(iqpt_ctx* c) {
     c->ovl_zero = true;
     c->last_ovl = false;
     c->sky_last = nullptr;             // everything before is ordered on `stream` now
+    if (c->hyb_pend) {
+        IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_spec4, 0));
+        c->hyb_pend = false;
+    }
     return IQPT_OK;
 }
 
@@ -387,6 +403,8 @@ void free_split(iqpt_ctx* c) {
     if (c->d_fan_lanes) (void)hipFree(c->d_fan_lanes);
     c->d_fan_lanes = nullptr;
     c->n_chain_pix = c->n_fan_tiles = 0;
+    if (c->d_skip) (void)hipFree(c->d_skip);
+    c->d_skip = nullptr;
     c->spec_rho_valid = false;           // a new pixel list: no chain history, no plan
     c->spec_plan_n = 0;
     c->spec_rho_pending = false;
@@ -403,8 +421,21 @@ void free_split(iqpt_ctx* c) {
 // of a split tile stays with the chain kernel).
 int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const std::vector<uint32_t>& split,
                       const uint32_t* sp_pix) {
-    std::vector<uint32_t> chain_pix, fan_tiles(anchor);
-    std::vector<uint64_t> fan_lanes(anchor.size(), ~0ull);
+    // with the sky kernel on (sky_active), certain-miss pixels are its own: the fan kernel's lanes exclude them,
+    // and tiles left with no lane leave its list
+    std::vector<uint32_t> chain_pix, fan_tiles;
+    std::vector<uint64_t> fan_lanes;
+    const bool sky = c->sky_active && c->h_miss.size() == (size_t)c->cull_ntx * c->cull_nty;
+    for (uint32_t t : anchor) {
+        const uint64_t own = sky ? ~c->h_miss[t] : ~0ull;
+        const uint32_t tx = t % c->cull_ntx, ty = t / c->cull_ntx;
+        const uint32_t npt = std::min(iqpt::kCullTile, c->ncols - tx * iqpt::kCullTile) *
+                             std::min(iqpt::kCullTile, c->set.nrows - ty * iqpt::kCullTile);
+        if (own & (npt == 64u ? ~0ull : ((1ull << npt) - 1ull))) {
+            fan_tiles.push_back(t);
+            fan_lanes.push_back(own);
+        }
+    }
     const bool per_pixel = !c->d_mats && c->h_sph.size() == c->nsph && c->nsph <= 64;
     iqiv::camera_in ci;
     ci.width = c->width;
@@ -416,6 +447,7 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
     uint32_t cc = 0;
     cam_constants(c->cam, &cc, &ci.near_rw, &ci.far_rw);
     ci.cam_const = (int)cc;
+    c->h_specmask.assign((size_t)c->cull_ntx * c->cull_nty, 0ull);
     for (size_t st = 0; st < split.size(); ++st) {
         uint64_t lanes = 0;
         for (uint32_t i = 0; i < iqpt::kQueueChunk; ++i) {
@@ -432,9 +464,14 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
                     sphere = !(b.ok && iqiv::sphere_culled(b, ctr, c->h_sph[k].w));
                 }
             }
-            if (sphere) chain_pix.push_back(pix);
-            else lanes |= 1ull << i;
+            if (sphere) {
+                chain_pix.push_back(pix);
+                c->h_specmask[split[st]] |= 1ull << i;
+            } else {
+                lanes |= 1ull << i;
+            }
         }
+        if (sky) lanes &= ~c->h_miss[split[st]];
         if (lanes) {
             fan_tiles.push_back(split[st]);
             fan_lanes.push_back(lanes);
@@ -454,6 +491,21 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
     }
     c->n_chain_pix = (uint32_t)chain_pix.size();
     c->n_fan_tiles = (uint32_t)fan_tiles.size();
+    // hybrid launches: the plain kernel skips the sphere pixels and (sky kernel on) the certain misses
+    if (c->d_skip) (void)hipFree(c->d_skip);
+    c->d_skip = nullptr;
+    if (per_pixel && !chain_pix.empty()) {
+        const size_t nt = (size_t)c->cull_ntx * c->cull_nty;
+        std::vector<uint32_t> skip(2 * nt);
+        for (size_t t = 0; t < nt; ++t) {
+            const uint64_t m = c->h_specmask[t] | (sky ? c->h_miss[t] : 0ull);
+            skip[2 * t] = (uint32_t)m;
+            skip[2 * t + 1] = (uint32_t)(m >> 32);
+        }
+        if (hipMalloc(&c->d_skip, skip.size() * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "hybrid skip masks");
+        IQPT_HIP(hipMemcpy(c->d_skip, skip.data(), skip.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
     return IQPT_OK;
 }
 
@@ -637,6 +689,8 @@ int build_cull(iqpt_ctx* c) {
     // candidates: C4 +66 % per launch whether the pixels are folded in the refill or by a kernel of their own
     // (profiles/r03/ab_certain.json, ab_streamed_certain_fold_rejected.json)
     c->certain_valid = false;
+    c->sky_active = false;
+    c->h_miss.clear();
     if (c->d_certain) (void)hipFree(c->d_certain);
     c->d_certain = nullptr;
     std::vector<uint32_t> certain;
@@ -658,9 +712,11 @@ int build_cull(iqpt_ctx* c) {
         c->certain_valid = true;
         // the tiles holding certain-miss pixels: iqpt_sky_kernel's work list (one wave each)
         std::vector<uint32_t> sky;
+        c->h_miss.assign(ntiles, 0ull);
         for (uint32_t t = 0; t < ntiles; ++t) {
             const uint64_t m = (uint64_t)certain[2 * (size_t)ntiles + 2 * (size_t)t] |
                                ((uint64_t)certain[2 * (size_t)ntiles + 2 * (size_t)t + 1] << 32);
+            c->h_miss[t] = m;
             if (m) {
                 sky.push_back(t);
                 c->n_sky_pixels += (uint32_t)__builtin_popcountll(m);
@@ -673,6 +729,8 @@ int build_cull(iqpt_ctx* c) {
             c->n_sky_tiles = (uint32_t)sky.size();
         }
     }
+    c->sky_active = c->sky_on && c->certain_on && c->certain_valid && c->n_sky_tiles > 0;
+    if (!c->sky_active) c->h_miss.clear();
     // queue order over tiles (a queue chunk is one tile): most expensive first, so the pixels that set
     // the end of the launch are cheap ones. Cost = candidate triangle pairs + 8 x candidate sphere pairs
     // (a camera ray that can hit a sphere starts an Oren-Nayar path: more rays and the scatter shading).
@@ -1236,6 +1294,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream3) (void)hipStreamSynchronize(c->stream3);
+    if (c->stream4) (void)hipStreamSynchronize(c->stream4);
     free_comm(c);
     free_scene(c);
     if (c->d_lin) (void)hipFree(c->d_lin);
@@ -1250,6 +1309,9 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream3) (void)hipStreamDestroy(c->stream3);
+    if (c->stream4) (void)hipStreamDestroy(c->stream4);
+    for (hipEvent_t e : {c->ev_h0, c->ev_spec4})
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : {c->ev_pipe_end, c->ev_copy_cur, c->ev_copy_alt})
         if (e) (void)hipEventDestroy(e);
     free_split(c);
@@ -1825,6 +1887,21 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
     }
     if (!ovl && !pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
+    // hybrid launches: overlapped plain launches whose sphere pixels — the longest per-pixel
+    // chains, which bound a launch at N = 1 — run in the spec kernel on stream4, pipelined across launches; the
+    // plain kernel skips them (and the certain misses, the sky kernel's: d_skip). A hybrid chain starts joined.
+    bool hybrid = false;
+    if (c->hybrid_mode != 0 && ovl && c->d_skip && c->n_chain_pix > 0 && !(opt & iqpt::kOptMaterials) &&
+        spp <= iqpt::kAccTableMax && iqpt::spec_variant_exists(c->max_depth, opt)) {
+        iqpt::kspec probe;
+        std::memset(&probe, 0, sizeof probe);
+        probe.m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
+        int occ_h = 0;
+        hybrid = iqpt::spec_lds(p, probe) <= c->lds_per_block && probe.m_cap <= 65535u &&
+                 iqpt::spec_occupancy(p, probe, opt, &occ_h) == 0 && occ_h >= 1;
+        (void)hipGetLastError();
+    }
+    if (hybrid && !c->hyb_pend && (st = join_streams(c)) != IQPT_OK) return st;
     hipStream_t ls = c->stream;                       // the launch's stream
     if (ovl) {
         opt |= iqpt::kOptOverlap;
@@ -1909,6 +1986,119 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->pipe_kind = kind;
         return IQPT_OK;
     };
+    // ---- the spec kernel's buffers, parameters, plan and history (pipelined spec launches on `stream`,
+    // hybrid launches on `stream4`): every enqueue of these on the spec kernel's stream `ss`
+    auto spec_buffers = [&](hipStream_t ss, iqpt::kspec& ks2) -> int {
+        std::memset(&ks2, 0, sizeof ks2);
+        const uint32_t n = c->n_chain_pix;
+        const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
+        if (n > 0 && (n > c->spec_n || m_cap > c->spec_mcap)) {
+            IQPT_HIP(hipStreamSynchronize(c->stream));
+            if (c->stream4) IQPT_HIP(hipStreamSynchronize(c->stream4));
+            for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_plan})
+                if (b) (void)hipFree(b);
+            for (void* b : {(void*)c->h_spec_rho, (void*)c->h_spec_plan})
+                if (b) (void)hipHostFree(b);
+            c->d_spec = nullptr;
+            c->d_spec_res = nullptr;
+            c->d_spec_plan = nullptr;
+            c->h_spec_rho = c->h_spec_plan = nullptr;
+            c->spec_n = c->spec_mcap = 0;
+            c->spec_plan_n = 0;
+            c->spec_rho_pending = c->spec_plan_up = false;
+            const size_t slots = (size_t)n * m_cap;
+            if ((!c->ev_spec_rho && hipEventCreateWithFlags(&c->ev_spec_rho, hipEventDisableTiming) != hipSuccess) ||
+                (!c->ev_spec_plan && hipEventCreateWithFlags(&c->ev_spec_plan, hipEventDisableTiming) != hipSuccess) ||
+                slots * 16 > iqpt::kSplitResBudget ||
+                hipMalloc(&c->d_spec, (2 * (size_t)n + 2) * sizeof(uint32_t)) != hipSuccess ||
+                hipMalloc(&c->d_spec_res, slots * sizeof(float4_storage)) != hipSuccess ||
+                hipMalloc(&c->d_spec_plan, 3 * (size_t)n * sizeof(uint32_t)) != hipSuccess ||
+                hipHostMalloc(&c->h_spec_rho, (size_t)n * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc(&c->h_spec_plan, 3 * (size_t)n * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
+                (void)hipGetLastError();
+                return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec buffers");
+            }
+            // the statistics counters run from here (iqpt_debug_spec_info reads and clears them)
+            IQPT_HIP(hipMemsetAsync(c->d_spec + 2 * (size_t)n, 0, 2 * sizeof(uint32_t), ss));
+            c->spec_n = n;
+            c->spec_mcap = m_cap;
+            c->spec_rho_valid = false;
+        }
+        p.ovl_err = c->d_ovl_err;
+        ks2.n = n;
+        ks2.m_cap = m_cap;
+        ks2.rho0 = c->spec_rho0;
+        ks2.margin_div = c->spec_margin_div;
+        ks2.pix = c->d_chain_pix;
+        ks2.m = c->d_spec;
+        ks2.rho = c->d_spec + n;
+        ks2.run_count = c->d_spec + 2 * (size_t)n;
+        ks2.res = c->d_spec_res;
+        // a new pixel list: no history, and the statistics counters behind it (d_spec + 2 n) restart too
+        // (ADVICE r3: after a list that shrank n they pointed into the old history)
+        if (n > 0 && !c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, ((size_t)n + 2) * sizeof(uint32_t), ss));
+        c->spec_rho_valid = c->spec_rho_valid || n > 0;
+        return IQPT_OK;
+    };
+    auto spec_plan = [&](hipStream_t ss, iqpt::kspec& ks2) -> int {
+        const uint32_t n = ks2.n;
+        // the plan: built from the history read after an earlier launch (asynchronous), or, for tests,
+        // synchronously from the current history
+        if (n > 0 && c->spec_plan_mode >= 2) {
+            IQPT_HIP(hipStreamSynchronize(ss));
+            IQPT_HIP(hipMemcpy(c->h_spec_rho, ks2.rho, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+            const uint32_t nb = spec_build_plan(c, p, ks2, opt, c->h_spec_rho, c->h_spec_plan);
+            IQPT_HIP(hipMemcpy(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
+                               hipMemcpyHostToDevice));
+            c->spec_plan_n = n;
+            c->spec_plan_blocks = nb;
+        } else if (n > 0 && c->spec_plan_mode == 1 && c->spec_rho_pending &&
+                   hipEventQuery(c->ev_spec_rho) == hipSuccess &&
+                   (!c->spec_plan_up || hipEventQuery(c->ev_spec_plan) == hipSuccess)) {
+            const uint32_t nb = spec_build_plan(c, p, ks2, opt, c->h_spec_rho, c->h_spec_plan);
+            IQPT_HIP(hipMemcpyAsync(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
+                                    hipMemcpyHostToDevice, ss));
+            IQPT_HIP(hipEventRecord(c->ev_spec_plan, ss));
+            c->spec_plan_up = true;
+            c->spec_rho_pending = false;
+            c->spec_plan_n = n;
+            c->spec_plan_blocks = nb;
+            c->spec_plan_age = 0;
+        }
+        if (n > 0 && c->spec_plan_mode >= 1 && c->spec_plan_n == n) {
+            ks2.order = c->d_spec_plan;
+            ks2.blocks = c->d_spec_plan + n;
+            ks2.nblocks = c->spec_plan_blocks;
+        }
+        if (c->spec_tl_on && n > 0) {
+            const size_t nb = ks2.blocks ? ks2.nblocks : (n + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
+            if (nb > c->spec_tl_blocks) {
+                IQPT_HIP(hipStreamSynchronize(ss));
+                if (c->d_spec_tl) (void)hipFree(c->d_spec_tl);
+                c->d_spec_tl = nullptr;
+                c->spec_tl_blocks = 0;
+                if (hipMalloc(&c->d_spec_tl, nb * 8 * sizeof(unsigned long long)) != hipSuccess) {
+                    (void)hipGetLastError();
+                    return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec timeline");
+                }
+                c->spec_tl_blocks = nb;
+            }
+            IQPT_HIP(hipMemsetAsync(c->d_spec_tl, 0, nb * 8 * sizeof(unsigned long long), ss));
+            ks2.tl = c->d_spec_tl;
+        }
+        return IQPT_OK;
+    };
+    // read this launch's history for the next plan: before the first plan, then every kSpecReplan launches
+    auto spec_history = [&](hipStream_t ss, const iqpt::kspec& ks2) -> int {
+        const uint32_t n = ks2.n;
+        if (n > 0 && c->spec_plan_mode == 1 && !c->spec_rho_pending &&
+            (c->spec_plan_n != n || ++c->spec_plan_age >= iqpt::kSpecReplan)) {
+            IQPT_HIP(hipMemcpyAsync(c->h_spec_rho, ks2.rho, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, ss));
+            IQPT_HIP(hipEventRecord(c->ev_spec_rho, ss));
+            c->spec_rho_pending = true;
+        }
+        return IQPT_OK;
+    };
     // certain-miss pixels: plain launches hand them to iqpt_sky_kernel, ahead of the plain
     // kernel on the launch's stream; the plain kernel skips them. Consecutive sky kernels order themselves
     // through ev_sky (overlapped launches alternate streams); their pixels are disjoint from the plain kernel's.
@@ -1928,11 +2118,42 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         IQPT_HIP(hipEventRecord(c->ev_sky, ss));
         c->sky_last = ss;
     }
+    // a hybrid launch's plain kernel skips the misses only while the sky kernel renders them (d_skip was built
+    // with sky_active): otherwise the plain path without the spec kernel
+    if (hybrid && sky != c->sky_active) hybrid = false;
+    const iqpt::kparams p_spec = p;
+    if (hybrid) p.miss = c->d_skip;
     if (ovl) {
         le = iqpt::launch_render(ls, p, grid, lds, stream_batches, opt);
         c->ovl_epoch += 1;
         c->next_on_main = !c->next_on_main;
         if (le != 0) c->ovl_zero = true;     // a failed launch breaks the chain's counts: restart it
+        if (hybrid && le == 0) {
+            // the sphere pixels: the spec kernel on stream4 (after everything `stream` held when the hybrid chain
+            // started; later ones after the previous spec kernel), its plan and history on stream4 too
+            if ((!c->stream4 && hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) ||
+                (!c->ev_h0 && hipEventCreateWithFlags(&c->ev_h0, hipEventDisableTiming) != hipSuccess) ||
+                (!c->ev_spec4 && hipEventCreateWithFlags(&c->ev_spec4, hipEventDisableTiming) != hipSuccess)) {
+                (void)hipGetLastError();
+                return iqpt::fail(IQPT_ERR_HIP, "hybrid spec stream");
+            }
+            if (!c->hyb_pend) {
+                IQPT_HIP(hipEventRecord(c->ev_h0, c->stream));
+                IQPT_HIP(hipStreamWaitEvent(c->stream4, c->ev_h0, 0));
+            }
+            iqpt::kspec ks2;
+            if ((st = spec_buffers(c->stream4, ks2)) != IQPT_OK) return st;
+            if ((st = spec_plan(c->stream4, ks2)) != IQPT_OK) return st;
+            iqpt::kparams ph = p_spec;
+            ph.miss = nullptr;
+            ph.ovl_err = c->d_ovl_err;
+            le = iqpt::launch_spec(c->stream4, ph, ks2, opt);
+            if (le == 0 && (st = spec_history(c->stream4, ks2)) != IQPT_OK) return st;
+            IQPT_HIP(hipEventRecord(c->ev_spec4, c->stream4));
+            c->hyb_pend = true;
+            e1b = take_event(c);
+            if (e1b) (void)hipEventRecord(e1b, c->stream4);
+        }
     } else if (fan_pipe) {
         // pipelined FAN launch: the split tiles in the plain kernel on stream (queue[0], zeroed there), the
         // anchored tiles in the fan kernel on stream2
@@ -1992,6 +2213,12 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             const uint32_t grid_s = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_s, (uint64_t)c->num_cus * occ));
             le = iqpt::launch_render(c->stream, ps, grid_s, lds, stream_batches, opt);
         }
+        if (le == 0 && fan_beside_chain && c->sky_active) {
+            // the certain-miss pixels the fan lists left out, ahead of the fan kernel
+            iqpt::kparams pm = p;
+            pm.miss = c->d_certain + 2 * (size_t)c->cull_ntx * c->cull_nty;
+            le = iqpt::launch_sky(c->stream2, pm, c->d_sky_tiles, c->n_sky_tiles, opt);
+        }
         if (le == 0 && fan_beside_chain && c->n_fan_tiles > 0) {
             p.tile_order = c->d_fan_tiles;
             p.fan_lanes = c->d_fan_lanes;
@@ -2018,102 +2245,21 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         // every pixel without a sphere in reach in the fan kernel on stream2; the sphere pixels in
         // iqpt_spec_kernel on stream (slots, then the walk)
         iqpt::kspec ks2;
-        std::memset(&ks2, 0, sizeof ks2);
-        const uint32_t n = c->n_chain_pix;
-        const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
-        if (n > 0 && (n > c->spec_n || m_cap > c->spec_mcap)) {
-            IQPT_HIP(hipStreamSynchronize(c->stream));
-            for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_plan})
-                if (b) (void)hipFree(b);
-            for (void* b : {(void*)c->h_spec_rho, (void*)c->h_spec_plan})
-                if (b) (void)hipHostFree(b);
-            c->d_spec = nullptr;
-            c->d_spec_res = nullptr;
-            c->d_spec_plan = nullptr;
-            c->h_spec_rho = c->h_spec_plan = nullptr;
-            c->spec_n = c->spec_mcap = 0;
-            c->spec_plan_n = 0;
-            c->spec_rho_pending = c->spec_plan_up = false;
-            const size_t slots = (size_t)n * m_cap;
-            if ((!c->ev_spec_rho && hipEventCreateWithFlags(&c->ev_spec_rho, hipEventDisableTiming) != hipSuccess) ||
-                (!c->ev_spec_plan && hipEventCreateWithFlags(&c->ev_spec_plan, hipEventDisableTiming) != hipSuccess) ||
-                slots * 16 > iqpt::kSplitResBudget ||
-                hipMalloc(&c->d_spec, (2 * (size_t)n + 2) * sizeof(uint32_t)) != hipSuccess ||
-                hipMalloc(&c->d_spec_res, slots * sizeof(float4_storage)) != hipSuccess ||
-                hipMalloc(&c->d_spec_plan, 3 * (size_t)n * sizeof(uint32_t)) != hipSuccess ||
-                hipHostMalloc(&c->h_spec_rho, (size_t)n * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc(&c->h_spec_plan, 3 * (size_t)n * sizeof(uint32_t), hipHostMallocDefault) != hipSuccess) {
-                (void)hipGetLastError();
-                return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec buffers");
-            }
-            // the statistics counters run from here (iqpt_debug_spec_info reads and clears them)
-            IQPT_HIP(hipMemsetAsync(c->d_spec + 2 * (size_t)n, 0, 2 * sizeof(uint32_t), c->stream));
-            c->spec_n = n;
-            c->spec_mcap = m_cap;
-            c->spec_rho_valid = false;
-        }
-        p.ovl_err = c->d_ovl_err;          // bit 3: a chain slot no lane traced (never expected)
-        ks2.n = n;
-        ks2.m_cap = m_cap;
-        ks2.rho0 = c->spec_rho0;
-        ks2.margin_div = c->spec_margin_div;
-        ks2.pix = c->d_chain_pix;
-        ks2.m = c->d_spec;
-        ks2.rho = c->d_spec + n;
-        ks2.run_count = c->d_spec + 2 * (size_t)n;
-        ks2.res = c->d_spec_res;
-        // a new pixel list: no history, and the statistics counters behind it (d_spec + 2 n) restart too
-        // (ADVICE r3: after a list that shrank n they pointed into the old history)
-        if (n > 0 && !c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, ((size_t)n + 2) * sizeof(uint32_t), c->stream));
-        c->spec_rho_valid = c->spec_rho_valid || n > 0;
+        if ((st = spec_buffers(c->stream, ks2)) != IQPT_OK) return st;
         if (c->specfan_mode == 0 && (st = pipe_begin()) != IQPT_OK) return st;
         iqpt::kparams pf = p;
         pf.tile_order = c->d_fan_tiles;
         pf.fan_lanes = c->d_fan_lanes;
-        // the plan: built from the history read after an earlier launch (asynchronous), or, for tests,
-        // synchronously from the current history
-        if (n > 0 && c->spec_plan_mode >= 2) {
-            IQPT_HIP(hipStreamSynchronize(c->stream));
-            IQPT_HIP(hipMemcpy(c->h_spec_rho, ks2.rho, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost));
-            const uint32_t nb = spec_build_plan(c, p, ks2, opt, c->h_spec_rho, c->h_spec_plan);
-            IQPT_HIP(hipMemcpy(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
-                               hipMemcpyHostToDevice));
-            c->spec_plan_n = n;
-            c->spec_plan_blocks = nb;
-        } else if (n > 0 && c->spec_plan_mode == 1 && c->spec_rho_pending &&
-                   hipEventQuery(c->ev_spec_rho) == hipSuccess &&
-                   (!c->spec_plan_up || hipEventQuery(c->ev_spec_plan) == hipSuccess)) {
-            const uint32_t nb = spec_build_plan(c, p, ks2, opt, c->h_spec_rho, c->h_spec_plan);
-            IQPT_HIP(hipMemcpyAsync(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
-                                    hipMemcpyHostToDevice, c->stream));
-            IQPT_HIP(hipEventRecord(c->ev_spec_plan, c->stream));
-            c->spec_plan_up = true;
-            c->spec_rho_pending = false;
-            c->spec_plan_n = n;
-            c->spec_plan_blocks = nb;
-            c->spec_plan_age = 0;
+        // the certain-miss pixels the fan lists left out: the sky kernel, ahead of the fan
+        // kernel on its stream (consecutive launches' sky kernels are ordered there)
+        if (c->sky_active) {
+            iqpt::kparams pm = pf;
+            pm.miss = c->d_certain + 2 * (size_t)c->cull_ntx * c->cull_nty;
+            le = iqpt::launch_sky(c->specfan_mode == 0 ? c->stream2 : c->stream, pm, c->d_sky_tiles, c->n_sky_tiles, opt);
+            if (le != 0) return iqpt::hip_fail((hipError_t)le, "sky kernel launch");
         }
-        if (n > 0 && c->spec_plan_mode >= 1 && c->spec_plan_n == n) {
-            ks2.order = c->d_spec_plan;
-            ks2.blocks = c->d_spec_plan + n;
-            ks2.nblocks = c->spec_plan_blocks;
-        }
-        if (c->spec_tl_on && n > 0) {
-            const size_t nb = ks2.blocks ? ks2.nblocks : (n + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
-            if (nb > c->spec_tl_blocks) {
-                IQPT_HIP(hipStreamSynchronize(c->stream));
-                if (c->d_spec_tl) (void)hipFree(c->d_spec_tl);
-                c->d_spec_tl = nullptr;
-                c->spec_tl_blocks = 0;
-                if (hipMalloc(&c->d_spec_tl, nb * 8 * sizeof(unsigned long long)) != hipSuccess) {
-                    (void)hipGetLastError();
-                    return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec timeline");
-                }
-                c->spec_tl_blocks = nb;
-            }
-            IQPT_HIP(hipMemsetAsync(c->d_spec_tl, 0, nb * 8 * sizeof(unsigned long long), c->stream));
-            ks2.tl = c->d_spec_tl;
-        }
+        if ((st = spec_plan(c->stream, ks2)) != IQPT_OK) return st;
+        const uint32_t n = ks2.n;
         if (c->specfan_mode == 2) {
             // one grid: no second stream, no join
             ks2.fan_tiles = c->n_fan_tiles;
@@ -2127,13 +2273,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream2, pf, c->n_fan_tiles, opt);
             if ((st = pipe_end(1)) != IQPT_OK) return st;
         }
-        // read this launch's history for the next plan: before the first plan, then every kSpecReplan launches
-        if (n > 0 && c->spec_plan_mode == 1 && !c->spec_rho_pending && le == 0 &&
-            (c->spec_plan_n != n || ++c->spec_plan_age >= iqpt::kSpecReplan)) {
-            IQPT_HIP(hipMemcpyAsync(c->h_spec_rho, ks2.rho, (size_t)n * sizeof(uint32_t), hipMemcpyDeviceToHost, c->stream));
-            IQPT_HIP(hipEventRecord(c->ev_spec_rho, c->stream));
-            c->spec_rho_pending = true;
-        }
+        if (le == 0 && (st = spec_history(c->stream, ks2)) != IQPT_OK) return st;
     } else if (split) {
         // prep -> round 1 (runs, anchored tiles, light split pixels) -> stitch -> round 2 (leftovers); with
         // the fan kernel the anchored tiles leave round 1 for iqpt_fan_kernel on stream2
@@ -2163,9 +2303,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     c->split_last = split;
     c->chain_last = chain;
     c->fan_last = fan || fan_beside_chain || fan_split || spec;
-    c->spec_last = spec;
+    c->spec_last = spec || hybrid;
+    c->hybrid_last = hybrid;
     c->last_ls = ls;
-    c->last_ovl = ovl;
+    // hybrid launches: a frame copy joins every stream (the spec kernel writes the frame on stream4)
+    c->last_ovl = ovl && !hybrid;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1) (void)hipEventRecord(e1, ls);
     if (e0 && e1) c->timed.push_back({e0, e1, e1b});
@@ -2529,6 +2671,16 @@ int iqpt_debug_set_sky(iqpt_ctx* c, int on) {
     if (st) return st;
     c->sky_on = on != 0;
     c->cull_valid = false;
+    return IQPT_OK;
+}
+
+/* Internal (A/B, tests): hybrid launches — 1: overlapped plain launches send the sphere pixels
+ * to the spec kernel on a stream of their own; 0 (the default until measured): off. */
+int iqpt_debug_set_hybrid(iqpt_ctx* c, int mode) {
+    if (!c || mode < 0 || mode > 1) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or mode not 0..1");
+    int st = enter(c);
+    if (st) return st;
+    c->hybrid_mode = mode;
     return IQPT_OK;
 }
 
@@ -2947,7 +3099,8 @@ int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
     out8[2] = ns;
     // launch mode: 1 split, 2 chain (anchored tiles plain), 3 fan (split tiles plain), 4 chain + fan, 5 split + fan,
     // 6 spec (sphere pixels slot-parallel, the rest fan)
-    out8[7] = c->spec_last ? 6
+    // 7 hybrid (overlapped plain kernel + the sphere pixels in the spec kernel + sky kernel)
+    out8[7] = c->hybrid_last ? 7 : c->spec_last ? 6
                            : (c->split_last ? (c->fan_last ? 5 : 1)
                                             : (c->chain_last ? (c->fan_last ? 4 : 2) : (c->fan_last ? 3 : 0)));
     if (!c->d_split || ns == 0) return IQPT_OK;

@@ -169,13 +169,15 @@ class PathTracer:
 
     def launch_mode(self) -> str:
         """How the last launch ran: "plain", "split" (speculative runs + stitch), "chain" (chain kernel beside
-        the plain kernel), "fan" (fan kernel beside the plain kernel), "chain+fan", "split+fan" or "spec", from
+        the plain kernel), "fan" (fan kernel beside the plain kernel), "chain+fan", "split+fan", "spec" or "hybrid"
+        (overlapped plain launches with the sphere pixels in the spec kernel), from
         iqpt_debug_split_info. Synchronises."""
         import ctypes as C
         self._lib.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
         info = (C.c_ulonglong * 8)()
         check(self._lib.iqpt_debug_split_info(self._h, info), "iqpt_debug_split_info")
-        return {1: "split", 2: "chain", 3: "fan", 4: "chain+fan", 5: "split+fan", 6: "spec"}.get(int(info[7]), "plain")
+        return {1: "split", 2: "chain", 3: "fan", 4: "chain+fan", 5: "split+fan", 6: "spec",
+                7: "hybrid"}.get(int(info[7]), "plain")
 
     def kernel_span(self) -> float:
         """First start to last end (ms) of the launches of the last kernel_time() call (iqpt_kernel_span)."""

@@ -39,3 +39,22 @@ def test_c5_full_width_band(require_gpu):
     assert np.array_equal(bgra, fr.bgra)
     assert np.array_equal(pt.read_rng(), fr.states)
     assert pt.rays() == int(fr.rays.sum())
+
+
+@pytest.mark.parametrize("preset,w,h,x0,y0,launches", [
+    ("mesh10k", 1920, 1080, 952, 500, [256, 256]),     # C4: the bench's 256-spp launch (bench.py --config c4)
+    ("mixed", 3840, 2160, 1900, 1080, [16, 16]),       # C5: the bench's 16-spp launch (bench.py --config c5 --spp 16)
+])
+def test_bench_launch_shapes_on_a_crop(require_gpu, preset, w, h, x0, y0, launches):
+    """C4 and C5 at the spp per launch their bench lines run (those shapes were checked only by the
+    bench's own verify band), on a 16x16 crop through the mesh: two launches, so both camera-ray paths the
+    first launches of a streamed scene time (tile masks, then the BVH) run at that launch size."""
+    ps = pixel_set(w, h, x0, x0 + 16, y0, 1, 16)
+    pt, lin, bgra = gpu_render(preset, w, h, 0, 8, pixels=ps, launches=launches)
+    fr = oracle_render(preset, w, h, 0, 8, pixels=ps, launches=launches)
+    c = compare(lin, fr.lin)
+    assert c["rmse"] < 1e-5, c
+    assert c["bitexact"] == c["npix"] == 256, c
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    assert pt.rays() == int(fr.rays.sum())

@@ -43,6 +43,7 @@ def _render(preset, w, h, launches, sky=True, ps=None, overlap=True, frame0=None
     lin, bgra = pt.read()
     px, tl = C.c_uint32(0), C.c_uint32(0)
     L.check(lib.iqpt_debug_sky_info(pt.handle, C.byref(px), C.byref(tl)), "iqpt_debug_sky_info")
+    pt._scene = sc                      # the scene owns the packet's arrays: keep it alive with the context
     return pt, lin, bgra, px.value, pk, cam
 
 

@@ -1,7 +1,7 @@
 """Slot-parallel sphere pixels (IQPT_SPLIT_SPEC) vs the CPU oracle, bit for bit.
 
 Only the pixels whose own camera-ray bundle may reach a sphere can take more than two draws per sample.
-Every slot of their window (the sample that starts 2j draws into the pixel's XORWOW stream) is evaluated
+Lanes follow the chain from starting slots spread over a window (slot j: the sample that starts 2j draws into the pixel's XORWOW stream) and stop where they meet a slot another lane took; the slots are evaluated
 in parallel, the chain 0 -> j + n_j -> ... is walked afterwards and folded in sample order, and a chain
 that leaves its window continues in a new window (another round of the same block); every other pixel
 runs in the fan kernel, in the same grid (iqpt_specfan_kernel) or beside it. The result must be the reference's sequential chain (path_tracer.cu:330-366, random.cu:66-107):
@@ -45,6 +45,17 @@ def test_cornell_crop_spec(require_gpu, launches):
     pt, lin, bgra = gpu_render("cornell", 1920, 1080, 0, 8, pixels=ps, launches=launches, split=SPLIT_SPEC)
     assert mode_of(pt) == 6
     fr = oracle_render("cornell", 1920, 1080, 0, 8, pixels=ps, launches=launches)
+    _check(pt, lin, bgra, fr)
+
+
+def test_spec_at_the_launch_limit(require_gpu):
+    """One launch of kAccTableMax = 1,024 samples, the largest a render is cut into: the spec block's slot
+    marks take 32 pixels x 3,072 bytes of LDS, so the runtime checks the block against the device's limit and
+    one resident block and otherwise falls back to the plain kernel — the bits either way."""
+    ps = pixel_set(1920, 1080, 920, 952, 480, 1, 8)
+    pt, lin, bgra = gpu_render("cornell", 1920, 1080, 0, 8, pixels=ps, launches=[1024], split=SPLIT_SPEC)
+    assert mode_of(pt) in (0, 6)
+    fr = oracle_render("cornell", 1920, 1080, 0, 8, pixels=ps, launches=[1024])
     _check(pt, lin, bgra, fr)
 
 
