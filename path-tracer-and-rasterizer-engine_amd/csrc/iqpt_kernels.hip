@@ -3250,6 +3250,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         rd[11] = 0u;
         rd[12] = 0u;
         rd[13] = pix;
+        rd[14] = (s.rho[q] != 0u && s.rho[q] < kSpecChainRho) ? 1u : 0u;   // follow the chain (mixed slot counts)
     } else if (!valid && l == 0u) {
         // no pixel (the grid's last block): an empty, finished record (every field is read by the rounds)
         for (uint32_t i = 0; i < 16u; ++i) rd[i] = 0u;
@@ -3268,17 +3269,22 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     while (__syncthreads_or(rd[7] == 0u)) {
         const bool live = rd[7] == 0u;
         const uint32_t js = rd[0], M = rd[1];
-        // ---- the window's slot marks: 0 not taken, kSpecTaken taken by a lane, else the slots its sample used
+        // ---- per pixel, two ways to cover the window (rd[14], from the pixel's last chain):
+        //  * follow (mixed slot counts, rho < kSpecChainRho): lane l starts at M l / L rounded down to even and
+        //    follows the chain, stopping at a slot another lane took (the chains have met) or kSpecOvershoot
+        //    slots past the next lane's start (they did not: the walker then starts a new round at the first
+        //    slot no lane traced). Even starts: a chain of 2-slot samples stays on one parity;
+        //  * every slot (samples of 2+ slots, which rarely change parity, so chains from different starts
+        //    seldom meet): lane l traces slots [M l / L, M (l + 1) / L) back to back.
+        // Marks: 0 not traced, kSpecTaken a lane is tracing it, else the slots its sample used.
+        const bool follow = rd[14] != 0u;
+        auto start_of = [&](uint32_t k) { return follow ? ((M * k / L) & ~1u) : M * k / L; };
         for (uint32_t i = l; i < M; i += L) ln[i] = 0u;
-        // ---- this lane's chain starts at slot j0 = M l / L rounded down to even (relative to js), with the state
-        // 2 j0 draws in. Even: a pixel whose samples all take an even number of slots (camera ray -> sphere ->
-        // wall: 2) has its chain on even slots only, and a chain from an odd slot would never meet it.
-        const uint32_t j0 = (M * l / L) & ~1u;
-        const bool first_ok = live && j0 < M && (l == 0u || ((M * (l - 1u) / L) & ~1u) < j0);
-        // a lane that has not met another chain this far past the next lane's start gives up: the walker then
-        // continues from the first slot no lane traced in a new round (rare; bounds the cost of chains that
-        // do not meet)
-        const uint32_t j_stop = l + 1u < L ? min(M, ((M * (l + 1u) / L) & ~1u) + kSpecOvershoot) : M;
+        const uint32_t j0 = start_of(l), jn = l + 1u < L ? start_of(l + 1u) : M;
+        // every slot: the lanes' ranges [start_of(l), start_of(l + 1)) tile [0, M) (empty ones idle); follow:
+        // one lane per distinct start (the first), lane 0 always — so slot 0 is always traced
+        const bool first_ok = live && j0 < M && (follow ? (l == 0u || start_of(l - 1u) < j0) : j0 < jn);
+        const uint32_t j_stop = follow ? (l + 1u < L ? min(M, jn + kSpecOvershoot) : M) : jn;
         rng6 st = {rd[2], rd[3], rd[4], rd[5], rd[6], p.rng[5 * (size_t)p.npix + rd[13]] + 2u * (js + j0) * IQ_XORWOW_WEYL};
         xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, live ? 2u * j0 : 0u);
         lst[l * 5u] = st.v0;
@@ -3292,10 +3298,13 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         bool active = first_ok;
         ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         int depth = 0;
-        // a slot's sample starts here: its camera ray (two draws); its scatters draw two more each, so when it
-        // ends having used n slots the state is the one slot j + n starts from
+        rng6 base = st;
+        // a slot's sample starts here: its camera ray (two draws; the state they leave is slot j + 1's); its
+        // scatters draw two more each, so when it ends having used n slots the state is the one slot j + n
+        // starts from
         auto start_slot = [&]() {
             camera_ray<OPT>(p, px, py, st, ray);
+            base = st;
             depth = 0;
         };
         if (active) start_slot();
@@ -3370,11 +3379,18 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                     // follow the chain: the next sample starts at slot j + n from the state this one left.
                     // A slot another lane has taken is on a chain that lane follows to the window's end
                     // (or to a slot taken before it), so this lane's chain has merged into it and stops.
-                    j += n;
-                    if (j >= j_stop || *reinterpret_cast<volatile uint8_t*>(ln + j) != 0u) {
+                    if (follow) {
+                        j += n;
+                        if (j >= j_stop || *reinterpret_cast<volatile uint8_t*>(ln + j) != 0u) {
+                            active = false;
+                        } else {
+                            ln[j] = kSpecTaken;
+                            start_slot();
+                        }
+                    } else if (++j == j_stop) {
                         active = false;
                     } else {
-                        ln[j] = kSpecTaken;
+                        st = base;                   // slot j starts where slot j - 1's camera draws ended
                         start_slot();
                     }
                 }
@@ -3431,16 +3447,22 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             k += cw;
             __syncthreads();
         }
-        if (walker && live) {
+        if (walker && live && k == rd[11]) {
+            // no sample folded this round: impossible (slot 0 of a round is always traced); end the pixel with
+            // an error bit rather than loop
+            atomicOr(p.ovl_err, 8u);
+            rd[7] = 1u;
+        } else if (walker && live) {
             rd[8] = __float_as_uint(ax);
             rd[9] = __float_as_uint(ay);
             rd[10] = __float_as_uint(az);
             rd[11] = k;
             const uint32_t pix = rd[13];
             // the state at the chain's end, slot js + jw: from the start of the last range at or below it
+            // (the lanes' start slots, as in the slot phase)
             uint32_t kk = L - 1u;
-            while (kk > 0u && M * kk / L > jw) --kk;
-            const uint32_t jk = M * kk / L;
+            while (kk > 0u && start_of(kk) > jw) --kk;
+            const uint32_t jk = start_of(kk);
             uint32_t v0 = lst[kk * 5u], v1 = lst[kk * 5u + 1u], v2 = lst[kk * 5u + 2u], v3 = lst[kk * 5u + 3u],
                      v4 = lst[kk * 5u + 4u];
             xorwow_skip_v(v0, v1, v2, v3, v4, 2u * (jw - jk));
@@ -3470,6 +3492,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                 atomicAdd(s.run_count + 1, 1u);
                 const uint32_t rem = p.spp - k;
                 rd[1] = min(s.m_cap, max(16u, 3u * rem + 4u));
+                rd[14] = 0u;                  // later rounds trace every slot (no untraced slot can end them)
             }
         }
         if (rec && rounds == 0u) t_rec[2] = __builtin_amdgcn_s_memrealtime();

@@ -525,8 +525,10 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     for (uint32_t q = 0; q < n; ++q) {
         const uint32_t r = rho[q] ? rho[q] : ks.rho0;
         const uint32_t m = iqpt::spec_window(r, p.spp, ks.m_cap, ks.margin_div);
-        // lanes follow the chain (round 4): each window slot is traced about once, as one ray
-        w[q] = (double)m;
+        // a pixel that follows chains (round 4, rho < kSpecChainRho) traces each slot of its chain once: about
+        // one ray per window slot; one that traces every slot pays the slots' mean length (rho) on each
+        w[q] = (rho[q] != 0u && rho[q] < iqpt::kSpecChainRho) ? (double)m
+                                                                : (double)m * (double)std::max<uint32_t>(r, 256u) / 256.0;
         total += w[q];
         wmax = std::max(wmax, w[q]);
     }

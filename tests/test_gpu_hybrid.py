@@ -23,6 +23,7 @@ def _render(w, h, launches, hybrid=True, sky=True, preset="cornell", copies=Fals
     cam = make_camera(w, h)
     pt = PathTracer(w, h, max_depth=8)
     pt._scene = sc
+    pt.set_split(_lib.SPLIT_OFF)             # small frames: AUTO would take spec launches (no overlapped plain kernel)
     _lib.check(lib.iqpt_debug_set_hybrid(pt.handle, 1 if hybrid else 0), "iqpt_debug_set_hybrid")
     _lib.check(lib.iqpt_debug_set_sky(pt.handle, 1 if sky else 0), "iqpt_debug_set_sky")
     pt.set_camera(cam)

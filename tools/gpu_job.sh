@@ -4,7 +4,7 @@
 mkdir -p gpurun_out
 O=gpurun_out
 R=r04_03
-timeout -k 10 900 python -u -m pytest tests/test_gpu_spec.py tests/test_gpu_hybrid.py tests/test_gpu_sky.py tests/test_gpu_certain.py tests/test_gpu_bench_multirank.py -x -q --timeout 300 --timeout-method thread > $O/${R}_tests.log 2>&1 || { tail -60 $O/${R}_tests.log; exit 1; }
+timeout -k 10 900 python -u -m pytest tests/test_gpu_spec.py tests/test_gpu_hybrid.py tests/test_gpu_sky.py tests/test_gpu_certain.py tests/test_gpu_bench_multirank.py -x -v --timeout 300 --timeout-method thread > $O/${R}_tests.log 2>&1 || { tail -60 $O/${R}_tests.log; exit 1; }
 tail -2 $O/${R}_tests.log
 line() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); print('$2', d['ms_per_step'], d['value'], d['config']['launch_mode'], d['bitexact_frac_vs_oracle'], d.get('gather_check'), d['roofline'].get('kernel_avg_ms'))"; }
 for n in 8 4 2; do
