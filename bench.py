@@ -81,6 +81,9 @@ def parse():
     ap.add_argument("--hybrid", default="off", choices=["on", "off"],
                     help="A/B: hybrid launches, the sphere pixels in the spec kernel beside overlapped plain launches "
                          "(iqpt_debug_set_hybrid, DESIGN.md §3.13)")
+    ap.add_argument("--hybrid-rho", type=float, default=0.0,
+                    help="hybrid launches: only sphere pixels whose last chain used >= this many slots per sample go "
+                         "to the spec kernel (0: all)")
     ap.add_argument("--sky", default="on", choices=["on", "off"],
                     help="A/B: certain-miss pixels in iqpt_sky_kernel (iqpt_debug_set_sky, DESIGN.md §3.12)")
     ap.add_argument("--kernel-options", type=lambda v: int(v, 0), default=0,
@@ -463,8 +466,8 @@ def main():
     if args.hybrid == "on":
         import ctypes as C
         lb = _lib.load()
-        lb.iqpt_debug_set_hybrid.argtypes = [C.c_void_p, C.c_int]
-        _lib.check(lb.iqpt_debug_set_hybrid(pt._h, 1), "iqpt_debug_set_hybrid")
+        lb.iqpt_debug_set_hybrid.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_hybrid(pt._h, 1, int(round(args.hybrid_rho * 256))), "iqpt_debug_set_hybrid")
     if args.sky == "off":
         import ctypes as C
         lb = _lib.load()
@@ -523,12 +526,18 @@ def main():
     # inside the timed steps, and the gather of step k runs while step k + 1 renders.
     stream_gather = lib_gather and args.gather == "frame" and not args.gather_sync
 
+    host = {"render": 0.0, "gather": 0.0}          # host time inside the library's calls (timed steps)
+
     def step():
         nonlocal assembled
+        h0 = time.perf_counter()
         pt.render(spp_step)
+        h1 = time.perf_counter()
+        host["render"] += h1 - h0
         if stream_gather:
             pt.gather_frame_async(0, frame_dev.data_ptr() if rank == 0 else 0,
                                   frame_dev.numel() * 4 if rank == 0 else 0)
+            host["gather"] += time.perf_counter() - h1
             assembled = frame_dev
         elif lib_gather:
             # --gather-sync / --gather accum: the blocking form
@@ -561,6 +570,7 @@ def main():
     pt.kernel_time()                                   # discard warmup timings
     torch.cuda.synchronize()
     barrier()
+    host["render"] = host["gather"] = 0.0
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -622,7 +632,11 @@ def main():
     mine = {"rank": rank, "render_span_ms": round(kern_span_ms / max(1, launches), 4),
             "step_ms": round(elapsed / args.steps * 1e3, 4),
             "gather_ms": round(gather_ms / gathers, 4) if gathers else None,
-            "outside_render_ms": round(elapsed / args.steps * 1e3 - kern_span_ms / max(1, launches), 4)}
+            "outside_render_ms": round(elapsed / args.steps * 1e3 - kern_span_ms / max(1, launches), 4),
+            # the host's time per step inside iqpt_render / iqpt_gather_frame_async: a host slower than the GPU
+            # leaves the GPU idle between launches
+            "host_render_ms": round(host["render"] / args.steps * 1e3, 4),
+            "host_gather_ms": round(host["gather"] / args.steps * 1e3, 4)}
     per_rank = [None] * world if world > 1 else [mine]
     if world > 1:
         dist.all_gather_object(per_rank, mine)
@@ -674,7 +688,7 @@ def main():
                                       + (" (RCCL ncclGather inside libiqpt: iqpt_gather_frame_async)" if lib_gather
                                          else " (gloo via host, rehearsal)")),
                        "split": args.split, "overlap": args.overlap, "certain": args.certain, "sky": args.sky,
-                       "hybrid": args.hybrid,
+                       "hybrid": args.hybrid, **({"hybrid_rho": args.hybrid_rho} if args.hybrid_rho else {}),
                        "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
                        **({"spec_cap": args.spec_cap} if args.spec_cap else {})},

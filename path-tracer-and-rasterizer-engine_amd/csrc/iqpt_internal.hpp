@@ -211,9 +211,6 @@ constexpr uint32_t kSpecReplan = 64;        // launches between two spec plans (
 constexpr uint32_t kSpecPixPerBlock = 16;   // sphere pixels per iqpt_spec_kernel block without a plan (16 lanes each)
 constexpr uint32_t kSpecMaxPixPerBlock = 32;   // a plan's blocks: 256 / (8, 16, 32 or 64) pixels
 constexpr uint32_t kSpecRho0 = 576;      // 2.25 slots per sample before a pixel has a history (sphere pixels take ~2)
-// spec kernel: a pixel whose last chain used fewer than 1.75 slots per sample (x 256) follows chains (its samples
-// mix 1- and 2-slot ones, so chains from different starts meet within a few samples); the others trace every slot
-constexpr uint32_t kSpecChainRho = 448;
 
 // The spec window of a sphere pixel whose last chain used rho256 / 256 slots per sample: that many slots
 // for spp samples plus a margin of 1 / margin_div of the extra slots (at least 4) and 4, within

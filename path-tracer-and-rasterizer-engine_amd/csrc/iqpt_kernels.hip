@@ -3144,15 +3144,10 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
 // jitter (camera.cu:24-25) plus 2 per Oren-Nayar scatter (material.cu:10), and what a sample does from
 // stream offset 2j ("slot" j) depends on j alone. One kernel, L = 8, 16, 32 or 64 lanes per sphere pixel
 // (16 without a plan; a plan gives the pixels with the most work per lane more lanes, runtime):
-//  * slots (round 4: coalescing chains): the pixel's window of M slots (its last chain's slots per sample,
-//    spec_window) gets L starting points j0 = M l / L; lane l steps its state to its start and FOLLOWS THE
-//    CHAIN from there — a sample that used n slots leaves exactly the state slot j + n starts from — taking
-//    each slot it traces in an LDS mark, until the window's end or a slot another lane has taken: from that
-//    slot on, the chain is the other lane's (chains from different starts meet and then coincide), so the
-//    lane stops. Slot 0 is on the true chain, hence by induction every slot of the true chain is traced by
-//    some lane; the waste is only each lane's prefix before it meets the true chain (one or two samples)
-//    instead of every dead slot of the window (the earlier form traced all M slots: rho x the chain's work
-//    at rho slots per sample). One ray per live lane per iteration; colours go to HBM, slot counts to LDS;
+//  * slots: the pixel's window of M slots (its last chain's slots per sample, spec_window) is cut into L
+//    ranges; each lane steps its state to its range's first slot and traces the range's slots back to
+//    back (the next slot's state is the one the current slot's camera draws leave), one ray per live lane
+//    per iteration; colours go to HBM, the slot counts to LDS;
 //  * walk: one lane per pixel follows the chain 0 -> j + n_j -> ... in LDS, a batch of chain samples at a
 //    time; the pixel's lanes gather their colours, form the mean terms with the plain kernel's table
 //    values and count each sample's rays (its slots, or max_depth when it ended on a scatter at
@@ -3165,8 +3160,6 @@ constexpr uint32_t kSpecLanes = 16;                    // lanes per sphere pixel
 constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per block without a plan
 constexpr uint32_t kSpecMaxPix = 32;                   // pixels per block at 8 lanes each
 constexpr uint32_t kSpecBatch = 512;                   // walk: chain samples gathered per block and batch
-constexpr uint8_t kSpecTaken = 0xffu;                  // slot mark: a lane is tracing it (slot counts are <= 17)
-constexpr uint32_t kSpecOvershoot = 24u;               // slots a lane may follow past the next lane's start
 static_assert(kSpecPix == kSpecPixPerBlock && kSpecMaxPix == kSpecMaxPixPerBlock, "runtime and kernel agree on the spec block");
 
 __host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth, uint32_t spp,
@@ -3250,7 +3243,6 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         rd[11] = 0u;
         rd[12] = 0u;
         rd[13] = pix;
-        rd[14] = (s.rho[q] != 0u && s.rho[q] < kSpecChainRho) ? 1u : 0u;   // follow the chain (mixed slot counts)
     } else if (!valid && l == 0u) {
         // no pixel (the grid's last block): an empty, finished record (every field is read by the rounds)
         for (uint32_t i = 0; i < 16u; ++i) rd[i] = 0u;
@@ -3269,22 +3261,12 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     while (__syncthreads_or(rd[7] == 0u)) {
         const bool live = rd[7] == 0u;
         const uint32_t js = rd[0], M = rd[1];
-        // ---- per pixel, two ways to cover the window (rd[14], from the pixel's last chain):
-        //  * follow (mixed slot counts, rho < kSpecChainRho): lane l starts at M l / L rounded down to even and
-        //    follows the chain, stopping at a slot another lane took (the chains have met) or kSpecOvershoot
-        //    slots past the next lane's start (they did not: the walker then starts a new round at the first
-        //    slot no lane traced). Even starts: a chain of 2-slot samples stays on one parity;
-        //  * every slot (samples of 2+ slots, which rarely change parity, so chains from different starts
-        //    seldom meet): lane l traces slots [M l / L, M (l + 1) / L) back to back.
-        // Marks: 0 not traced, kSpecTaken a lane is tracing it, else the slots its sample used.
-        const bool follow = rd[14] != 0u;
-        auto start_of = [&](uint32_t k) { return follow ? ((M * k / L) & ~1u) : M * k / L; };
-        for (uint32_t i = l; i < M; i += L) ln[i] = 0u;
-        const uint32_t j0 = start_of(l), jn = l + 1u < L ? start_of(l + 1u) : M;
-        // every slot: the lanes' ranges [start_of(l), start_of(l + 1)) tile [0, M) (empty ones idle); follow:
-        // one lane per distinct start (the first), lane 0 always — so slot 0 is always traced
-        const bool first_ok = live && j0 < M && (follow ? (l == 0u || start_of(l - 1u) < j0) : j0 < jn);
-        const uint32_t j_stop = follow ? (l + 1u < L ? min(M, jn + kSpecOvershoot) : M) : jn;
+        // ---- slots [js + j0, js + j1) of this lane, relative slot indices j: every slot of the window is traced
+        // (round 4 measured a chain-following alternative — lanes follow the chain from spread starts and stop
+        // where chains meet — bit-exact but slower: 2-slot samples rarely change parity, so chains from
+        // different starts seldom meet)
+        auto start_of = [&](uint32_t k) { return M * k / L; };
+        const uint32_t j0 = start_of(l), j1 = start_of(l + 1u);
         rng6 st = {rd[2], rd[3], rd[4], rd[5], rd[6], p.rng[5 * (size_t)p.npix + rd[13]] + 2u * (js + j0) * IQ_XORWOW_WEYL};
         xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, live ? 2u * j0 : 0u);
         lst[l * 5u] = st.v0;
@@ -3292,16 +3274,12 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         lst[l * 5u + 2u] = st.v2;
         lst[l * 5u + 3u] = st.v3;
         lst[l * 5u + 4u] = st.v4;
-        __syncthreads();                                 // the marks are clear before any lane takes a slot
-        if (first_ok) ln[j0] = kSpecTaken;
         uint32_t j = j0;
-        bool active = first_ok;
+        bool active = live && j0 < j1;
         ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         int depth = 0;
         rng6 base = st;
-        // a slot's sample starts here: its camera ray (two draws; the state they leave is slot j + 1's); its
-        // scatters draw two more each, so when it ends having used n slots the state is the one slot j + n
-        // starts from
+        // a slot's sample starts here: its camera ray, and the state its two draws leave (the next slot's)
         auto start_slot = [&]() {
             camera_ray<OPT>(p, px, py, st, ray);
             base = st;
@@ -3374,20 +3352,8 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                     cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
                     cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
                     res[j] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
-                    const uint32_t n = (uint32_t)depth + 1u + md_end;  // slots: 1 + its scatters
-                    ln[j] = (uint8_t)n;
-                    // follow the chain: the next sample starts at slot j + n from the state this one left.
-                    // A slot another lane has taken is on a chain that lane follows to the window's end
-                    // (or to a slot taken before it), so this lane's chain has merged into it and stops.
-                    if (follow) {
-                        j += n;
-                        if (j >= j_stop || *reinterpret_cast<volatile uint8_t*>(ln + j) != 0u) {
-                            active = false;
-                        } else {
-                            ln[j] = kSpecTaken;
-                            start_slot();
-                        }
-                    } else if (++j == j_stop) {
+                    ln[j] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
+                    if (++j == j1) {
                         active = false;
                     } else {
                         st = base;                   // slot j starts where slot j - 1's camera draws ended
@@ -3409,12 +3375,8 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             if (walker && live) {
                 uint32_t c = 0;
                 while (c < batch && k + c < p.spp && jw < M) {
-                    const uint32_t nj = ln[jw];
-                    // a chain slot no lane traced (a lane gave up before meeting another chain): the round ends
-                    // here and the next one starts a window at this slot, like a chain that left its window
-                    if (nj == 0u) break;
                     lp[c++] = (uint16_t)jw;
-                    jw += nj;
+                    jw += ln[jw];
                 }
                 lds_w[2 * g] = c;
             }
@@ -3447,12 +3409,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             k += cw;
             __syncthreads();
         }
-        if (walker && live && k == rd[11]) {
-            // no sample folded this round: impossible (slot 0 of a round is always traced); end the pixel with
-            // an error bit rather than loop
-            atomicOr(p.ovl_err, 8u);
-            rd[7] = 1u;
-        } else if (walker && live) {
+        if (walker && live) {
             rd[8] = __float_as_uint(ax);
             rd[9] = __float_as_uint(ay);
             rd[10] = __float_as_uint(az);
@@ -3492,7 +3449,6 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                 atomicAdd(s.run_count + 1, 1u);
                 const uint32_t rem = p.spp - k;
                 rd[1] = min(s.m_cap, max(16u, 3u * rem + 4u));
-                rd[14] = 0u;                  // later rounds trace every slot (no untraced slot can end them)
             }
         }
         if (rec && rounds == 0u) t_rec[2] = __builtin_amdgcn_s_memrealtime();

@@ -247,6 +247,13 @@ struct iqpt_ctx {
     uint32_t* d_skip = nullptr;         // per tile (2 words): pixels the plain kernel skips in hybrid launches —
                                         // the sphere pixels (the spec kernel's) and, with the sky kernel, the misses
     std::vector<uint64_t> h_specmask;   // per tile: its sphere pixels (build_pixel_split)
+    std::vector<uint32_t> h_chain_pix;  // the sphere pixels' storage indices (d_chain_pix on the host)
+    // hybrid selection: only sphere pixels whose last chain used >= hybrid_rho slots per sample (x 256) go to the
+    // spec kernel (0: all); chosen from the history once it arrives, applied at a join (plan + skip masks)
+    uint32_t hybrid_rho = 0;
+    bool hyb_sel = false;               // d_skip_sel and the plan hold a selection
+    uint32_t hyb_sel_n = 0;             // pixels selected
+    uint32_t* d_skip_sel = nullptr;     // per tile (2 words): the selection's pixels | misses (sky kernel on)
     hipEvent_t ev_pipe_end = nullptr;    // on `stream`, after the last pipelined launch's first kernel
     hipEvent_t ev_copy_cur = nullptr, ev_copy_alt = nullptr;   // on `stream3`, after the copy of d_bgra / d_bgra_alt
     bool copy_pend_cur = false, copy_pend_alt = false;
@@ -405,6 +412,9 @@ void free_split(iqpt_ctx* c) {
     c->n_chain_pix = c->n_fan_tiles = 0;
     if (c->d_skip) (void)hipFree(c->d_skip);
     c->d_skip = nullptr;
+    if (c->d_skip_sel) (void)hipFree(c->d_skip_sel);
+    c->d_skip_sel = nullptr;
+    c->hyb_sel = false;
     c->spec_rho_valid = false;           // a new pixel list: no chain history, no plan
     c->spec_plan_n = 0;
     c->spec_rho_pending = false;
@@ -491,6 +501,8 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
     }
     c->n_chain_pix = (uint32_t)chain_pix.size();
     c->n_fan_tiles = (uint32_t)fan_tiles.size();
+    c->h_chain_pix = chain_pix;
+    c->hyb_sel = false;
     // hybrid launches: the plain kernel skips the sphere pixels and (sky kernel on) the certain misses
     if (c->d_skip) (void)hipFree(c->d_skip);
     c->d_skip = nullptr;
@@ -518,17 +530,18 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
 // <= E. Each block holds one lane class (256 lanes), pixels sorted by work per lane, and the blocks run
 // heaviest per lane first, so the launch's longest block starts first and light blocks fill the tail.
 uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec& ks, int opt, const uint32_t* rho,
-                         uint32_t* h) {
+                         uint32_t* h, const std::vector<char>* sel = nullptr) {
     const uint32_t n = ks.n;
     std::vector<double> w(n);
     double total = 0.0, wmax = 0.0;
     for (uint32_t q = 0; q < n; ++q) {
+        if (sel && !(*sel)[q]) {          // hybrid selection: not the spec kernel's this time (no block)
+            w[q] = 0.0;
+            continue;
+        }
         const uint32_t r = rho[q] ? rho[q] : ks.rho0;
         const uint32_t m = iqpt::spec_window(r, p.spp, ks.m_cap, ks.margin_div);
-        // a pixel that follows chains (round 4, rho < kSpecChainRho) traces each slot of its chain once: about
-        // one ray per window slot; one that traces every slot pays the slots' mean length (rho) on each
-        w[q] = (rho[q] != 0u && rho[q] < iqpt::kSpecChainRho) ? (double)m
-                                                                : (double)m * (double)std::max<uint32_t>(r, 256u) / 256.0;
+        w[q] = (double)m * (double)std::max<uint32_t>(r, 256u) / 256.0;
         total += w[q];
         wmax = std::max(wmax, w[q]);
     }
@@ -542,7 +555,8 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     };
     auto lanes_at = [&](double e) {
         double sum = 0.0;
-        for (uint32_t q = 0; q < n; ++q) sum += (double)(8u << lsh_of(q, e));
+        for (uint32_t q = 0; q < n; ++q)
+            if (!sel || (*sel)[q]) sum += (double)(8u << lsh_of(q, e));
         return sum;
     };
     double e = total / cap;                      // several block-waves: balanced work per lane
@@ -567,22 +581,23 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     }
     // counting sort by (lane class, work per lane) descending
     constexpr uint32_t kB = 1024;
-    std::vector<uint32_t> key(n), cnt(4 * kB + 1, 0);
+    std::vector<uint32_t> key(n), cnt(4 * kB + 2, 0);
     for (uint32_t q = 0; q < n; ++q) {
         const double pe = w[q] / (double)(8u << lsh[q]);
         const uint32_t b = emax > 0.0 ? std::min<uint32_t>(kB - 1, (uint32_t)(pe / emax * (kB - 1))) : 0u;
-        key[q] = (3u - lsh[q]) * kB + (kB - 1 - b);       // ascending key: 64 lanes first, heaviest first
-        cnt[key[q] + 1]++;
+        key[q] = (sel && !(*sel)[q]) ? 4 * kB : (3u - lsh[q]) * kB + (kB - 1 - b);   // ascending key: 64 lanes first,
+        cnt[key[q] + 1]++;                                                            // heaviest first, unselected last
     }
-    for (uint32_t k = 0; k < 4 * kB; ++k) cnt[k + 1] += cnt[k];
+    for (uint32_t k = 0; k < 4 * kB + 1; ++k) cnt[k + 1] += cnt[k];
     for (uint32_t q = 0; q < n; ++q) h[cnt[key[q]]++] = q;
+    const uint32_t nsel = sel ? (uint32_t)std::count(sel->begin(), sel->end(), (char)1) : n;
     // blocks of one class, then ordered by their first (heaviest) pixel's work per lane
     struct blk { double e; uint32_t first, word; };
     std::vector<blk> blocks;
-    for (uint32_t i = 0; i < n;) {
+    for (uint32_t i = 0; i < nsel;) {
         const uint32_t k = lsh[h[i]], per = iqpt::kSpecMaxPixPerBlock >> k;
         uint32_t m = 0;
-        while (m < per && i + m < n && lsh[h[i + m]] == k) ++m;
+        while (m < per && i + m < nsel && lsh[h[i + m]] == k) ++m;
         blocks.push_back({w[h[i]] / (double)(8u << k), i, m | (k << 8)});
         i += m;
     }
@@ -1904,6 +1919,61 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         (void)hipGetLastError();
     }
     if (hybrid && !c->hyb_pend && (st = join_streams(c)) != IQPT_OK) return st;
+    if (hybrid && c->hybrid_rho != 0 && c->spec_plan_mode == 1 && c->spec_rho_pending && c->spec_n >= c->n_chain_pix &&
+        c->h_chain_pix.size() == c->n_chain_pix && hipEventQuery(c->ev_spec_rho) == hipSuccess) {
+        // the chain history of an earlier launch is here: only the sphere pixels whose chains used >= hybrid_rho
+        // slots per sample (the launch's longest) stay with the spec kernel. The plan and the plain kernel's skip
+        // masks change together, from a state where nothing reads them (joined and synchronised)
+        if ((st = join_streams(c)) != IQPT_OK) return st;
+        IQPT_HIP(hipStreamSynchronize(c->stream));
+        const uint32_t n = c->n_chain_pix;
+        std::vector<char> sel(n, 0);
+        uint32_t nsel = 0;
+        for (uint32_t q = 0; q < n; ++q) {
+            sel[q] = (c->h_spec_rho[q] == 0u || c->h_spec_rho[q] >= c->hybrid_rho) ? 1 : 0;
+            nsel += (uint32_t)sel[q];
+        }
+        iqpt::kspec probe;
+        std::memset(&probe, 0, sizeof probe);
+        probe.n = n;
+        probe.m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
+        probe.rho0 = c->spec_rho0;
+        probe.margin_div = c->spec_margin_div;
+        const uint32_t nb = spec_build_plan(c, p, probe, opt, c->h_spec_rho, c->h_spec_plan, &sel);
+        IQPT_HIP(hipMemcpy(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
+                           hipMemcpyHostToDevice));
+        c->spec_plan_n = n;
+        c->spec_plan_blocks = nb;
+        c->spec_plan_age = 0;
+        c->spec_rho_pending = false;
+        c->spec_plan_up = false;
+        const size_t nt = (size_t)c->cull_ntx * c->cull_nty;
+        std::vector<uint32_t> skip(2 * nt, 0u);
+        if (c->sky_active && c->h_miss.size() == nt)
+            for (size_t t = 0; t < nt; ++t) {
+                skip[2 * t] = (uint32_t)c->h_miss[t];
+                skip[2 * t + 1] = (uint32_t)(c->h_miss[t] >> 32);
+            }
+        for (uint32_t q = 0; q < n; ++q) {
+            if (!sel[q]) continue;
+            const uint32_t pix = c->h_chain_pix[q];
+            uint32_t col, row;
+            iqpt::tile_decode(pix, c->ncols, c->set.nrows, &col, &row);
+            const uint32_t tx = col / iqpt::kCullTile, ty = row / iqpt::kCullTile;
+            const uint32_t th = std::min(iqpt::kCullTile, c->set.nrows - ty * iqpt::kCullTile);
+            const uint32_t bit = pix - (ty * iqpt::kCullTile * c->ncols + tx * iqpt::kCullTile * th);
+            const size_t t = (size_t)ty * c->cull_ntx + tx;
+            skip[2 * t + bit / 32u] |= 1u << (bit % 32u);
+        }
+        if (!c->d_skip_sel && hipMalloc(&c->d_skip_sel, skip.size() * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            c->d_skip_sel = nullptr;
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "hybrid selection masks");
+        }
+        IQPT_HIP(hipMemcpy(c->d_skip_sel, skip.data(), skip.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+        c->hyb_sel = true;
+        c->hyb_sel_n = nsel;
+    }
     hipStream_t ls = c->stream;                       // the launch's stream
     if (ovl) {
         opt |= iqpt::kOptOverlap;
@@ -1994,7 +2064,24 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         std::memset(&ks2, 0, sizeof ks2);
         const uint32_t n = c->n_chain_pix;
         const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
-        if (n > 0 && (n > c->spec_n || m_cap > c->spec_mcap)) {
+        if (n > 0 && n <= c->spec_n && m_cap > c->spec_mcap) {
+            // a longer launch on the same pixel list: only the slot results grow (the history, the plan and a
+            // hybrid selection stay)
+            IQPT_HIP(hipStreamSynchronize(c->stream));
+            if (c->stream4) IQPT_HIP(hipStreamSynchronize(c->stream4));
+            if (c->d_spec_res) (void)hipFree(c->d_spec_res);
+            c->d_spec_res = nullptr;
+            c->spec_mcap = 0;
+            const size_t slots = (size_t)c->spec_n * m_cap;
+            if (slots * 16 > iqpt::kSplitResBudget ||
+                hipMalloc(&c->d_spec_res, slots * sizeof(float4_storage)) != hipSuccess) {
+                (void)hipGetLastError();
+                c->d_spec_res = nullptr;
+                return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec slot results");
+            }
+            c->spec_mcap = m_cap;
+        }
+        if (n > 0 && n > c->spec_n) {
             IQPT_HIP(hipStreamSynchronize(c->stream));
             if (c->stream4) IQPT_HIP(hipStreamSynchronize(c->stream4));
             for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_plan})
@@ -2008,6 +2095,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             c->spec_n = c->spec_mcap = 0;
             c->spec_plan_n = 0;
             c->spec_rho_pending = c->spec_plan_up = false;
+            c->hyb_sel = false;
             const size_t slots = (size_t)n * m_cap;
             if ((!c->ev_spec_rho && hipEventCreateWithFlags(&c->ev_spec_rho, hipEventDisableTiming) != hipSuccess) ||
                 (!c->ev_spec_plan && hipEventCreateWithFlags(&c->ev_spec_plan, hipEventDisableTiming) != hipSuccess) ||
@@ -2124,7 +2212,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // with sky_active): otherwise the plain path without the spec kernel
     if (hybrid && sky != c->sky_active) hybrid = false;
     const iqpt::kparams p_spec = p;
-    if (hybrid) p.miss = c->d_skip;
+    if (hybrid) p.miss = c->hyb_sel ? c->d_skip_sel : c->d_skip;
     if (ovl) {
         le = iqpt::launch_render(ls, p, grid, lds, stream_batches, opt);
         c->ovl_epoch += 1;
@@ -2145,11 +2233,19 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             }
             iqpt::kspec ks2;
             if ((st = spec_buffers(c->stream4, ks2)) != IQPT_OK) return st;
-            if ((st = spec_plan(c->stream4, ks2)) != IQPT_OK) return st;
+            if (c->hyb_sel && c->spec_plan_n == ks2.n) {
+                // the selection's plan (blocks over the selected pixels only)
+                ks2.order = c->d_spec_plan;
+                ks2.blocks = c->d_spec_plan + ks2.n;
+                ks2.nblocks = c->spec_plan_blocks;
+            } else if ((st = spec_plan(c->stream4, ks2)) != IQPT_OK) {
+                return st;
+            }
             iqpt::kparams ph = p_spec;
             ph.miss = nullptr;
             ph.ovl_err = c->d_ovl_err;
-            le = iqpt::launch_spec(c->stream4, ph, ks2, opt);
+            // (a selection may hold no pixel: the plain kernel has them all, nothing to launch)
+            if (!(c->hyb_sel && c->hyb_sel_n == 0)) le = iqpt::launch_spec(c->stream4, ph, ks2, opt);
             if (le == 0 && (st = spec_history(c->stream4, ks2)) != IQPT_OK) return st;
             IQPT_HIP(hipEventRecord(c->ev_spec4, c->stream4));
             c->hyb_pend = true;
@@ -2633,6 +2729,7 @@ int iqpt_debug_read_spec_plan(iqpt_ctx* c, uint32_t* order, uint32_t* blocks, ui
     int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
+    if (c->stream4) IQPT_HIP(hipStreamSynchronize(c->stream4));     // hybrid launches: the spec kernel's stream
     const uint32_t np = c->n_chain_pix;
     if (!c->spec_plan_n || c->spec_plan_n != np || np > cap || !c->d_spec_plan) return IQPT_OK;
     IQPT_HIP(hipMemcpy(order, c->d_spec_plan, (size_t)np * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -2677,12 +2774,23 @@ int iqpt_debug_set_sky(iqpt_ctx* c, int on) {
 }
 
 /* Internal (A/B, tests): hybrid launches — 1: overlapped plain launches send the sphere pixels
- * to the spec kernel on a stream of their own; 0 (the default until measured): off. */
-int iqpt_debug_set_hybrid(iqpt_ctx* c, int mode) {
+ * to the spec kernel on a stream of their own; 0: off. rho256: once the chain history is in, only the pixels
+ * whose last chain used >= rho256 / 256 slots per sample (0: all sphere pixels). */
+int iqpt_debug_set_hybrid(iqpt_ctx* c, int mode, uint32_t rho256) {
     if (!c || mode < 0 || mode > 1) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or mode not 0..1");
     int st = enter(c);
     if (st) return st;
     c->hybrid_mode = mode;
+    c->hybrid_rho = rho256;
+    c->hyb_sel = false;
+    return IQPT_OK;
+}
+
+/* Internal (tools): the sphere pixels of the current hybrid selection (0 before one) and of the split. */
+int iqpt_debug_hybrid_info(iqpt_ctx* c, uint32_t* selected, uint32_t* sphere_pixels) {
+    if (!c || !selected || !sphere_pixels) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    *selected = c->hyb_sel ? c->hyb_sel_n : 0u;
+    *sphere_pixels = c->n_chain_pix;
     return IQPT_OK;
 }
 
