@@ -94,6 +94,15 @@ def parse():
     ap.add_argument("--share-of", type=int, default=0,
                     help="rehearsal at N = 1: render rank 0's rows of an N-way C3 split (one GPU's share; "
                          "with --self-gather the per-step gather path too)")
+    ap.add_argument("--gather-ctas", type=int, default=None,
+                    help="A/B: RCCL blocks per frame gather (ncclConfig_t::maxCTAs; 0: RCCL's choice; "
+                         "default: the library's)")
+    ap.add_argument("--gather-prio", type=int, default=None, choices=[-1, 0, 1],
+                    help="A/B: the communicator stream's priority (0: the library default)")
+    ap.add_argument("--gather-skip", type=int, default=0, choices=[0, 1, 2, 3],
+                    help="measurement only (wrong frames): 1 leaves out the collective, 2 the root's assembly")
+    ap.add_argument("--no-kernel-timing", action="store_true",
+                    help="A/B: no timing events around launches (kernel times and the roofline read 0)")
     ap.add_argument("--self-gather", action="store_true",
                     help="test: run the per-step gather path at N = 1 (a one-rank process group)")
     ap.add_argument("--spec-cap", type=float, default=0.0,
@@ -458,6 +467,11 @@ def main():
         _lib.check(_lib.load().iqpt_debug_set_kernel_options(pt.handle, args.kernel_options),
                    "iqpt_debug_set_kernel_options")
     pt.set_overlap(_lib.OVERLAP_AUTO if args.overlap == "auto" else _lib.OVERLAP_OFF)
+    if args.no_kernel_timing:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_timing.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_timing(pt._h, 0), "iqpt_debug_set_timing")
     if args.certain == "off":
         import ctypes as C
         lb = _lib.load()
@@ -498,6 +512,13 @@ def main():
     if lib_gather:
         uid = [iqpt.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
+        if args.gather_ctas is not None or args.gather_prio is not None or args.gather_skip:
+            import ctypes as C
+            lb = _lib.load()
+            lb.iqpt_debug_set_gather.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int]
+            _lib.check(lb.iqpt_debug_set_gather(pt._h, 2 if args.gather_ctas is None else args.gather_ctas,
+                                                0 if args.gather_prio is None else args.gather_prio,
+                                                args.gather_skip), "iqpt_debug_set_gather")
         pt.comm_init(rank, world, uid[0])
     frame_dev = (torch.zeros((cfg.width * cfg.height, words), dtype=dtype, device="cuda")
                  if lib_gather and rank == 0 else None)

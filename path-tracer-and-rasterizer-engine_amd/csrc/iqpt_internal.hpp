@@ -207,6 +207,7 @@ struct kspec {
                                      // s_memrealtime at start, after round 0's slots and walk, at the end
                                      // (| rounds << 48)
 };
+constexpr int kGatherCtas = 2;              // RCCL blocks per frame gather (iqpt_debug_set_gather)
 constexpr uint32_t kSpecReplan = 64;        // launches between two spec plans (the history read behind them)
 constexpr uint32_t kSpecPixPerBlock = 16;   // sphere pixels per iqpt_spec_kernel block without a plan (16 lanes each)
 constexpr uint32_t kSpecMaxPixPerBlock = 32;   // a plan's blocks: 256 / (8, 16, 32 or 64) pixels
@@ -392,6 +393,10 @@ int launch_sky(void* stream, const kparams& p, const uint32_t* tiles, uint32_t n
 bool fan_variant_exists(int opt);
 uint32_t fan_lds(const kparams& p);
 int launch_fan(void* stream, const kparams& p, uint32_t ntiles, int opt);
+// Events (hipEvent_t, either may be null) recorded by the dispatch of the next render / spec / fan / sky
+// kernel this thread launches (hipExtLaunchKernel) rather than by marker packets of their own; a launch
+// function that launches nothing leaves them bound — the caller unbinds (nullptr, nullptr).
+void bind_launch_events(void* start, void* stop);
 constexpr int kRenderBlock = 256;
 constexpr uint32_t kQueueChunk = 64;
 const char* render_kernel_name();

@@ -26,6 +26,7 @@
 //  * Every floating-point operation follows the reference's order with contraction off
 //    (-ffp-contract=off) and the shared transcendentals of iq_fp.h; every shortcut below is exact
 //    (argued where it is taken). Results are bit-identical to the CPU oracle.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 // the transcendentals of iq_fp.h use the short exact division forms in this TU's GPU pass
@@ -3586,9 +3587,24 @@ __host__ __device__ inline uint32_t chain_lds_bytes(uint32_t ntri_pairs, uint32_
            (uint32_t)(max_depth > 1 ? max_depth : 1) * kChainBlock * 4u;
 }
 
+// Events bound to the next kernel launch (bind_launch_events): recorded by the dispatch itself
+// (hipExtLaunchKernel) instead of as marker packets of their own between two kernels on the stream.
+namespace {
+thread_local hipEvent_t tl_ev_start = nullptr, tl_ev_stop = nullptr;
+template <typename F, typename... Args>
+void dispatch(F kernel, const dim3& grid, const dim3& block, uint32_t lds, hipStream_t stream, Args... args) {
+    const hipEvent_t a = tl_ev_start, z = tl_ev_stop;
+    tl_ev_start = tl_ev_stop = nullptr;
+    if (a || z)
+        hipExtLaunchKernelGGL(kernel, grid, block, lds, stream, a, z, 0u, args...);
+    else
+        hipLaunchKernelGGL(kernel, grid, block, lds, stream, args...);
+}
+}  // namespace
+
 template <int MAXD, bool STREAM, int OPT>
 int launch_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_render_kernel<MAXD, STREAM, OPT>), dim3(grid), dim3(kRenderBlock), lds, stream, p);
+    dispatch(iqpt_render_kernel<MAXD, STREAM, OPT>, dim3(grid), dim3(kRenderBlock), lds, stream, p);
     return (int)hipGetLastError();
 }
 template <int MAXD, bool STREAM, int OPT>
@@ -3665,6 +3681,11 @@ const variant* find_variant(int max_depth, bool stream, int opt) {
 }
 
 }  // namespace
+
+void bind_launch_events(void* start, void* stop) {
+    tl_ev_start = (hipEvent_t)start;
+    tl_ev_stop = (hipEvent_t)stop;
+}
 
 int launch_rng_init(void* stream, uint32_t width, uint32_t x0, uint32_t ncols, uint32_t y0, uint32_t ystep,
                     uint32_t nrows, uint64_t seed, const uint32_t* tables, uint32_t* rng) {
@@ -3814,7 +3835,7 @@ const chain_variant* find_chain(int max_depth, int opt, uint32_t lanes) {
 namespace {
 template <int OPT>
 int fan_launch_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_fan_kernel<OPT>), dim3(grid), dim3(kFanBlock), lds, stream, p);
+    dispatch(iqpt_fan_kernel<OPT>, dim3(grid), dim3(kFanBlock), lds, stream, p);
     return (int)hipGetLastError();
 }
 struct fan_variant {
@@ -3845,8 +3866,8 @@ bool fan_variant_exists(int opt) { return find_fan(opt) != nullptr; }
 namespace {
 template <int OPT>
 int sky_launch_t(hipStream_t stream, const kparams& p, const uint32_t* tiles, uint32_t ntiles, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_sky_kernel<OPT>), dim3((ntiles + kSkyBlock / 64u - 1u) / (kSkyBlock / 64u)),
-                       dim3(kSkyBlock), lds, stream, p, tiles, ntiles);
+    dispatch(iqpt_sky_kernel<OPT>, dim3((ntiles + kSkyBlock / 64u - 1u) / (kSkyBlock / 64u)), dim3(kSkyBlock), lds,
+             stream, p, tiles, ntiles);
     return (int)hipGetLastError();
 }
 struct sky_variant {
@@ -3890,8 +3911,8 @@ int launch_fan(void* stream, const kparams& p, uint32_t ntiles, int opt) {
 namespace {
 template <int MAXD, int OPT>
 int spec_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_spec_kernel<MAXD, OPT>), dim3(s.blocks ? s.nblocks : (s.n + kSpecPix - 1u) / kSpecPix),
-                       dim3(kSpecBlock), lds, stream, p, s);
+    dispatch(iqpt_spec_kernel<MAXD, OPT>, dim3(s.blocks ? s.nblocks : (s.n + kSpecPix - 1u) / kSpecPix),
+             dim3(kSpecBlock), lds, stream, p, s);
     return (int)hipGetLastError();
 }
 template <int MAXD, int OPT>

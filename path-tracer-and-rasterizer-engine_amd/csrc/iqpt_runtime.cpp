@@ -254,7 +254,11 @@ struct iqpt_ctx {
     bool hyb_sel = false;               // d_skip_sel and the plan hold a selection
     uint32_t hyb_sel_n = 0;             // pixels selected
     uint32_t* d_skip_sel = nullptr;     // per tile (2 words): the selection's pixels | misses (sky kernel on)
-    hipEvent_t ev_pipe_end = nullptr;    // on `stream`, after the last pipelined launch's first kernel
+    hipEvent_t ev_pipe_end = nullptr;    // on `stream`, recorded by a copy behind a pipelined launch
+    // the events the last pipelined launch's kernels recorded at their ends on `stream` / `stream2` (timing
+    // events bound to the dispatches), or null: a copy behind the launch waits for them instead of recording
+    // markers of its own
+    hipEvent_t end1 = nullptr, end2 = nullptr;
     hipEvent_t ev_copy_cur = nullptr, ev_copy_alt = nullptr;   // on `stream3`, after the copy of d_bgra / d_bgra_alt
     bool copy_pend_cur = false, copy_pend_alt = false;
     unsigned long long* d_spec_tl = nullptr;   // iqpt_debug_spec_timeline: per spec block timestamps
@@ -313,6 +317,13 @@ struct iqpt_ctx {
     uint32_t* d_grecv = nullptr;         // root: comm_world x comm_stride x 4 words
     uint32_t* d_gframe = nullptr;        // root: the assembled W x H x 4 words of iqpt_gather_read
     std::vector<std::pair<hipEvent_t, hipEvent_t>> gtimed;   // per gather: cstream events around it (iqpt_comm_time)
+    // the gather's share of the CUs it runs beside (iqpt_debug_set_gather, before iqpt_comm_init): RCCL's
+    // blocks per collective (ncclConfig_t::maxCTAs; 0: RCCL's choice) and cstream's priority (-1 lowest,
+    // 0 the default, 1 highest)
+    int gather_ctas = iqpt::kGatherCtas;
+    int gather_prio = 0;
+    int gather_skip = 0;                 // measurement only: 1 skips the collective, 2 the root's assembly
+    bool timing_on = true;               // the launches' timing events (iqpt_debug_set_timing)
 };
 
 namespace {
@@ -1133,6 +1144,7 @@ int check_dev_err(iqpt_ctx* c) {
 }
 
 hipEvent_t take_event(iqpt_ctx* c) {
+    if (!c->timing_on) return nullptr;
     if (!c->event_pool.empty()) {
         hipEvent_t e = c->event_pool.back();
         c->event_pool.pop_back();
@@ -1149,6 +1161,7 @@ hipEvent_t take_event(iqpt_ctx* c) {
 struct rccl_api {
     ncclResult_t (*get_unique_id)(ncclUniqueId*) = nullptr;
     ncclResult_t (*comm_init_rank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_init_config)(ncclComm_t*, int, ncclUniqueId, int, ncclConfig_t*) = nullptr;   // optional
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*gather)(const void*, void*, size_t, ncclDataType_t, int, ncclComm_t, hipStream_t) = nullptr;
     const char* (*error_string)(ncclResult_t) = nullptr;
@@ -1169,6 +1182,7 @@ const rccl_api& rccl() {
         }
         api.get_unique_id = reinterpret_cast<decltype(api.get_unique_id)>(dlsym(h, "ncclGetUniqueId"));
         api.comm_init_rank = reinterpret_cast<decltype(api.comm_init_rank)>(dlsym(h, "ncclCommInitRank"));
+        api.comm_init_config = reinterpret_cast<decltype(api.comm_init_config)>(dlsym(h, "ncclCommInitRankConfig"));
         api.comm_destroy = reinterpret_cast<decltype(api.comm_destroy)>(dlsym(h, "ncclCommDestroy"));
         api.gather = reinterpret_cast<decltype(api.gather)>(dlsym(h, "ncclGather"));
         api.error_string = reinterpret_cast<decltype(api.error_string)>(dlsym(h, "ncclGetErrorString"));
@@ -2018,7 +2032,15 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
     if (!ovl && !chain && !fan && !spec) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
     hipEvent_t e0 = take_event(c), e1 = take_event(c), e1b = nullptr;
-    if (e0) (void)hipEventRecord(e0, ls);
+    // pipelined spec launches: the timing events are recorded by the spec and fan kernels' dispatches (no
+    // marker packets between consecutive kernels on the two streams: -0.012 ms per step at N = 8, -0.04 with
+    // a copy and gather every step, r04 run 12)
+    const bool bind_spec = spec && c->specfan_mode == 0 && c->n_chain_pix > 0;
+    // overlapped launches: recorded by the launch's first kernel on `ls` (the sky kernel or the plain kernel)
+    // and its last (the plain kernel)
+    const bool bind_ovl = ovl && !hybrid && tune_slot < 0;
+    bool e0_bound = false, e1_bound = false;
+    if (e0 && !bind_spec && !bind_ovl) (void)hipEventRecord(e0, ls);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
     int le = 0;
     // pipelined launches (spec, FAN): the frame buffer this launch writes (the other one once copies are
@@ -2044,15 +2066,19 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     };
     // ... and its end: no join; the copy stream and every other entry point wait for both streams
     auto pipe_end = [&](int kind) -> int {
-        IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
         if (!c->ev_pipe_end && hipEventCreateWithFlags(&c->ev_pipe_end, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
             return iqpt::fail(IQPT_ERR_HIP, "pipelined launch events");
         }
-        IQPT_HIP(hipEventRecord(c->ev_pipe_end, c->stream));
         if (int s = ensure_copy_stream(c)) return s;
-        e1b = take_event(c);
-        if (e1b) (void)hipEventRecord(e1b, c->stream2);
+        // the kernels' own end events (bound timing events) where there are some; otherwise a copy records
+        // markers on both streams when it is asked for
+        c->end1 = e1_bound ? e1 : nullptr;
+        c->end2 = e1b;
+        if (!e1b) {
+            e1b = take_event(c);
+            if (e1b) (void)hipEventRecord(e1b, c->stream2);
+        }
         c->s2_pending = true;
         c->pipe = le == 0;
         c->pipe_kind = kind;
@@ -2203,7 +2229,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
         const hipStream_t ss = ovl ? ls : c->stream;
         if (c->sky_last && c->sky_last != ss) IQPT_HIP(hipStreamWaitEvent(ss, c->ev_sky, 0));
+        const bool b0 = bind_ovl && e0 && p.spp > 0;
+        if (b0) iqpt::bind_launch_events(e0, nullptr);
         le = iqpt::launch_sky(ss, p, c->d_sky_tiles, c->n_sky_tiles, opt);
+        iqpt::bind_launch_events(nullptr, nullptr);
+        e0_bound = b0 && le == 0;
         if (le != 0) return iqpt::hip_fail((hipError_t)le, "sky kernel launch");
         IQPT_HIP(hipEventRecord(c->ev_sky, ss));
         c->sky_last = ss;
@@ -2214,7 +2244,14 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     const iqpt::kparams p_spec = p;
     if (hybrid) p.miss = c->hyb_sel ? c->d_skip_sel : c->d_skip;
     if (ovl) {
+        if (bind_ovl) iqpt::bind_launch_events(e0_bound ? nullptr : e0, e1);
         le = iqpt::launch_render(ls, p, grid, lds, stream_batches, opt);
+        iqpt::bind_launch_events(nullptr, nullptr);
+        if (bind_ovl) {
+            if (le != 0 && e0 && !e0_bound) (void)hipEventRecord(e0, ls);   // (not read: the launch failed)
+            e0_bound = true;
+            e1_bound = le == 0 && e1 != nullptr;
+        }
         c->ovl_epoch += 1;
         c->next_on_main = !c->next_on_main;
         if (le != 0) c->ovl_zero = true;     // a failed launch breaks the chain's counts: restart it
@@ -2367,8 +2404,23 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             if (n > 0) le = iqpt::launch_spec(c->stream, p, ks2, opt);
             if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream, pf, c->n_fan_tiles, opt);
         } else {
-            if (n > 0) le = iqpt::launch_spec(c->stream, p, ks2, opt);
-            if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream2, pf, c->n_fan_tiles, opt);
+            if (n > 0) {
+                iqpt::bind_launch_events(e0, e1);
+                le = iqpt::launch_spec(c->stream, p, ks2, opt);
+                iqpt::bind_launch_events(nullptr, nullptr);
+                e1_bound = le == 0 && e1 != nullptr;
+                if (le != 0 && e0) (void)hipEventRecord(e0, c->stream);   // (unrecorded events are not read)
+            }
+            if (le == 0 && c->n_fan_tiles > 0) {
+                e1b = take_event(c);
+                iqpt::bind_launch_events(nullptr, e1b);
+                le = iqpt::launch_fan(c->stream2, pf, c->n_fan_tiles, opt);
+                iqpt::bind_launch_events(nullptr, nullptr);
+                if (le != 0 && e1b) {
+                    c->event_pool.push_back(e1b);
+                    e1b = nullptr;
+                }
+            }
             if ((st = pipe_end(1)) != IQPT_OK) return st;
         }
         if (le == 0 && (st = spec_history(c->stream, ks2)) != IQPT_OK) return st;
@@ -2407,7 +2459,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // hybrid launches: a frame copy joins every stream (the spec kernel writes the frame on stream4)
     c->last_ovl = ovl && !hybrid;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
-    if (e1) (void)hipEventRecord(e1, ls);
+    if (e1 && !e1_bound) (void)hipEventRecord(e1, ls);
     if (e0 && e1) c->timed.push_back({e0, e1, e1b});
     if (le != 0) return iqpt::hip_fail((hipError_t)le, "render kernel launch");
     c->last_opt = opt;
@@ -2636,6 +2688,7 @@ int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
     int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
+    c->end1 = c->end2 = nullptr;        // (the events go back to the pool)
     double sum = 0.0, span = 0.0;
     for (auto& tl : c->timed) {
         float ms = 0.0f, end = 0.0f;
@@ -2786,6 +2839,27 @@ int iqpt_debug_set_hybrid(iqpt_ctx* c, int mode, uint32_t rho256) {
     return IQPT_OK;
 }
 
+/* Internal (A/B): the gather's footprint beside the render kernels, for the next iqpt_comm_init — RCCL's
+ * blocks per collective (ncclConfig_t::maxCTAs; 0: RCCL's own choice) and the communicator stream's priority
+ * (-1 the lowest; 0 HIP's default, the default; 1 the highest); skip (measurement only, wrong frames): 1 leaves
+ * out the collective, 2 the root's assembly. */
+int iqpt_debug_set_gather(iqpt_ctx* c, int ctas, int prio, int skip) {
+    if (!c || ctas < 0 || ctas > 64 || prio < -1 || prio > 1 || skip < 0 || skip > 3)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL, ctas not 0..64, prio not -1..1 or skip not 0..3");
+    c->gather_ctas = ctas;
+    c->gather_prio = prio;
+    c->gather_skip = skip;
+    return IQPT_OK;
+}
+
+/* Internal (A/B): the timing events around launches and gathers (iqpt_kernel_time, iqpt_comm_time) — 1 on (the
+ * default), 0 off: those then report nothing. Each event is a packet on its stream between two kernels. */
+int iqpt_debug_set_timing(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->timing_on = on != 0;
+    return IQPT_OK;
+}
+
 /* Internal (tools): the sphere pixels of the current hybrid selection (0 before one) and of the split. */
 int iqpt_debug_hybrid_info(iqpt_ctx* c, uint32_t* selected, uint32_t* sphere_pixels) {
     if (!c || !selected || !sphere_pixels) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
@@ -2914,8 +2988,10 @@ int copy_frame_async(iqpt_ctx* c, uint32_t* dst, hipEvent_t wait, hipStream_t* u
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "second frame buffer for pipelined copies");
         }
         if ((st = ensure_copy_stream(c)) != IQPT_OK) return st;
-        IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_pipe_end, 0));
-        IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_s2, 0));
+        if (!c->end1) IQPT_HIP(hipEventRecord(c->ev_pipe_end, c->stream));
+        if (!c->end2) IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
+        IQPT_HIP(hipStreamWaitEvent(c->stream3, c->end1 ? c->end1 : c->ev_pipe_end, 0));
+        IQPT_HIP(hipStreamWaitEvent(c->stream3, c->end2 ? c->end2 : c->ev_s2, 0));
         if (wait) IQPT_HIP(hipStreamWaitEvent(c->stream3, wait, 0));
         const int le = iqpt::launch_relayout(c->stream3, c->d_bgra, dst, c->ncols, c->set.nrows, 1, 1, true);
         if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
@@ -3000,7 +3076,15 @@ int iqpt_comm_init(iqpt_ctx* c, int rank, int world, const void* id, size_t byte
     IQPT_HIP(hipStreamSynchronize(c->stream));
     free_comm(c);
     const uint64_t stride = (uint64_t)((c->height + split - 1u) / split) * c->width;
-    if (hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) != hipSuccess ||
+    // the communicator's stream (its priority: iqpt_debug_set_gather; the lowest measured slower, r04 run 9:
+    // the gather then finishes later and the double-buffered copies wait for it)
+    int prio_least = 0, prio_greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) {
+        (void)hipGetLastError();
+        prio_least = prio_greatest = 0;
+    }
+    const int prio = c->gather_prio < 0 ? prio_least : (c->gather_prio > 0 ? prio_greatest : 0);
+    if (hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gdone[0], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gdone[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gcopy, hipEventDisableTiming) != hipSuccess ||
@@ -3017,7 +3101,17 @@ int iqpt_comm_init(iqpt_ctx* c, int rank, int world, const void* id, size_t byte
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     ncclComm_t comm = nullptr;
-    const ncclResult_t r = rccl().comm_init_rank(&comm, world, u, rank);    // collective over the ranks
+    // collective over the ranks; a frame of a few MB per rank needs few of RCCL's blocks, and every block
+    // it runs takes a CU slot from the render kernels beside it (ncclConfig_t::maxCTAs)
+    ncclResult_t r;
+    if (c->gather_ctas > 0 && rccl().comm_init_config) {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.minCTAs = 1;
+        cfg.maxCTAs = c->gather_ctas;
+        r = rccl().comm_init_config(&comm, world, u, rank, &cfg);
+    } else {
+        r = rccl().comm_init_rank(&comm, world, u, rank);
+    }
     if (r != ncclSuccess) {
         free_comm(c);
         return rccl_fail(r, "ncclCommInitRank");
@@ -3048,10 +3142,13 @@ int gather_enqueue(iqpt_ctx* c, uint32_t b, hipStream_t from, int root, uint32_t
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "gather receive buffer");
         }
     }
-    const ncclResult_t r = rccl().gather(c->d_gsend[b], is_root ? c->d_grecv : nullptr, (size_t)c->comm_stride * words,
-                                         ncclUint32, root, static_cast<ncclComm_t>(c->comm), c->cstream);
-    if (r != ncclSuccess) return rccl_fail(r, "ncclGather");
-    if (is_root) {
+    if (!(c->gather_skip & 1)) {
+        const ncclResult_t r = rccl().gather(c->d_gsend[b], is_root ? c->d_grecv : nullptr,
+                                             (size_t)c->comm_stride * words, ncclUint32, root,
+                                             static_cast<ncclComm_t>(c->comm), c->cstream);
+        if (r != ncclSuccess) return rccl_fail(r, "ncclGather");
+    }
+    if (is_root && !(c->gather_skip & 2)) {
         const int le = iqpt::launch_assemble_rows(c->cstream, c->d_grecv, dst, c->width, c->height,
                                                   (uint32_t)c->comm_world, c->set.ystep,
                                                   c->set.y0 - (uint32_t)c->comm_rank, c->comm_stride, words);
