@@ -101,6 +101,8 @@ def parse():
                     help="A/B: the communicator stream's priority (0: the library default)")
     ap.add_argument("--gather-skip", type=int, default=0, choices=[0, 1, 2, 3],
                     help="measurement only (wrong frames): 1 leaves out the collective, 2 the root's assembly")
+    ap.add_argument("--spec-even", choices=["on", "off"], default=None,
+                    help="A/B: the spec kernel traces only the even slots of 2-slot pixels (default: the library's)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="A/B: no timing events around launches (kernel times and the roofline read 0)")
     ap.add_argument("--self-gather", action="store_true",
@@ -467,6 +469,11 @@ def main():
         _lib.check(_lib.load().iqpt_debug_set_kernel_options(pt.handle, args.kernel_options),
                    "iqpt_debug_set_kernel_options")
     pt.set_overlap(_lib.OVERLAP_AUTO if args.overlap == "auto" else _lib.OVERLAP_OFF)
+    if args.spec_even is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec_even.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_spec_even(pt._h, 1 if args.spec_even == "on" else 0), "iqpt_debug_set_spec_even")
     if args.no_kernel_timing:
         import ctypes as C
         lb = _lib.load()
@@ -657,7 +664,8 @@ def main():
             # the host's time per step inside iqpt_render / iqpt_gather_frame_async: a host slower than the GPU
             # leaves the GPU idle between launches
             "host_render_ms": round(host["render"] / args.steps * 1e3, 4),
-            "host_gather_ms": round(host["gather"] / args.steps * 1e3, 4)}
+            "host_gather_ms": round(host["gather"] / args.steps * 1e3, 4),
+            "bitexact_frac_vs_oracle": verify["bitexact_frac"] if verify else None}
     per_rank = [None] * world if world > 1 else [mine]
     if world > 1:
         dist.all_gather_object(per_rank, mine)
@@ -710,6 +718,7 @@ def main():
                                          else " (gloo via host, rehearsal)")),
                        "split": args.split, "overlap": args.overlap, "certain": args.certain, "sky": args.sky,
                        "hybrid": args.hybrid, **({"hybrid_rho": args.hybrid_rho} if args.hybrid_rho else {}),
+                       **({"spec_even": args.spec_even} if args.spec_even else {}),
                        "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
                        **({"spec_cap": args.spec_cap} if args.spec_cap else {})},

@@ -3244,6 +3244,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         rd[11] = 0u;
         rd[12] = 0u;
         rd[13] = pix;
+        rd[14] = (s.even2 && s.rho[q] == 512u) ? 1u : 0u;   // its last chain's samples took two slots each
     } else if (!valid && l == 0u) {
         // no pixel (the grid's last block): an empty, finished record (every field is read by the rounds)
         for (uint32_t i = 0; i < 16u; ++i) rd[i] = 0u;
@@ -3262,11 +3263,14 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     while (__syncthreads_or(rd[7] == 0u)) {
         const bool live = rd[7] == 0u;
         const uint32_t js = rd[0], M = rd[1];
-        // ---- slots [js + j0, js + j1) of this lane, relative slot indices j: every slot of the window is traced
-        // (round 4 measured a chain-following alternative — lanes follow the chain from spread starts and stop
-        // where chains meet — bit-exact but slower: 2-slot samples rarely change parity, so chains from
-        // different starts seldom meet)
-        auto start_of = [&](uint32_t k) { return M * k / L; };
+        // ---- slots [js + j0, js + j1) of this lane, relative slot indices j. Every slot of the window is
+        // traced, or (rd[14], round 0 of a pixel whose last chain took exactly two slots per sample) only
+        // the even ones: a chain of 2-slot samples from slot 0 visits even slots alone, and the first odd
+        // slot it lands on (a sample of 1 or 3 slots) ends the round there; the next round traces every
+        // slot from it
+        const uint32_t step = rd[14] != 0u ? 2u : 1u;
+        const uint32_t ME = (M + step - 1u) / step;      // slots of the window this round traces
+        auto start_of = [&](uint32_t k) { return step * (ME * k / L); };
         const uint32_t j0 = start_of(l), j1 = start_of(l + 1u);
         rng6 st = {rd[2], rd[3], rd[4], rd[5], rd[6], p.rng[5 * (size_t)p.npix + rd[13]] + 2u * (js + j0) * IQ_XORWOW_WEYL};
         xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, live ? 2u * j0 : 0u);
@@ -3354,10 +3358,16 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                     cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
                     res[j] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
                     ln[j] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
-                    if (++j == j1) {
+                    if (step == 2u && j + 1u < M) ln[j + 1u] = 0u;       // untraced: ends the walk there
+                    j += step;
+                    if (j >= j1) {
                         active = false;
                     } else {
                         st = base;                   // slot j starts where slot j - 1's camera draws ended
+                        if (step == 2u) {            // ... two draws after slot j - 1's start
+                            (void)xorwow_next(st);
+                            (void)xorwow_next(st);
+                        }
                         start_slot();
                     }
                 }
@@ -3376,8 +3386,10 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             if (walker && live) {
                 uint32_t c = 0;
                 while (c < batch && k + c < p.spp && jw < M) {
+                    const uint32_t nj = ln[jw];
+                    if (nj == 0u) break;                 // an untraced (odd) slot: the round ends here
                     lp[c++] = (uint16_t)jw;
-                    jw += ln[jw];
+                    jw += nj;
                 }
                 lds_w[2 * g] = c;
             }
@@ -3450,6 +3462,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                 atomicAdd(s.run_count + 1, 1u);
                 const uint32_t rem = p.spp - k;
                 rd[1] = min(s.m_cap, max(16u, 3u * rem + 4u));
+                rd[14] = 0u;                           // later rounds trace every slot
             }
         }
         if (rec && rounds == 0u) t_rec[2] = __builtin_amdgcn_s_memrealtime();

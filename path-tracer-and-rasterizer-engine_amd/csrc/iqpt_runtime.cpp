@@ -324,6 +324,7 @@ struct iqpt_ctx {
     int gather_prio = 0;
     int gather_skip = 0;                 // measurement only: 1 skips the collective, 2 the root's assembly
     bool timing_on = true;               // the launches' timing events (iqpt_debug_set_timing)
+    bool spec_even = false;              // kspec::even2 (iqpt_debug_set_spec_even)
 };
 
 namespace {
@@ -552,7 +553,10 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
         }
         const uint32_t r = rho[q] ? rho[q] : ks.rho0;
         const uint32_t m = iqpt::spec_window(r, p.spp, ks.m_cap, ks.margin_div);
-        w[q] = (double)m * (double)std::max<uint32_t>(r, 256u) / 256.0;
+        // slots traced: the window's, or its even ones for a pixel whose last chain took two slots per
+        // sample (the kernel's round 0)
+        const uint32_t traced = (ks.even2 && r == 512u) ? (m + 1u) / 2u : m;
+        w[q] = (double)traced * (double)std::max<uint32_t>(r, 256u) / 256.0;
         total += w[q];
         wmax = std::max(wmax, w[q]);
     }
@@ -1953,6 +1957,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         probe.m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
         probe.rho0 = c->spec_rho0;
         probe.margin_div = c->spec_margin_div;
+        probe.even2 = c->spec_even ? 1u : 0u;
         const uint32_t nb = spec_build_plan(c, p, probe, opt, c->h_spec_rho, c->h_spec_plan, &sel);
         IQPT_HIP(hipMemcpy(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
                            hipMemcpyHostToDevice));
@@ -2145,6 +2150,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.m_cap = m_cap;
         ks2.rho0 = c->spec_rho0;
         ks2.margin_div = c->spec_margin_div;
+        ks2.even2 = c->spec_even ? 1u : 0u;
         ks2.pix = c->d_chain_pix;
         ks2.m = c->d_spec;
         ks2.rho = c->d_spec + n;
@@ -2849,6 +2855,14 @@ int iqpt_debug_set_gather(iqpt_ctx* c, int ctas, int prio, int skip) {
     c->gather_ctas = ctas;
     c->gather_prio = prio;
     c->gather_skip = skip;
+    return IQPT_OK;
+}
+
+/* Internal (A/B, tests): the spec kernel traces only the even slots of a pixel whose last chain took two
+ * slots per sample (1) or every slot of every window (0). Same bits either way. */
+int iqpt_debug_set_spec_even(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->spec_even = on != 0;
     return IQPT_OK;
 }
 

@@ -1,7 +1,7 @@
 """Slot-parallel sphere pixels (IQPT_SPLIT_SPEC) vs the CPU oracle, bit for bit.
 
 Only the pixels whose own camera-ray bundle may reach a sphere can take more than two draws per sample.
-Lanes follow the chain from starting slots spread over a window (slot j: the sample that starts 2j draws into the pixel's XORWOW stream) and stop where they meet a slot another lane took; the slots are evaluated
+The slots of a window (slot j: the sample that starts 2j draws into the pixel's XORWOW stream) are evaluated
 in parallel, the chain 0 -> j + n_j -> ... is walked afterwards and folded in sample order, and a chain
 that leaves its window continues in a new window (another round of the same block); every other pixel
 runs in the fan kernel, in the same grid (iqpt_specfan_kernel) or beside it. The result must be the reference's sequential chain (path_tracer.cu:330-366, random.cu:66-107):
