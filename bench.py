@@ -344,16 +344,16 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode: str, s
             out["executed_work"] = {"achieved": round(ex, 4), "frac": round(ex / FP32_PEAK_TFLOPS, 5),
                                     "flops_per_ray": work["flops_per_ray"], "per_ray": work.get("per_ray"),
                                     "source": str(Path(work_path).resolve().relative_to(REPO))}
-    # the counted rays include the camera rays of certain-hit and certain-miss (sky) pixels, resolved by a
-    # per-pixel proof instead of per-ray tests: the rate of rays that ran a per-ray closest-hit test
-    if t > 0:
-        out["traced_rays_per_launch"] = round(rays_per_launch * (1.0 - certain_ray_frac))
-        out["traced_rays_per_s"] = round(rays_per_launch * (1.0 - certain_ray_frac) / t, 1)
     else:
         # the brute-force price exceeds the peak: the kernel skips that work, so it is no roofline
         out.update(achieved=None, frac=None, flops_per_ray=None,
                    work_basis="none: run tools/work_counters.py for the executed-work price",
                    reference_equivalent={"achieved": round(ref_tflops, 2), "flops_per_ray": f_ray})
+    # the counted rays include the camera rays of certain-hit and certain-miss (sky) pixels, resolved by a
+    # per-pixel proof instead of per-ray tests: the rate of rays that ran a per-ray closest-hit test
+    if t > 0:
+        out["traced_rays_per_launch"] = round(rays_per_launch * (1.0 - certain_ray_frac))
+        out["traced_rays_per_s"] = round(rays_per_launch * (1.0 - certain_ray_frac) / t, 1)
     if t > 0:
         alg = BYTES_PER_PIXEL_LAUNCH * npix_owned
         out["hbm"] = {"achieved": round(alg / t / 1e9, 2), "peak": HBM_PEAK_GBPS, "unit": "GB/s",

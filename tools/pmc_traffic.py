@@ -8,7 +8,11 @@ read side is doubled; WRITE_SIZE is exact for 16-B-per-lane stores. The render k
 mostly 4-B-per-lane RNG planes + 16-B accumulators, so the x2 is an upper-bound correction; both
 the raw and corrected values are written.
 
-usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <config> <out.json> <spp_per_launch> [last]
+usage: pmc_traffic.py <fetch_counter_collection.csv> <write_counter_collection.csv> <config> <out.json> <spp_per_launch> [last] [kernels]
+
+kernels: comma-separated kernel-name substrings whose per-dispatch averages are summed into the launch's
+bytes (default iqpt_render_kernel; round 4's C2 launches are iqpt_render_kernel + iqpt_sky_kernel, one
+dispatch of each per launch).
 
 last: average only the last `last` dispatches of each pass (the launches after the runtime's first-launch
 tuning, which alternates the masks and BVH-primary variants over its first launches on streamed scenes).
@@ -22,11 +26,11 @@ import sys
 from collections import defaultdict
 
 
-def per_kernel(path, counter):
+def per_kernel(path, counter, kernel="iqpt_render_kernel"):
     vals = defaultdict(list)
     with open(path) as f:
         for row in csv.DictReader(f):
-            if row.get("Counter_Name") == counter and "iqpt_render_kernel" in row.get("Kernel_Name", ""):
+            if row.get("Counter_Name") == counter and kernel in row.get("Kernel_Name", ""):
                 vals[row.get("Dispatch_Id")].append(float(row["Counter_Value"]))
     per_dispatch = [sum(vals[d]) for d in sorted(vals, key=int)]
     return per_dispatch
@@ -35,18 +39,26 @@ def per_kernel(path, counter):
 def main():
     fetch_csv, write_csv, config, out, spp = sys.argv[1:6]
     last = int(sys.argv[6]) if len(sys.argv) > 6 else 0
-    f = per_kernel(fetch_csv, "FETCH_SIZE")
-    w = per_kernel(write_csv, "WRITE_SIZE")
-    if last:
-        f, w = f[-last:], w[-last:]
-    if not f or not w:
-        raise SystemExit("no iqpt_render_kernel rows found")
-    f_avg = sum(f) / len(f) * 1024.0
-    w_avg = sum(w) / len(w) * 1024.0
-    res = {"config": config, "spp_per_launch": int(spp), "kernel": "iqpt_render_kernel",
-           "dispatches_fetch": len(f), "dispatches_write": len(w), "last_dispatches_only": last or None,
+    kernels = sys.argv[7].split(",") if len(sys.argv) > 7 else ["iqpt_render_kernel"]
+    parts = {}
+    for k in kernels:
+        f = per_kernel(fetch_csv, "FETCH_SIZE", k)
+        w = per_kernel(write_csv, "WRITE_SIZE", k)
+        if last:
+            f, w = f[-last:], w[-last:]
+        if not f or not w:
+            raise SystemExit(f"no {k} rows found")
+        parts[k] = {"dispatches_fetch": len(f), "dispatches_write": len(w),
+                    "fetch_bytes_raw": sum(f) / len(f) * 1024.0, "write_bytes": sum(w) / len(w) * 1024.0}
+    f_avg = sum(v["fetch_bytes_raw"] for v in parts.values())
+    w_avg = sum(v["write_bytes"] for v in parts.values())
+    first = parts[kernels[0]]
+    res = {"config": config, "spp_per_launch": int(spp), "kernel": "+".join(kernels),
+           "dispatches_fetch": first["dispatches_fetch"], "dispatches_write": first["dispatches_write"],
+           "last_dispatches_only": last or None,
            "fetch_bytes_raw": f_avg, "write_bytes": w_avg, "fetch_bytes_corrected": 2 * f_avg,
            "hbm_bytes_per_launch": 2 * f_avg + w_avg,
+           **({"per_kernel": parts} if len(kernels) > 1 else {}),
            "note": "FETCH_SIZE doubled per MI355X_MICROARCH.md §HBM (gfx950 tallies 128-B requests at 64 B)"}
     with open(out, "w") as fh:
         json.dump(res, fh, indent=1)
