@@ -99,8 +99,9 @@ def parse():
                          "default: the library's)")
     ap.add_argument("--gather-prio", type=int, default=None, choices=[-1, 0, 1],
                     help="A/B: the communicator stream's priority (0: the library default)")
-    ap.add_argument("--gather-skip", type=int, default=0, choices=[0, 1, 2, 3],
-                    help="measurement only (wrong frames): 1 leaves out the collective, 2 the root's assembly")
+    ap.add_argument("--gather-skip", type=int, default=0, choices=range(8),
+                    help="measurement only (wrong frames): 1 leaves out the collective, 2 the root's assembly, "
+                         "4 the render streams' waits for the frame copies")
     ap.add_argument("--spec-even", choices=["on", "off"], default=None,
                     help="A/B: the spec kernel traces only the even slots of 2-slot pixels (default: the library's)")
     ap.add_argument("--no-kernel-timing", action="store_true",

@@ -322,7 +322,8 @@ struct iqpt_ctx {
     // 0 the default, 1 highest)
     int gather_ctas = iqpt::kGatherCtas;
     int gather_prio = 0;
-    int gather_skip = 0;                 // measurement only: 1 skips the collective, 2 the root's assembly
+    int gather_skip = 0;                 // measurement only: 1 skips the collective, 2 the root's assembly,
+                                         // 4 the render streams' waits for the frame copies
     bool timing_on = true;               // the launches' timing events (iqpt_debug_set_timing)
     bool spec_even = false;              // kspec::even2 (iqpt_debug_set_spec_even)
 };
@@ -2059,8 +2060,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             p.bgra = c->d_bgra;
         }
         if (c->copy_pend_cur) {
-            IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
-            IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_copy_cur, 0));
+            if (!(c->gather_skip & 4)) {
+                IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
+                IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_copy_cur, 0));
+            }
             c->copy_pend_cur = false;
         }
         if (!pipe_next) {
@@ -2848,10 +2851,10 @@ int iqpt_debug_set_hybrid(iqpt_ctx* c, int mode, uint32_t rho256) {
 /* Internal (A/B): the gather's footprint beside the render kernels, for the next iqpt_comm_init — RCCL's
  * blocks per collective (ncclConfig_t::maxCTAs; 0: RCCL's own choice) and the communicator stream's priority
  * (-1 the lowest; 0 HIP's default, the default; 1 the highest); skip (measurement only, wrong frames): 1 leaves
- * out the collective, 2 the root's assembly. */
+ * out the collective, 2 the root's assembly, 4 the render streams' waits for the copies of their frame buffers. */
 int iqpt_debug_set_gather(iqpt_ctx* c, int ctas, int prio, int skip) {
-    if (!c || ctas < 0 || ctas > 64 || prio < -1 || prio > 1 || skip < 0 || skip > 3)
-        return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL, ctas not 0..64, prio not -1..1 or skip not 0..3");
+    if (!c || ctas < 0 || ctas > 64 || prio < -1 || prio > 1 || skip < 0 || skip > 7)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL, ctas not 0..64, prio not -1..1 or skip not 0..7");
     c->gather_ctas = ctas;
     c->gather_prio = prio;
     c->gather_skip = skip;
