@@ -259,8 +259,22 @@ struct iqpt_ctx {
     // events bound to the dispatches), or null: a copy behind the launch waits for them instead of recording
     // markers of its own
     hipEvent_t end1 = nullptr, end2 = nullptr;
-    hipEvent_t ev_copy_cur = nullptr, ev_copy_alt = nullptr;   // on `stream3`, after the copy of d_bgra / d_bgra_alt
-    bool copy_pend_cur = false, copy_pend_alt = false;
+    // copies behind pipelined launches (iqpt_copy_frame_device_async, the gather's send copy): from the first
+    // one on, pipelined launches write a ring of kPipeRing frame buffers in turn (d_bgra points at the one
+    // the last launch wrote). Copy s (1-based, copy_seq counts them) records pev[s % kPipeRing] on stream3
+    // after reading its launch's buffer; pseq[b] is the last copy that read ring buffer b. A launch about
+    // to write buffer b that a copy newer than pwaited read makes both render streams wait for copy
+    // copy_seq - 1 (two launches back when every launch is copied), which stream3's order makes cover every
+    // buffer copied up to it: one wait per kPipeRing - 1 launches instead of one per launch (each wait is a
+    // packet on both streams between two kernels: r04 run 21, 0.015-0.02 ms per share-8 step)
+    uint32_t* d_pring[iqpt::kPipeRing] = {};
+    hipEvent_t pev[iqpt::kPipeRing] = {};
+    uint64_t pseq[iqpt::kPipeRing] = {};
+    uint64_t copy_seq = 0, pwaited = 0;
+    int pidx = 0;
+    bool pring_on = false;
+    uint32_t* d_bgra_own = nullptr;     // the allocations behind d_bgra / d_bgra_alt (views that swap)
+    uint32_t* d_alt_own = nullptr;
     unsigned long long* d_spec_tl = nullptr;   // iqpt_debug_spec_timeline: per spec block timestamps
     size_t spec_tl_blocks = 0;
     bool spec_tl_on = false;
@@ -343,10 +357,11 @@ int join_streams(iqpt_ctx* c) {
         IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
         c->s2_pending = false;
     }
-    // pipelined spec launches: `stream` also waits for the frame copies still reading a frame buffer
-    if (c->copy_pend_cur) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
-    if (c->copy_pend_alt) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_alt, 0));
-    c->copy_pend_cur = c->copy_pend_alt = false;
+    // pipelined launches: `stream` also waits for the frame copies still reading a frame buffer
+    if (c->copy_seq > c->pwaited) {
+        IQPT_HIP(hipStreamWaitEvent(c->stream, c->pev[c->copy_seq % iqpt::kPipeRing], 0));
+        c->pwaited = c->copy_seq;
+    }
     c->pipe = false;
     c->next_on_main = true;
     c->ovl_zero = true;
@@ -362,9 +377,7 @@ int join_streams(iqpt_ctx* c) {
 // Pipelined launches: the frame-copy stream and its two events, created when the first pipelined launch
 // ends, so that iqpt_frame_stream names the stream the next copy goes on before any copy was asked for.
 int ensure_copy_stream(iqpt_ctx* c) {
-    if ((!c->stream3 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) ||
-        (!c->ev_copy_cur && hipEventCreateWithFlags(&c->ev_copy_cur, hipEventDisableTiming) != hipSuccess) ||
-        (!c->ev_copy_alt && hipEventCreateWithFlags(&c->ev_copy_alt, hipEventDisableTiming) != hipSuccess)) {
+    if (!c->stream3 && hipStreamCreateWithFlags(&c->stream3, hipStreamNonBlocking) != hipSuccess) {
         (void)hipGetLastError();
         return iqpt::fail(IQPT_ERR_HIP, "frame copy stream");
     }
@@ -1301,6 +1314,7 @@ int iqpt_create(int device, uint32_t width, uint32_t height, const iqpt_pixel_se
         hipMalloc(&c->d_queue, (4 + iqpt::kOverlapQueueWords) * sizeof(uint32_t)) != hipSuccess ||
         hipMalloc(&c->d_ovl_err, sizeof(uint32_t)) != hipSuccess)
         return cleanup(iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "device allocation of the frame state failed"));
+    c->d_bgra_own = c->d_bgra;
     // path_tracer.cu:134-135: both buffers start at zero
     if (hipMemsetAsync(c->d_lin, 0, n * sizeof(float4_storage), c->stream) != hipSuccess ||
         hipMemsetAsync(c->d_bgra, 0, n * sizeof(uint32_t), c->stream) != hipSuccess ||
@@ -1334,8 +1348,13 @@ int iqpt_destroy(iqpt_ctx* c) {
     free_comm(c);
     free_scene(c);
     if (c->d_lin) (void)hipFree(c->d_lin);
-    if (c->d_bgra) (void)hipFree(c->d_bgra);
-    if (c->d_bgra_alt) (void)hipFree(c->d_bgra_alt);
+    if (c->d_bgra_own) (void)hipFree(c->d_bgra_own);
+    else if (c->d_bgra) (void)hipFree(c->d_bgra);       // (a context whose creation failed half way)
+    if (c->d_alt_own) (void)hipFree(c->d_alt_own);
+    for (int i = 0; i < iqpt::kPipeRing; ++i) {
+        if (c->d_pring[i]) (void)hipFree(c->d_pring[i]);
+        if (c->pev[i]) (void)hipEventDestroy(c->pev[i]);
+    }
     if (c->d_rng) (void)hipFree(c->d_rng);
     if (c->d_rays) (void)hipFree(c->d_rays);
     if (c->d_queue) (void)hipFree(c->d_queue);
@@ -1348,8 +1367,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->stream4) (void)hipStreamDestroy(c->stream4);
     for (hipEvent_t e : {c->ev_h0, c->ev_spec4})
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {c->ev_pipe_end, c->ev_copy_cur, c->ev_copy_alt})
-        if (e) (void)hipEventDestroy(e);
+    if (c->ev_pipe_end) (void)hipEventDestroy(c->ev_pipe_end);
     free_split(c);
     for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_tl, (void*)c->d_spec_plan})
         if (b) (void)hipFree(b);
@@ -2017,6 +2035,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         std::memcpy(p.xcd_off, c->xcd_off, sizeof p.xcd_off);
         p.ovl_err = c->d_ovl_err;
         c->chain_q_ready[0] = c->chain_q_ready[1] = false;   // the overlapped launches' words (chain sets)
+        if (c->copy_seq > c->pwaited) {    // copies behind earlier pipelined launches may still read d_bgra
+            IQPT_HIP(hipStreamWaitEvent(ls, c->pev[c->copy_seq % iqpt::kPipeRing], 0));
+            c->pwaited = c->copy_seq;
+        }
         if (c->d_bgra_alt) {
             std::swap(c->d_bgra, c->d_bgra_alt);
             p.bgra = c->d_bgra;
@@ -2053,18 +2075,18 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // asynchronous), after the copy that read it two launches ago; the second stream after everything
     // `stream` held unless the launch continues a pipeline
     auto pipe_begin = [&]() -> int {
-        if (c->d_bgra_alt) {
-            std::swap(c->d_bgra, c->d_bgra_alt);
-            std::swap(c->ev_copy_cur, c->ev_copy_alt);
-            std::swap(c->copy_pend_cur, c->copy_pend_alt);
+        if (c->pring_on) {
+            c->pidx = (c->pidx + 1) % iqpt::kPipeRing;
+            c->d_bgra = c->d_pring[c->pidx];
             p.bgra = c->d_bgra;
-        }
-        if (c->copy_pend_cur) {
-            if (!(c->gather_skip & 4)) {
-                IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_copy_cur, 0));
-                IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_copy_cur, 0));
+            if (c->pseq[c->pidx] > c->pwaited) {
+                const uint64_t tgt = std::max<uint64_t>(c->pseq[c->pidx], c->copy_seq - 1u);
+                if (!(c->gather_skip & 4)) {
+                    IQPT_HIP(hipStreamWaitEvent(c->stream, c->pev[tgt % iqpt::kPipeRing], 0));
+                    IQPT_HIP(hipStreamWaitEvent(c->stream2, c->pev[tgt % iqpt::kPipeRing], 0));
+                }
+                c->pwaited = tgt;
             }
-            c->copy_pend_cur = false;
         }
         if (!pipe_next) {
             IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
@@ -2998,11 +3020,18 @@ int copy_frame_async(iqpt_ctx* c, uint32_t* dst, hipEvent_t wait, hipStream_t* u
     hipStream_t cs = c->stream;
     if (c->pipe) {
         // pipelined spec launches: the copy on stream3 behind both kernels of the last launch; from here on
-        // the launches alternate two frame buffers
-        if (!c->d_bgra_alt && hipMalloc(&c->d_bgra_alt, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) {
-            (void)hipGetLastError();
-            c->d_bgra_alt = nullptr;
-            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "second frame buffer for pipelined copies");
+        // the launches write the ring of frame buffers in turn
+        if (!c->pring_on) {
+            for (int i = 0; i < iqpt::kPipeRing; ++i) {
+                if ((!c->d_pring[i] && hipMalloc(&c->d_pring[i], (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) ||
+                    (!c->pev[i] && hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming) != hipSuccess)) {
+                    (void)hipGetLastError();
+                    return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "frame buffers for pipelined copies");
+                }
+                c->pseq[i] = 0;
+            }
+            c->pidx = iqpt::kPipeRing - 1;     // the next launch writes d_pring[0]
+            c->pring_on = true;
         }
         if ((st = ensure_copy_stream(c)) != IQPT_OK) return st;
         if (!c->end1) IQPT_HIP(hipEventRecord(c->ev_pipe_end, c->stream));
@@ -3012,18 +3041,22 @@ int copy_frame_async(iqpt_ctx* c, uint32_t* dst, hipEvent_t wait, hipStream_t* u
         if (wait) IQPT_HIP(hipStreamWaitEvent(c->stream3, wait, 0));
         const int le = iqpt::launch_relayout(c->stream3, c->d_bgra, dst, c->ncols, c->set.nrows, 1, 1, true);
         if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
-        IQPT_HIP(hipEventRecord(c->ev_copy_cur, c->stream3));
-        c->copy_pend_cur = true;
+        c->copy_seq += 1;
+        IQPT_HIP(hipEventRecord(c->pev[c->copy_seq % iqpt::kPipeRing], c->stream3));
+        if (c->d_bgra == c->d_pring[c->pidx]) c->pseq[c->pidx] = c->copy_seq;
         *used = c->stream3;
         return IQPT_OK;
     }
     if (c->last_ovl && c->last_ls) {
         // overlapped launches in flight: copy on the last launch's stream without joining, so the next
         // launch still overlaps this one (from here on overlapped launches alternate two frame buffers)
-        if (!c->d_bgra_alt && hipMalloc(&c->d_bgra_alt, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) {
-            (void)hipGetLastError();
-            c->d_bgra_alt = nullptr;
-            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "second frame buffer for overlapped copies");
+        if (!c->d_bgra_alt) {
+            if (hipMalloc(&c->d_bgra_alt, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) {
+                (void)hipGetLastError();
+                c->d_bgra_alt = nullptr;
+                return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "second frame buffer for overlapped copies");
+            }
+            c->d_alt_own = c->d_bgra_alt;
         }
         cs = c->last_ls;
         if (cs == c->stream2) c->s2_pending = true;
