@@ -209,6 +209,7 @@ struct kspec {
                                      // s_memrealtime at start, after round 0's slots and walk, at the end
                                      // (| rounds << 48)
 };
+constexpr int kSendRing = 4;                // the multi-GPU gather's send buffers, used in turn
 constexpr int kPipeRing = 6;                // frame buffers pipelined launches write in turn once copies follow them
 constexpr int kGatherCtas = 2;              // RCCL blocks per frame gather (iqpt_debug_set_gather)
 constexpr uint32_t kSpecReplan = 64;        // launches between two spec plans (the history read behind them)

@@ -264,9 +264,10 @@ struct iqpt_ctx {
     // the last launch wrote). Copy s (1-based, copy_seq counts them) records pev[s % kPipeRing] on stream3
     // after reading its launch's buffer; pseq[b] is the last copy that read ring buffer b. A launch about
     // to write buffer b that a copy newer than pwaited read makes both render streams wait for copy
-    // copy_seq - 1 (two launches back when every launch is copied), which stream3's order makes cover every
-    // buffer copied up to it: one wait per kPipeRing - 1 launches instead of one per launch (each wait is a
-    // packet on both streams between two kernels: r04 run 21, 0.015-0.02 ms per share-8 step)
+    // copy_seq - 2 (three launches back when every launch is copied: a copy still in flight is not waited
+    // for), which stream3's order makes cover every buffer copied up to it: one wait per kPipeRing - 2
+    // launches instead of one per launch (each wait is a packet on both streams between two kernels:
+    // r04 run 21, 0.015-0.02 ms per share-8 step)
     uint32_t* d_pring[iqpt::kPipeRing] = {};
     hipEvent_t pev[iqpt::kPipeRing] = {};
     uint64_t pseq[iqpt::kPipeRing] = {};
@@ -315,15 +316,17 @@ struct iqpt_ctx {
     uint32_t dev_err = 0;
     // multi-GPU frame delivery (iqpt_comm_init): an RCCL communicator over the ranks of one
     // frame's cyclic row split and its own stream. A gather copies the rank's pixels (compact order, padded
-    // to comm_stride pixels) into one of two send buffers in turn — the copy of gather g waits only for
-    // gather g - 2 — then ncclGather to the root, which assembles the frame from the rank blocks.
+    // to comm_stride pixels) into one of kSendRing send buffers in turn — the copy of gather g waits only for
+    // gather g - kSendRing — then ncclGather to the root, which assembles the frame from the rank blocks.
     void* comm = nullptr;                // ncclComm_t
     int comm_rank = 0, comm_world = 0;
     uint64_t comm_stride = 0;            // pixels per rank block: the most rows any rank owns x W
     hipStream_t cstream = nullptr;
-    uint32_t* d_gsend[2] = {nullptr, nullptr};   // comm_stride x 4 words each
-    hipEvent_t ev_gdone[2] = {nullptr, nullptr}; // on cstream, after the gather that read d_gsend[i]
-    bool gdone_pend[2] = {false, false};
+    // send buffers in turn (the copy of gather g waits for gather g - kSendRing, long done: with two, a
+    // gather slowed by the renders beside it held the next copies and, through them, the render streams)
+    uint32_t* d_gsend[iqpt::kSendRing] = {};     // comm_stride x 4 words each
+    hipEvent_t ev_gdone[iqpt::kSendRing] = {};   // on cstream, after the gather that read d_gsend[i]
+    bool gdone_pend[iqpt::kSendRing] = {};
     uint32_t gpar = 0;                   // the send buffer of the next gather
     hipEvent_t ev_gcopy = nullptr;       // after the copy into the send buffer (cstream waits for it)
     hipEvent_t ev_gend = nullptr;        // on cstream, after the last gather (every other entry point joins it)
@@ -1220,11 +1223,18 @@ void free_comm(iqpt_ctx* c) {
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     if (c->comm && rccl().comm_destroy) (void)rccl().comm_destroy(static_cast<ncclComm_t>(c->comm));
     c->comm = nullptr;
-    for (uint32_t** b : {&c->d_gsend[0], &c->d_gsend[1], &c->d_grecv, &c->d_gframe}) {
+    for (int i = 0; i < iqpt::kSendRing; ++i) {
+        if (c->d_gsend[i]) (void)hipFree(c->d_gsend[i]);
+        c->d_gsend[i] = nullptr;
+        if (c->ev_gdone[i]) (void)hipEventDestroy(c->ev_gdone[i]);
+        c->ev_gdone[i] = nullptr;
+        c->gdone_pend[i] = false;
+    }
+    for (uint32_t** b : {&c->d_grecv, &c->d_gframe}) {
         if (*b) (void)hipFree(*b);
         *b = nullptr;
     }
-    for (hipEvent_t* e : {&c->ev_gdone[0], &c->ev_gdone[1], &c->ev_gcopy, &c->ev_gend}) {
+    for (hipEvent_t* e : {&c->ev_gcopy, &c->ev_gend}) {
         if (*e) (void)hipEventDestroy(*e);
         *e = nullptr;
     }
@@ -1235,7 +1245,6 @@ void free_comm(iqpt_ctx* c) {
     c->gtimed.clear();
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
     c->cstream = nullptr;
-    c->gdone_pend[0] = c->gdone_pend[1] = false;
     c->comm_pend = false;
     c->comm_world = 0;
 }
@@ -2080,7 +2089,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             c->d_bgra = c->d_pring[c->pidx];
             p.bgra = c->d_bgra;
             if (c->pseq[c->pidx] > c->pwaited) {
-                const uint64_t tgt = std::max<uint64_t>(c->pseq[c->pidx], c->copy_seq - 1u);
+                const uint64_t tgt = std::max<uint64_t>(c->pseq[c->pidx], c->copy_seq > 2u ? c->copy_seq - 2u : 0u);
                 if (!(c->gather_skip & 4)) {
                     IQPT_HIP(hipStreamWaitEvent(c->stream, c->pev[tgt % iqpt::kPipeRing], 0));
                     IQPT_HIP(hipStreamWaitEvent(c->stream2, c->pev[tgt % iqpt::kPipeRing], 0));
@@ -3135,19 +3144,19 @@ int iqpt_comm_init(iqpt_ctx* c, int rank, int world, const void* id, size_t byte
     }
     const int prio = c->gather_prio < 0 ? prio_least : (c->gather_prio > 0 ? prio_greatest : 0);
     if (hipStreamCreateWithPriority(&c->cstream, hipStreamNonBlocking, prio) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_gdone[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_gdone[1], hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gcopy, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_gend, hipEventDisableTiming) != hipSuccess) {
         (void)hipGetLastError();
         free_comm(c);
         return iqpt::fail(IQPT_ERR_HIP, "communicator stream / events");
     }
-    if (hipMalloc(&c->d_gsend[0], stride * 16) != hipSuccess || hipMalloc(&c->d_gsend[1], stride * 16) != hipSuccess) {
-        (void)hipGetLastError();
-        free_comm(c);
-        return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "gather send buffers");
-    }
+    for (int i = 0; i < iqpt::kSendRing; ++i)
+        if (hipMalloc(&c->d_gsend[i], stride * 16) != hipSuccess ||
+            hipEventCreateWithFlags(&c->ev_gdone[i], hipEventDisableTiming) != hipSuccess) {
+            (void)hipGetLastError();
+            free_comm(c);
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "gather send buffers");
+        }
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     ncclComm_t comm = nullptr;
@@ -3210,7 +3219,7 @@ int gather_enqueue(iqpt_ctx* c, uint32_t b, hipStream_t from, int root, uint32_t
     IQPT_HIP(hipEventRecord(c->ev_gend, c->cstream));
     c->gdone_pend[b] = true;
     c->comm_pend = true;
-    c->gpar = b ^ 1u;
+    c->gpar = (b + 1u) % (uint32_t)iqpt::kSendRing;
     return IQPT_OK;
 }
 
