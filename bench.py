@@ -104,6 +104,8 @@ def parse():
                          "4 the render streams' waits for the frame copies")
     ap.add_argument("--spec-even", choices=["on", "off"], default=None,
                     help="A/B: the spec kernel traces only the even slots of 2-slot pixels (default: the library's)")
+    ap.add_argument("--spec-pred", choices=["on", "off"], default=None,
+                    help="A/B: the spec kernel's predicted chains (default: the library's)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="A/B: no timing events around launches (kernel times and the roofline read 0)")
     ap.add_argument("--self-gather", action="store_true",
@@ -475,6 +477,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_spec_even.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_spec_even(pt._h, 1 if args.spec_even == "on" else 0), "iqpt_debug_set_spec_even")
+    if args.spec_pred is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec_pred.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_spec_pred(pt._h, 1 if args.spec_pred == "on" else 0), "iqpt_debug_set_spec_pred")
     if args.no_kernel_timing:
         import ctypes as C
         lb = _lib.load()
@@ -720,6 +727,7 @@ def main():
                        "split": args.split, "overlap": args.overlap, "certain": args.certain, "sky": args.sky,
                        "hybrid": args.hybrid, **({"hybrid_rho": args.hybrid_rho} if args.hybrid_rho else {}),
                        **({"spec_even": args.spec_even} if args.spec_even else {}),
+                       **({"spec_pred": args.spec_pred} if args.spec_pred else {}),
                        "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
                        **({"spec_cap": args.spec_cap} if args.spec_cap else {})},

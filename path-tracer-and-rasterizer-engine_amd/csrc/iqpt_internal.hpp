@@ -203,6 +203,8 @@ struct kspec {
     const uint32_t* order;           // a plan (else null): sphere pixel q at each position, heaviest first
     const uint32_t* blocks;          // per plan block: first position, count | log2(lanes / 8) << 8
     uint32_t nblocks;                // plan blocks (the spec part of the grid)
+    uint32_t pred;                   // predicted chains: camera rays of every slot, scattered rays along the
+                                     // chain as predicted from them (iqpt_debug_set_spec_pred)
     uint32_t even2;                  // round 0 of a pixel whose last chain took 2 slots per sample traces
                                      // only the even slots (iqpt_debug_set_spec_even)
     unsigned long long* tl;          // measurement (iqpt_debug_spec_timeline), else null: per spec block

@@ -3161,6 +3161,7 @@ constexpr uint32_t kSpecLanes = 16;                    // lanes per sphere pixel
 constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per block without a plan
 constexpr uint32_t kSpecMaxPix = 32;                   // pixels per block at 8 lanes each
 constexpr uint32_t kSpecBatch = 512;                   // walk: chain samples gathered per block and batch
+constexpr uint8_t kSpecPend = 0xffu;                   // predicted chains: a slot whose camera ray hit a sphere
 static_assert(kSpecPix == kSpecPixPerBlock && kSpecMaxPix == kSpecMaxPixPerBlock, "runtime and kernel agree on the spec block");
 
 __host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth, uint32_t spp,
@@ -3244,7 +3245,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         rd[11] = 0u;
         rd[12] = 0u;
         rd[13] = pix;
-        rd[14] = (s.even2 && s.rho[q] == 512u) ? 1u : 0u;   // its last chain's samples took two slots each
+        rd[14] = (s.even2 && !s.pred && s.rho[q] == 512u) ? 1u : 0u;   // its last chain's samples took two slots each
     } else if (!valid && l == 0u) {
         // no pixel (the grid's last block): an empty, finished record (every field is read by the rounds)
         for (uint32_t i = 0; i < 16u; ++i) rd[i] = 0u;
@@ -3279,6 +3280,60 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         lst[l * 5u + 2u] = st.v2;
         lst[l * 5u + 3u] = st.v3;
         lst[l * 5u + 4u] = st.v4;
+        if (s.pred) {
+            // ---- predicted chains (kspec::pred), phase A: the camera ray of every slot of the
+            // window, one per lane per iteration — every lane at depth 0, so every iteration takes the tile
+            // masks. A ray that ends (an emissive triangle, the sky) is the whole sample: its colour and one
+            // slot. A ray that hits a sphere leaves its hit (t, sphere) and the mark kSpecPend; the walk
+            // completes such samples along the chain only.
+            uint32_t j = j0;
+            bool active = live && j0 < j1;
+            while (__any(active)) {
+                if (rec_w) ++iters;
+                ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+                if (active) camera_ray<OPT>(p, px, py, st, ray);   // st: slot j + 1's start
+                float closest = kTMax;
+                int kind = kHitNone;
+                uint32_t hidx = 0;
+                {
+                    const uint32_t* lane_mask = active ? p.cull + (size_t)lds_cm[g].z * p.cull_stride : nullptr;
+                    uint4 cm = lds_cm[g];
+                    const uint64_t act = __ballot(active);
+                    const uint32_t first = (uint32_t)__builtin_ctzll(act);
+                    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
+                    const bool uni = __ballot(active && cm.z != t0) == 0ull;
+                    if (uni) {
+                        cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
+                        cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
+                    }
+                    const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
+                    intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, false, active, ray,
+                                          closest, kind, hidx, p.cull_wt, uni_mask);
+                }
+                if (active) {
+                    if (kind == kHitSphere) {
+                        res[j] = make_float4(closest, __uint_as_float(hidx), 0.0f, 0.0f);
+                        ln[j] = kSpecPend;
+                    } else {
+                        // emissive(1, 10) or the sky gradient (:308-313), clamped (:345-347), 0 + colour
+                        float cx = 10.0f, cy = 10.0f, cz = 10.0f;
+                        if (kind != kHitTri) {
+                            const float a = (ray.dy + 1.0f) * 0.5f;
+                            const float one_a = 1.0f - a;
+                            cx = one_a + a * 0.5f;
+                            cy = one_a + a * 0.7f;
+                            cz = one_a + a * 1.0f;
+                        }
+                        cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                        cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                        cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                        res[j] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                        ln[j] = 1u;
+                    }
+                    if (++j == j1) active = false;
+                }
+            }
+        } else {
         uint32_t j = j0;
         bool active = live && j0 < j1;
         ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -3373,6 +3428,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                 }
             }
         }
+        }
 
         // ---- walk: the colours are this block's own stores (complete: vmcnt 0), read back from L2
         __builtin_amdgcn_s_waitcnt(0);
@@ -3382,6 +3438,166 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         uint16_t* lp = lds_pos + g * batch;
         float ax = __uint_as_float(rd[8]), ay = __uint_as_float(rd[9]), az = __uint_as_float(rd[10]);
         uint32_t k = rd[11];
+        if (s.pred) {
+            const uint32_t d0 = p.rng[5 * (size_t)p.npix + rd[13]];
+            // phase B, batch by batch: the chain's next positions as predicted (a pending sample takes two
+            // slots: camera ray, sphere, scattered ray, then an emissive wall or the sky), the pending samples
+            // among them completed by the pixel's lanes, the chain checked against their true slot counts —
+            // it runs up to the first sample that took other than two (a second sphere, max_depth), and the
+            // next batch starts where that sample really ends — then folded as below
+            while (__syncthreads_or(walker && live && k < p.spp && jw < M)) {
+                if (walker && live) {
+                    uint32_t c = 0, jj = jw;
+                    while (c < batch && k + c < p.spp && jj < M) {
+                        lp[c++] = (uint16_t)jj;
+                        const uint32_t nj = ln[jj];
+                        jj += nj == kSpecPend ? 2u : nj;
+                    }
+                    lds_w[2 * g] = c;
+                }
+                __syncthreads();
+                const uint32_t cw = (valid && live) ? lds_w[2 * g] : 0u;
+                {
+                    uint32_t ii = l, jc = 0;
+                    bool active = false, resume = false;
+                    ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+                    rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
+                    int depth = 0;
+                    float r_closest = 0.0f;
+                    uint32_t r_hidx = 0;
+                    // this lane's next pending position (l, l + L, ...): the slot's state from its range's
+                    // start state stepped on, its camera ray again, the hit phase A left
+                    auto next_pending = [&]() {
+                        active = false;
+                        while (ii < cw) {
+                            const uint32_t jp = lp[ii];
+                            ii += L;
+                            if (ln[jp] != kSpecPend) continue;
+                            uint32_t kk = L - 1u;
+                            while (kk > 0u && start_of(kk) > jp) --kk;
+                            const uint32_t jk = start_of(kk);
+                            st.v0 = lst[kk * 5u];
+                            st.v1 = lst[kk * 5u + 1u];
+                            st.v2 = lst[kk * 5u + 2u];
+                            st.v3 = lst[kk * 5u + 3u];
+                            st.v4 = lst[kk * 5u + 4u];
+                            xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * (jp - jk));
+                            st.d = d0 + 2u * (js + jp) * IQ_XORWOW_WEYL;
+                            camera_ray<OPT>(p, px, py, st, ray);
+                            const uint32_t* src = reinterpret_cast<const uint32_t*>(res + jp);
+                            r_closest = __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                            r_hidx = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            jc = jp;
+                            depth = 0;
+                            resume = true;
+                            active = true;
+                            return;
+                        }
+                    };
+                    next_pending();
+                    while (__any(active)) {
+                        if (rec_w) ++iters;
+                        // scattered rays over every pair (a resumed sample's camera ray has its hit already)
+                        float closest = kTMax;
+                        int kind = kHitNone;
+                        uint32_t hidx = 0;
+                        intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, nullptr, 0u, 0u, true, active && !resume,
+                                              ray, closest, kind, hidx, p.cull_wt, nullptr);
+                        if (resume) {
+                            closest = r_closest;
+                            kind = kHitSphere;
+                            hidx = r_hidx;
+                            resume = false;
+                        }
+                        if (active) {
+                            bool term = false;
+                            uint32_t md_end = 0;
+                            float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
+                            if (kind == kHitSphere) {
+                                const float* sq = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
+                                const float sc = oren_nayar_scatter<OPT>(make_float4(sq[0], sq[2], sq[4], sq[6]), closest, ray, st);
+                                if (depth + 1 >= p.max_depth) {
+                                    term = true;
+                                    md_end = 1;
+                                    Lx = sc;
+                                    Ly = sc;
+                                    Lz = sc;
+                                } else {
+                                    lds_stk[(uint32_t)depth * kSpecBlock + threadIdx.x] = sc;
+                                    ++depth;
+                                }
+                            } else if (kind == kHitTri) {
+                                term = true;
+                                Lx = 10.0f;
+                                Ly = 10.0f;
+                                Lz = 10.0f;
+                            } else {
+                                term = true;
+                                const float a = (ray.dy + 1.0f) * 0.5f;
+                                const float one_a = 1.0f - a;
+                                Lx = one_a + a * 0.5f;
+                                Ly = one_a + a * 0.7f;
+                                Lz = one_a + a * 1.0f;
+                            }
+                            if (term) {
+                                float cx = Lx, cy = Ly, cz = Lz;
+                                for (int i = depth - 1; i >= 0; --i) {
+                                    const float rr = lds_stk[(uint32_t)i * kSpecBlock + threadIdx.x];
+                                    cx = cx * rr;
+                                    cy = cy * rr;
+                                    cz = cz * rr;
+                                }
+                                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                                res[jc] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                                ln[jc] = (uint8_t)((uint32_t)depth + 1u + md_end);
+                                next_pending();
+                            }
+                        }
+                    }
+                }
+                __builtin_amdgcn_s_waitcnt(0);
+                __syncthreads();
+                // the chain through the batch: up to the first position the true slot counts do not reach
+                if (walker && live) {
+                    uint32_t c2 = 0, jn = jw;
+                    for (uint32_t i = 0; i < cw; ++i) {
+                        if (lp[i] != jn) break;
+                        jn = lp[i] + ln[lp[i]];
+                        c2 = i + 1u;
+                    }
+                    lds_w[2 * g] = c2;
+                    lds_w[2 * g + 1] = jn;
+                }
+                __syncthreads();
+                const uint32_t cv = (valid && live) ? lds_w[2 * g] : 0u;
+                for (uint32_t i = l; i < cv; i += L) {
+                    const uint32_t* src = reinterpret_cast<const uint32_t*>(res + lp[i]);
+                    const float cx = __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    const float cy = __uint_as_float(__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    const float cz = __uint_as_float(__hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    const float2 tv = tab[k + i];
+                    float qx, qy, qz;
+                    mean_terms<OPT>(cx, cy, cz, tab_n[k + i], tv.x, p.mean_tiny, qx, qy, qz);
+                    lds_c[g * batch + i] = make_float4(qx, qy, qz, tv.y);
+                    const uint32_t n = ln[lp[i]];
+                    lane_rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
+                }
+                __syncthreads();
+                if (walker && live) {
+#pragma unroll 4
+                    for (uint32_t i = 0; i < cv; ++i) {
+                        const float4 v = lds_c[g * batch + i];
+                        ax = v.x + ax * v.w;
+                        ay = v.y + ay * v.w;
+                        az = v.z + az * v.w;
+                    }
+                    jw = lds_w[2 * g + 1];
+                }
+                k += cv;
+            }
+        } else
         for (uint32_t r0 = 0; r0 < p.spp; r0 += batch) {
             if (walker && live) {
                 uint32_t c = 0;

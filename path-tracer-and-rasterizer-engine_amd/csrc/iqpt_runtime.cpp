@@ -343,6 +343,7 @@ struct iqpt_ctx {
                                          // 4 the render streams' waits for the frame copies
     bool timing_on = true;               // the launches' timing events (iqpt_debug_set_timing)
     bool spec_even = false;              // kspec::even2 (iqpt_debug_set_spec_even)
+    bool spec_pred = false;              // kspec::pred (iqpt_debug_set_spec_pred; measured slower, r04 run 25)
 };
 
 namespace {
@@ -572,8 +573,10 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
         const uint32_t m = iqpt::spec_window(r, p.spp, ks.m_cap, ks.margin_div);
         // slots traced: the window's, or its even ones for a pixel whose last chain took two slots per
         // sample (the kernel's round 0)
-        const uint32_t traced = (ks.even2 && r == 512u) ? (m + 1u) / 2u : m;
-        w[q] = (double)traced * (double)std::max<uint32_t>(r, 256u) / 256.0;
+        const uint32_t traced = (ks.even2 && !ks.pred && r == 512u) ? (m + 1u) / 2u : m;
+        // predicted chains: a camera ray per slot of the window, the rest of the chain's samples once
+        w[q] = ks.pred ? (double)m + (double)p.spp * (double)(std::max<uint32_t>(r, 256u) - 256u) / 256.0 * 2.0
+                       : (double)traced * (double)std::max<uint32_t>(r, 256u) / 256.0;
         total += w[q];
         wmax = std::max(wmax, w[q]);
     }
@@ -1986,6 +1989,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         probe.rho0 = c->spec_rho0;
         probe.margin_div = c->spec_margin_div;
         probe.even2 = c->spec_even ? 1u : 0u;
+        probe.pred = c->spec_pred ? 1u : 0u;
         const uint32_t nb = spec_build_plan(c, p, probe, opt, c->h_spec_rho, c->h_spec_plan, &sel);
         IQPT_HIP(hipMemcpy(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
                            hipMemcpyHostToDevice));
@@ -2185,6 +2189,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.rho0 = c->spec_rho0;
         ks2.margin_div = c->spec_margin_div;
         ks2.even2 = c->spec_even ? 1u : 0u;
+        ks2.pred = c->spec_pred ? 1u : 0u;
         ks2.pix = c->d_chain_pix;
         ks2.m = c->d_spec;
         ks2.rho = c->d_spec + n;
@@ -2897,6 +2902,14 @@ int iqpt_debug_set_gather(iqpt_ctx* c, int ctas, int prio, int skip) {
 int iqpt_debug_set_spec_even(iqpt_ctx* c, int on) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     c->spec_even = on != 0;
+    return IQPT_OK;
+}
+
+/* Internal (A/B, tests): the spec kernel's predicted chains (1: camera rays of every slot, scattered rays
+ * along the chain as predicted from them) or every slot traced whole (0). Same bits either way. */
+int iqpt_debug_set_spec_pred(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->spec_pred = on != 0;
     return IQPT_OK;
 }
 
