@@ -3164,11 +3164,16 @@ constexpr uint32_t kSpecBatch = 512;                   // walk: chain samples ga
 constexpr uint8_t kSpecPend = 0xffu;                   // predicted chains: a slot whose camera ray hit a sphere
 static_assert(kSpecPix == kSpecPixPerBlock && kSpecMaxPix == kSpecMaxPixPerBlock, "runtime and kernel agree on the spec block");
 
+// Scatter records a spec lane keeps: one per bounce that continues (depth + 1 < max_depth); the last scatter
+// ends the sample without a record. max_depth - 1 of them (not max_depth) keeps a C2 block at 31.9 KB of LDS,
+// 5 blocks per CU instead of 4.
+__host__ __device__ inline uint32_t spec_stack_depth(int max_depth) { return max_depth > 2 ? (uint32_t)(max_depth - 1) : 1u; }
+
 __host__ __device__ inline uint32_t spec_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth, uint32_t spp,
                                                    uint32_t m_cap) {
     const uint32_t sp4 = (spp + 3u) & ~3u;
     return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + kSpecMaxPix * 16u +
-           kSpecBatch * 16u + sp4 * 12u + (uint32_t)(max_depth > 1 ? max_depth : 1) * kSpecBlock * 4u +
+           kSpecBatch * 16u + sp4 * 12u + spec_stack_depth(max_depth) * kSpecBlock * 4u +
            kSpecBlock * 20u + kSpecMaxPix * 64u + kSpecBatch * 2u + kSpecMaxPix * 8u + kSpecMaxPix * m_cap;
 }
 
@@ -3183,7 +3188,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     float2* tab = reinterpret_cast<float2*>(lds_c + kSpecBatch);
     float* tab_n = reinterpret_cast<float*>(tab + sp4);
     float* lds_stk = tab_n + sp4;                                                                  // [depth][thread]
-    uint32_t* lds_st = reinterpret_cast<uint32_t*>(lds_stk + (size_t)(p.max_depth > 1 ? p.max_depth : 1) * kSpecBlock);
+    uint32_t* lds_st = reinterpret_cast<uint32_t*>(lds_stk + (size_t)spec_stack_depth(p.max_depth) * kSpecBlock);
     // per pixel: 0 the round's first slot (absolute), 1 its window, 2..6 the state there (v0..v4), 7 done,
     // and the walker's running mean (8..10), samples folded (11), storage index (13) — kept in
     // LDS across the slot loop, whose registers they would otherwise take
