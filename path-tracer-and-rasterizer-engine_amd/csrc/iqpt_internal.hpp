@@ -216,7 +216,9 @@ constexpr int kPipeRing = 6;                // frame buffers pipelined launches 
 constexpr int kGatherCtas = 2;              // RCCL blocks per frame gather (iqpt_debug_set_gather)
 constexpr uint32_t kSpecReplan = 64;        // launches between two spec plans (the history read behind them)
 constexpr uint32_t kSpecPixPerBlock = 16;   // sphere pixels per iqpt_spec_kernel block without a plan (16 lanes each)
-constexpr uint32_t kSpecMaxPixPerBlock = 32;   // a plan's blocks: 256 / (8, 16, 32 or 64) pixels
+constexpr uint32_t kSpecMaxPixPerBlock = 32;   // a plan's blocks: 256 / (8, 16, 24, 32, 48 or 64) pixels
+constexpr uint32_t kSpecBlockLanes = 256;      // iqpt_spec_kernel's block
+constexpr int kSpecLaneClasses = 6;            // lanes per pixel: 8, 16, 24, 32, 48, 64
 constexpr uint32_t kSpecRho0 = 576;      // 2.25 slots per sample before a pixel has a history (sphere pixels take ~2)
 
 // The spec window of a sphere pixel whose last chain used rho256 / 256 slots per sample: that many slots

@@ -3207,18 +3207,18 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     }
     if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);   // these chains are the launch's longest
 
-    // the block's pixels: a plan's block (s.blocks: first position in s.order, count, 8 << lsh lanes per
-    // pixel) or the next 16 sphere pixels, 16 lanes each
-    uint32_t first = bid * kSpecPix, cnt = min(kSpecPix, s.n - min(s.n, bid * kSpecPix)), lsh = 1;
+    // the block's pixels: a plan's block (s.blocks: first position in s.order, count | lanes per pixel << 8)
+    // or the next 16 sphere pixels, 16 lanes each
+    uint32_t first = bid * kSpecPix, cnt = min(kSpecPix, s.n - min(s.n, bid * kSpecPix)), L = kSpecLanes;
     if (s.blocks) {
         first = s.blocks[2 * bid];
         const uint32_t w = s.blocks[2 * bid + 1];
         cnt = w & 0xffu;
-        lsh = w >> 8;
+        L = w >> 8;                                        // lanes per pixel: 8, 16, 24, 32, 48 or 64
     }
-    const uint32_t L = 8u << lsh;                         // lanes per pixel: 8, 16, 32 or 64
-    const uint32_t batch = min(64u, 16u << lsh);          // walk: chain samples per pixel and batch
-    const uint32_t g = threadIdx.x >> (3u + lsh), l = threadIdx.x & (L - 1u);
+    const uint32_t batch = min(64u, 2u * L);              // walk: chain samples per pixel and batch
+    // pixel g of the block on lanes [g L, g L + L) (a class that does not divide 256 leaves the last lanes idle)
+    const uint32_t g = threadIdx.x / L, l = threadIdx.x - g * L;
     const bool valid = g < cnt, walker = valid && l == 0u;
     const uint32_t q = valid ? (s.order ? s.order[first + g] : first + g) : 0u;
     const uint32_t pix = valid ? s.pix[q] : 0u;

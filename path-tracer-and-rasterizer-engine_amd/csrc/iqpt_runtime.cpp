@@ -583,15 +583,20 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     int occ = 0;
     if (iqpt::spec_occupancy(p, ks, opt, &occ) != 0 || occ < 1) occ = 1;
     const double cap = c->spec_cap * (double)c->num_cus * occ * 256.0;     // resident lanes, a little slack
-    auto lsh_of = [&](uint32_t q, double e) -> uint8_t {
+    // lane classes: 256 / lanes pixels per block (a class that does not divide 256 leaves lanes idle); the
+    // in-between classes let a plan use resident lanes that the next power of two would overfill (most
+    // sphere pixels have the same work: r04 run 27)
+    static constexpr uint32_t kLanes[iqpt::kSpecLaneClasses] = {8u, 16u, 24u, 32u, 48u, 64u};
+    constexpr uint8_t kTop = iqpt::kSpecLaneClasses - 1;
+    auto cls_of = [&](uint32_t q, double e) -> uint8_t {
         uint8_t k = 0;
-        while (k < 3 && w[q] > e * (double)(8u << k)) ++k;
+        while (k < kTop && w[q] > e * (double)kLanes[k]) ++k;
         return k;
     };
     auto lanes_at = [&](double e) {
         double sum = 0.0;
         for (uint32_t q = 0; q < n; ++q)
-            if (!sel || (*sel)[q]) sum += (double)(8u << lsh_of(q, e));
+            if (!sel || (*sel)[q]) sum += (double)kLanes[cls_of(q, e)];
         return sum;
     };
     double e = total / cap;                      // several block-waves: balanced work per lane
@@ -604,36 +609,37 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
         }
         e = hi;
     }
-    std::vector<uint8_t> lsh(n);
+    std::vector<uint8_t> cls(n);
     double emax = 0.0;
     for (uint32_t q = 0; q < n; ++q) {
-        uint8_t k = lsh_of(q, e);
-        if (c->spec_plan_mode == 3) k = 2;
-        if (c->spec_plan_mode == 4) k = 3;
-        if (c->spec_plan_mode == 5) k = (uint8_t)(q % 4u);
-        lsh[q] = k;
-        emax = std::max(emax, w[q] / (double)(8u << k));
+        uint8_t k = cls_of(q, e);
+        if (c->spec_plan_mode == 3) k = 3;                                // 32 lanes
+        if (c->spec_plan_mode == 4) k = kTop;                             // 64 lanes
+        if (c->spec_plan_mode == 5) k = (uint8_t)(q % iqpt::kSpecLaneClasses);   // every class
+        cls[q] = k;
+        emax = std::max(emax, w[q] / (double)kLanes[k]);
     }
     // counting sort by (lane class, work per lane) descending
     constexpr uint32_t kB = 1024;
-    std::vector<uint32_t> key(n), cnt(4 * kB + 2, 0);
+    constexpr uint32_t kC = iqpt::kSpecLaneClasses;
+    std::vector<uint32_t> key(n), cnt((kC + 1) * kB + 2, 0);
     for (uint32_t q = 0; q < n; ++q) {
-        const double pe = w[q] / (double)(8u << lsh[q]);
+        const double pe = w[q] / (double)kLanes[cls[q]];
         const uint32_t b = emax > 0.0 ? std::min<uint32_t>(kB - 1, (uint32_t)(pe / emax * (kB - 1))) : 0u;
-        key[q] = (sel && !(*sel)[q]) ? 4 * kB : (3u - lsh[q]) * kB + (kB - 1 - b);   // ascending key: 64 lanes first,
-        cnt[key[q] + 1]++;                                                            // heaviest first, unselected last
-    }
-    for (uint32_t k = 0; k < 4 * kB + 1; ++k) cnt[k + 1] += cnt[k];
+        key[q] = (sel && !(*sel)[q]) ? kC * kB : (kTop - cls[q]) * kB + (kB - 1 - b);   // ascending key: most lanes
+        cnt[key[q] + 1]++;                                                                // first, heaviest first,
+    }                                                                                     // unselected last
+    for (uint32_t k = 0; k < kC * kB + 1; ++k) cnt[k + 1] += cnt[k];
     for (uint32_t q = 0; q < n; ++q) h[cnt[key[q]]++] = q;
     const uint32_t nsel = sel ? (uint32_t)std::count(sel->begin(), sel->end(), (char)1) : n;
     // blocks of one class, then ordered by their first (heaviest) pixel's work per lane
     struct blk { double e; uint32_t first, word; };
     std::vector<blk> blocks;
     for (uint32_t i = 0; i < nsel;) {
-        const uint32_t k = lsh[h[i]], per = iqpt::kSpecMaxPixPerBlock >> k;
+        const uint32_t k = cls[h[i]], per = (uint32_t)iqpt::kSpecBlockLanes / kLanes[k];
         uint32_t m = 0;
-        while (m < per && i + m < nsel && lsh[h[i + m]] == k) ++m;
-        blocks.push_back({w[h[i]] / (double)(8u << k), i, m | (k << 8)});
+        while (m < per && i + m < nsel && cls[h[i + m]] == k) ++m;
+        blocks.push_back({w[h[i]] / (double)kLanes[k], i, m | (kLanes[k] << 8)});
         i += m;
     }
     std::stable_sort(blocks.begin(), blocks.end(), [](const blk& a, const blk& b) { return a.e > b.e; });
@@ -2841,7 +2847,7 @@ int iqpt_debug_read_spec_plan(iqpt_ctx* c, uint32_t* order, uint32_t* blocks, ui
 
 /* Internal (tests, A/B): the spec plan — 0 none (16 lanes per pixel, list order), 1 from an asynchronous
  * read of the history (the default), 2 rebuilt synchronously before every launch, 3 / 4 the same with
- * every pixel on 32 / 64 lanes, 5 the same with the lane count cycling over 8, 16, 32, 64. Drops the plan. */
+ * every pixel on 32 / 64 lanes, 5 the same with the lane count cycling over 8, 16, 24, 32, 48, 64. Drops the plan. */
 int iqpt_debug_spec_plan(iqpt_ctx* c, int mode) {
     if (!c || mode < 0 || mode > 5) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or mode not 0..5");
     c->spec_plan_mode = mode;
