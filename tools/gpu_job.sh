@@ -1,17 +1,19 @@
-# r04 run 28: spec lane classes 24 and 48 besides 8, 16, 32, 64 (a plan can use the 5th resident block): tests, shares
+# r04 run 29: the final round-4 tree — pytest -m gpu, smoke, the driver's default line, share steps with the
+# gather, rocprofv3 kernel-trace stats of the default bench and of the share-8 gather step
 mkdir -p gpurun_out
 O=gpurun_out
-R=r04_28
-timeout -k 10 900 python -u -m pytest tests/test_gpu_spec.py tests/test_gpu_spec_pred.py tests/test_gpu_spec_even.py tests/test_gpu_bench_multirank.py tests/test_gpu_hybrid.py tests/test_gpu_comm.py -x -q --timeout 300 --timeout-method thread > $O/${R}_tests.log 2>&1 || { tail -40 $O/${R}_tests.log; exit 1; }
+R=r04_29
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/${R}_tests.log 2>&1 || { tail -40 $O/${R}_tests.log; exit 1; }
 tail -2 $O/${R}_tests.log
-pr() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; p=(d.get('per_rank') or [{}])[0]; print('$2', d['ms_per_step'], r.get('kernel_avg_ms'), p.get('gather_ms'), d['bitexact_frac_vs_oracle'], d['config']['launch_mode'])"; }
-for pass in 1 2; do
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/${R}_smoke.log 2>&1 || { tail -20 $O/${R}_smoke.log; exit 1; }
+tail -1 $O/${R}_smoke.log
+pr() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; p=(d.get('per_rank') or [{}])[0]; print('$2', d['value'], d['ms_per_step'], r.get('kernel_avg_ms'), r.get('frac'), p.get('gather_ms'), d['bitexact_frac_vs_oracle'], d['config']['launch_mode'], (d.get('cpu_baseline') or {}).get('value'))"; }
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/${R}_default.json 2> $O/${R}_default.err || { tail -20 $O/${R}_default.err; exit 1; }
+pr $O/${R}_default.json default
 for n in 8 4 2; do
-timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --share-of $n > $O/${R}_s${n}_$pass.json 2> $O/${R}_e.err || { tail -20 $O/${R}_e.err; exit 1; }
-pr $O/${R}_s${n}_$pass.json share${n}_nogather
-timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --share-of $n --self-gather > $O/${R}_s${n}g_$pass.json 2> $O/${R}_e.err || { tail -20 $O/${R}_e.err; exit 1; }
-pr $O/${R}_s${n}g_$pass.json share${n}_gather
-done
+timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --share-of $n --self-gather > $O/${R}_s${n}g.json 2> $O/${R}_e.err || { tail -20 $O/${R}_e.err; exit 1; }
+pr $O/${R}_s${n}g.json share${n}_gather
 done
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace -d $O/${R}_prof -o trace -- python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --share-of 8 > $O/${R}_prof.log 2>&1 || { tail -20 $O/${R}_prof.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${R}_stats_n1 -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/${R}_stats_n1.log 2>&1 || { tail -20 $O/${R}_stats_n1.log; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${R}_stats_s8 -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --share-of 8 --self-gather > $O/${R}_stats_s8.log 2>&1 || { tail -20 $O/${R}_stats_s8.log; exit 1; }
