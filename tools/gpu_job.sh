@@ -1,19 +1,14 @@
-# r04 run 29: the final round-4 tree — pytest -m gpu, smoke, the driver's default line, share steps with the
-# gather, rocprofv3 kernel-trace stats of the default bench and of the share-8 gather step
+# r04 run 30: final-tree spec kernel diagnostics at the N = 8 share — per-block timeline (beside the fan kernel
+# and alone) and the PMC instruction mix of the spec / fan / sky kernels
 mkdir -p gpurun_out
 O=gpurun_out
-R=r04_29
-timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/${R}_tests.log 2>&1 || { tail -40 $O/${R}_tests.log; exit 1; }
-tail -2 $O/${R}_tests.log
-timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/${R}_smoke.log 2>&1 || { tail -20 $O/${R}_smoke.log; exit 1; }
-tail -1 $O/${R}_smoke.log
-pr() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; p=(d.get('per_rank') or [{}])[0]; print('$2', d['value'], d['ms_per_step'], r.get('kernel_avg_ms'), r.get('frac'), p.get('gather_ms'), d['bitexact_frac_vs_oracle'], d['config']['launch_mode'], (d.get('cpu_baseline') or {}).get('value'))"; }
-timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/${R}_default.json 2> $O/${R}_default.err || { tail -20 $O/${R}_default.err; exit 1; }
-pr $O/${R}_default.json default
-for n in 8 4 2; do
-timeout -k 10 300 python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --share-of $n --self-gather > $O/${R}_s${n}g.json 2> $O/${R}_e.err || { tail -20 $O/${R}_e.err; exit 1; }
-pr $O/${R}_s${n}g.json share${n}_gather
-done
+R=r04_30
+timeout -k 10 200 python3 tools/spec_timeline.py --share 8 --specfan 0 --out $O/${R}_timeline_n8_beside.json > $O/${R}_tl0.log 2>&1 || { tail -20 $O/${R}_tl0.log; exit 1; }
+tail -8 $O/${R}_tl0.log
+timeout -k 10 200 python3 tools/spec_timeline.py --share 8 --specfan 1 --out $O/${R}_timeline_n8_alone.json > $O/${R}_tl1.log 2>&1 || { tail -20 $O/${R}_tl1.log; exit 1; }
+tail -8 $O/${R}_tl1.log
 export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${R}_stats_n1 -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/${R}_stats_n1.log 2>&1 || { tail -20 $O/${R}_stats_n1.log; exit 1; }
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/${R}_stats_s8 -o run -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --share-of 8 --self-gather > $O/${R}_stats_s8.log 2>&1 || { tail -20 $O/${R}_stats_s8.log; exit 1; }
+A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32"
+B="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+timeout -s KILL 150 rocprofv3 --pmc $A --kernel-trace --output-format csv -d $O/${R}_mixa -o run -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --verify-rows 0 --share-of 8 > $O/${R}_mixa.log 2>&1 || { tail -20 $O/${R}_mixa.log; exit 1; }
+timeout -s KILL 150 rocprofv3 --pmc $B --kernel-trace --output-format csv -d $O/${R}_mixb -o run -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --verify-rows 0 --share-of 8 > $O/${R}_mixb.log 2>&1 || { tail -20 $O/${R}_mixb.log; exit 1; }
