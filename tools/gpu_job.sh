@@ -1,14 +1,13 @@
-# r04 run 30: final-tree spec kernel diagnostics at the N = 8 share — per-block timeline (beside the fan kernel
-# and alone) and the PMC instruction mix of the spec / fan / sky kernels
+# r04 run 34: spec kernel at 5 blocks per CU with the plan's lanes capped at 0.78 of them (= 0.97 of 4 blocks)
 mkdir -p gpurun_out
 O=gpurun_out
-R=r04_30
-timeout -k 10 200 python3 tools/spec_timeline.py --share 8 --specfan 0 --out $O/${R}_timeline_n8_beside.json > $O/${R}_tl0.log 2>&1 || { tail -20 $O/${R}_tl0.log; exit 1; }
-tail -8 $O/${R}_tl0.log
-timeout -k 10 200 python3 tools/spec_timeline.py --share 8 --specfan 1 --out $O/${R}_timeline_n8_alone.json > $O/${R}_tl1.log 2>&1 || { tail -20 $O/${R}_tl1.log; exit 1; }
-tail -8 $O/${R}_tl1.log
-export TMPDIR=/tmp
-A="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_BRANCH SQ_INSTS_VALU_TRANS_F32"
-B="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
-timeout -s KILL 150 rocprofv3 --pmc $A --kernel-trace --output-format csv -d $O/${R}_mixa -o run -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --verify-rows 0 --share-of 8 > $O/${R}_mixa.log 2>&1 || { tail -20 $O/${R}_mixa.log; exit 1; }
-timeout -s KILL 150 rocprofv3 --pmc $B --kernel-trace --output-format csv -d $O/${R}_mixb -o run -- python3 bench.py --steps 3 --warmup 2 --no-cpu-baseline --verify-rows 0 --share-of 8 > $O/${R}_mixb.log 2>&1 || { tail -20 $O/${R}_mixb.log; exit 1; }
+R=r04_34
+pr() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; p=(d.get('per_rank') or [{}])[0]; print('$2', d['ms_per_step'], r.get('kernel_avg_ms'), p.get('gather_ms'), d['bitexact_frac_vs_oracle'], d['config']['launch_mode'])"; }
+for pass in 1 2; do
+for cap in 0.78 0.85; do
+for n in 8 4 2; do
+timeout -k 10 300 python3 bench.py --steps 40 --warmup 5 --no-cpu-baseline --share-of $n --spec-cap $cap > $O/${R}_s${n}_c${cap}_$pass.json 2> $O/${R}_e.err || { tail -20 $O/${R}_e.err; exit 1; }
+pr $O/${R}_s${n}_c${cap}_$pass.json share${n}_cap$cap
+done
+done
+done

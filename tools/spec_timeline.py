@@ -28,6 +28,7 @@ ap.add_argument("--share", type=int, default=8)
 ap.add_argument("--specfan", type=int, default=1)
 ap.add_argument("--warm", type=int, default=3)
 ap.add_argument("--plan", type=int, default=1, help="iqpt_debug_spec_plan mode (0 none, 1 asynchronous)")
+ap.add_argument("--cap", type=float, default=0.0, help="iqpt_debug_set_spec_cap (0: the default)")
 ap.add_argument("--out", default="")
 args = ap.parse_args()
 
@@ -44,6 +45,9 @@ lb.iqpt_debug_set_specfan.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
 _lib.check(lb.iqpt_debug_set_specfan(pt._h, args.specfan, 0xffffffff), "iqpt_debug_set_specfan")
 lb.iqpt_debug_spec_plan.argtypes = [C.c_void_p, C.c_int]
 _lib.check(lb.iqpt_debug_spec_plan(pt._h, args.plan), "iqpt_debug_spec_plan")
+if args.cap:
+    lb.iqpt_debug_set_spec_cap.argtypes = [C.c_void_p, C.c_double]
+    _lib.check(lb.iqpt_debug_set_spec_cap(pt._h, args.cap), "iqpt_debug_set_spec_cap")
 pt.set_camera(cam)
 pt.upload_packet(pk)
 for _ in range(args.warm):
@@ -73,7 +77,7 @@ def pct(a):
     return {str(q): round(float(np.percentile(a, q)), 1) for q in (0, 10, 50, 90, 99, 100)}
 
 
-res = {"share": args.share, "specfan": args.specfan, "plan": args.plan, "blocks": int(n.value),
+res = {"share": args.share, "specfan": args.specfan, "plan": args.plan, "cap": args.cap or None, "blocks": int(n.value),
        "kernel_us": round(float(end.max()), 1),
        "start_us": pct(start), "slots_us": pct(slots_end - start), "walk_us": pct(walk_end - slots_end),
        "later_rounds_us": pct(end - walk_end), "end_us": pct(end),
