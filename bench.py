@@ -106,6 +106,9 @@ def parse():
                     help="A/B: the spec kernel traces only the even slots of 2-slot pixels (default: the library's)")
     ap.add_argument("--spec-pred", choices=["on", "off"], default=None,
                     help="A/B: the spec kernel's predicted chains (default: the library's)")
+    ap.add_argument("--sky-order", choices=["ahead", "behind"], default=None,
+                    help="A/B: overlapped launches run the sky kernel ahead of or behind the plain kernel "
+                         "(default: the library's, behind)")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="A/B: no timing events around launches (kernel times and the roofline read 0)")
     ap.add_argument("--self-gather", action="store_true",
@@ -482,6 +485,12 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_spec_pred.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_spec_pred(pt._h, 1 if args.spec_pred == "on" else 0), "iqpt_debug_set_spec_pred")
+    if args.sky_order is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_sky_order.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_sky_order(pt._h, 1 if args.sky_order == "behind" else 0),
+                   "iqpt_debug_set_sky_order")
     if args.no_kernel_timing:
         import ctypes as C
         lb = _lib.load()

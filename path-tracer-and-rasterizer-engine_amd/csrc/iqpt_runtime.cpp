@@ -343,6 +343,8 @@ struct iqpt_ctx {
                                          // 4 the render streams' waits for the frame copies
     bool timing_on = true;               // the launches' timing events (iqpt_debug_set_timing)
     bool spec_even = false;              // kspec::even2 (iqpt_debug_set_spec_even)
+    bool sky_after = true;               // overlapped launches: the sky kernel behind the plain kernel (r04 run 35:
+                                         // 0.988-0.992 -> 0.975-0.982 ms per C2 step)
     bool spec_pred = false;              // kspec::pred (iqpt_debug_set_spec_pred; measured slower, r04 run 25)
 };
 
@@ -2272,22 +2274,28 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     const bool sky = c->sky_on && c->certain_on && c->certain_valid && c->n_sky_tiles > 0 && p.certain != nullptr &&
                      !stream_batches && !split && !chain && !fan && !spec && tune_slot < 0 &&
                      !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax && iqpt::sky_variant_exists(opt);
+    // overlapped launches may put the sky kernel behind the plain kernel on the launch's stream
+    // (iqpt_debug_set_sky_order), so the plain kernel, whose sphere tiles carry the launch's longest chains,
+    // is not queued behind it
+    const bool sky_deferred = sky && ovl && bind_ovl && c->sky_after;
     if (sky) {
         p.miss = c->d_certain + 2 * (size_t)c->cull_ntx * c->cull_nty;
         if (!c->ev_sky && hipEventCreateWithFlags(&c->ev_sky, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
             return iqpt::fail(IQPT_ERR_HIP, "sky kernel event");
         }
-        const hipStream_t ss = ovl ? ls : c->stream;
-        if (c->sky_last && c->sky_last != ss) IQPT_HIP(hipStreamWaitEvent(ss, c->ev_sky, 0));
-        const bool b0 = bind_ovl && e0 && p.spp > 0;
-        if (b0) iqpt::bind_launch_events(e0, nullptr);
-        le = iqpt::launch_sky(ss, p, c->d_sky_tiles, c->n_sky_tiles, opt);
-        iqpt::bind_launch_events(nullptr, nullptr);
-        e0_bound = b0 && le == 0;
-        if (le != 0) return iqpt::hip_fail((hipError_t)le, "sky kernel launch");
-        IQPT_HIP(hipEventRecord(c->ev_sky, ss));
-        c->sky_last = ss;
+        if (!sky_deferred) {
+            const hipStream_t ss = ovl ? ls : c->stream;
+            if (c->sky_last && c->sky_last != ss) IQPT_HIP(hipStreamWaitEvent(ss, c->ev_sky, 0));
+            const bool b0 = bind_ovl && e0 && p.spp > 0;
+            if (b0) iqpt::bind_launch_events(e0, nullptr);
+            le = iqpt::launch_sky(ss, p, c->d_sky_tiles, c->n_sky_tiles, opt);
+            iqpt::bind_launch_events(nullptr, nullptr);
+            e0_bound = b0 && le == 0;
+            if (le != 0) return iqpt::hip_fail((hipError_t)le, "sky kernel launch");
+            IQPT_HIP(hipEventRecord(c->ev_sky, ss));
+            c->sky_last = ss;
+        }
     }
     // a hybrid launch's plain kernel skips the misses only while the sky kernel renders them (d_skip was built
     // with sky_active): otherwise the plain path without the spec kernel
@@ -2295,13 +2303,23 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     const iqpt::kparams p_spec = p;
     if (hybrid) p.miss = c->hyb_sel ? c->d_skip_sel : c->d_skip;
     if (ovl) {
-        if (bind_ovl) iqpt::bind_launch_events(e0_bound ? nullptr : e0, e1);
+        if (bind_ovl) iqpt::bind_launch_events(e0_bound ? nullptr : e0, sky_deferred ? nullptr : e1);
         le = iqpt::launch_render(ls, p, grid, lds, stream_batches, opt);
         iqpt::bind_launch_events(nullptr, nullptr);
         if (bind_ovl) {
             if (le != 0 && e0 && !e0_bound) (void)hipEventRecord(e0, ls);   // (not read: the launch failed)
             e0_bound = true;
+            e1_bound = le == 0 && e1 != nullptr && !sky_deferred;
+        }
+        if (sky_deferred && le == 0) {
+            if (c->sky_last && c->sky_last != ls) IQPT_HIP(hipStreamWaitEvent(ls, c->ev_sky, 0));
+            iqpt::bind_launch_events(nullptr, e1);
+            le = iqpt::launch_sky(ls, p, c->d_sky_tiles, c->n_sky_tiles, opt);
+            iqpt::bind_launch_events(nullptr, nullptr);
             e1_bound = le == 0 && e1 != nullptr;
+            if (le != 0) return iqpt::hip_fail((hipError_t)le, "sky kernel launch");
+            IQPT_HIP(hipEventRecord(c->ev_sky, ls));
+            c->sky_last = ls;
         }
         c->ovl_epoch += 1;
         c->next_on_main = !c->next_on_main;
@@ -2916,6 +2934,14 @@ int iqpt_debug_set_spec_even(iqpt_ctx* c, int on) {
 int iqpt_debug_set_spec_pred(iqpt_ctx* c, int on) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     c->spec_pred = on != 0;
+    return IQPT_OK;
+}
+
+/* Internal (A/B): overlapped launches run the sky kernel ahead of the plain kernel on the launch's stream (0)
+ * or behind it (1, the default). Same bits either way. */
+int iqpt_debug_set_sky_order(iqpt_ctx* c, int after) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    c->sky_after = after != 0;
     return IQPT_OK;
 }
 

@@ -110,3 +110,31 @@ def test_sky_row_share_and_large_frame_counter(require_gpu):
     assert c["bitexact"] == c["npix"], c
     assert np.array_equal(pt.read_rng(), fr.states)
     pt.close()
+
+
+@pytest.mark.parametrize("after", [0, 1])
+def test_sky_kernel_ahead_of_and_behind_the_plain_kernel(require_gpu, after):
+    """Overlapped launches with the sky kernel queued ahead of or behind (the default) the plain kernel
+    (iqpt_debug_set_sky_order): the oracle's bits, four launches on alternating streams."""
+    from iqpt import PathTracer, make_camera
+    L, lib = _lib()
+    lib.iqpt_debug_set_sky_order.argtypes = [C.c_void_p, C.c_int]
+    w, h, launches = 480, 270, [16, 8, 64, 3]
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, max_depth=8)
+    pt._scene = sc
+    pt.set_split(L.SPLIT_OFF)
+    L.check(lib.iqpt_debug_set_sky_order(pt.handle, after), "iqpt_debug_set_sky_order")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    for s in launches:
+        pt.render(s)
+    lin, bgra = pt.read()
+    fr = _oracle(pk, cam, w, h, launches)
+    c = compare(lin, fr.lin)
+    assert c["rmse"] < RMSE_TOL and c["bitexact"] == c["npix"], c
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    assert pt.rays() == int(fr.rays.sum())
+    pt.close()
