@@ -78,12 +78,6 @@ def parse():
                     help="overlapped launches on two streams (iqpt_set_overlap, DESIGN.md §3.8)")
     ap.add_argument("--certain", default="on", choices=["on", "off"],
                     help="A/B: certain pixels folded at once (iqpt_debug_set_certain, DESIGN.md §3.3)")
-    ap.add_argument("--hybrid", default="off", choices=["on", "off"],
-                    help="A/B: hybrid launches, the sphere pixels in the spec kernel beside overlapped plain launches "
-                         "(iqpt_debug_set_hybrid, DESIGN.md §3.13)")
-    ap.add_argument("--hybrid-rho", type=float, default=0.0,
-                    help="hybrid launches: only sphere pixels whose last chain used >= this many slots per sample go "
-                         "to the spec kernel (0: all)")
     ap.add_argument("--sky", default="on", choices=["on", "off"],
                     help="A/B: certain-miss pixels in iqpt_sky_kernel (iqpt_debug_set_sky, DESIGN.md §3.12)")
     ap.add_argument("--kernel-options", type=lambda v: int(v, 0), default=0,
@@ -102,10 +96,6 @@ def parse():
     ap.add_argument("--gather-skip", type=int, default=0, choices=range(8),
                     help="measurement only (wrong frames): 1 leaves out the collective, 2 the root's assembly, "
                          "4 the render streams' waits for the frame copies")
-    ap.add_argument("--spec-even", choices=["on", "off"], default=None,
-                    help="A/B: the spec kernel traces only the even slots of 2-slot pixels (default: the library's)")
-    ap.add_argument("--spec-pred", choices=["on", "off"], default=None,
-                    help="A/B: the spec kernel's predicted chains (default: the library's)")
     ap.add_argument("--sky-order", choices=["ahead", "behind"], default=None,
                     help="A/B: overlapped launches run the sky kernel ahead of or behind the plain kernel "
                          "(default: the library's, behind)")
@@ -275,8 +265,7 @@ def certain_pixels(pt, _lib) -> int:
 LAUNCH_KERNELS = {"plain": "iqpt_render_kernel", "spec": "iqpt_spec_kernel + iqpt_fan_kernel",
                   "fan": "iqpt_render_kernel + iqpt_fan_kernel", "chain": "iqpt_chain_kernel + iqpt_render_kernel",
                   "chain+fan": "iqpt_chain_kernel + iqpt_fan_kernel", "split": "iqpt_render_kernel (split rounds)",
-                  "split+fan": "iqpt_render_kernel (split rounds) + iqpt_fan_kernel",
-                  "hybrid": "iqpt_render_kernel + iqpt_spec_kernel + iqpt_sky_kernel"}
+                  "split+fan": "iqpt_render_kernel (split rounds) + iqpt_fan_kernel"}
 
 
 def mix_for_launch(cfg_name: str, launch_mode: str, split_ways: int, explicit: str):
@@ -330,13 +319,15 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode: str, s
     pmc, pmc_src = find_pmc(cfg.name, spp, args.pmc_json) if world == 1 and not args.share_of else (None, "N > 1: per-rank PMC not collected")
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
     busy, wsplit, mix_src = mix_for_launch(cfg.name, launch_mode, split_ways, args.pmc_mix_json)
-    work_path = args.work_json or newest_work(cfg.name)
-    work = load_json(work_path, cfg.name)
+    work_path, work_why = (args.work_json, None) if args.work_json else newest_work(cfg.name)
+    work = load_json(work_path, cfg.name) if work_path else None
     out = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS,
            "kernel": LAUNCH_KERNELS.get(launch_mode, launch_mode), "launch_mode": launch_mode,
            "kernel_avg_ms": round(kern_avg_ms, 4), "traffic": traffic,
            "valu_busy_frac": busy, "wave_time_split": wsplit, "mix_source": mix_src}
     ex = work["flops_per_ray"] * rays_per_launch / t / 1e12 if (work and work.get("flops_per_ray") and t > 0) else None
+    if work_why:
+        out["executed_work"] = {"missing": work_why}
     if ex is not None and ref_tflops > FP32_PEAK_TFLOPS:
         out.update(achieved=round(ex, 4), frac=round(ex / FP32_PEAK_TFLOPS, 5),
                    flops_per_ray=work["flops_per_ray"], work_basis="executed tests per ray (" + Path(work_path).name + ")",
@@ -349,7 +340,8 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode: str, s
             # the tests the kernel actually executes (the tile masks skip most of the brute-force ones)
             out["executed_work"] = {"achieved": round(ex, 4), "frac": round(ex / FP32_PEAK_TFLOPS, 5),
                                     "flops_per_ray": work["flops_per_ray"], "per_ray": work.get("per_ray"),
-                                    "source": str(Path(work_path).resolve().relative_to(REPO))}
+                                    "source": str(Path(work_path).resolve().relative_to(REPO)),
+                                    "kernel_sha16": work.get("kernel_sha16")}
     else:
         # the brute-force price exceeds the peak: the kernel skips that work, so it is no roofline
         out.update(achieved=None, frac=None, flops_per_ray=None,
@@ -379,11 +371,23 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode: str, s
     return out
 
 
-def newest_work(cfg_name: str) -> str:
-    """The newest executed-work profile of the config (tools/work_counters.py: profiles/r0*/work_<config>*.json)."""
+def newest_work(cfg_name: str):
+    """The newest executed-work profile of the config (tools/work_counters.py: profiles/r0*/work_<config>*.json)
+    taken on THESE kernel sources (its kernel_sha16 equals the build's, iqpt._build.kernel_source_sha16): counts of
+    another kernel price work this kernel may not do. Returns (path, None) or (None, why)."""
+    from iqpt._build import kernel_source_sha16
+    want = kernel_source_sha16()
     cands = sorted((REPO / "profiles").glob(f"r0*/work_{cfg_name}*.json"), key=lambda q: (q.parent.name, q.name),
                    reverse=True)
-    return str(cands[0]) if cands else str(REPO / "profiles" / "r02" / f"work_{cfg_name}.json")
+    seen = []
+    for c in cands:
+        d = load_json(str(c), cfg_name)
+        if d and d.get("kernel_sha16") == want:
+            return str(c), None
+        if d:
+            seen.append(f"{c.relative_to(REPO)} ({d.get('kernel_sha16') or 'no kernel hash'})")
+    return None, (f"no executed-work profile of kernel sources {want}: run tools/work_counters.py --config "
+                  f"{cfg_name}" + (f"; stale: {', '.join(seen[:3])}" if seen else ""))
 
 
 def fma_flavour_rmse():
@@ -475,16 +479,6 @@ def main():
         _lib.check(_lib.load().iqpt_debug_set_kernel_options(pt.handle, args.kernel_options),
                    "iqpt_debug_set_kernel_options")
     pt.set_overlap(_lib.OVERLAP_AUTO if args.overlap == "auto" else _lib.OVERLAP_OFF)
-    if args.spec_even is not None:
-        import ctypes as C
-        lb = _lib.load()
-        lb.iqpt_debug_set_spec_even.argtypes = [C.c_void_p, C.c_int]
-        _lib.check(lb.iqpt_debug_set_spec_even(pt._h, 1 if args.spec_even == "on" else 0), "iqpt_debug_set_spec_even")
-    if args.spec_pred is not None:
-        import ctypes as C
-        lb = _lib.load()
-        lb.iqpt_debug_set_spec_pred.argtypes = [C.c_void_p, C.c_int]
-        _lib.check(lb.iqpt_debug_set_spec_pred(pt._h, 1 if args.spec_pred == "on" else 0), "iqpt_debug_set_spec_pred")
     if args.sky_order is not None:
         import ctypes as C
         lb = _lib.load()
@@ -501,11 +495,6 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_certain.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_certain(pt._h, 0), "iqpt_debug_set_certain")
-    if args.hybrid == "on":
-        import ctypes as C
-        lb = _lib.load()
-        lb.iqpt_debug_set_hybrid.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
-        _lib.check(lb.iqpt_debug_set_hybrid(pt._h, 1, int(round(args.hybrid_rho * 256))), "iqpt_debug_set_hybrid")
     if args.sky == "off":
         import ctypes as C
         lb = _lib.load()
@@ -734,9 +723,6 @@ def main():
                                       + (" (RCCL ncclGather inside libiqpt: iqpt_gather_frame_async)" if lib_gather
                                          else " (gloo via host, rehearsal)")),
                        "split": args.split, "overlap": args.overlap, "certain": args.certain, "sky": args.sky,
-                       "hybrid": args.hybrid, **({"hybrid_rho": args.hybrid_rho} if args.hybrid_rho else {}),
-                       **({"spec_even": args.spec_even} if args.spec_even else {}),
-                       **({"spec_pred": args.spec_pred} if args.spec_pred else {}),
                        "launch_mode": launch_mode,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
                        **({"spec_cap": args.spec_cap} if args.spec_cap else {})},

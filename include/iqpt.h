@@ -268,13 +268,19 @@ int iqpt_frame_stream(iqpt_ctx* ctx, void** stream);
  * iqpt_gather_accum: collective, synchronous; the float4 accumulators (W*H*16 bytes of device memory) on the root.
  * iqpt_gather_read: collective, synchronous; the whole frame's accumulator (W*H*4 floats) and BGRA8 (W*H*4
  *   bytes) into the root's host buffers (either may be NULL; other ranks' pointers are ignored) — the
- *   multi-GPU iqpt_read. */
+ *   multi-GPU iqpt_read. Both planes cross the interconnect on every call.
+ * iqpt_gather_read_select: the same for the planes in `what` only (IQPT_GATHER_ACCUM | IQPT_GATHER_FRAME; every
+ *   rank passes the same value, the collectives must match): a present that needs the BGRA8 frame alone moves
+ *   4 instead of 20 bytes per pixel. */
 #define IQPT_COMM_ID_BYTES 128
 int iqpt_comm_unique_id(void* id, size_t bytes);
 int iqpt_comm_init(iqpt_ctx* ctx, int rank, int world, const void* id, size_t bytes);
 int iqpt_gather_frame_async(iqpt_ctx* ctx, int root, void* dst_device, size_t bytes);
 int iqpt_gather_accum(iqpt_ctx* ctx, int root, void* dst_device, size_t bytes);
 int iqpt_gather_read(iqpt_ctx* ctx, int root, float* lin_rgba, uint8_t* bgra);
+#define IQPT_GATHER_ACCUM 1
+#define IQPT_GATHER_FRAME 2
+int iqpt_gather_read_select(iqpt_ctx* ctx, int root, int what, float* lin_rgba, uint8_t* bgra);
 int iqpt_comm_stream(iqpt_ctx* ctx, void** stream);
 /* Sum of the gathers' durations on the communicator's stream (from the rank's copy being done to the end
  * of the gather and, on the root, of the assembly: the transfer plus any wait for slower ranks) and their

@@ -198,15 +198,13 @@ struct kspec {
     uint32_t* rho;                   // slots per sample x 256 of q's last chain (0: none)
     uint32_t* run_count;             // [1]: chains finished past their window (statistics)
     float4_storage* res;             // res[q m_cap + j]: clamped colour of slot j
-    uint32_t fan_tiles;              // fused launches (iqpt_specfan_kernel): fan tiles in the same grid
-    uint32_t lead;                   // fused launches: spec blocks placed before every fan block
+    // parity pixels: round 0 of a pixel whose last chain took >= parity_rho / 256 slots
+    // per sample traces the even slots of its window first, the odd ones only from where its chain lands on
+    // one (pooled over the block's lanes); 0: every slot of every window
+    uint32_t parity_rho;
     const uint32_t* order;           // a plan (else null): sphere pixel q at each position, heaviest first
     const uint32_t* blocks;          // per plan block: first position, count | log2(lanes / 8) << 8
     uint32_t nblocks;                // plan blocks (the spec part of the grid)
-    uint32_t pred;                   // predicted chains: camera rays of every slot, scattered rays along the
-                                     // chain as predicted from them (iqpt_debug_set_spec_pred)
-    uint32_t even2;                  // round 0 of a pixel whose last chain took 2 slots per sample traces
-                                     // only the even slots (iqpt_debug_set_spec_even)
     unsigned long long* tl;          // measurement (iqpt_debug_spec_timeline), else null: per spec block
                                      // s_memrealtime at start, after round 0's slots and walk, at the end
                                      // (| rounds << 48)
@@ -220,6 +218,7 @@ constexpr uint32_t kSpecMaxPixPerBlock = 32;   // a plan's blocks: 256 / (8, 16,
 constexpr uint32_t kSpecBlockLanes = 256;      // iqpt_spec_kernel's block
 constexpr int kSpecLaneClasses = 6;            // lanes per pixel: 8, 16, 24, 32, 48, 64
 constexpr uint32_t kSpecRho0 = 576;      // 2.25 slots per sample before a pixel has a history (sphere pixels take ~2)
+constexpr uint32_t kSpecParityRho = 480; // parity pixels: >= 1.875 slots per sample in their last chain (kspec::parity_rho)
 
 // The spec window of a sphere pixel whose last chain used rho256 / 256 slots per sample: that many slots
 // for spp samples plus a margin of 1 / margin_div of the extra slots (at least 4) and 4, within
@@ -362,6 +361,8 @@ int launch_tile_list(void* stream, const uint32_t* cull, uint32_t ntiles, uint32
 // Device probe of the camera transforms (iqpt_debug_camera_rays): general and kOptCamAxis forms.
 int launch_camera_probe(void* stream, const kparams& p, const float* ndc, float* gen, float* axis, uint32_t n,
                         bool do_axis);
+// Test only: `blocks` blocks, each filling lds_bytes of LDS with a pattern (iqpt_debug_poison_lds).
+int launch_lds_poison(void* stream, uint32_t pattern, uint32_t lds_bytes, uint32_t blocks);
 // Device probe of the shared math (iqpt_debug_libm).
 int launch_libm(void* stream, int fn, const float* a, const float* b, float* out, uint32_t n);
 // grid_blocks = persistent grid size; lds_bytes dynamic LDS; stream = hipStream_t; opt = kOpt* mask.
@@ -389,8 +390,6 @@ uint32_t spec_lds(const kparams& p, const kspec& s);
 int launch_spec(void* stream, const kparams& p, const kspec& s, int opt);
 // resident iqpt_spec_kernel blocks per CU for this launch
 int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks);
-// spec blocks and s.fan_tiles fan tiles (p.tile_order / p.fan_lanes) in one grid
-int launch_specfan(void* stream, const kparams& p, const kspec& s, int opt);
 // Certain-miss pixels (iqpt_sky_kernel): the p.miss pixels of `ntiles` tiles (tiles[i]),
 // lane = pixel, one wave per tile; resident scenes, reference materials, spp <= kAccTableMax.
 bool sky_variant_exists(int opt);

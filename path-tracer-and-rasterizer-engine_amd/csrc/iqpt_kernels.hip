@@ -19,10 +19,10 @@
 //    the two primitives stay sequential, so results are unchanged bit for bit.
 //  * Small scenes stay resident in LDS for the whole launch; large scenes are streamed through LDS
 //    in batches behind workgroup barriers (workgroup-uniform loop).
-//  * The scatter_record stack (path_tracer.cu:243, 321-324) is a register shift register: under
-//    the reference materials every non-terminal record is an Oren–Nayar scatter whose
-//    (attenuation * cos/pdf) is the same in x, y and z, so a record is one float and the backward
-//    product keeps its exact evaluation order.
+//  * The scatter_record stack (path_tracer.cu:243, 321-324) lives in LDS, one float per thread per
+//    level (bank-conflict free): under the reference materials every non-terminal record is an
+//    Oren–Nayar scatter whose (attenuation * cos/pdf) is the same in x, y and z, so a record is one
+//    float, and the backward product reads them newest to oldest in the reference's order.
 //  * Every floating-point operation follows the reference's order with contraction off
 //    (-ffp-contract=off) and the shared transcendentals of iq_fp.h; every shortcut below is exact
 //    (argued where it is taken). Results are bit-identical to the CPU oracle.
@@ -2142,6 +2142,18 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
 // compiles them (tests/test_gpu_libm.py compares them with the oracle's host build, bit for bit).
 // fn: 0 sin, 1 cos, 2 tan, 3 acos, 4 atan2(a, b), 5 asin, 6 atan (the oracle's iqo_libm_batch
 // numbering), 7 / 8 sin / cos of iq_sincosf, 9 iq_sqrt_guarded, 10 iq_rcp_guarded, 11 iq_div.
+// Test only (iqpt_debug_poison_lds): fills every byte of its dynamic LDS with `pattern` and leaves. A grid of
+// these at the largest allocation a block may have, several per CU, leaves non-zero values wherever the next
+// kernels' LDS allocations land, so a kernel that reads an LDS word before writing it sees garbage and its
+// results differ from the oracle's (r04 run 16's one-off parity failure).
+__global__ __launch_bounds__(256) void iqpt_lds_poison_kernel(uint32_t pattern, uint32_t words) {
+    extern __shared__ uint32_t lds_words[];
+    for (uint32_t i = threadIdx.x; i < words; i += 256u) lds_words[i] = pattern ^ (i * 0x9e3779b9u);
+    __syncthreads();
+    // keep the stores (the kernel's only effect is the LDS contents it leaves behind)
+    if (lds_words[threadIdx.x % (words ? words : 1u)] == 0x12345678u && pattern == 0x0badf00du) __builtin_trap();
+}
+
 __global__ __launch_bounds__(256) void iqpt_libm_kernel(int fn, const float* a, const float* b, float* out,
                                                         uint32_t n) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -3161,7 +3173,6 @@ constexpr uint32_t kSpecLanes = 16;                    // lanes per sphere pixel
 constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per block without a plan
 constexpr uint32_t kSpecMaxPix = 32;                   // pixels per block at 8 lanes each
 constexpr uint32_t kSpecBatch = 512;                   // walk: chain samples gathered per block and batch
-constexpr uint8_t kSpecPend = 0xffu;                   // predicted chains: a slot whose camera ray hit a sphere
 static_assert(kSpecPix == kSpecPixPerBlock && kSpecMaxPix == kSpecMaxPixPerBlock, "runtime and kernel agree on the spec block");
 
 // Scatter records a spec lane keeps: one per bounce that continues (depth + 1 < max_depth); the last scatter
@@ -3248,9 +3259,13 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         rd[9] = a[1];
         rd[10] = a[2];
         rd[11] = 0u;
-        rd[12] = 0u;
+        rd[12] = q;
         rd[13] = pix;
-        rd[14] = (s.even2 && !s.pred && s.rho[q] == 512u) ? 1u : 0u;   // its last chain's samples took two slots each
+        // parity pixel (round 0 traces the even slots first): its last chain took at least s.parity_rho / 256
+        // slots per sample (two-slot samples: camera ray, sphere, scattered ray); 0 = every slot (round 4)
+        const uint32_t r0 = s.rho[q] ? s.rho[q] : s.rho0;
+        rd[14] = (s.parity_rho != 0u && r0 >= s.parity_rho) ? 1u : 0u;
+        rd[15] = 0u;
     } else if (!valid && l == 0u) {
         // no pixel (the grid's last block): an empty, finished record (every field is read by the rounds)
         for (uint32_t i = 0; i < 16u; ++i) rd[i] = 0u;
@@ -3269,13 +3284,13 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     while (__syncthreads_or(rd[7] == 0u)) {
         const bool live = rd[7] == 0u;
         const uint32_t js = rd[0], M = rd[1];
-        // ---- slots [js + j0, js + j1) of this lane, relative slot indices j. Every slot of the window is
-        // traced, or (rd[14], round 0 of a pixel whose last chain took exactly two slots per sample) only
-        // the even ones: a chain of 2-slot samples from slot 0 visits even slots alone, and the first odd
-        // slot it lands on (a sample of 1 or 3 slots) ends the round there; the next round traces every
-        // slot from it
+        // ---- slot pass: slots [js + j0, js + j1) of this lane (relative slot indices j). Every slot of the
+        // window, or (rd[14]: round 0 of a parity pixel) its even slots only: a pixel whose samples take two
+        // slots each (camera ray, sphere, scattered ray) has a chain 0, 2, 4, ... of even slots, so the odd
+        // ones (the scatters' draws) need tracing only from where the chain first lands on one (a sample of one
+        // or three slots): the fix-up pass below, pooled over the block's lanes
         const uint32_t step = rd[14] != 0u ? 2u : 1u;
-        const uint32_t ME = (M + step - 1u) / step;      // slots of the window this round traces
+        const uint32_t ME = (M + step - 1u) / step;     // slots this pass traces
         auto start_of = [&](uint32_t k) { return step * (ME * k / L); };
         const uint32_t j0 = start_of(l), j1 = start_of(l + 1u);
         rng6 st = {rd[2], rd[3], rd[4], rd[5], rd[6], p.rng[5 * (size_t)p.npix + rd[13]] + 2u * (js + j0) * IQ_XORWOW_WEYL};
@@ -3285,299 +3300,172 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         lst[l * 5u + 2u] = st.v2;
         lst[l * 5u + 3u] = st.v3;
         lst[l * 5u + 4u] = st.v4;
-        if (s.pred) {
-            // ---- predicted chains (kspec::pred), phase A: the camera ray of every slot of the
-            // window, one per lane per iteration — every lane at depth 0, so every iteration takes the tile
-            // masks. A ray that ends (an emissive triangle, the sky) is the whole sample: its colour and one
-            // slot. A ray that hits a sphere leaves its hit (t, sphere) and the mark kSpecPend; the walk
-            // completes such samples along the chain only.
-            uint32_t j = j0;
-            bool active = live && j0 < j1;
-            while (__any(active)) {
-                if (rec_w) ++iters;
-                ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-                if (active) camera_ray<OPT>(p, px, py, st, ray);   // st: slot j + 1's start
-                float closest = kTMax;
-                int kind = kHitNone;
-                uint32_t hidx = 0;
-                {
-                    const uint32_t* lane_mask = active ? p.cull + (size_t)lds_cm[g].z * p.cull_stride : nullptr;
-                    uint4 cm = lds_cm[g];
-                    const uint64_t act = __ballot(active);
-                    const uint32_t first = (uint32_t)__builtin_ctzll(act);
-                    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
-                    const bool uni = __ballot(active && cm.z != t0) == 0ull;
-                    if (uni) {
-                        cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
-                        cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
-                    }
-                    const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
-                    intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, false, active, ray,
-                                          closest, kind, hidx, p.cull_wt, uni_mask);
-                }
-                if (active) {
-                    if (kind == kHitSphere) {
-                        res[j] = make_float4(closest, __uint_as_float(hidx), 0.0f, 0.0f);
-                        ln[j] = kSpecPend;
-                    } else {
-                        // emissive(1, 10) or the sky gradient (:308-313), clamped (:345-347), 0 + colour
-                        float cx = 10.0f, cy = 10.0f, cz = 10.0f;
-                        if (kind != kHitTri) {
-                            const float a = (ray.dy + 1.0f) * 0.5f;
-                            const float one_a = 1.0f - a;
-                            cx = one_a + a * 0.5f;
-                            cy = one_a + a * 0.7f;
-                            cz = one_a + a * 1.0f;
-                        }
-                        cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-                        cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-                        cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                        res[j] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
-                        ln[j] = 1u;
-                    }
-                    if (++j == j1) active = false;
-                }
-            }
-        } else {
-        uint32_t j = j0;
+
+        // The lane's slots: consecutive slots j, j + sp, ... < je of pixel group gg (its own in the slot pass;
+        // in the fix-up pass a run of another pixel's odd slots, several runs in turn). Each slot is a whole
+        // sample from its start state; the next one starts sp slots further (2 sp draws after this one's start:
+        // the 2 camera draws then 2 (sp - 1) more).
+        uint32_t gg = g, jc = j0, je = j1, sp = step;
+        uint32_t cpx = px, cpy = py;
+        float4* cres = res;
+        uint8_t* cln = ln;
         bool active = live && j0 < j1;
+        // fix-up pass: this lane's share [fa, fb) of the block's pooled odd slots (lds_w holds the prefix sums
+        // over the block's pixels of their fix-up slot counts)
+        uint32_t fa = 0, fb = 0;
+        bool fix = false;
         ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
         int depth = 0;
         rng6 base = st;
         // a slot's sample starts here: its camera ray, and the state its two draws leave (the next slot's)
         auto start_slot = [&]() {
-            camera_ray<OPT>(p, px, py, st, ray);
+            camera_ray<OPT>(p, cpx, cpy, st, ray);
             base = st;
             depth = 0;
         };
-        if (active) start_slot();
-        while (__any(active)) {
-            if (rec_w) ++iters;
-            // closest hit (path_tracer.cu:253-295): camera rays over their tile's mask pairs in index order
-            float closest = kTMax;
-            int kind = kHitNone;
-            uint32_t hidx = 0;
-            {
-                const bool cull = !__any(active && depth != 0);
-                const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[g].z * p.cull_stride : nullptr;
-                uint4 cm = lds_cm[g];
-                const uint64_t act = __ballot(active);
-                const uint32_t first = (uint32_t)__builtin_ctzll(act);
-                const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
-                const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
-                if (uni) {
-                    cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
-                    cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
-                }
-                const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
-                intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray,
-                                      closest, kind, hidx, p.cull_wt, uni_mask);
-            }
-            if (active) {
-                // shade (path_tracer.cu:297-316) under the reference's materials
-                bool term = false;
-                uint32_t md_end = 0;
-                float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
-                if (kind == kHitSphere) {
-                    const float* sq = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
-                    const float sc = oren_nayar_scatter<OPT>(make_float4(sq[0], sq[2], sq[4], sq[6]), closest, ray, st);
-                    if (depth + 1 >= p.max_depth) {
-                        term = true;                 // the last record is this scatter (biased, :252)
-                        md_end = 1;
-                        Lx = sc;
-                        Ly = sc;
-                        Lz = sc;
-                    } else {
-                        lds_stk[(uint32_t)depth * kSpecBlock + threadIdx.x] = sc;
-                        ++depth;
+        // the next run of the fix-up share: pixel group gg holding pooled index fa, its odd slots from there on
+        // (within [fa, fb)), the state at the first one stepped from the nearest slot-pass start state below it
+        auto next_run = [&]() -> bool {
+            if (fa >= fb) return false;
+            uint32_t h = 0;
+            while (h + 1u < cnt && lds_w[h + 1u] <= fa) ++h;
+            const uint32_t* rh = lds_rd + h * 16u;
+            const uint32_t Mh = rh[1], jsh = rh[0], ph = rh[13];
+            const uint32_t n_here = min(fb, lds_w[h + 1u]) - fa;
+            jc = rh[15] + 2u * (fa - lds_w[h]);           // an odd slot at or after where the chain got stuck
+            je = jc + 2u * n_here;
+            fa += n_here;
+            gg = h;
+            sp = 2u;
+            uint32_t tcol = 0, trow = 0;
+            tile_decode(ph, p.ncols, p.nrows, &tcol, &trow);
+            cpx = p.x0 + tcol;
+            cpy = p.y0 + trow * p.ystep;
+            cres = reinterpret_cast<float4*>(s.res) + (size_t)rh[12] * s.m_cap;
+            cln = lds_n + (size_t)h * s.m_cap;
+            // the pass-0 ranges of pixel h (even starts: 2 (ME_h k / L))
+            const uint32_t MEh = (Mh + 1u) / 2u;
+            uint32_t kk = L - 1u;
+            while (kk > 0u && 2u * (MEh * kk / L) > jc) --kk;
+            const uint32_t jk = 2u * (MEh * kk / L);
+            const uint32_t* lh = lds_st + (size_t)h * L * 5u + kk * 5u;
+            st = {lh[0], lh[1], lh[2], lh[3], lh[4], p.rng[5 * (size_t)p.npix + ph] + 2u * (jsh + jc) * IQ_XORWOW_WEYL};
+            xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * (jc - jk));
+            (void)Mh;
+            return true;
+        };
+        auto trace = [&]() {
+            if (active) start_slot();
+            while (__any(active)) {
+                if (rec_w) ++iters;
+                // closest hit (path_tracer.cu:253-295): camera rays over their tile's mask pairs in index order
+                float closest = kTMax;
+                int kind = kHitNone;
+                uint32_t hidx = 0;
+                {
+                    const bool cull = !__any(active && depth != 0);
+                    uint4 cm = lds_cm[gg];
+                    const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)cm.z * p.cull_stride : nullptr;
+                    const uint64_t act = __ballot(active);
+                    const uint32_t first = (uint32_t)__builtin_ctzll(act);
+                    const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
+                    const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
+                    if (uni) {
+                        cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
+                        cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
                     }
-                } else if (kind == kHitTri) {
-                    term = true;                     // emissive(1, 10)
-                    Lx = 10.0f;
-                    Ly = 10.0f;
-                    Lz = 10.0f;
-                } else {
-                    term = true;                     // sky gradient, :308-313
-                    const float a = (ray.dy + 1.0f) * 0.5f;
-                    const float one_a = 1.0f - a;
-                    Lx = one_a + a * 0.5f;
-                    Ly = one_a + a * 0.7f;
-                    Lz = one_a + a * 1.0f;
+                    const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
+                    intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray,
+                                          closest, kind, hidx, p.cull_wt, uni_mask);
                 }
-                if (term) {
-                    // backward product (:321-324), clamp (:345-347), 0 + colour (:341, 348)
-                    float cx = Lx, cy = Ly, cz = Lz;
-                    for (int i = depth - 1; i >= 0; --i) {
-                        const float rr = lds_stk[(uint32_t)i * kSpecBlock + threadIdx.x];
-                        cx = cx * rr;
-                        cy = cy * rr;
-                        cz = cz * rr;
-                    }
-                    cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-                    cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-                    cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                    res[j] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
-                    ln[j] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
-                    if (step == 2u && j + 1u < M) ln[j + 1u] = 0u;       // untraced: ends the walk there
-                    j += step;
-                    if (j >= j1) {
-                        active = false;
-                    } else {
-                        st = base;                   // slot j starts where slot j - 1's camera draws ended
-                        if (step == 2u) {            // ... two draws after slot j - 1's start
-                            (void)xorwow_next(st);
-                            (void)xorwow_next(st);
+                if (active) {
+                    // shade (path_tracer.cu:297-316) under the reference's materials
+                    bool term = false;
+                    uint32_t md_end = 0;
+                    float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
+                    if (kind == kHitSphere) {
+                        const float* sq = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
+                        const float sc = oren_nayar_scatter<OPT>(make_float4(sq[0], sq[2], sq[4], sq[6]), closest, ray, st);
+                        if (depth + 1 >= p.max_depth) {
+                            term = true;                 // the last record is this scatter (biased, :252)
+                            md_end = 1;
+                            Lx = sc;
+                            Ly = sc;
+                            Lz = sc;
+                        } else {
+                            lds_stk[(uint32_t)depth * kSpecBlock + threadIdx.x] = sc;
+                            ++depth;
                         }
-                        start_slot();
+                    } else if (kind == kHitTri) {
+                        term = true;                     // emissive(1, 10)
+                        Lx = 10.0f;
+                        Ly = 10.0f;
+                        Lz = 10.0f;
+                    } else {
+                        term = true;                     // sky gradient, :308-313
+                        const float a = (ray.dy + 1.0f) * 0.5f;
+                        const float one_a = 1.0f - a;
+                        Lx = one_a + a * 0.5f;
+                        Ly = one_a + a * 0.7f;
+                        Lz = one_a + a * 1.0f;
+                    }
+                    if (term) {
+                        // backward product (:321-324), clamp (:345-347), 0 + colour (:341, 348)
+                        float cx = Lx, cy = Ly, cz = Lz;
+                        for (int i = depth - 1; i >= 0; --i) {
+                            const float rr = lds_stk[(uint32_t)i * kSpecBlock + threadIdx.x];
+                            cx = cx * rr;
+                            cy = cy * rr;
+                            cz = cz * rr;
+                        }
+                        cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                        cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                        cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                        cres[jc] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                        cln[jc] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
+                        // slot pass over even slots: the odd slot after this one is untraced (0: the walk stops there)
+                        if (!fix && sp == 2u && jc + 1u < M) cln[jc + 1u] = 0u;
+                        jc += sp;
+                        if (jc < je) {
+                            st = base;                   // slot jc starts where slot jc - 1's camera draws ended ...
+                            if (sp == 2u) {              // ... or two draws after that
+                                (void)xorwow_next(st);
+                                (void)xorwow_next(st);
+                            }
+                            start_slot();
+                        } else if (next_run()) {
+                            start_slot();
+                        } else {
+                            active = false;
+                        }
                     }
                 }
             }
-        }
-        }
-
-        // ---- walk: the colours are this block's own stores (complete: vmcnt 0), read back from L2
-        __builtin_amdgcn_s_waitcnt(0);
-        __syncthreads();
-        if (rec && rounds == 0u) t_rec[1] = __builtin_amdgcn_s_memrealtime();
+        };
         uint32_t jw = 0;                                 // walker: the chain's next relative slot
         uint16_t* lp = lds_pos + g * batch;
         float ax = __uint_as_float(rd[8]), ay = __uint_as_float(rd[9]), az = __uint_as_float(rd[10]);
         uint32_t k = rd[11];
-        if (s.pred) {
-            const uint32_t d0 = p.rng[5 * (size_t)p.npix + rd[13]];
-            // phase B, batch by batch: the chain's next positions as predicted (a pending sample takes two
-            // slots: camera ray, sphere, scattered ray, then an emissive wall or the sky), the pending samples
-            // among them completed by the pixel's lanes, the chain checked against their true slot counts —
-            // it runs up to the first sample that took other than two (a second sphere, max_depth), and the
-            // next batch starts where that sample really ends — then folded as below
-            while (__syncthreads_or(walker && live && k < p.spp && jw < M)) {
+        // batches of chain samples up to the window's end, the launch's spp, or a slot not traced yet (an odd
+        // slot of a parity pixel before the fix-up pass)
+        auto walk = [&]() {
+            for (uint32_t r0 = 0; r0 < p.spp; r0 += batch) {
                 if (walker && live) {
-                    uint32_t c = 0, jj = jw;
-                    while (c < batch && k + c < p.spp && jj < M) {
-                        lp[c++] = (uint16_t)jj;
-                        const uint32_t nj = ln[jj];
-                        jj += nj == kSpecPend ? 2u : nj;
+                    uint32_t c = 0;
+                    while (c < batch && k + c < p.spp && jw < M) {
+                        const uint32_t nj = ln[jw];
+                        if (nj == 0u) break;
+                        lp[c++] = (uint16_t)jw;
+                        jw += nj;
                     }
                     lds_w[2 * g] = c;
                 }
                 __syncthreads();
                 const uint32_t cw = (valid && live) ? lds_w[2 * g] : 0u;
-                {
-                    uint32_t ii = l, jc = 0;
-                    bool active = false, resume = false;
-                    ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-                    rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
-                    int depth = 0;
-                    float r_closest = 0.0f;
-                    uint32_t r_hidx = 0;
-                    // this lane's next pending position (l, l + L, ...): the slot's state from its range's
-                    // start state stepped on, its camera ray again, the hit phase A left
-                    auto next_pending = [&]() {
-                        active = false;
-                        while (ii < cw) {
-                            const uint32_t jp = lp[ii];
-                            ii += L;
-                            if (ln[jp] != kSpecPend) continue;
-                            uint32_t kk = L - 1u;
-                            while (kk > 0u && start_of(kk) > jp) --kk;
-                            const uint32_t jk = start_of(kk);
-                            st.v0 = lst[kk * 5u];
-                            st.v1 = lst[kk * 5u + 1u];
-                            st.v2 = lst[kk * 5u + 2u];
-                            st.v3 = lst[kk * 5u + 3u];
-                            st.v4 = lst[kk * 5u + 4u];
-                            xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * (jp - jk));
-                            st.d = d0 + 2u * (js + jp) * IQ_XORWOW_WEYL;
-                            camera_ray<OPT>(p, px, py, st, ray);
-                            const uint32_t* src = reinterpret_cast<const uint32_t*>(res + jp);
-                            r_closest = __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                            r_hidx = __hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                            jc = jp;
-                            depth = 0;
-                            resume = true;
-                            active = true;
-                            return;
-                        }
-                    };
-                    next_pending();
-                    while (__any(active)) {
-                        if (rec_w) ++iters;
-                        // scattered rays over every pair (a resumed sample's camera ray has its hit already)
-                        float closest = kTMax;
-                        int kind = kHitNone;
-                        uint32_t hidx = 0;
-                        intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, nullptr, 0u, 0u, true, active && !resume,
-                                              ray, closest, kind, hidx, p.cull_wt, nullptr);
-                        if (resume) {
-                            closest = r_closest;
-                            kind = kHitSphere;
-                            hidx = r_hidx;
-                            resume = false;
-                        }
-                        if (active) {
-                            bool term = false;
-                            uint32_t md_end = 0;
-                            float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
-                            if (kind == kHitSphere) {
-                                const float* sq = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
-                                const float sc = oren_nayar_scatter<OPT>(make_float4(sq[0], sq[2], sq[4], sq[6]), closest, ray, st);
-                                if (depth + 1 >= p.max_depth) {
-                                    term = true;
-                                    md_end = 1;
-                                    Lx = sc;
-                                    Ly = sc;
-                                    Lz = sc;
-                                } else {
-                                    lds_stk[(uint32_t)depth * kSpecBlock + threadIdx.x] = sc;
-                                    ++depth;
-                                }
-                            } else if (kind == kHitTri) {
-                                term = true;
-                                Lx = 10.0f;
-                                Ly = 10.0f;
-                                Lz = 10.0f;
-                            } else {
-                                term = true;
-                                const float a = (ray.dy + 1.0f) * 0.5f;
-                                const float one_a = 1.0f - a;
-                                Lx = one_a + a * 0.5f;
-                                Ly = one_a + a * 0.7f;
-                                Lz = one_a + a * 1.0f;
-                            }
-                            if (term) {
-                                float cx = Lx, cy = Ly, cz = Lz;
-                                for (int i = depth - 1; i >= 0; --i) {
-                                    const float rr = lds_stk[(uint32_t)i * kSpecBlock + threadIdx.x];
-                                    cx = cx * rr;
-                                    cy = cy * rr;
-                                    cz = cz * rr;
-                                }
-                                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-                                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-                                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                                res[jc] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
-                                ln[jc] = (uint8_t)((uint32_t)depth + 1u + md_end);
-                                next_pending();
-                            }
-                        }
-                    }
-                }
-                __builtin_amdgcn_s_waitcnt(0);
-                __syncthreads();
-                // the chain through the batch: up to the first position the true slot counts do not reach
-                if (walker && live) {
-                    uint32_t c2 = 0, jn = jw;
-                    for (uint32_t i = 0; i < cw; ++i) {
-                        if (lp[i] != jn) break;
-                        jn = lp[i] + ln[lp[i]];
-                        c2 = i + 1u;
-                    }
-                    lds_w[2 * g] = c2;
-                    lds_w[2 * g + 1] = jn;
-                }
-                __syncthreads();
-                const uint32_t cv = (valid && live) ? lds_w[2 * g] : 0u;
-                for (uint32_t i = l; i < cv; i += L) {
+                // the pixel's lanes gather the chain samples' colours and form their mean terms c / n and
+                // (n - 1) / n (sample k of the launch), and count their rays: the walker is left the
+                // multiply-add chain of the running mean alone
+                for (uint32_t i = l; i < cw; i += L) {
                     const uint32_t* src = reinterpret_cast<const uint32_t*>(res + lp[i]);
                     const float cx = __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
                     const float cy = __uint_as_float(__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
@@ -3590,58 +3478,49 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                     lane_rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
                 }
                 __syncthreads();
-                if (walker && live) {
+                if (walker && live)
 #pragma unroll 4
-                    for (uint32_t i = 0; i < cv; ++i) {
+                    for (uint32_t i = 0; i < cw; ++i) {
                         const float4 v = lds_c[g * batch + i];
                         ax = v.x + ax * v.w;
                         ay = v.y + ay * v.w;
                         az = v.z + az * v.w;
                     }
-                    jw = lds_w[2 * g + 1];
-                }
-                k += cv;
+                k += cw;
+                __syncthreads();
             }
-        } else
-        for (uint32_t r0 = 0; r0 < p.spp; r0 += batch) {
-            if (walker && live) {
-                uint32_t c = 0;
-                while (c < batch && k + c < p.spp && jw < M) {
-                    const uint32_t nj = ln[jw];
-                    if (nj == 0u) break;                 // an untraced (odd) slot: the round ends here
-                    lp[c++] = (uint16_t)jw;
-                    jw += nj;
-                }
-                lds_w[2 * g] = c;
-            }
+        };
+        // the slot pass and its walk, then (parity pixels whose chain landed on an odd slot at jw, if any in the
+        // block) the fix-up pass — every odd slot from there to the window's end, the even ones being traced, so
+        // the walk then runs to the window's end — and the walk again. The block's fix-up slots are pooled and
+        // shared evenly by all its lanes: a few chains need them, most do not.
+        for (uint32_t pass = 0;; ++pass) {
+            trace();
+            // walk: the colours are this block's own stores (complete: vmcnt 0), read back from L2
+            __builtin_amdgcn_s_waitcnt(0);
             __syncthreads();
-            const uint32_t cw = (valid && live) ? lds_w[2 * g] : 0u;
-            // the pixel's lanes gather the chain samples' colours and form their mean terms c / n and
-            // (n - 1) / n (sample k of the launch), and count their rays: the walker is left the
-            // multiply-add chain of the running mean alone
-            for (uint32_t i = l; i < cw; i += L) {
-                const uint32_t* src = reinterpret_cast<const uint32_t*>(res + lp[i]);
-                const float cx = __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                const float cy = __uint_as_float(__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                const float cz = __uint_as_float(__hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                const float2 tv = tab[k + i];
-                float qx, qy, qz;
-                mean_terms<OPT>(cx, cy, cz, tab_n[k + i], tv.x, p.mean_tiny, qx, qy, qz);
-                lds_c[g * batch + i] = make_float4(qx, qy, qz, tv.y);
-                const uint32_t n = ln[lp[i]];
-                lane_rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
+            if (rec && rounds == 0u && pass == 0u) t_rec[1] = __builtin_amdgcn_s_memrealtime();
+            walk();
+            if (pass == 1u) break;
+            const bool stuck = walker && live && k < p.spp && jw < M && ln[jw] == 0u;
+            if (!__syncthreads_or(stuck)) break;
+            if (walker) rd[15] = stuck ? jw : M;
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                uint32_t acc = 0;
+                for (uint32_t h = 0; h < cnt; ++h) {
+                    lds_w[h] = acc;
+                    const uint32_t* rh = lds_rd + h * 16u;
+                    if (rh[7] == 0u && rh[15] < rh[1]) acc += (rh[1] - rh[15] + 1u) / 2u;
+                }
+                lds_w[cnt] = acc;
             }
             __syncthreads();
-            if (walker && live)
-#pragma unroll 4
-                for (uint32_t i = 0; i < cw; ++i) {
-                    const float4 v = lds_c[g * batch + i];
-                    ax = v.x + ax * v.w;
-                    ay = v.y + ay * v.w;
-                    az = v.z + az * v.w;
-                }
-            k += cw;
-            __syncthreads();
+            const uint32_t F = lds_w[cnt];
+            fa = (uint32_t)(((uint64_t)F * threadIdx.x) / kSpecBlock);
+            fb = (uint32_t)(((uint64_t)F * (threadIdx.x + 1u)) / kSpecBlock);
+            fix = true;
+            active = next_run();
         }
         if (walker && live) {
             rd[8] = __float_as_uint(ax);
@@ -3650,7 +3529,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             rd[11] = k;
             const uint32_t pix = rd[13];
             // the state at the chain's end, slot js + jw: from the start of the last range at or below it
-            // (the lanes' start slots, as in the slot phase)
+            // (the lanes' start slots, as in the slot pass)
             uint32_t kk = L - 1u;
             while (kk > 0u && start_of(kk) > jw) --kk;
             const uint32_t jk = start_of(kk);
@@ -3679,11 +3558,12 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                 p.rng[5 * (size_t)p.npix + pix] = p.rng[5 * (size_t)p.npix + pix] + 2u * jt * IQ_XORWOW_WEYL;
                 s.rho[q] = (uint32_t)(((uint64_t)jt * 256u) / p.spp);
             } else {
-                // the chain left its window: a new one from its end, sized for the remaining samples
+                // the chain left its window: a new one from its end, sized for the remaining samples, every
+                // slot traced
                 atomicAdd(s.run_count + 1, 1u);
                 const uint32_t rem = p.spp - k;
                 rd[1] = min(s.m_cap, max(16u, 3u * rem + 4u));
-                rd[14] = 0u;                           // later rounds trace every slot
+                rd[14] = 0u;
             }
         }
         if (rec && rounds == 0u) t_rec[2] = __builtin_amdgcn_s_memrealtime();
@@ -3787,28 +3667,6 @@ __global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p)
 template <int MAXD, int OPT>
 __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams p, const kspec s) {
     spec_body<MAXD, OPT>(p, s, blockIdx.x);
-}
-
-// Spec and fan blocks in one launch: the sphere pixels' blocks and the fan tiles share
-// one grid, so the launch needs no second stream and no cross-queue join (two event hops per launch).
-// The first s.lead blocks are spec blocks (the longest chains start first); the other spec blocks are
-// spread evenly among the fan blocks: of the positions b' = b - lead, a(b') = floor((b' + 1) R / (R + F))
-// of the first b' + 1 are spec blocks (R = spec blocks left, F = fan tiles).
-template <int MAXD, int OPT>
-__global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specfan_kernel(const kparams p, const kspec s) {
-    const uint32_t ns = s.blocks ? s.nblocks : (s.n + kSpecPix - 1u) / kSpecPix;
-    const uint32_t lead = min(s.lead, ns);
-    const uint32_t b = blockIdx.x;
-    if (b < lead) {
-        spec_body<MAXD, OPT>(p, s, b);
-        return;
-    }
-    const uint64_t r = ns - lead, tot = r + s.fan_tiles, bp = b - lead;
-    const uint32_t a1 = (uint32_t)(((bp + 1u) * r) / tot), a0 = (uint32_t)((bp * r) / tot);
-    if (a1 > a0)
-        spec_body<MAXD, OPT>(p, s, lead + a0);
-    else
-        fan_body<OPT>(p, (uint32_t)(bp - a1));
 }
 
 // LDS bytes of the chain kernel for a launch (scene pairs, mean table, mask slots, ring, group words,
@@ -3946,6 +3804,13 @@ int launch_assemble_rows(void* stream, const uint32_t* src, uint32_t* dst, uint3
     if (n == 0) return 0;
     hipLaunchKernelGGL(iqpt_assemble_rows_kernel, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                        src, dst, width, height, world, split, base, stride, words);
+    return (int)hipGetLastError();
+}
+
+int launch_lds_poison(void* stream, uint32_t pattern, uint32_t lds_bytes, uint32_t blocks) {
+    if (blocks == 0 || lds_bytes < 4) return 0;
+    hipLaunchKernelGGL(iqpt_lds_poison_kernel, dim3(blocks), dim3(256), lds_bytes, (hipStream_t)stream, pattern,
+                       lds_bytes / 4u);
     return (int)hipGetLastError();
 }
 
@@ -4114,7 +3979,9 @@ const sky_variant kSkyVariants[] = {
     {kOptFastDiv | kOptCamAxis, sky_launch_t<kOptDefault | kOptCamAxis>},
 };
 const sky_variant* find_sky(int opt) {
-    if ((opt & (kOptAccTable | kOptCamConst)) != (kOptAccTable | kOptCamConst) || (opt & (kOptMaterials | kOptStats)))
+    // (kOptStats launches keep the sky kernel: it runs no intersection test, and the instrumented plain kernel
+    // beside it then counts the tests of the pixels it renders in production, tools/work_counters.py)
+    if ((opt & (kOptAccTable | kOptCamConst)) != (kOptAccTable | kOptCamConst) || (opt & kOptMaterials))
         return nullptr;
     for (const sky_variant& v : kSkyVariants)
         if (v.key == (opt & kFanKeyBits)) return &v;
@@ -4150,23 +4017,15 @@ int spec_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t
     return (int)hipGetLastError();
 }
 template <int MAXD, int OPT>
-int specfan_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_specfan_kernel<MAXD, OPT>),
-                       dim3((s.blocks ? s.nblocks : (s.n + kSpecPix - 1u) / kSpecPix) + s.fan_tiles),
-                       dim3(kSpecBlock), lds, stream, p, s);
-    return (int)hipGetLastError();
-}
-template <int MAXD, int OPT>
 int spec_occ_t(uint32_t lds, int* blocks) {
     return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_spec_kernel<MAXD, OPT>, kSpecBlock, lds);
 }
 struct spec_variant {
     int maxd, opt;
     int (*launch)(hipStream_t, const kparams&, const kspec&, uint32_t);
-    int (*launch_fused)(hipStream_t, const kparams&, const kspec&, uint32_t);
     int (*occ)(uint32_t, int*);
 };
-#define IQPT_SV(M, O) {M, O, spec_launch_t<M, O>, specfan_launch_t<M, O>, spec_occ_t<M, O>}
+#define IQPT_SV(M, O) {M, O, spec_launch_t<M, O>, spec_occ_t<M, O>}
 #define IQPT_SV2(O) IQPT_SV(8, O), IQPT_SV(16, O)
 const spec_variant kSpecVariants[] = {
     IQPT_SV2(kOptDefault | kOptPrio),
@@ -4201,16 +4060,6 @@ int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks) {
     const spec_variant* v = find_spec(p.max_depth, opt);
     if (!v) return (int)hipErrorInvalidDeviceFunction;
     return v->occ(spec_lds(p, s), blocks);
-}
-
-int launch_specfan(void* stream, const kparams& p, const kspec& s, int opt) {
-    const spec_variant* v = find_spec(p.max_depth, opt);
-    if (!v || !find_fan(opt) || p.max_depth > 16 || p.cull == nullptr || p.cull_wt > 16u || p.spp > kAccTableMax ||
-        s.m_cap > 65535u || (s.fan_tiles > 0 && p.tile_order == nullptr))
-        return (int)hipErrorInvalidDeviceFunction;
-    if (p.spp == 0 || (s.n == 0 && s.fan_tiles == 0)) return 0;
-    const uint32_t ls = spec_lds(p, s), lf = fan_lds(p);
-    return v->launch_fused((hipStream_t)stream, p, s, ls > lf ? ls : lf);
 }
 
 bool chain_variant_exists(int max_depth, int opt, uint32_t lanes) {

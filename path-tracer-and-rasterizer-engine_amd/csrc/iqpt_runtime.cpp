@@ -209,10 +209,9 @@ struct iqpt_ctx {
                                             // against 1/4, 5 % of the chains take a second round instead of 0.6 %,
                                             // yet -4 % per launch at N = 2 / 4 / 8, profiles/r03/spec_margins.json)
     // spec launches (iqpt_debug_set_specfan): 0 the two kernels on two streams, pipelined (the default), 1 one
-    // after the other on one stream (measurement), 2 spec + fan blocks in one grid (iqpt_specfan_kernel)
+    // after the other on one stream (measurement)
     int specfan_mode = 0;
     bool fan_pipe = true;                // FAN launches pipelined (iqpt_debug_set_pipe)
-    uint32_t spec_lead = 0xffffffffu;       // fused: spec blocks ahead of every fan block (all by default)
     // spec plan: the sphere pixels ordered by their last chain's work, heaviest first, the
     // heavy ones with 32 or 64 lanes; built on the host from an asynchronous read of the history (performance
     // only: every plan gives the same bits). iqpt_debug_spec_plan: 0 off, 1 asynchronous (default), 2..5
@@ -237,23 +236,6 @@ struct iqpt_ctx {
     bool pipe = false;                   // the last launch was pipelined and nothing has joined since
     int pipe_kind = 0;                   // ... a spec launch (1) or a fan launch (2)
     hipStream_t stream3 = nullptr;
-    // hybrid launches: the spec kernel over the sphere pixels on `stream4`, pipelined across
-    // launches, beside the overlapped plain kernel (which skips those pixels, d_skip) and the sky kernel
-    hipStream_t stream4 = nullptr;
-    int hybrid_mode = 0;                // iqpt_debug_set_hybrid: 0 off, 1 on (overlapped plain launches only)
-    bool hyb_pend = false;              // a hybrid spec kernel is in flight on stream4 (joined by join_streams)
-    bool hybrid_last = false;           // the last launch was hybrid
-    hipEvent_t ev_h0 = nullptr, ev_spec4 = nullptr;
-    uint32_t* d_skip = nullptr;         // per tile (2 words): pixels the plain kernel skips in hybrid launches —
-                                        // the sphere pixels (the spec kernel's) and, with the sky kernel, the misses
-    std::vector<uint64_t> h_specmask;   // per tile: its sphere pixels (build_pixel_split)
-    std::vector<uint32_t> h_chain_pix;  // the sphere pixels' storage indices (d_chain_pix on the host)
-    // hybrid selection: only sphere pixels whose last chain used >= hybrid_rho slots per sample (x 256) go to the
-    // spec kernel (0: all); chosen from the history once it arrives, applied at a join (plan + skip masks)
-    uint32_t hybrid_rho = 0;
-    bool hyb_sel = false;               // d_skip_sel and the plan hold a selection
-    uint32_t hyb_sel_n = 0;             // pixels selected
-    uint32_t* d_skip_sel = nullptr;     // per tile (2 words): the selection's pixels | misses (sky kernel on)
     hipEvent_t ev_pipe_end = nullptr;    // on `stream`, recorded by a copy behind a pipelined launch
     // the events the last pipelined launch's kernels recorded at their ends on `stream` / `stream2` (timing
     // events bound to the dispatches), or null: a copy behind the launch waits for them instead of recording
@@ -342,10 +324,8 @@ struct iqpt_ctx {
     int gather_skip = 0;                 // measurement only: 1 skips the collective, 2 the root's assembly,
                                          // 4 the render streams' waits for the frame copies
     bool timing_on = true;               // the launches' timing events (iqpt_debug_set_timing)
-    bool spec_even = false;              // kspec::even2 (iqpt_debug_set_spec_even)
     bool sky_after = true;               // overlapped launches: the sky kernel behind the plain kernel (r04 run 35:
                                          // 0.988-0.992 -> 0.975-0.982 ms per C2 step)
-    bool spec_pred = false;              // kspec::pred (iqpt_debug_set_spec_pred; measured slower, r04 run 25)
 };
 
 namespace {
@@ -373,10 +353,6 @@ int join_streams(iqpt_ctx* c) {
     c->ovl_zero = true;
     c->last_ovl = false;
     c->sky_last = nullptr;             // everything before is ordered on `stream` now
-    if (c->hyb_pend) {
-        IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_spec4, 0));
-        c->hyb_pend = false;
-    }
     return IQPT_OK;
 }
 
@@ -442,11 +418,6 @@ void free_split(iqpt_ctx* c) {
     if (c->d_fan_lanes) (void)hipFree(c->d_fan_lanes);
     c->d_fan_lanes = nullptr;
     c->n_chain_pix = c->n_fan_tiles = 0;
-    if (c->d_skip) (void)hipFree(c->d_skip);
-    c->d_skip = nullptr;
-    if (c->d_skip_sel) (void)hipFree(c->d_skip_sel);
-    c->d_skip_sel = nullptr;
-    c->hyb_sel = false;
     c->spec_rho_valid = false;           // a new pixel list: no chain history, no plan
     c->spec_plan_n = 0;
     c->spec_rho_pending = false;
@@ -489,12 +460,14 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
     uint32_t cc = 0;
     cam_constants(c->cam, &cc, &ci.near_rw, &ci.far_rw);
     ci.cam_const = (int)cc;
-    c->h_specmask.assign((size_t)c->cull_ntx * c->cull_nty, 0ull);
     for (size_t st = 0; st < split.size(); ++st) {
         uint64_t lanes = 0;
         for (uint32_t i = 0; i < iqpt::kQueueChunk; ++i) {
             const uint32_t pix = sp_pix[st * iqpt::kQueueChunk + i];
             if (pix == ~0u) continue;
+            // a certain miss is the sky kernel's whenever it runs (also without the per-pixel test below:
+            // ADVICE r4, a resident scene of more than 64 spheres put them in the spec / chain list as well)
+            if (sky && ((c->h_miss[split[st]] >> i) & 1ull)) continue;
             bool sphere = !per_pixel;
             if (per_pixel) {
                 uint32_t col, row;
@@ -508,7 +481,6 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
             }
             if (sphere) {
                 chain_pix.push_back(pix);
-                c->h_specmask[split[st]] |= 1ull << i;
             } else {
                 lanes |= 1ull << i;
             }
@@ -533,23 +505,6 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
     }
     c->n_chain_pix = (uint32_t)chain_pix.size();
     c->n_fan_tiles = (uint32_t)fan_tiles.size();
-    c->h_chain_pix = chain_pix;
-    c->hyb_sel = false;
-    // hybrid launches: the plain kernel skips the sphere pixels and (sky kernel on) the certain misses
-    if (c->d_skip) (void)hipFree(c->d_skip);
-    c->d_skip = nullptr;
-    if (per_pixel && !chain_pix.empty()) {
-        const size_t nt = (size_t)c->cull_ntx * c->cull_nty;
-        std::vector<uint32_t> skip(2 * nt);
-        for (size_t t = 0; t < nt; ++t) {
-            const uint64_t m = c->h_specmask[t] | (sky ? c->h_miss[t] : 0ull);
-            skip[2 * t] = (uint32_t)m;
-            skip[2 * t + 1] = (uint32_t)(m >> 32);
-        }
-        if (hipMalloc(&c->d_skip, skip.size() * sizeof(uint32_t)) != hipSuccess)
-            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "hybrid skip masks");
-        IQPT_HIP(hipMemcpy(c->d_skip, skip.data(), skip.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-    }
     return IQPT_OK;
 }
 
@@ -562,23 +517,15 @@ int build_pixel_split(iqpt_ctx* c, const std::vector<uint32_t>& anchor, const st
 // <= E. Each block holds one lane class (256 lanes), pixels sorted by work per lane, and the blocks run
 // heaviest per lane first, so the launch's longest block starts first and light blocks fill the tail.
 uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec& ks, int opt, const uint32_t* rho,
-                         uint32_t* h, const std::vector<char>* sel = nullptr) {
+                         uint32_t* h) {
     const uint32_t n = ks.n;
     std::vector<double> w(n);
     double total = 0.0, wmax = 0.0;
     for (uint32_t q = 0; q < n; ++q) {
-        if (sel && !(*sel)[q]) {          // hybrid selection: not the spec kernel's this time (no block)
-            w[q] = 0.0;
-            continue;
-        }
         const uint32_t r = rho[q] ? rho[q] : ks.rho0;
         const uint32_t m = iqpt::spec_window(r, p.spp, ks.m_cap, ks.margin_div);
-        // slots traced: the window's, or its even ones for a pixel whose last chain took two slots per
-        // sample (the kernel's round 0)
-        const uint32_t traced = (ks.even2 && !ks.pred && r == 512u) ? (m + 1u) / 2u : m;
-        // predicted chains: a camera ray per slot of the window, the rest of the chain's samples once
-        w[q] = ks.pred ? (double)m + (double)p.spp * (double)(std::max<uint32_t>(r, 256u) - 256u) / 256.0 * 2.0
-                       : (double)traced * (double)std::max<uint32_t>(r, 256u) / 256.0;
+        // slots traced (the window's) times their mean length
+        w[q] = (double)m * (double)std::max<uint32_t>(r, 256u) / 256.0;
         total += w[q];
         wmax = std::max(wmax, w[q]);
     }
@@ -597,8 +544,7 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     };
     auto lanes_at = [&](double e) {
         double sum = 0.0;
-        for (uint32_t q = 0; q < n; ++q)
-            if (!sel || (*sel)[q]) sum += (double)kLanes[cls_of(q, e)];
+        for (uint32_t q = 0; q < n; ++q) sum += (double)kLanes[cls_of(q, e)];
         return sum;
     };
     double e = total / cap;                      // several block-waves: balanced work per lane
@@ -628,19 +574,18 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     for (uint32_t q = 0; q < n; ++q) {
         const double pe = w[q] / (double)kLanes[cls[q]];
         const uint32_t b = emax > 0.0 ? std::min<uint32_t>(kB - 1, (uint32_t)(pe / emax * (kB - 1))) : 0u;
-        key[q] = (sel && !(*sel)[q]) ? kC * kB : (kTop - cls[q]) * kB + (kB - 1 - b);   // ascending key: most lanes
-        cnt[key[q] + 1]++;                                                                // first, heaviest first,
-    }                                                                                     // unselected last
+        key[q] = (kTop - cls[q]) * kB + (kB - 1 - b);   // ascending key: most lanes first, heaviest first
+        cnt[key[q] + 1]++;
+    }
     for (uint32_t k = 0; k < kC * kB + 1; ++k) cnt[k + 1] += cnt[k];
     for (uint32_t q = 0; q < n; ++q) h[cnt[key[q]]++] = q;
-    const uint32_t nsel = sel ? (uint32_t)std::count(sel->begin(), sel->end(), (char)1) : n;
     // blocks of one class, then ordered by their first (heaviest) pixel's work per lane
     struct blk { double e; uint32_t first, word; };
     std::vector<blk> blocks;
-    for (uint32_t i = 0; i < nsel;) {
+    for (uint32_t i = 0; i < n;) {
         const uint32_t k = cls[h[i]], per = (uint32_t)iqpt::kSpecBlockLanes / kLanes[k];
         uint32_t m = 0;
-        while (m < per && i + m < nsel && cls[h[i + m]] == k) ++m;
+        while (m < per && i + m < n && cls[h[i + m]] == k) ++m;
         blocks.push_back({w[h[i]] / (double)kLanes[k], i, m | (kLanes[k] << 8)});
         i += m;
     }
@@ -1364,7 +1309,6 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->stream2) (void)hipStreamSynchronize(c->stream2);
     if (c->stream3) (void)hipStreamSynchronize(c->stream3);
-    if (c->stream4) (void)hipStreamSynchronize(c->stream4);
     free_comm(c);
     free_scene(c);
     if (c->d_lin) (void)hipFree(c->d_lin);
@@ -1384,9 +1328,6 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
     if (c->stream2) (void)hipStreamDestroy(c->stream2);
     if (c->stream3) (void)hipStreamDestroy(c->stream3);
-    if (c->stream4) (void)hipStreamDestroy(c->stream4);
-    for (hipEvent_t e : {c->ev_h0, c->ev_spec4})
-        if (e) (void)hipEventDestroy(e);
     if (c->ev_pipe_end) (void)hipEventDestroy(c->ev_pipe_end);
     free_split(c);
     for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_tl, (void*)c->d_spec_plan})
@@ -1961,78 +1902,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
     }
     if (!ovl && !pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
-    // hybrid launches: overlapped plain launches whose sphere pixels — the longest per-pixel
-    // chains, which bound a launch at N = 1 — run in the spec kernel on stream4, pipelined across launches; the
-    // plain kernel skips them (and the certain misses, the sky kernel's: d_skip). A hybrid chain starts joined.
-    bool hybrid = false;
-    if (c->hybrid_mode != 0 && ovl && c->d_skip && c->n_chain_pix > 0 && !(opt & iqpt::kOptMaterials) &&
-        spp <= iqpt::kAccTableMax && iqpt::spec_variant_exists(c->max_depth, opt)) {
-        iqpt::kspec probe;
-        std::memset(&probe, 0, sizeof probe);
-        probe.m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
-        int occ_h = 0;
-        hybrid = iqpt::spec_lds(p, probe) <= c->lds_per_block && probe.m_cap <= 65535u &&
-                 iqpt::spec_occupancy(p, probe, opt, &occ_h) == 0 && occ_h >= 1;
-        (void)hipGetLastError();
-    }
-    if (hybrid && !c->hyb_pend && (st = join_streams(c)) != IQPT_OK) return st;
-    if (hybrid && c->hybrid_rho != 0 && c->spec_plan_mode == 1 && c->spec_rho_pending && c->spec_n >= c->n_chain_pix &&
-        c->h_chain_pix.size() == c->n_chain_pix && hipEventQuery(c->ev_spec_rho) == hipSuccess) {
-        // the chain history of an earlier launch is here: only the sphere pixels whose chains used >= hybrid_rho
-        // slots per sample (the launch's longest) stay with the spec kernel. The plan and the plain kernel's skip
-        // masks change together, from a state where nothing reads them (joined and synchronised)
-        if ((st = join_streams(c)) != IQPT_OK) return st;
-        IQPT_HIP(hipStreamSynchronize(c->stream));
-        const uint32_t n = c->n_chain_pix;
-        std::vector<char> sel(n, 0);
-        uint32_t nsel = 0;
-        for (uint32_t q = 0; q < n; ++q) {
-            sel[q] = (c->h_spec_rho[q] == 0u || c->h_spec_rho[q] >= c->hybrid_rho) ? 1 : 0;
-            nsel += (uint32_t)sel[q];
-        }
-        iqpt::kspec probe;
-        std::memset(&probe, 0, sizeof probe);
-        probe.n = n;
-        probe.m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
-        probe.rho0 = c->spec_rho0;
-        probe.margin_div = c->spec_margin_div;
-        probe.even2 = c->spec_even ? 1u : 0u;
-        probe.pred = c->spec_pred ? 1u : 0u;
-        const uint32_t nb = spec_build_plan(c, p, probe, opt, c->h_spec_rho, c->h_spec_plan, &sel);
-        IQPT_HIP(hipMemcpy(c->d_spec_plan, c->h_spec_plan, ((size_t)n + 2 * (size_t)nb) * sizeof(uint32_t),
-                           hipMemcpyHostToDevice));
-        c->spec_plan_n = n;
-        c->spec_plan_blocks = nb;
-        c->spec_plan_age = 0;
-        c->spec_rho_pending = false;
-        c->spec_plan_up = false;
-        const size_t nt = (size_t)c->cull_ntx * c->cull_nty;
-        std::vector<uint32_t> skip(2 * nt, 0u);
-        if (c->sky_active && c->h_miss.size() == nt)
-            for (size_t t = 0; t < nt; ++t) {
-                skip[2 * t] = (uint32_t)c->h_miss[t];
-                skip[2 * t + 1] = (uint32_t)(c->h_miss[t] >> 32);
-            }
-        for (uint32_t q = 0; q < n; ++q) {
-            if (!sel[q]) continue;
-            const uint32_t pix = c->h_chain_pix[q];
-            uint32_t col, row;
-            iqpt::tile_decode(pix, c->ncols, c->set.nrows, &col, &row);
-            const uint32_t tx = col / iqpt::kCullTile, ty = row / iqpt::kCullTile;
-            const uint32_t th = std::min(iqpt::kCullTile, c->set.nrows - ty * iqpt::kCullTile);
-            const uint32_t bit = pix - (ty * iqpt::kCullTile * c->ncols + tx * iqpt::kCullTile * th);
-            const size_t t = (size_t)ty * c->cull_ntx + tx;
-            skip[2 * t + bit / 32u] |= 1u << (bit % 32u);
-        }
-        if (!c->d_skip_sel && hipMalloc(&c->d_skip_sel, skip.size() * sizeof(uint32_t)) != hipSuccess) {
-            (void)hipGetLastError();
-            c->d_skip_sel = nullptr;
-            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "hybrid selection masks");
-        }
-        IQPT_HIP(hipMemcpy(c->d_skip_sel, skip.data(), skip.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        c->hyb_sel = true;
-        c->hyb_sel_n = nsel;
-    }
     hipStream_t ls = c->stream;                       // the launch's stream
     if (ovl) {
         opt |= iqpt::kOptOverlap;
@@ -2087,7 +1956,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     const bool bind_spec = spec && c->specfan_mode == 0 && c->n_chain_pix > 0;
     // overlapped launches: recorded by the launch's first kernel on `ls` (the sky kernel or the plain kernel)
     // and its last (the plain kernel)
-    const bool bind_ovl = ovl && !hybrid && tune_slot < 0;
+    const bool bind_ovl = ovl && tune_slot < 0;
     bool e0_bound = false, e1_bound = false;
     if (e0 && !bind_spec && !bind_ovl) (void)hipEventRecord(e0, ls);
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot], c->stream);
@@ -2135,17 +2004,15 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->pipe_kind = kind;
         return IQPT_OK;
     };
-    // ---- the spec kernel's buffers, parameters, plan and history (pipelined spec launches on `stream`,
-    // hybrid launches on `stream4`): every enqueue of these on the spec kernel's stream `ss`
+    // ---- the spec kernel's buffers, parameters, plan and history (pipelined spec launches on `stream`):
+    // every enqueue of these on the spec kernel's stream `ss`
     auto spec_buffers = [&](hipStream_t ss, iqpt::kspec& ks2) -> int {
         std::memset(&ks2, 0, sizeof ks2);
         const uint32_t n = c->n_chain_pix;
         const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
         if (n > 0 && n <= c->spec_n && m_cap > c->spec_mcap) {
-            // a longer launch on the same pixel list: only the slot results grow (the history, the plan and a
-            // hybrid selection stay)
+            // a longer launch on the same pixel list: only the slot results grow (the history and the plan stay)
             IQPT_HIP(hipStreamSynchronize(c->stream));
-            if (c->stream4) IQPT_HIP(hipStreamSynchronize(c->stream4));
             if (c->d_spec_res) (void)hipFree(c->d_spec_res);
             c->d_spec_res = nullptr;
             c->spec_mcap = 0;
@@ -2160,7 +2027,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
         if (n > 0 && n > c->spec_n) {
             IQPT_HIP(hipStreamSynchronize(c->stream));
-            if (c->stream4) IQPT_HIP(hipStreamSynchronize(c->stream4));
             for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_plan})
                 if (b) (void)hipFree(b);
             for (void* b : {(void*)c->h_spec_rho, (void*)c->h_spec_plan})
@@ -2172,7 +2038,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             c->spec_n = c->spec_mcap = 0;
             c->spec_plan_n = 0;
             c->spec_rho_pending = c->spec_plan_up = false;
-            c->hyb_sel = false;
             const size_t slots = (size_t)n * m_cap;
             if ((!c->ev_spec_rho && hipEventCreateWithFlags(&c->ev_spec_rho, hipEventDisableTiming) != hipSuccess) ||
                 (!c->ev_spec_plan && hipEventCreateWithFlags(&c->ev_spec_plan, hipEventDisableTiming) != hipSuccess) ||
@@ -2196,8 +2061,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.m_cap = m_cap;
         ks2.rho0 = c->spec_rho0;
         ks2.margin_div = c->spec_margin_div;
-        ks2.even2 = c->spec_even ? 1u : 0u;
-        ks2.pred = c->spec_pred ? 1u : 0u;
         ks2.pix = c->d_chain_pix;
         ks2.m = c->d_spec;
         ks2.rho = c->d_spec + n;
@@ -2297,11 +2160,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             c->sky_last = ss;
         }
     }
-    // a hybrid launch's plain kernel skips the misses only while the sky kernel renders them (d_skip was built
-    // with sky_active): otherwise the plain path without the spec kernel
-    if (hybrid && sky != c->sky_active) hybrid = false;
-    const iqpt::kparams p_spec = p;
-    if (hybrid) p.miss = c->hyb_sel ? c->d_skip_sel : c->d_skip;
     if (ovl) {
         if (bind_ovl) iqpt::bind_launch_events(e0_bound ? nullptr : e0, sky_deferred ? nullptr : e1);
         le = iqpt::launch_render(ls, p, grid, lds, stream_batches, opt);
@@ -2324,40 +2182,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->ovl_epoch += 1;
         c->next_on_main = !c->next_on_main;
         if (le != 0) c->ovl_zero = true;     // a failed launch breaks the chain's counts: restart it
-        if (hybrid && le == 0) {
-            // the sphere pixels: the spec kernel on stream4 (after everything `stream` held when the hybrid chain
-            // started; later ones after the previous spec kernel), its plan and history on stream4 too
-            if ((!c->stream4 && hipStreamCreateWithFlags(&c->stream4, hipStreamNonBlocking) != hipSuccess) ||
-                (!c->ev_h0 && hipEventCreateWithFlags(&c->ev_h0, hipEventDisableTiming) != hipSuccess) ||
-                (!c->ev_spec4 && hipEventCreateWithFlags(&c->ev_spec4, hipEventDisableTiming) != hipSuccess)) {
-                (void)hipGetLastError();
-                return iqpt::fail(IQPT_ERR_HIP, "hybrid spec stream");
-            }
-            if (!c->hyb_pend) {
-                IQPT_HIP(hipEventRecord(c->ev_h0, c->stream));
-                IQPT_HIP(hipStreamWaitEvent(c->stream4, c->ev_h0, 0));
-            }
-            iqpt::kspec ks2;
-            if ((st = spec_buffers(c->stream4, ks2)) != IQPT_OK) return st;
-            if (c->hyb_sel && c->spec_plan_n == ks2.n) {
-                // the selection's plan (blocks over the selected pixels only)
-                ks2.order = c->d_spec_plan;
-                ks2.blocks = c->d_spec_plan + ks2.n;
-                ks2.nblocks = c->spec_plan_blocks;
-            } else if ((st = spec_plan(c->stream4, ks2)) != IQPT_OK) {
-                return st;
-            }
-            iqpt::kparams ph = p_spec;
-            ph.miss = nullptr;
-            ph.ovl_err = c->d_ovl_err;
-            // (a selection may hold no pixel: the plain kernel has them all, nothing to launch)
-            if (!(c->hyb_sel && c->hyb_sel_n == 0)) le = iqpt::launch_spec(c->stream4, ph, ks2, opt);
-            if (le == 0 && (st = spec_history(c->stream4, ks2)) != IQPT_OK) return st;
-            IQPT_HIP(hipEventRecord(c->ev_spec4, c->stream4));
-            c->hyb_pend = true;
-            e1b = take_event(c);
-            if (e1b) (void)hipEventRecord(e1b, c->stream4);
-        }
     } else if (fan_pipe) {
         // pipelined FAN launch: the split tiles in the plain kernel on stream (queue[0], zeroed there), the
         // anchored tiles in the fan kernel on stream2
@@ -2464,12 +2288,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
         if ((st = spec_plan(c->stream, ks2)) != IQPT_OK) return st;
         const uint32_t n = ks2.n;
-        if (c->specfan_mode == 2) {
-            // one grid: no second stream, no join
-            ks2.fan_tiles = c->n_fan_tiles;
-            ks2.lead = c->spec_lead;
-            le = iqpt::launch_specfan(c->stream, pf, ks2, opt);
-        } else if (c->specfan_mode == 1) {
+        if (c->specfan_mode == 1) {
             if (n > 0) le = iqpt::launch_spec(c->stream, p, ks2, opt);
             if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream, pf, c->n_fan_tiles, opt);
         } else {
@@ -2522,11 +2341,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     c->split_last = split;
     c->chain_last = chain;
     c->fan_last = fan || fan_beside_chain || fan_split || spec;
-    c->spec_last = spec || hybrid;
-    c->hybrid_last = hybrid;
+    c->spec_last = spec;
     c->last_ls = ls;
-    // hybrid launches: a frame copy joins every stream (the spec kernel writes the frame on stream4)
-    c->last_ovl = ovl && !hybrid;
+    c->last_ovl = ovl;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1 && !e1_bound) (void)hipEventRecord(e1, ls);
     if (e0 && e1) c->timed.push_back({e0, e1, e1b});
@@ -2851,7 +2668,6 @@ int iqpt_debug_read_spec_plan(iqpt_ctx* c, uint32_t* order, uint32_t* blocks, ui
     int st = enter(c);
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
-    if (c->stream4) IQPT_HIP(hipStreamSynchronize(c->stream4));     // hybrid launches: the spec kernel's stream
     const uint32_t np = c->n_chain_pix;
     if (!c->spec_plan_n || c->spec_plan_n != np || np > cap || !c->d_spec_plan) return IQPT_OK;
     IQPT_HIP(hipMemcpy(order, c->d_spec_plan, (size_t)np * sizeof(uint32_t), hipMemcpyDeviceToHost));
@@ -2895,19 +2711,6 @@ int iqpt_debug_set_sky(iqpt_ctx* c, int on) {
     return IQPT_OK;
 }
 
-/* Internal (A/B, tests): hybrid launches — 1: overlapped plain launches send the sphere pixels
- * to the spec kernel on a stream of their own; 0: off. rho256: once the chain history is in, only the pixels
- * whose last chain used >= rho256 / 256 slots per sample (0: all sphere pixels). */
-int iqpt_debug_set_hybrid(iqpt_ctx* c, int mode, uint32_t rho256) {
-    if (!c || mode < 0 || mode > 1) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or mode not 0..1");
-    int st = enter(c);
-    if (st) return st;
-    c->hybrid_mode = mode;
-    c->hybrid_rho = rho256;
-    c->hyb_sel = false;
-    return IQPT_OK;
-}
-
 /* Internal (A/B): the gather's footprint beside the render kernels, for the next iqpt_comm_init — RCCL's
  * blocks per collective (ncclConfig_t::maxCTAs; 0: RCCL's own choice) and the communicator stream's priority
  * (-1 the lowest; 0 HIP's default, the default; 1 the highest); skip (measurement only, wrong frames): 1 leaves
@@ -2918,22 +2721,6 @@ int iqpt_debug_set_gather(iqpt_ctx* c, int ctas, int prio, int skip) {
     c->gather_ctas = ctas;
     c->gather_prio = prio;
     c->gather_skip = skip;
-    return IQPT_OK;
-}
-
-/* Internal (A/B, tests): the spec kernel traces only the even slots of a pixel whose last chain took two
- * slots per sample (1) or every slot of every window (0). Same bits either way. */
-int iqpt_debug_set_spec_even(iqpt_ctx* c, int on) {
-    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    c->spec_even = on != 0;
-    return IQPT_OK;
-}
-
-/* Internal (A/B, tests): the spec kernel's predicted chains (1: camera rays of every slot, scattered rays
- * along the chain as predicted from them) or every slot traced whole (0). Same bits either way. */
-int iqpt_debug_set_spec_pred(iqpt_ctx* c, int on) {
-    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    c->spec_pred = on != 0;
     return IQPT_OK;
 }
 
@@ -2950,14 +2737,6 @@ int iqpt_debug_set_sky_order(iqpt_ctx* c, int after) {
 int iqpt_debug_set_timing(iqpt_ctx* c, int on) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     c->timing_on = on != 0;
-    return IQPT_OK;
-}
-
-/* Internal (tools): the sphere pixels of the current hybrid selection (0 before one) and of the split. */
-int iqpt_debug_hybrid_info(iqpt_ctx* c, uint32_t* selected, uint32_t* sphere_pixels) {
-    if (!c || !selected || !sphere_pixels) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    *selected = c->hyb_sel ? c->hyb_sel_n : 0u;
-    *sphere_pixels = c->n_chain_pix;
     return IQPT_OK;
 }
 
@@ -2997,16 +2776,16 @@ int iqpt_debug_set_pipe(iqpt_ctx* c, int fan_pipe) {
     return IQPT_OK;
 }
 
-/* Internal (A/B): how spec launches run the fan tiles beside the sphere pixels — 0 two kernels on two
- * streams, pipelined across launches (the default), 1 two kernels on one stream, 2 one grid
- * (iqpt_specfan_kernel) — and, in one grid, how many spec blocks precede every fan block (0xffffffff: all;
- * the rest are spread evenly). */
+/* Internal (A/B, measurement): how spec launches run the fan tiles beside the sphere pixels — 0 two kernels on
+ * two streams, pipelined across launches (the default), 1 two kernels one after the other on one stream. (Round
+ * 4's mode 2, spec and fan blocks in one grid, measured slower and is archived: branch round4-ab-archive.)
+ * `lead` is ignored. */
 int iqpt_debug_set_specfan(iqpt_ctx* c, int mode, uint32_t lead) {
-    if (!c || mode < 0 || mode > 2) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or mode not 0..2");
+    (void)lead;
+    if (!c || mode < 0 || mode > 1) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or mode not 0..1");
     int st = enter(c);
     if (st) return st;
     c->specfan_mode = mode;
-    c->spec_lead = lead;
     return IQPT_OK;
 }
 
@@ -3040,6 +2819,20 @@ int iqpt_debug_set_fan(iqpt_ctx* c, int on) {
 
 /* Internal (tests): lower the kernels' forward-progress bounds (0 keeps a bound's default) and bias the
  * per-tile wait targets of overlapped launches, so that tests can force each error path. */
+/* Internal (tests): after joining the context's streams, fills the LDS of every CU with non-zero garbage (blocks of
+ * the largest per-block allocation, eight per CU) on the context's stream, ahead of the next launch, which then
+ * starts joined behind it: a kernel that reads LDS before writing it gives other bits than the oracle. */
+int iqpt_debug_poison_lds(iqpt_ctx* c, uint32_t pattern) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    const uint32_t bytes = c->lds_per_block & ~3u;
+    const int le = iqpt::launch_lds_poison(c->stream, pattern, bytes, (uint32_t)c->num_cus * 8u);
+    if (le != 0) return iqpt::hip_fail((hipError_t)le, "LDS poison kernel");
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    return IQPT_OK;
+}
+
 int iqpt_debug_set_limits(iqpt_ctx* c, uint32_t spin_limit, uint32_t iter_limit, uint32_t wait_bias) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     c->spin_limit = spin_limit ? spin_limit : iqpt::kOverlapSpinLimit;
@@ -3341,9 +3134,18 @@ int iqpt_gather_accum(iqpt_ctx* c, int root, void* dst_device, size_t bytes) {
 int iqpt_gather_read(iqpt_ctx* c, int root, float* lin_rgba, uint8_t* bgra) {
     int st = comm_check(c, root);
     if (st) return st;
-    // every rank takes part in the same gathers; the root's pointers choose what is read back (the others'
-    // are ignored): both are gathered unless the root asked for neither
-    return gather_sync(c, root, 3, lin_rgba, bgra);
+    // every rank takes part in the same two gathers (the accumulators, then the BGRA8 frame) whatever the
+    // root's pointers are: which collectives run cannot depend on one rank's arguments; the root's pointers
+    // only choose what is copied back to the host (NULL: not copied)
+    return gather_sync(c, root, IQPT_GATHER_ACCUM | IQPT_GATHER_FRAME, lin_rgba, bgra);
+}
+
+int iqpt_gather_read_select(iqpt_ctx* c, int root, int what, float* lin_rgba, uint8_t* bgra) {
+    int st = comm_check(c, root);
+    if (st) return st;
+    if (what < 1 || what > (IQPT_GATHER_ACCUM | IQPT_GATHER_FRAME))
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "what must be IQPT_GATHER_ACCUM, IQPT_GATHER_FRAME or both");
+    return gather_sync(c, root, what, lin_rgba, bgra);
 }
 
 int iqpt_comm_time(iqpt_ctx* c, double* total_ms, uint64_t* gathers) {
@@ -3410,8 +3212,7 @@ int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
     out8[2] = ns;
     // launch mode: 1 split, 2 chain (anchored tiles plain), 3 fan (split tiles plain), 4 chain + fan, 5 split + fan,
     // 6 spec (sphere pixels slot-parallel, the rest fan)
-    // 7 hybrid (overlapped plain kernel + the sphere pixels in the spec kernel + sky kernel)
-    out8[7] = c->hybrid_last ? 7 : c->spec_last ? 6
+    out8[7] = c->spec_last ? 6
                            : (c->split_last ? (c->fan_last ? 5 : 1)
                                             : (c->chain_last ? (c->fan_last ? 4 : 2) : (c->fan_last ? 3 : 0)));
     if (!c->d_split || ns == 0) return IQPT_OK;

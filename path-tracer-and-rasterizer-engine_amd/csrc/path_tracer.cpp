@@ -101,7 +101,7 @@ void path_tracer::draw_scene(const scene& scn, std::vector<shader>& /*shaders*/,
     m_time = 0.0f;
     // sync with the previous launch and fetch its frame (:382-386); sharded: the whole frame on rank 0
     uint8_t* host = reinterpret_cast<uint8_t*>(m_host_pixels.data());
-    if (m_comm) IQPT_THROW_FAILED(iqpt_gather_read(m_ctx, 0, nullptr, host));
+    if (m_comm) IQPT_THROW_FAILED(iqpt_gather_read_select(m_ctx, 0, IQPT_GATHER_FRAME, nullptr, host));
     else IQPT_THROW_FAILED(iqpt_read(m_ctx, nullptr, host));
     m_image_updated = true;
     if (scn.modified() || !m_have_packet) {                                // :389-392
@@ -131,7 +131,7 @@ uint64_t path_tracer::rays_traced() const {
 void path_tracer::read_linear(std::vector<float>& rgba) const {
     if (m_comm) {                 // collective: the whole frame's accumulator on rank 0
         rgba.resize((size_t)m_camera->get_width() * m_camera->get_height() * 4);
-        IQPT_THROW_FAILED(iqpt_gather_read(m_ctx, 0, rgba.data(), nullptr));
+        IQPT_THROW_FAILED(iqpt_gather_read_select(m_ctx, 0, IQPT_GATHER_ACCUM, rgba.data(), nullptr));
         return;
     }
     uint64_t n = 0;

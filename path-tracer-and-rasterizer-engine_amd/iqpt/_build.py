@@ -63,6 +63,18 @@ def _headers() -> list[Path]:
     return sorted(CSRC.glob("*.h")) + sorted(CSRC.glob("*.hpp")) + sorted(INCLUDE.glob("*.h"))
 
 
+def kernel_source_sha16() -> str:
+    """16 hex digits of SHA-256 over the device-code sources (the .hip kernels and every header they include):
+    the identity of the kernels a measurement profile describes (tools/work_counters.py writes it, bench.py
+    refuses a profile of other sources)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(CSRC.glob("*.hip")) + _headers():
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
 def build_lib(force: bool = False, stats: bool = False, flags: tuple[str, ...] = (),
               target: Path | None = None) -> Path:
     """Compile the HIP kernels + runtime into libiqpt.so (gfx950); stats=True adds the instrumented

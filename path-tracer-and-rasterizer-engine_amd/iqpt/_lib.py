@@ -23,6 +23,8 @@ DEFAULT_MAX_DEPTH = 5
 SPLIT_AUTO, SPLIT_OFF, SPLIT_ON, SPLIT_CHAIN, SPLIT_FAN, SPLIT_SPEC = -1, 0, 1, 2, 3, 4   # IQPT_SPLIT_* (iqpt_set_split)
 OVERLAP_OFF, OVERLAP_AUTO = 0, 1               # IQPT_OVERLAP_* (iqpt_set_overlap)
 COMM_ID_BYTES = 128                            # IQPT_COMM_ID_BYTES (iqpt_comm_unique_id)
+GATHER_ACCUM = 1                               # IQPT_GATHER_ACCUM / IQPT_GATHER_FRAME (iqpt_gather_read_select)
+GATHER_FRAME = 2
 
 
 class IqptError(RuntimeError):
@@ -120,6 +122,7 @@ SIGNATURES = [
     ("iqpt_gather_frame_async", C.c_int, [_P, C.c_int, _P, C.c_size_t]),
     ("iqpt_gather_accum", C.c_int, [_P, C.c_int, _P, C.c_size_t]),
     ("iqpt_gather_read", C.c_int, [_P, C.c_int, _FP, C.POINTER(C.c_uint8)]),
+    ("iqpt_gather_read_select", C.c_int, [_P, C.c_int, C.c_int, _FP, C.POINTER(C.c_uint8)]),
     ("iqpt_comm_stream", C.c_int, [_P, C.POINTER(C.c_void_p)]),
     ("iqpt_comm_time", C.c_int, [_P, C.POINTER(C.c_double), C.POINTER(C.c_uint64)]),
     ("iqpt_scene_create", C.c_int, [C.POINTER(_P)]),

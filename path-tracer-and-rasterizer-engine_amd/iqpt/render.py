@@ -124,6 +124,7 @@ class PathTracer:
         dist.pixel_set_for_rank). `uid` from comm_unique_id() on one rank, shared out of band."""
         b = (C.c_uint8 * _lib.COMM_ID_BYTES).from_buffer_copy(bytes(uid))
         check(self._lib.iqpt_comm_init(self._h, rank, world, b, _lib.COMM_ID_BYTES), "iqpt_comm_init")
+        self._comm_rank = rank
 
     def gather_frame_async(self, root: int, dst_ptr: int, nbytes: int):
         """Collective: the BGRA8 frame gathered to `root` and assembled there (W x H uint32 into dst_ptr, a
@@ -136,14 +137,21 @@ class PathTracer:
         """Collective, synchronous: the float4 accumulators of the whole frame on `root` (device buffer)."""
         check(self._lib.iqpt_gather_accum(self._h, root, C.c_void_p(dst_ptr or None), nbytes), "iqpt_gather_accum")
 
-    def gather_read(self, root: int):
-        """Collective, synchronous: (lin [W*H,4] float32, bgra [W*H,4] uint8) of the whole frame on `root`
-        (row-major), None elsewhere (iqpt_gather_read)."""
-        lin = np.empty((self.width * self.height, 4), dtype=np.float32)
-        bgra = np.empty((self.width * self.height, 4), dtype=np.uint8)
-        check(self._lib.iqpt_gather_read(self._h, root, lin.ctypes.data_as(C.POINTER(C.c_float)),
-                                         bgra.ctypes.data_as(C.POINTER(C.c_uint8))), "iqpt_gather_read")
-        return lin, bgra
+    def gather_read(self, root: int, what: str = "both"):
+        """Collective, synchronous (every rank calls it with the same `what`): on `root` the whole frame's
+        (lin [W*H,4] float32, bgra [W*H,4] uint8), row-major, with None for a plane not asked for ("accum",
+        "frame" or "both"; iqpt_gather_read_select); None on every other rank."""
+        sel = {"accum": _lib.GATHER_ACCUM, "frame": _lib.GATHER_FRAME,
+               "both": _lib.GATHER_ACCUM | _lib.GATHER_FRAME}[what]
+        is_root = root == getattr(self, "_comm_rank", None)
+        lin = (np.empty((self.width * self.height, 4), dtype=np.float32)
+               if is_root and sel & _lib.GATHER_ACCUM else None)
+        bgra = (np.empty((self.width * self.height, 4), dtype=np.uint8)
+                if is_root and sel & _lib.GATHER_FRAME else None)
+        check(self._lib.iqpt_gather_read_select(
+            self._h, root, sel, lin.ctypes.data_as(C.POINTER(C.c_float)) if lin is not None else None,
+            bgra.ctypes.data_as(C.POINTER(C.c_uint8)) if bgra is not None else None), "iqpt_gather_read_select")
+        return (lin, bgra) if is_root else None
 
     def comm_time(self) -> tuple[float, int]:
         """(ms, gathers): the gathers' summed durations on the communicator stream since the last call."""
@@ -169,15 +177,14 @@ class PathTracer:
 
     def launch_mode(self) -> str:
         """How the last launch ran: "plain", "split" (speculative runs + stitch), "chain" (chain kernel beside
-        the plain kernel), "fan" (fan kernel beside the plain kernel), "chain+fan", "split+fan", "spec" or "hybrid"
-        (overlapped plain launches with the sphere pixels in the spec kernel), from
+        the plain kernel), "fan" (fan kernel beside the plain kernel), "chain+fan", "split+fan" or "spec", from
         iqpt_debug_split_info. Synchronises."""
         import ctypes as C
         self._lib.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
         info = (C.c_ulonglong * 8)()
         check(self._lib.iqpt_debug_split_info(self._h, info), "iqpt_debug_split_info")
         return {1: "split", 2: "chain", 3: "fan", 4: "chain+fan", 5: "split+fan", 6: "spec",
-                7: "hybrid"}.get(int(info[7]), "plain")
+                }.get(int(info[7]), "plain")
 
     def kernel_span(self) -> float:
         """First start to last end (ms) of the launches of the last kernel_time() call (iqpt_kernel_span)."""

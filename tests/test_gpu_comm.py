@@ -45,6 +45,12 @@ def test_full_frame_gather_equals_read_and_oracle(require_gpu):
     assert np.array_equal(acc.cpu().numpy().view(np.uint32), lin.view(np.uint32))
     ms, n = pt.comm_time()
     assert n == 6 and ms > 0.0               # 3 frame gathers, 2 in gather_read (accumulators, frame), 1 accum
+    # the select form runs only the collectives asked for (a present needs the BGRA8 frame alone)
+    flin, fbgra = pt.gather_read(0, "frame")
+    assert flin is None and np.array_equal(fbgra, bgra)
+    alin, abgra = pt.gather_read(0, "accum")
+    assert abgra is None and np.array_equal(alin.view(np.uint32), lin.view(np.uint32))
+    assert pt.comm_time()[1] == 2
     fr = oracle_render("cornell", w, h, spp, 8, launches=[spp] * 3)
     assert np.array_equal(lin.view(np.uint32), fr.lin.view(np.uint32))
     pt.close()

@@ -138,3 +138,44 @@ def test_sky_kernel_ahead_of_and_behind_the_plain_kernel(require_gpu, after):
     assert np.array_equal(pt.read_rng(), fr.states)
     assert pt.rays() == int(fr.rays.sum())
     pt.close()
+
+
+@pytest.mark.parametrize("split", ["spec", "chain"])
+def test_sky_with_more_than_64_spheres(require_gpu, split):
+    """a resident scene of more than 64 spheres skips the per-pixel sphere test of the split
+    tiles, so every pixel of a split tile went to the spec / chain kernel's list — the certain misses too, which
+    the sky kernel also renders on the other stream. The Cornell box plus 70 small spheres (a grid above the
+    floor, resident in LDS), a row share, spec and chain launches with the sky kernel on: bit for bit against
+    the oracle, and the sky kernel still has pixels."""
+    from iqpt import PathTracer, make_camera
+    L, lib = _lib()
+    from iqpt.scene import Scene
+    sc = Scene()
+    sc.add_preset("cornell")
+    for i in range(70):
+        x, z = -0.9 + 0.26 * (i % 7), -0.4 + 0.12 * (i // 7)
+        sc.add_model(f"ball{i}", "sphere", scale=0.04, translation=(x, -0.45, z, 0.0))
+    pk = sc.build_packet()
+    assert int(pk.num_drawcalls[L.MESH_SPHERES]) == 72
+    w, h, world, rank = 480, 270, 4, 1
+    n = len(range(rank, h, world))
+    ps = pixel_set(w, h, 0, w, rank, world, n)
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    pt.set_split(L.SPLIT_SPEC if split == "spec" else L.SPLIT_CHAIN)
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    for s in (8, 24):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    px, tiles = C.c_uint32(0), C.c_uint32(0)
+    L.check(lib.iqpt_debug_sky_info(pt.handle, C.byref(px), C.byref(tiles)), "iqpt_debug_sky_info")
+    assert px.value > 0
+    c = compare(lin, fr.lin)
+    assert c["rmse"] < RMSE_TOL and c["bitexact"] == c["npix"], c
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    assert pt.rays() == int(fr.rays.sum())
+    pt.close()

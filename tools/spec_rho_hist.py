@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Distribution of the sphere pixels' chain lengths (slots per sample of their last chain, the spec kernel's
-history) on rank 0's share of C2 — what the hybrid selection threshold (bench.py --hybrid-rho) cuts.
+history) on rank 0's share of C2 (the spread of chain lengths the spec plan works from).
 
     spec_rho_hist.py [--share 1]"""
 import argparse

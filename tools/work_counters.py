@@ -23,6 +23,7 @@ sys.path.insert(0, str(REPO / "path-tracer-and-rasterizer-engine_amd"))
 
 import iqpt  # noqa: E402
 from iqpt import _build, _lib  # noqa: E402
+from iqpt._build import kernel_source_sha16  # noqa: E402
 from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
 
 K_STATS = 1 << 7
@@ -49,7 +50,8 @@ def main():
     sc.add_preset(cfg.preset)
     pk = sc.build_packet()
     cam = make_camera(cfg.width, cfg.height)
-    # 1) the production choice
+    # 1) the production choice (plain launches: the instrumented variants are plain-kernel ones; with the sky
+    # kernel and certain pixels as in production — their rays are counted, their tests are none)
     pt = iqpt.PathTracer(cfg.width, cfg.height, max_depth=cfg.max_depth)
     pt.set_split(_lib.SPLIT_OFF)
     pt.set_camera(cam)
@@ -87,6 +89,9 @@ def main():
     fpr = FLOP_MT * per["mt_tests"] + FLOP_SPHERE * per["sphere_tests"] + \
         FLOP_NODE * (per["tri_bvh_node_tests"] + per["sph_bvh_node_tests"])
     out = {"config": cfg.name, "preset": cfg.preset, "spp_per_launch": spp, "launches": args.launches,
+           # the kernel sources these counts were taken from: bench.py prices a line only with a profile of the
+           # same sources (round 4's C2 line carried round 2's counts)
+           "kernel_sha16": kernel_source_sha16(),
            "rays": rays, "production_options": prod_opt, "stats_options": stats_opt,
            "per_ray": {k: round(x, 4) for k, x in per.items()}, "flops_per_ray": round(fpr, 2),
            "flop_weights": {"mt": FLOP_MT, "sphere": FLOP_SPHERE, "node": FLOP_NODE},
