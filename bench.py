@@ -103,6 +103,15 @@ def parse():
                     help="A/B: no timing events around launches (kernel times and the roofline read 0)")
     ap.add_argument("--self-gather", action="store_true",
                     help="test: run the per-step gather path at N = 1 (a one-rank process group)")
+    ap.add_argument("--anyhit", type=int, default=None, choices=[0, 1],
+                    help="A/B: any-hit queries for triangle-only scenes (iqpt_debug_set_anyhit; default: the library's, on)")
+    ap.add_argument("--spec-parity-max", type=float, default=None,
+                    help="A/B: spec parity pixels' upper bound in slots per sample (iqpt_debug_set_spec_parity_max)")
+    ap.add_argument("--spec-prio", type=int, default=None,
+                    help="A/B: spec kernel progress-fair priority step in iterations (iqpt_debug_set_spec_prio; 0 off)")
+    ap.add_argument("--spec-parity", type=float, default=None,
+                    help="A/B: spec parity pixels' threshold in slots per sample (iqpt_debug_set_spec_parity; 0 = every "
+                         "slot traced, the round-4 kernel; default: the library's 1.875)")
     ap.add_argument("--spec-cap", type=float, default=0.0,
                     help="A/B: a spec plan's lanes as a fraction of the resident lanes (iqpt_debug_set_spec_cap; 0 = default)")
     ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain", "fan", "spec"],
@@ -500,6 +509,27 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_sky.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_sky(pt._h, 0), "iqpt_debug_set_sky")
+    if args.anyhit is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_anyhit.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_anyhit(pt._h, args.anyhit), "iqpt_debug_set_anyhit")
+    if args.spec_parity_max is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec_parity_max.argtypes = [C.c_void_p, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_spec_parity_max(pt._h, min(0xffffffff, int(round(args.spec_parity_max * 256)))),
+                   "iqpt_debug_set_spec_parity_max")
+    if args.spec_prio is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec_prio.argtypes = [C.c_void_p, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_spec_prio(pt._h, args.spec_prio), "iqpt_debug_set_spec_prio")
+    if args.spec_parity is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec_parity.argtypes = [C.c_void_p, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_spec_parity(pt._h, int(round(args.spec_parity * 256))), "iqpt_debug_set_spec_parity")
     if args.spec_cap:
         import ctypes as C
         lb = _lib.load()
@@ -620,6 +650,12 @@ def main():
     kern_span_ms = pt.kernel_span()
     gather_ms, gathers = pt.comm_time() if lib_gather else (0.0, 0)
     launch_mode = pt.launch_mode()
+    import ctypes as C
+    _lb = _lib.load()
+    _lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    _o = C.c_int(0)
+    _lib.check(_lb.iqpt_debug_last_options(pt.handle, C.byref(_o)), "iqpt_debug_last_options")
+    last_opt = _o.value                                # the render-kernel option set of the last launch
     certain_px = certain_pixels(pt, _lib) if args.certain != "off" else 0
     sky_px = sky_pixels(pt, _lib) if (args.certain != "off" and args.sky != "off") else 0
 
@@ -724,8 +760,15 @@ def main():
                                          else " (gloo via host, rehearsal)")),
                        "split": args.split, "overlap": args.overlap, "certain": args.certain, "sky": args.sky,
                        "launch_mode": launch_mode,
+                       # the plain kernel's option bits of the last launch (iqpt_internal.hpp kOpt*): for streamed
+                       # scenes bit 12 (kOptBvhPrimary) says whether camera rays took the BVH or the tile lists
+                       "kernel_option_bits": hex(last_opt),
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
-                       **({"spec_cap": args.spec_cap} if args.spec_cap else {})},
+                       **({"spec_cap": args.spec_cap} if args.spec_cap else {}),
+                       **({"spec_parity": args.spec_parity} if args.spec_parity is not None else {}),
+                       **({"anyhit": args.anyhit} if args.anyhit is not None else {}),
+                       **({"spec_prio": args.spec_prio} if args.spec_prio is not None else {}),
+                       **({"spec_parity_max": args.spec_parity_max} if args.spec_parity_max is not None else {})},
             "n_ranks_seen": n_ranks_seen,
             "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             **({"gather": "stream-ordered" if stream_gather else "blocking", "gather_check": gather_check}

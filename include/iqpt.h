@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define IQPT_ABI_VERSION 4
+#define IQPT_ABI_VERSION 5
 
 typedef enum iqpt_status {
     IQPT_OK = 0,

@@ -71,7 +71,7 @@ struct kparams {
     uint32_t tri_batch;              // LDS batch (triangles or triangle pairs, by layout)
     uint32_t sph_batch;              // LDS batch (spheres or sphere pairs, by layout)
     float4_storage* lin;             // npix
-    uint32_t* bgra;                  // npix
+    uint32_t* bgra;                  // npix, compact row-major order (tile_to_compact), possibly padded after npix
     uint32_t* rng;                   // 6 planes of npix words: v0..v4, d
     unsigned long long* rays;        // closest-hit query counters: kRaySlots slots, kRaySlotStride apart (summed on read)
     uint32_t* queue;                 // tile dequeue head (zeroed before every launch)
@@ -173,6 +173,11 @@ struct kparams {
     // queue length of the plain kernel's tile queue (tile_order[0 .. nqueue)); 0: every tile (ntiles).
     // Chain launches give the plain kernel the anchored tiles only.
     uint32_t nqueue;
+    // any-hit scene: no sphere and the reference's hard-wired materials, so every triangle is emissive
+    // (path_tracer.cu:278) and every accepted triangle ends the path with the same clamped colour: a ray's
+    // result depends only on whether some triangle accepts it, not on which one is closest. The BVH traversal
+    // and the candidate-list loop then stop at the first accepted triangle (C4).
+    uint32_t anyhit;
 };
 // The ray count is spread over kRaySlots counters 128 B apart: thousands of waves add their counts as
 // they end, and one counter would serialise those atomics at the end of every launch.
@@ -202,6 +207,9 @@ struct kspec {
     // per sample traces the even slots of its window first, the odd ones only from where its chain lands on
     // one (pooled over the block's lanes); 0: every slot of every window
     uint32_t parity_rho;
+    uint32_t parity_hi;              // ... and at most parity_hi / 256 slots per sample
+    uint32_t prio_q;                 // progress-fair priority: a wave's level drops by one per prio_q slot-loop
+                                     // iterations (0: level 3 throughout)
     const uint32_t* order;           // a plan (else null): sphere pixel q at each position, heaviest first
     const uint32_t* blocks;          // per plan block: first position, count | log2(lanes / 8) << 8
     uint32_t nblocks;                // plan blocks (the spec part of the grid)
@@ -216,9 +224,10 @@ constexpr uint32_t kSpecReplan = 64;        // launches between two spec plans (
 constexpr uint32_t kSpecPixPerBlock = 16;   // sphere pixels per iqpt_spec_kernel block without a plan (16 lanes each)
 constexpr uint32_t kSpecMaxPixPerBlock = 32;   // a plan's blocks: 256 / (8, 16, 24, 32, 48 or 64) pixels
 constexpr uint32_t kSpecBlockLanes = 256;      // iqpt_spec_kernel's block
-constexpr int kSpecLaneClasses = 6;            // lanes per pixel: 8, 16, 24, 32, 48, 64
+constexpr int kSpecLaneClasses = 4;            // lanes per pixel: 8, 16, 32, 64 (round 4's 24 and 48 split waves)
 constexpr uint32_t kSpecRho0 = 576;      // 2.25 slots per sample before a pixel has a history (sphere pixels take ~2)
 constexpr uint32_t kSpecParityRho = 480; // parity pixels: >= 1.875 slots per sample in their last chain (kspec::parity_rho)
+constexpr uint32_t kSpecParityHi = 528;  // ... and <= 2.0625 (kspec::parity_hi)
 
 // The spec window of a sphere pixel whose last chain used rho256 / 256 slots per sample: that many slots
 // for spp samples plus a margin of 1 / margin_div of the extra slots (at least 4) and 4, within
@@ -234,6 +243,7 @@ __host__ __device__ inline uint32_t spec_window(uint32_t rho256, uint32_t spp, u
 // iqpt_split_prep_kernel / iqpt_split_stitch_kernel (kOptSplit).
 struct ksplit {
     uint32_t ns_cap, spp, m_cap, g_max, run_len, heavy_rho;
+    uint32_t ncols, nrows;           // the owned set (the BGRA8 frame's compact order)
     int32_t max_depth;
     uint64_t frame0;
     float mean_tiny;
@@ -308,6 +318,16 @@ __host__ __device__ inline void tile_decode(uint32_t s, uint32_t ncols, uint32_t
     *row = ty * kCullTile + w / tw;
 }
 
+// The BGRA8 frame is stored in COMPACT row-major order over the owned set (round 5), unlike the other pixel
+// planes: nothing reads it on the device, so its readbacks need no reorder and a pipelined launch's frame buffer
+// is the multi-GPU gather's send buffer as it is. A kernel writes pixel s (tile-major storage
+// index) at tile_to_compact(s).
+__host__ __device__ inline uint32_t tile_to_compact(uint32_t s, uint32_t ncols, uint32_t nrows) {
+    uint32_t col, row;
+    tile_decode(s, ncols, nrows, &col, &row);
+    return row * ncols + col;
+}
+
 // Kernel option bits (all exact: each shortcut reproduces the reference's bits, see the kernel).
 constexpr int kOptCamConst = 1 << 0;   // launch-constant 1/w of the inverse projection
 constexpr int kOptAccTable = 1 << 1;   // running-mean 1/n, (n-1)/n table; c in {0,1} without a division
@@ -358,6 +378,9 @@ int launch_tile_count(void* stream, const uint32_t* cull, uint32_t ntiles, uint3
                       uint32_t* cnt_tri, uint32_t* cnt_sph);
 int launch_tile_list(void* stream, const uint32_t* cull, uint32_t ntiles, uint32_t wt, uint32_t stride,
                      const uint32_t* off_tri, const uint32_t* off_sph, uint32_t* list);
+// Any-hit scenes: each tile's triangle candidate list reordered by how many of the tile's central rays a pair hits
+// (any order gives the same bits there; the candidate-list loop leaves sooner)
+int launch_tile_list_order(void* stream, const kbin& b, const uint32_t* off_tri, uint32_t* list);
 // Device probe of the camera transforms (iqpt_debug_camera_rays): general and kOptCamAxis forms.
 int launch_camera_probe(void* stream, const kparams& p, const float* ndc, float* gen, float* axis, uint32_t n,
                         bool do_axis);

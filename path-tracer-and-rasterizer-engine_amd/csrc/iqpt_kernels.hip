@@ -923,11 +923,15 @@ __device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, floa
             cnt[0] += 1u;
             if (hit && leaf) cnt[1] += link & 0xffu;
         }
-        if (hit && leaf) bvh_leaf<OPT>(p, link & 0x7fffffffu, r, closest, kind, idx);
+        if (hit && leaf) {
+            bvh_leaf<OPT>(p, link & 0x7fffffffu, r, closest, kind, idx);
+            // any-hit scenes (kparams::anyhit): an accepted triangle decides the ray, whichever it is
+            if (p.anyhit && kind == kHitTri) return;
+        }
         i = (hit || leaf) ? i + 1 : link;
     }
     const float4* __restrict__ tris = reinterpret_cast<const float4*>(p.tris);
-    for (uint32_t a = 0; a < p.bvh_nalways; ++a) {
+    for (uint32_t a = 0; a < p.bvh_nalways && !(p.anyhit && kind == kHitTri); ++a) {
         const uint32_t k = p.bvh_always[a];
         float c2 = closest;
         int kd = kHitNone;
@@ -1248,8 +1252,11 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // tile, 2 leftovers [chunk_next, chunk_end) of the leftover list, 3 the light pixels of a split tile
     // (anchored) — and the split tile's first slot and storage index
     uint32_t chunk_kind = 0, chunk_sp0 = 0, chunk_first = 0, chunk_r = 0;
-    // the chunk's tile's certain pixels (kparams::certain): they take the whole launch at once (refill)
-    constexpr bool kCertain = !kSplit && !STREAM && (OPT & kOptAccTable) && !(OPT & kOptMaterials) && !(OPT & kOptStats);
+    // the chunk's tile's certain pixels (kparams::certain): they take the whole launch at once (refill). Resident
+    // scenes only (streamed: DESIGN.md §3.3; round 5 measured the BVH-primary variants with certain pixels and the
+    // sky kernel on C4 slower too, 135 -> 161 ms). The instrumented (kOptStats) variants too, so that the
+    // executed-work counts are the production launch's (tools/work_counters.py).
+    constexpr bool kCertain = !kSplit && !STREAM && (OPT & kOptAccTable) && !(OPT & kOptMaterials);
     uint64_t chunk_certain = 0;
     // ... and its certain-miss pixels (kparams::miss): iqpt_sky_kernel renders them, this kernel skips them
     uint64_t chunk_miss = 0;
@@ -1274,7 +1281,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
         const uint32_t g8 = to_u8(255.0f * iq_sqrtf(acc.y));
         const uint32_t b8 = to_u8(255.0f * iq_sqrtf(acc.z));
         const uint32_t pix = tile_store_index(px - p.x0, (py - p.y0) / p.ystep, p.ncols, p.nrows);
-        p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+        p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
         // one 16-byte store: the reference never writes w (path_tracer.cu:356-358), and w is 0 from
         // iqpt_create's clear on (iqpt_checkpoint_load refuses a non-zero w), so writing 0 keeps its
         // bits while filling whole lines (three 4-byte stores left partial lines: C4 wrote 2.9x)
@@ -1676,6 +1683,8 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     if (tri_mask != nullptr)
                         test_triangle_pair<OPT>(q0, q1, q2, q3, q4, ray, closest, kind, hidx, 2 * j,
                                                 2 * j + 1 < p.ntri);
+                    // any-hit scenes: the wave leaves once every list lane has an accepted triangle
+                    if (p.anyhit && __ballot(tri_mask != nullptr && kind != kHitTri) == 0ull) break;
                     j = jn;
                     q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4;
                 }
@@ -2282,15 +2291,25 @@ __global__ __launch_bounds__(256) void iqpt_bin_kernel(const kbin b) {
 // and sphere of its tile (iq_interval.h tri_culled / sphere_culled, the tests the tile masks are built with), so
 // every camera ray of the pixel misses everything and ends on the sky gradient (path_tracer.cu:307-316) —
 // into certain[2 ntiles + 2 t], certain[2 ntiles + 2 t + 1] (iqpt_sky_kernel's pixels).
+// Tiles with more candidate pairs than this are left uncertain (both masks 0: traced as usual): a pixel's
+// proofs test up to every candidate, and streamed scenes (round 5) can have thousands per tile (C5's mesh).
+constexpr uint32_t kCertainMaxPairs = 96;
+
 __global__ __launch_bounds__(64) void iqpt_certain_kernel(const kbin b, uint32_t* certain) {
     const uint32_t t = blockIdx.x, lane = threadIdx.x;
     const uint32_t* m = b.cull + (size_t)t * b.stride;
     bool sph = false;
-    for (uint32_t w = b.wt; w < b.stride; ++w) sph = sph || m[w] != 0u;
+    uint32_t ncand = 0;
+    for (uint32_t w = 0; w < b.stride; ++w) {
+        const uint32_t mw = m[w];
+        ncand += (uint32_t)__builtin_popcount(mw);
+        if (w >= b.wt) sph = sph || mw != 0u;
+    }
+    const bool small = ncand <= kCertainMaxPairs;
     const uint32_t tx = t % b.ntx, ty = t / b.ntx;
     const uint32_t tw = min(kCullTile, b.ncols - tx * kCullTile), th = min(kCullTile, b.nrows - ty * kCullTile);
     bool ok = false, miss = false;
-    if (lane < tw * th) {
+    if (lane < tw * th && small) {
         const uint32_t col = tx * kCullTile + lane % tw, row = ty * kCullTile + lane / tw;
         iqiv::camera_in ci;
         ci.width = b.width;
@@ -2387,6 +2406,81 @@ __global__ __launch_bounds__(256) void iqpt_tile_list_kernel(const uint32_t* cul
     o = off_sph[t];
     for (uint32_t w = wt; w < stride; ++w)
         for (uint32_t b = m[w]; b; b &= b - 1u) list[o++] = (w - wt) * 32u + (uint32_t)__builtin_ctz(b);
+}
+
+// Any-hit scenes (kparams::anyhit: no sphere, every triangle emissive), round 5: a ray's result is whether some
+// triangle accepts it, so the order in which a tile's candidate list is tested changes no bit — only how soon every
+// lane of a wave has its hit and the wave leaves the list (the candidate-list loop of iqpt_render_kernel). One
+// wave per tile: each lane casts its pixel's central ray (a plain float camera: the score is a heuristic) at every
+// candidate pair of the tile, the pair's score is how many of the tile's lanes it hits, and the list is reordered
+// by descending score (ties: ascending index). Lists longer than kOrderMax keep their ascending order.
+constexpr uint32_t kOrderMax = 1024;
+
+__global__ __launch_bounds__(64) void iqpt_tile_list_order_kernel(const kbin b, const uint32_t* off_tri, uint32_t* list) {
+    __shared__ uint32_t sc[kOrderMax];
+    __shared__ uint32_t ix[kOrderMax];
+    const uint32_t t = blockIdx.x, lane = threadIdx.x;
+    const uint32_t a0 = off_tri[t], a1 = off_tri[t + 1];
+    const uint32_t n = a1 - a0;
+    if (n < 2u || n > kOrderMax) return;
+    const uint32_t tx = t % b.ntx, ty = t / b.ntx;
+    const uint32_t tw = min(kCullTile, b.ncols - tx * kCullTile), th = min(kCullTile, b.nrows - ty * kCullTile);
+    const bool inside = lane < tw * th;
+    const float x = (float)(b.x0 + tx * kCullTile + (inside ? lane % tw : 0u)) + 0.5f;
+    const float y = (float)(b.y0 + (ty * kCullTile + (inside ? lane / tw : 0u)) * b.ystep) + 0.5f;
+    const float xn = x / (float)b.width * 2.0f - 1.0f, yn = 1.0f - y / (float)b.height * 2.0f;
+    const float* P = b.inv_proj;
+    const float* V = b.inv_view;
+    float nr[4], fr[4];
+    for (int c = 0; c < 4; ++c) {
+        nr[c] = xn * P[c] + yn * P[4 + c] + P[12 + c];
+        fr[c] = xn * P[c] + yn * P[4 + c] + P[8 + c] + P[12 + c];
+    }
+    float o[3], f[3];
+    for (int c = 0; c < 3; ++c) {
+        const float nx = nr[0] / nr[3], ny = nr[1] / nr[3], nz = nr[2] / nr[3];
+        const float fx = fr[0] / fr[3], fy = fr[1] / fr[3], fz = fr[2] / fr[3];
+        o[c] = nx * V[c] + ny * V[4 + c] + nz * V[8 + c] + V[12 + c];
+        f[c] = fx * V[c] + fy * V[4 + c] + fz * V[8 + c] + V[12 + c];
+    }
+    float d[3] = {f[0] - o[0], f[1] - o[1], f[2] - o[2]};
+    const float il = 1.0f / sqrtf(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+    d[0] *= il;
+    d[1] *= il;
+    d[2] *= il;
+    for (uint32_t e = 0; e < n; ++e) {
+        const uint32_t j = list[a0 + e];
+        bool hit = false;
+        for (uint32_t h = 0; h < 2u && inside; ++h) {
+            const uint32_t kk = 2u * j + h;
+            if (kk >= b.ntri) break;
+            const float4_storage* tr = b.tris + (size_t)kk * kTriFloat4;
+            const float e1[3] = {tr[0].w, tr[1].x, tr[1].y}, e2[3] = {tr[1].z, tr[1].w, tr[2].x};
+            const float pv[3] = {d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0]};
+            const float det = e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2];
+            if (fabsf(det) < 1e-9f) continue;
+            const float inv = 1.0f / det;
+            const float tv[3] = {o[0] - tr[0].x, o[1] - tr[0].y, o[2] - tr[0].z};
+            const float u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv;
+            const float qv[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2], tv[0] * e1[1] - tv[1] * e1[0]};
+            const float v = (d[0] * qv[0] + d[1] * qv[1] + d[2] * qv[2]) * inv;
+            const float tt = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv;
+            hit = hit || (u >= 0.0f && v >= 0.0f && u + v <= 1.0f && tt > 0.0f);
+        }
+        const uint32_t s = (uint32_t)__popcll(__ballot(hit));
+        if (lane == 0) {
+            sc[e] = s;
+            ix[e] = j;
+        }
+    }
+    __syncthreads();
+    // rank by (score descending, position ascending): a permutation of [0, n)
+    for (uint32_t e = lane; e < n; e += 64u) {
+        const uint32_t s = sc[e];
+        uint32_t r = 0;
+        for (uint32_t q = 0; q < n; ++q) r += (sc[q] > s || (sc[q] == s && q < e)) ? 1u : 0u;
+        list[a0 + r] = ix[e];
+    }
 }
 
 // Compact row-major <-> tile-major reorder of pixel-state planes (one thread per 32-bit word).
@@ -2607,7 +2701,7 @@ __global__ __launch_bounds__(kStitchBlock) void iqpt_split_stitch_kernel(const k
             const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
             const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
             const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
-            s.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+            s.bgra[tile_to_compact(pix, s.ncols, s.nrows)] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
             reinterpret_cast<float4*>(s.lin)[pix] = make_float4(ax, ay, az, 0.0f);
             s.rng[pix] = st.v0;
             s.rng[(size_t)s.npix + pix] = st.v1;
@@ -2717,7 +2811,7 @@ __global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(co
                 const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
                 const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
                 const uint32_t bb = to_u8(255.0f * iq_sqrtf(az));
-                p.bgra[pix] = bb | (g8 << 8) | (r8 << 16) | (255u << 24);
+                p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = bb | (g8 << 8) | (r8 << 16) | (255u << 24);
                 reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
                 p.rng[pix] = ring_st[e];
                 p.rng[(size_t)p.npix + pix] = ring_st[kG * kR + e];
@@ -3053,7 +3147,7 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
             const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
             const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
             const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
-            p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+            p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
             reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
         }
         if (threadIdx.x == 0)
@@ -3142,7 +3236,7 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
             const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
             const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
             const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
-            p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+            p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
             reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
         }
     }
@@ -3168,6 +3262,14 @@ __device__ __forceinline__ void fan_body(const kparams& p, uint32_t bid) {
 //    leaves its window continues in a new window (another round).
 // Same bits as the plain kernel: the same per-sample code, the same mean terms, the chain's own slots as
 // rays, the state where the chain stops.
+// Wave-synchronous step: every lane of the wave is past its earlier LDS writes before any reads after it
+// (LDS operations of one wave complete in order; the fences keep the compiler from moving accesses across).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 constexpr uint32_t kSpecBlock = 256;
 constexpr uint32_t kSpecLanes = 16;                    // lanes per sphere pixel without a plan
 constexpr uint32_t kSpecPix = kSpecBlock / kSpecLanes; // sphere pixels per block without a plan
@@ -3225,11 +3327,15 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         first = s.blocks[2 * bid];
         const uint32_t w = s.blocks[2 * bid + 1];
         cnt = w & 0xffu;
-        L = w >> 8;                                        // lanes per pixel: 8, 16, 24, 32, 48 or 64
+        L = w >> 8;                                        // lanes per pixel: 8, 16, 32 or 64
     }
     const uint32_t batch = min(64u, 2u * L);              // walk: chain samples per pixel and batch
-    // pixel g of the block on lanes [g L, g L + L) (a class that does not divide 256 leaves the last lanes idle)
+    // pixel g of the block on lanes [g L, g L + L): L divides 64, so a pixel's lanes are one wave's, and each wave
+    // runs its pixels' rounds on its own (round 5: no block barrier after the start; a wave that needs no
+    // fix-up pass or second round does not wait for one that does)
     const uint32_t g = threadIdx.x / L, l = threadIdx.x - g * L;
+    const uint32_t gw0 = (threadIdx.x & ~63u) / L;              // the wave's first pixel group
+    const uint32_t gw1 = min(cnt, gw0 + 64u / L);                // ... and the end of its valid ones
     const bool valid = g < cnt, walker = valid && l == 0u;
     const uint32_t q = valid ? (s.order ? s.order[first + g] : first + g) : 0u;
     const uint32_t pix = valid ? s.pix[q] : 0u;
@@ -3261,10 +3367,12 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         rd[11] = 0u;
         rd[12] = q;
         rd[13] = pix;
-        // parity pixel (round 0 traces the even slots first): its last chain took at least s.parity_rho / 256
-        // slots per sample (two-slot samples: camera ray, sphere, scattered ray); 0 = every slot (round 4)
+        // parity pixel (round 0 traces the even slots first): its last chain took between s.parity_rho / 256 and
+        // s.parity_hi / 256 slots per sample (two-slot samples: camera ray, sphere, scattered ray; above, the chain
+        // has so many 3-slot samples that it lands on an odd slot early and the fix-up pass traces most odd slots
+        // anyway, after a walk: r05 run 7); parity_rho 0 = every slot (round 4)
         const uint32_t r0 = s.rho[q] ? s.rho[q] : s.rho0;
-        rd[14] = (s.parity_rho != 0u && r0 >= s.parity_rho) ? 1u : 0u;
+        rd[14] = (s.parity_rho != 0u && r0 >= s.parity_rho && r0 <= s.parity_hi) ? 1u : 0u;
         rd[15] = 0u;
     } else if (!valid && l == 0u) {
         // no pixel (the grid's last block): an empty, finished record (every field is read by the rounds)
@@ -3276,12 +3384,13 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     const bool rec_w = s.tl != nullptr && (threadIdx.x & 63u) == 0u;
     uint64_t t_rec[3] = {rec ? __builtin_amdgcn_s_memrealtime() : 0ull, 0ull, 0ull};
     uint32_t rounds = 0, iters = 0;                          // measurement: this wave's slot-loop iterations
+    uint32_t it_done = 0;                                     // this wave's slot-loop iterations so far (priority)
     uint32_t lane_rays = 0;                                  // rays of the chain samples this lane gathered
     __syncthreads();
 
     // Rounds: round 0 is the window; a chain that leaves it continues in a new window from its end
     // (never expected with the margins; bounded by spp rounds since each folds at least one sample)
-    while (__syncthreads_or(rd[7] == 0u)) {
+    while (__any(rd[7] == 0u)) {
         const bool live = rd[7] == 0u;
         const uint32_t js = rd[0], M = rd[1];
         // ---- slot pass: slots [js + j0, js + j1) of this lane (relative slot indices j). Every slot of the
@@ -3310,8 +3419,8 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         float4* cres = res;
         uint8_t* cln = ln;
         bool active = live && j0 < j1;
-        // fix-up pass: this lane's share [fa, fb) of the block's pooled odd slots (lds_w holds the prefix sums
-        // over the block's pixels of their fix-up slot counts)
+        // fix-up pass: this lane's share [fa, fb) of the wave's pooled odd slots (pw: the prefix sums over the
+        // wave's pixels of their fix-up slot counts, in the wave's own words of lds_w)
         uint32_t fa = 0, fb = 0;
         bool fix = false;
         ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -3325,14 +3434,16 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         };
         // the next run of the fix-up share: pixel group gg holding pooled index fa, its odd slots from there on
         // (within [fa, fb)), the state at the first one stepped from the nearest slot-pass start state below it
+        uint32_t* const pw = lds_w + 2u * gw0;
         auto next_run = [&]() -> bool {
             if (fa >= fb) return false;
-            uint32_t h = 0;
-            while (h + 1u < cnt && lds_w[h + 1u] <= fa) ++h;
+            uint32_t i = 0;
+            while (gw0 + i + 1u < gw1 && pw[i + 1u] <= fa) ++i;
+            const uint32_t h = gw0 + i;
             const uint32_t* rh = lds_rd + h * 16u;
             const uint32_t Mh = rh[1], jsh = rh[0], ph = rh[13];
-            const uint32_t n_here = min(fb, lds_w[h + 1u]) - fa;
-            jc = rh[15] + 2u * (fa - lds_w[h]);           // an odd slot at or after where the chain got stuck
+            const uint32_t n_here = min(fb, pw[i + 1u]) - fa;
+            jc = rh[15] + 2u * (fa - pw[i]);              // an odd slot at or after where the chain got stuck
             je = jc + 2u * n_here;
             fa += n_here;
             gg = h;
@@ -3358,6 +3469,18 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             if (active) start_slot();
             while (__any(active)) {
                 if (rec_w) ++iters;
+                // progress-fair VALU priority (s.prio_q, round 5): every spec block is resident from the start and
+                // the SIMDs arbitrate by priority, then age, so at one priority the youngest blocks (dispatched
+                // last) only issue when older waves stall and end last; a wave's priority falls from 3 by one
+                // level per prio_q iterations it has run, so a wave that lags keeps the higher level
+                if ((OPT & kOptPrio) && s.prio_q) {
+                    const uint32_t lvl = it_done / s.prio_q;
+                    if (lvl == 0u) __builtin_amdgcn_s_setprio(3);
+                    else if (lvl == 1u) __builtin_amdgcn_s_setprio(2);
+                    else if (lvl == 2u) __builtin_amdgcn_s_setprio(1);
+                    else __builtin_amdgcn_s_setprio(0);
+                }
+                ++it_done;
                 // closest hit (path_tracer.cu:253-295): camera rays over their tile's mask pairs in index order
                 float closest = kTMax;
                 int kind = kHitNone;
@@ -3447,12 +3570,14 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         float ax = __uint_as_float(rd[8]), ay = __uint_as_float(rd[9]), az = __uint_as_float(rd[10]);
         uint32_t k = rd[11];
         // batches of chain samples up to the window's end, the launch's spp, or a slot not traced yet (an odd
-        // slot of a parity pixel before the fix-up pass)
+        // slot of a parity pixel before the fix-up pass), while some walker of the wave can go on
         auto walk = [&]() {
-            for (uint32_t r0 = 0; r0 < p.spp; r0 += batch) {
-                if (walker && live) {
+            while (true) {
+                const bool more = walker && live && k < p.spp && jw < M && ln[jw] != 0u;
+                if (!__any(more)) break;
+                if (walker) {
                     uint32_t c = 0;
-                    while (c < batch && k + c < p.spp && jw < M) {
+                    while (more && c < batch && k + c < p.spp && jw < M) {
                         const uint32_t nj = ln[jw];
                         if (nj == 0u) break;
                         lp[c++] = (uint16_t)jw;
@@ -3460,7 +3585,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                     }
                     lds_w[2 * g] = c;
                 }
-                __syncthreads();
+                wave_sync();
                 const uint32_t cw = (valid && live) ? lds_w[2 * g] : 0u;
                 // the pixel's lanes gather the chain samples' colours and form their mean terms c / n and
                 // (n - 1) / n (sample k of the launch), and count their rays: the walker is left the
@@ -3477,7 +3602,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                     const uint32_t n = ln[lp[i]];
                     lane_rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
                 }
-                __syncthreads();
+                wave_sync();
                 if (walker && live)
 #pragma unroll 4
                     for (uint32_t i = 0; i < cw; ++i) {
@@ -3487,38 +3612,41 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                         az = v.z + az * v.w;
                     }
                 k += cw;
-                __syncthreads();
+                wave_sync();
             }
         };
         // the slot pass and its walk, then (parity pixels whose chain landed on an odd slot at jw, if any in the
-        // block) the fix-up pass — every odd slot from there to the window's end, the even ones being traced, so
-        // the walk then runs to the window's end — and the walk again. The block's fix-up slots are pooled and
-        // shared evenly by all its lanes: a few chains need them, most do not.
+        // wave) the fix-up pass — every odd slot from there to the window's end, the even ones being traced, so
+        // the walk then runs to the window's end — and the walk again. The wave's fix-up slots are pooled and
+        // shared evenly by its 64 lanes: a few chains need them, most do not.
         for (uint32_t pass = 0;; ++pass) {
             trace();
-            // walk: the colours are this block's own stores (complete: vmcnt 0), read back from L2
+            // walk: the colours are this wave's own stores (complete: vmcnt 0), read back from L2; the walk (and
+            // a fix-up pass) ends the wave's pixels: the highest priority
             __builtin_amdgcn_s_waitcnt(0);
-            __syncthreads();
+            wave_sync();
+            if ((OPT & kOptPrio) && s.prio_q) __builtin_amdgcn_s_setprio(3);
             if (rec && rounds == 0u && pass == 0u) t_rec[1] = __builtin_amdgcn_s_memrealtime();
             walk();
             if (pass == 1u) break;
             const bool stuck = walker && live && k < p.spp && jw < M && ln[jw] == 0u;
-            if (!__syncthreads_or(stuck)) break;
+            if (!__any(stuck)) break;
             if (walker) rd[15] = stuck ? jw : M;
-            __syncthreads();
-            if (threadIdx.x == 0) {
+            if (stuck) atomicAdd(s.run_count, 1u);       // statistics: chains that needed the fix-up pass
+            wave_sync();
+            if (__lane_id() == 0u) {
                 uint32_t acc = 0;
-                for (uint32_t h = 0; h < cnt; ++h) {
-                    lds_w[h] = acc;
+                for (uint32_t h = gw0; h < gw1; ++h) {
+                    pw[h - gw0] = acc;
                     const uint32_t* rh = lds_rd + h * 16u;
                     if (rh[7] == 0u && rh[15] < rh[1]) acc += (rh[1] - rh[15] + 1u) / 2u;
                 }
-                lds_w[cnt] = acc;
+                pw[gw1 > gw0 ? gw1 - gw0 : 0u] = acc;
             }
-            __syncthreads();
-            const uint32_t F = lds_w[cnt];
-            fa = (uint32_t)(((uint64_t)F * threadIdx.x) / kSpecBlock);
-            fb = (uint32_t)(((uint64_t)F * (threadIdx.x + 1u)) / kSpecBlock);
+            wave_sync();
+            const uint32_t F = pw[gw1 > gw0 ? gw1 - gw0 : 0u];
+            fa = (uint32_t)(((uint64_t)F * __lane_id()) / 64u);
+            fb = (uint32_t)(((uint64_t)F * (__lane_id() + 1u)) / 64u);
             fix = true;
             active = next_run();
         }
@@ -3548,7 +3676,7 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                 const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
                 const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
                 const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
-                p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+                p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
                 reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
                 p.rng[pix] = v0;
                 p.rng[(size_t)p.npix + pix] = v1;
@@ -3568,15 +3696,19 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         }
         if (rec && rounds == 0u) t_rec[2] = __builtin_amdgcn_s_memrealtime();
         ++rounds;
+        wave_sync();                                       // the walkers' records before the loop test
     }
     if (rec) {
         unsigned long long* o = s.tl + 8 * (size_t)bid;
         o[0] = t_rec[0];
         o[1] = t_rec[1];
         o[2] = t_rec[2];
-        o[3] = (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) | ((unsigned long long)rounds << 48);
     }
-    if (rec_w) s.tl[8 * (size_t)bid + 4 + threadIdx.x / 64u] = iters;
+    // per wave: its end (48 bits) | its slot-loop iterations << 48 (the block's end: the latest of its waves)
+    if (rec_w)
+        s.tl[8 * (size_t)bid + 4 + threadIdx.x / 64u] =
+            (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) | ((unsigned long long)min(iters, 0xffffu) << 48);
+    if (rec) s.tl[8 * (size_t)bid + 3] = (unsigned long long)rounds << 48;
     unsigned long long rays = lane_rays;
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
@@ -3645,7 +3777,7 @@ __global__ __launch_bounds__(kSkyBlock) void iqpt_sky_kernel(const kparams p, co
         const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
         const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
         const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
-        p.bgra[pix] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+        p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
         reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
         p.rng[pix] = st.v0;
         p.rng[(size_t)p.npix + pix] = st.v1;
@@ -3840,6 +3972,13 @@ int launch_certain(void* stream, const kbin& b, uint32_t* certain) {
     const uint32_t ntiles = b.ntx * b.nty;
     if (ntiles == 0) return 0;
     hipLaunchKernelGGL(iqpt_certain_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, b, certain);
+    return (int)hipGetLastError();
+}
+
+int launch_tile_list_order(void* stream, const kbin& b, const uint32_t* off_tri, uint32_t* list) {
+    const uint32_t ntiles = b.ntx * b.nty;
+    if (ntiles == 0) return 0;
+    hipLaunchKernelGGL(iqpt_tile_list_order_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, b, off_tri, list);
     return (int)hipGetLastError();
 }
 

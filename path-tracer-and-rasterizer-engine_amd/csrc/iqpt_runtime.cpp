@@ -205,6 +205,10 @@ struct iqpt_ctx {
     bool spec_rho_valid = false;
     bool spec_last = false;
     uint32_t spec_rho0 = iqpt::kSpecRho0;   // window of a pixel without history (iqpt_debug_set_spec)
+    uint32_t spec_parity_rho = iqpt::kSpecParityRho;   // parity pixels' threshold (iqpt_debug_set_spec_parity; 0 off)
+    uint32_t spec_parity_hi = iqpt::kSpecParityHi;     // ... and upper bound (iqpt_debug_set_spec_parity_max)
+    bool anyhit_on = true;                  // any-hit queries in triangle-only scenes (iqpt_debug_set_anyhit)
+    uint32_t spec_prio_q = 0;               // spec kernel progress-fair priority step (iqpt_debug_set_spec_prio; 0 off)
     uint32_t spec_margin_div = 16;          // window margin: 1/16 of the extra slots, at least 4 (iqpt_debug_set_spec;
                                             // against 1/4, 5 % of the chains take a second round instead of 0.6 %,
                                             // yet -4 % per launch at N = 2 / 4 / 8, profiles/r03/spec_margins.json)
@@ -329,6 +333,12 @@ struct iqpt_ctx {
 };
 
 namespace {
+
+// Words of a BGRA8 frame buffer: the owned pixels, padded to the multi-GPU gather's block once a communicator
+// exists (a pipelined launch's buffer is then the gather's send buffer itself)
+size_t frame_words(const iqpt_ctx* c) {
+    return std::max<size_t>((size_t)c->npix, (size_t)c->comm_stride);
+}
 
 int use_device(const iqpt_ctx* c) {
     IQPT_HIP(hipSetDevice(c->device));
@@ -524,8 +534,10 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     for (uint32_t q = 0; q < n; ++q) {
         const uint32_t r = rho[q] ? rho[q] : ks.rho0;
         const uint32_t m = iqpt::spec_window(r, p.spp, ks.m_cap, ks.margin_div);
-        // slots traced (the window's) times their mean length
-        w[q] = (double)m * (double)std::max<uint32_t>(r, 256u) / 256.0;
+        // slots traced (the window's; a parity pixel's even ones and, expected, a quarter of the window's odd
+        // ones in the pooled fix-up pass) times their mean length
+        const bool parity = ks.parity_rho != 0u && r >= ks.parity_rho && r <= ks.parity_hi;
+        w[q] = (double)m * (parity ? 0.625 : 1.0) * (double)std::max<uint32_t>(r, 256u) / 256.0;
         total += w[q];
         wmax = std::max(wmax, w[q]);
     }
@@ -535,7 +547,8 @@ uint32_t spec_build_plan(iqpt_ctx* c, const iqpt::kparams& p, const iqpt::kspec&
     // lane classes: 256 / lanes pixels per block (a class that does not divide 256 leaves lanes idle); the
     // in-between classes let a plan use resident lanes that the next power of two would overfill (most
     // sphere pixels have the same work: r04 run 27)
-    static constexpr uint32_t kLanes[iqpt::kSpecLaneClasses] = {8u, 16u, 24u, 32u, 48u, 64u};
+    static constexpr uint32_t kLanes[iqpt::kSpecLaneClasses] = {8u, 16u, 32u, 64u};   // dividing 64: a pixel's
+                                                                                           // lanes are one wave's
     constexpr uint8_t kTop = iqpt::kSpecLaneClasses - 1;
     auto cls_of = [&](uint32_t q, double e) -> uint8_t {
         uint8_t k = 0;
@@ -693,6 +706,24 @@ int build_cull(iqpt_ctx* c) {
     // a pixel of the next tile, so waves hold two tiles and their LDS batches test the union of both tiles'
     // candidates: C4 +66 % per launch whether the pixels are folded in the refill or by a kernel of their own
     // (profiles/r03/ab_certain.json, ab_streamed_certain_fold_rejected.json)
+    // per tile: candidate triangle pairs and sphere pairs (the queue order's cost, the lists' sizes, and the
+    // certain kernel's budget below); d_cnt is freed with the lists
+    uint32_t* d_cnt = nullptr;
+    IQPT_HIP(hipMalloc(&d_cnt, 2 * (size_t)ntiles * sizeof(uint32_t)));
+    std::vector<uint32_t> cnt(2 * (size_t)ntiles);
+    {
+        const int lcnt = iqpt::launch_tile_count(c->stream, c->d_cull, ntiles, c->cull_wt, c->cull_stride, d_cnt,
+                                                 d_cnt + ntiles);
+        hipError_t e = lcnt ? (hipError_t)lcnt : hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof(uint32_t),
+                                                                hipMemcpyDeviceToHost, c->stream);
+        if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+        if (e != hipSuccess) {
+            (void)hipFree(d_cnt);
+            return iqpt::hip_fail(e, "tile counts");
+        }
+    }
+    uint64_t cand = 0;
+    for (size_t t = 0; t < cnt.size(); ++t) cand += cnt[t];
     c->certain_valid = false;
     c->sky_active = false;
     c->h_miss.clear();
@@ -704,6 +735,9 @@ int build_cull(iqpt_ctx* c) {
     c->d_sky_tiles = nullptr;
     c->n_sky_tiles = 0;
     c->n_sky_pixels = 0;
+    // (resident scenes: streamed ones with certain pixels and the sky kernel — their BVH-primary variants, which
+    // have no LDS batches — measured slower on C4 in round 5, 135 -> 161 ms)
+    (void)cand;
     if (!c->d_mats && ntiles > 0 && resident_bytes <= iqpt::kLdsResidentBytes) {
         // per tile: the certain-hit mask (2 words), then after all tiles the certain-miss masks (2 words each)
         if (hipMalloc(&c->d_certain, 4 * (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
@@ -739,18 +773,6 @@ int build_cull(iqpt_ctx* c) {
     // queue order over tiles (a queue chunk is one tile): most expensive first, so the pixels that set
     // the end of the launch are cheap ones. Cost = candidate triangle pairs + 8 x candidate sphere pairs
     // (a camera ray that can hit a sphere starts an Oren-Nayar path: more rays and the scatter shading).
-    uint32_t* d_cnt = nullptr;
-    IQPT_HIP(hipMalloc(&d_cnt, 2 * (size_t)ntiles * sizeof(uint32_t)));
-    std::vector<uint32_t> cnt(2 * (size_t)ntiles);
-    const int lc = iqpt::launch_tile_count(c->stream, c->d_cull, ntiles, c->cull_wt, c->cull_stride, d_cnt,
-                                           d_cnt + ntiles);
-    hipError_t e = lc ? (hipError_t)lc : hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof(uint32_t),
-                                                        hipMemcpyDeviceToHost, c->stream);
-    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-    if (e != hipSuccess) {
-        (void)hipFree(d_cnt);
-        return iqpt::hip_fail(e, "tile counts");
-    }
     std::vector<uint32_t> cost(ntiles);
     for (uint32_t t = 0; t < ntiles; ++t) cost[t] = cnt[t] + 8u * cnt[ntiles + t];
     // a certain pixel costs a fold of its samples: a tile's cost scales with its uncertain pixels (fully
@@ -794,6 +816,9 @@ int build_cull(iqpt_ctx* c) {
                                 c->stream) == hipSuccess &&
                  iqpt::launch_tile_list(c->stream, c->d_cull, ntiles, c->cull_wt, c->cull_stride, d_off,
                                         d_off + ntiles + 1, c->d_list) == 0 &&
+                 // any-hit scenes: the lists most-hit pairs first (the launch's loop leaves at the wave's last hit)
+                 (!(c->nsph == 0 && !c->d_mats && c->anyhit_on) ||
+                  iqpt::launch_tile_list_order(c->stream, b, d_off, c->d_list) == 0) &&
                  hipStreamSynchronize(c->stream) == hipSuccess;
         }
         if (!ok) {
@@ -1637,6 +1662,8 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     }
     p.mats = c->d_mats;
     p.tri_shade = c->d_tri_shade;
+    // no sphere, no material table: every triangle emissive, a ray decided by its first accepted triangle
+    p.anyhit = (c->nsph == 0 && !c->d_mats && c->anyhit_on) ? 1u : 0u;
     p.rcp_width = 1.0f / (float)c->width;
     p.rcp_height = 1.0f / (float)c->height;
     const bool cam_axis = (opt & iqpt::kOptCamConst) && cam_axis_constants(c->cam, p.cam_ax);
@@ -1857,6 +1884,8 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks.frame0 = c->frame;
         ks.mean_tiny = p.mean_tiny;
         ks.npix = c->npix;
+        ks.ncols = c->ncols;
+        ks.nrows = c->set.nrows;
         ks.sp_pix = sp_pix;
         ks.sp_win = sp_pix + ns_cap;
         ks.sp_rho = sp_pix + 2 * ns_cap;
@@ -2061,6 +2090,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.m_cap = m_cap;
         ks2.rho0 = c->spec_rho0;
         ks2.margin_div = c->spec_margin_div;
+        ks2.parity_rho = c->spec_parity_rho;
+        ks2.parity_hi = c->spec_parity_hi;
+        ks2.prio_q = c->spec_prio_q;
         ks2.pix = c->d_chain_pix;
         ks2.m = c->d_spec;
         ks2.rho = c->d_spec + n;
@@ -2384,7 +2416,9 @@ int iqpt_read(iqpt_ctx* c, float* lin_rgba, uint8_t* bgra) {
     int st = enter(c);
     if (st) return st;
     if (lin_rgba && (st = fetch_compact(c, c->d_lin, 4, 1, lin_rgba)) != IQPT_OK) return st;
-    if (bgra && (st = fetch_compact(c, c->d_bgra, 1, 1, bgra)) != IQPT_OK) return st;
+    // the BGRA8 frame is stored in compact order already (tile_to_compact)
+    if (bgra) IQPT_HIP(hipMemcpyAsync(bgra, c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                      c->stream));
     IQPT_HIP(hipStreamSynchronize(c->stream));
     return check_dev_err(c);
 }
@@ -2451,9 +2485,9 @@ int iqpt_checkpoint_save(iqpt_ctx* c, const char* path) {
     // the file holds the compact row-major order (independent of the device layout)
     if ((st = check_dev_err(c)) != IQPT_OK) return st;     // never persist undefined state
     if ((st = fetch_compact(c, c->d_lin, 4, 1, lin.data())) != IQPT_OK ||
-        (st = fetch_compact(c, c->d_bgra, 1, 1, bgra.data())) != IQPT_OK ||
         (st = fetch_compact(c, c->d_rng, 1, 6, rng.data())) != IQPT_OK)
         return st;
+    IQPT_HIP(hipMemcpy(bgra.data(), c->d_bgra, n * sizeof(uint32_t), hipMemcpyDeviceToHost));   // compact already
     if ((st = read_rays(c, &rays)) != IQPT_OK) return st;
     ckpt_header h;
     std::memset(&h, 0, sizeof h);
@@ -2531,9 +2565,9 @@ int iqpt_checkpoint_load(iqpt_ctx* c, const char* path) {
     IQPT_HIP(hipStreamSynchronize(c->stream));
     const unsigned long long rays = h.rays;
     if ((st = store_compact(c, lin.data(), 4, 1, c->d_lin)) != IQPT_OK ||
-        (st = store_compact(c, bgra.data(), 1, 1, c->d_bgra)) != IQPT_OK ||
         (st = store_compact(c, rng.data(), 1, 6, c->d_rng)) != IQPT_OK)
         return st;
+    IQPT_HIP(hipMemcpy(c->d_bgra, bgra.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice));   // compact order
     {
         std::vector<unsigned long long> slots((size_t)iqpt::kRaySlots * iqpt::kRaySlotStride, 0ull);
         slots[0] = rays;
@@ -2603,8 +2637,9 @@ int iqpt_kernel_time(iqpt_ctx* c, double* total_ms, uint64_t* launches) {
 
 /* Internal (tools): the per-pixel split of the last camera / packet — sphere pixels (the chain and spec
  * kernels' list), fan tiles, anchored tiles, split tiles — and, after a spec launch, the sum of its
- * windows and of its chains' slots per sample, and the chains finished past their window since the last
- * call (out8[7]; the call clears it). Synchronises. */
+ * windows and of its chains' slots per sample, and since the last call (the call clears them) the chains
+ * finished past their window (out8[7] low 32 bits) and the parity chains that needed the fix-up pass (out8[7]
+ * high 32 bits). Synchronises. */
 int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
     if (!c || !out8) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     int st = enter(c);
@@ -2620,7 +2655,7 @@ int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
         std::vector<uint32_t> v(2 * (size_t)n + 2);
         IQPT_HIP(hipMemcpy(v.data(), c->d_spec, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
         out8[4] = c->spec_plan_n == n && c->spec_plan_mode ? c->spec_plan_blocks : 0;   // plan blocks (0: none)
-        out8[7] = v[2 * (size_t)n + 1];
+        out8[7] = (unsigned long long)v[2 * (size_t)n + 1] | ((unsigned long long)v[2 * (size_t)n] << 32);
         unsigned long long m = 0, rho = 0;
         for (uint32_t q = 0; q < n; ++q) {
             m += v[q];
@@ -2776,6 +2811,47 @@ int iqpt_debug_set_pipe(iqpt_ctx* c, int fan_pipe) {
     return IQPT_OK;
 }
 
+/* Internal (A/B): the spec kernel's progress-fair VALU priority — a wave's priority falls from 3 by one level per
+ * `q` slot-loop iterations it has run (0: 3 throughout, the round-4 behaviour). Same bits either way. */
+int iqpt_debug_set_spec_prio(iqpt_ctx* c, uint32_t q) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->spec_prio_q = q;
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): any-hit queries for triangle-only scenes under the reference's materials (1, the
+ * default) or the closest-hit search (0). Same bits either way. */
+int iqpt_debug_set_anyhit(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->anyhit_on = on != 0;
+    c->cull_valid = false;               // the candidate lists' order follows the setting
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): the spec kernel's parity pixels — a pixel whose last chain took at least rho256 / 256
+ * slots per sample traces the even slots of its window first and the odd ones only from where its chain lands on
+ * one (pooled over the block's lanes); 0 traces every slot of every window (round 4). Same bits either way. */
+int iqpt_debug_set_spec_parity(iqpt_ctx* c, uint32_t rho256) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->spec_parity_rho = rho256;
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): the parity pixels' upper bound (slots per sample x 256 of the last chain; 0xffffffff: none). */
+int iqpt_debug_set_spec_parity_max(iqpt_ctx* c, uint32_t rho256) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->spec_parity_hi = rho256;
+    return IQPT_OK;
+}
+
 /* Internal (A/B, measurement): how spec launches run the fan tiles beside the sphere pixels — 0 two kernels on
  * two streams, pipelined across launches (the default), 1 two kernels one after the other on one stream. (Round
  * 4's mode 2, spec and fan blocks in one grid, measured slower and is archived: branch round4-ab-archive.)
@@ -2848,9 +2924,8 @@ int iqpt_copy_frame_device(iqpt_ctx* c, void* dst_device, size_t bytes) {
     if (bytes < (size_t)c->npix * sizeof(uint32_t)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "destination too small");
     int st = enter(c);
     if (st) return st;
-    const int le = iqpt::launch_relayout(c->stream, c->d_bgra, static_cast<uint32_t*>(dst_device), c->ncols,
-                                         c->set.nrows, 1, 1, true);
-    if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
+    IQPT_HIP(hipMemcpyAsync(dst_device, c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                            c->stream));                    // compact order already
     IQPT_HIP(hipStreamSynchronize(c->stream));
     return check_dev_err(c);
 }
@@ -2859,6 +2934,23 @@ namespace {
 // The stream-ordered frame copy (iqpt_copy_frame_device_async, the gather's send copy): the BGRA8 frame in
 // compact order into dst, behind every render issued so far; `wait` (if not null) is waited for on the copy's
 // stream first; *used = that stream.
+// Pipelined launches, from the first copy or gather behind one on: the ring of frame buffers the launches write
+// in turn (each of frame_words(c): the multi-GPU gather sends a launch's buffer as it is).
+int ensure_ring(iqpt_ctx* c) {
+    if (c->pring_on) return IQPT_OK;
+    for (int i = 0; i < iqpt::kPipeRing; ++i) {
+        if ((!c->d_pring[i] && hipMalloc(&c->d_pring[i], frame_words(c) * sizeof(uint32_t)) != hipSuccess) ||
+            (!c->pev[i] && hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming) != hipSuccess)) {
+            (void)hipGetLastError();
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "frame buffers for pipelined copies");
+        }
+        c->pseq[i] = 0;
+    }
+    c->pidx = iqpt::kPipeRing - 1;     // the next launch writes d_pring[0]
+    c->pring_on = true;
+    return IQPT_OK;
+}
+
 int copy_frame_async(iqpt_ctx* c, uint32_t* dst, hipEvent_t wait, hipStream_t* used) {
     // no synchronisation here: an error the kernels raise for this launch is reported by the next
     // synchronising call (iqpt_sync, iqpt_read, ...); one already latched fails the copy now
@@ -2868,26 +2960,16 @@ int copy_frame_async(iqpt_ctx* c, uint32_t* dst, hipEvent_t wait, hipStream_t* u
     if (c->pipe) {
         // pipelined spec launches: the copy on stream3 behind both kernels of the last launch; from here on
         // the launches write the ring of frame buffers in turn
-        if (!c->pring_on) {
-            for (int i = 0; i < iqpt::kPipeRing; ++i) {
-                if ((!c->d_pring[i] && hipMalloc(&c->d_pring[i], (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) ||
-                    (!c->pev[i] && hipEventCreateWithFlags(&c->pev[i], hipEventDisableTiming) != hipSuccess)) {
-                    (void)hipGetLastError();
-                    return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "frame buffers for pipelined copies");
-                }
-                c->pseq[i] = 0;
-            }
-            c->pidx = iqpt::kPipeRing - 1;     // the next launch writes d_pring[0]
-            c->pring_on = true;
-        }
+        if ((st = ensure_ring(c)) != IQPT_OK) return st;
         if ((st = ensure_copy_stream(c)) != IQPT_OK) return st;
+        // a gather in flight read an earlier ring buffer: keep the ring's reuse events in one order
+        if (c->comm_pend) IQPT_HIP(hipStreamWaitEvent(c->stream3, c->ev_gend, 0));
         if (!c->end1) IQPT_HIP(hipEventRecord(c->ev_pipe_end, c->stream));
         if (!c->end2) IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
         IQPT_HIP(hipStreamWaitEvent(c->stream3, c->end1 ? c->end1 : c->ev_pipe_end, 0));
         IQPT_HIP(hipStreamWaitEvent(c->stream3, c->end2 ? c->end2 : c->ev_s2, 0));
         if (wait) IQPT_HIP(hipStreamWaitEvent(c->stream3, wait, 0));
-        const int le = iqpt::launch_relayout(c->stream3, c->d_bgra, dst, c->ncols, c->set.nrows, 1, 1, true);
-        if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
+        IQPT_HIP(hipMemcpyAsync(dst, c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream3));
         c->copy_seq += 1;
         IQPT_HIP(hipEventRecord(c->pev[c->copy_seq % iqpt::kPipeRing], c->stream3));
         if (c->d_bgra == c->d_pring[c->pidx]) c->pseq[c->pidx] = c->copy_seq;
@@ -2911,8 +2993,7 @@ int copy_frame_async(iqpt_ctx* c, uint32_t* dst, hipEvent_t wait, hipStream_t* u
         return st;
     }
     if (wait) IQPT_HIP(hipStreamWaitEvent(cs, wait, 0));
-    const int le = iqpt::launch_relayout(cs, c->d_bgra, dst, c->ncols, c->set.nrows, 1, 1, true);
-    if (le != 0) return iqpt::hip_fail((hipError_t)le, "frame reorder");
+    IQPT_HIP(hipMemcpyAsync(dst, c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToDevice, cs));
     *used = cs;
     return IQPT_OK;
 }
@@ -3018,17 +3099,39 @@ int iqpt_comm_init(iqpt_ctx* c, int rank, int world, const void* id, size_t byte
     c->comm_world = world;
     c->comm_stride = stride;
     c->gpar = 0;
+    // the frame buffers pipelined launches write are the gather's send buffers as they are: pad them to the rank
+    // block (the context's own buffer keeps its frame; a ring of the old size is dropped, rebuilt at the next copy)
+    if (stride > c->npix) {
+        uint32_t* nb = nullptr;
+        if (hipMalloc(&nb, (size_t)stride * sizeof(uint32_t)) != hipSuccess) {
+            (void)hipGetLastError();
+            free_comm(c);
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "padded frame buffer");
+        }
+        IQPT_HIP(hipMemsetAsync(nb, 0, (size_t)stride * sizeof(uint32_t), c->stream));
+        IQPT_HIP(hipMemcpyAsync(nb, c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+        IQPT_HIP(hipStreamSynchronize(c->stream));
+        if (c->d_bgra_alt == c->d_bgra_own) c->d_bgra_alt = nb;   // (the overlapped launches' views swap)
+        if (c->d_bgra == c->d_bgra_own || c->pring_on) c->d_bgra = nb;
+        (void)hipFree(c->d_bgra_own);
+        c->d_bgra_own = nb;
+        for (int i = 0; i < iqpt::kPipeRing; ++i) {
+            if (c->d_pring[i]) (void)hipFree(c->d_pring[i]);
+            c->d_pring[i] = nullptr;
+            c->pseq[i] = 0;
+        }
+        c->pring_on = false;
+        c->copy_seq = c->pwaited = 0;
+    }
     return IQPT_OK;
 }
 
 namespace {
-// One gather of `words` words per pixel from d_gsend[b] (filled on stream `from`) to the root, assembled
-// there into dst (W x H pixels) — on cstream, behind the copy and nothing else.
-int gather_enqueue(iqpt_ctx* c, uint32_t b, hipStream_t from, int root, uint32_t* dst, uint32_t words) {
-    IQPT_HIP(hipEventRecord(c->ev_gcopy, from));
-    IQPT_HIP(hipStreamWaitEvent(c->cstream, c->ev_gcopy, 0));
-    // timing (iqpt_comm_time): from the moment the copy is done to the end of the root's assembly — the
-    // transfer plus any wait for slower ranks inside the collective
+// One gather of `words` words per pixel (comm_stride pixels) from src to the root, assembled there into dst
+// (W x H pixels), on cstream behind whatever it already waits for.
+int gather_from(iqpt_ctx* c, const uint32_t* src, int root, uint32_t* dst, uint32_t words) {
+    // timing (iqpt_comm_time): from the moment the send buffer is complete to the end of the root's assembly —
+    // the transfer plus any wait for slower ranks inside the collective
     hipEvent_t t0 = take_event(c), t1 = take_event(c);
     if (t0) (void)hipEventRecord(t0, c->cstream);
     const bool is_root = root == c->comm_rank;
@@ -3040,7 +3143,7 @@ int gather_enqueue(iqpt_ctx* c, uint32_t b, hipStream_t from, int root, uint32_t
         }
     }
     if (!(c->gather_skip & 1)) {
-        const ncclResult_t r = rccl().gather(c->d_gsend[b], is_root ? c->d_grecv : nullptr,
+        const ncclResult_t r = rccl().gather(src, is_root ? c->d_grecv : nullptr,
                                              (size_t)c->comm_stride * words, ncclUint32, root,
                                              static_cast<ncclComm_t>(c->comm), c->cstream);
         if (r != ncclSuccess) return rccl_fail(r, "ncclGather");
@@ -3053,10 +3156,19 @@ int gather_enqueue(iqpt_ctx* c, uint32_t b, hipStream_t from, int root, uint32_t
     }
     if (t1) (void)hipEventRecord(t1, c->cstream);
     if (t0 && t1) c->gtimed.emplace_back(t0, t1);
-    IQPT_HIP(hipEventRecord(c->ev_gdone[b], c->cstream));
     IQPT_HIP(hipEventRecord(c->ev_gend, c->cstream));
-    c->gdone_pend[b] = true;
     c->comm_pend = true;
+    return IQPT_OK;
+}
+
+// ... from send buffer d_gsend[b], filled on stream `from`: behind that copy and nothing else
+int gather_enqueue(iqpt_ctx* c, uint32_t b, hipStream_t from, int root, uint32_t* dst, uint32_t words) {
+    IQPT_HIP(hipEventRecord(c->ev_gcopy, from));
+    IQPT_HIP(hipStreamWaitEvent(c->cstream, c->ev_gcopy, 0));
+    int st = gather_from(c, c->d_gsend[b], root, dst, words);
+    if (st) return st;
+    IQPT_HIP(hipEventRecord(c->ev_gdone[b], c->cstream));
+    c->gdone_pend[b] = true;
     c->gpar = (b + 1u) % (uint32_t)iqpt::kSendRing;
     return IQPT_OK;
 }
@@ -3085,9 +3197,14 @@ int gather_sync(iqpt_ctx* c, int root, int what, float* out_lin, uint8_t* out_bg
         const uint32_t words = k == 0 ? 4u : 1u;
         const uint32_t b = c->gpar;
         if (c->gdone_pend[b]) IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_gdone[b], 0));
-        const int le = iqpt::launch_relayout(c->stream, k == 0 ? reinterpret_cast<const uint32_t*>(c->d_lin) : c->d_bgra,
-                                             c->d_gsend[b], c->ncols, c->set.nrows, words, 1, true);
-        if (le != 0) return iqpt::hip_fail((hipError_t)le, "gather copy");
+        if (k == 0) {
+            const int le = iqpt::launch_relayout(c->stream, reinterpret_cast<const uint32_t*>(c->d_lin), c->d_gsend[b],
+                                                 c->ncols, c->set.nrows, words, 1, true);
+            if (le != 0) return iqpt::hip_fail((hipError_t)le, "gather copy");
+        } else {
+            IQPT_HIP(hipMemcpyAsync(c->d_gsend[b], c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToDevice,
+                                    c->stream));            // the BGRA8 frame is compact already
+        }
         if ((st = gather_enqueue(c, b, c->stream, root, c->d_gframe, words)) != IQPT_OK) return st;
         IQPT_HIP(hipStreamSynchronize(c->cstream));
         c->comm_pend = false;
@@ -3105,6 +3222,23 @@ int iqpt_gather_frame_async(iqpt_ctx* c, int root, void* dst_device, size_t byte
     if (st) return st;
     if (root == c->comm_rank && (!dst_device || bytes < (size_t)c->width * c->height * 4))
         return iqpt::fail(IQPT_ERR_INVALID_ARG, "root: destination NULL or smaller than W x H x 4 bytes");
+    if (c->pipe && c->d_bgra && !c->dev_err) {
+        // pipelined launches: the launch's frame buffer (compact order, padded to the rank block) is the send
+        // buffer — no copy: the communicator stream waits for the launch's kernels' own end events, gathers, and
+        // records the ring's reuse event (the next launches writing this buffer wait for it, pipe_begin)
+        if ((st = ensure_ring(c)) != IQPT_OK) return st;
+        if (!c->end1) IQPT_HIP(hipEventRecord(c->ev_pipe_end, c->stream));
+        if (!c->end2) IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
+        IQPT_HIP(hipStreamWaitEvent(c->cstream, c->end1 ? c->end1 : c->ev_pipe_end, 0));
+        IQPT_HIP(hipStreamWaitEvent(c->cstream, c->end2 ? c->end2 : c->ev_s2, 0));
+        // the ring's reuse events stay in one order whatever mixes copies (stream3) and gathers (cstream)
+        if (c->copy_seq > 0) IQPT_HIP(hipStreamWaitEvent(c->cstream, c->pev[c->copy_seq % iqpt::kPipeRing], 0));
+        if ((st = gather_from(c, c->d_bgra, root, static_cast<uint32_t*>(dst_device), 1u)) != IQPT_OK) return st;
+        c->copy_seq += 1;
+        IQPT_HIP(hipEventRecord(c->pev[c->copy_seq % iqpt::kPipeRing], c->cstream));
+        if (c->d_bgra == c->d_pring[c->pidx]) c->pseq[c->pidx] = c->copy_seq;
+        return IQPT_OK;
+    }
     const uint32_t b = c->gpar;
     hipStream_t used = nullptr;
     // the copy into send buffer b waits for the gather that read it two gathers ago (long done)

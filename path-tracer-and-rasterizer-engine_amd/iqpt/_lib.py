@@ -144,7 +144,7 @@ SIGNATURES = [
 _lib = None
 
 
-ABI_VERSION = 4      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
+ABI_VERSION = 5      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
 
 
 def load() -> C.CDLL:
@@ -156,11 +156,18 @@ def load() -> C.CDLL:
         raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
                           "(the HIP extension is required; there is no CPU fallback)")
     lib = C.CDLL(str(LIB_PATH))
+    # an A/B library of an earlier round (bench.py --lib, another path) may lack the newest entry points: those
+    # are left unbound there; the package's own library must export every one
+    own = LIB_PATH.resolve() == (_PKG / "libiqpt.so").resolve()
     for name, res, args in SIGNATURES:
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if own:
+                raise ImportError(f"{LIB_PATH} does not export {name}: rebuild with __graft_entry__.build()")
+            continue
         fn.restype = res
         fn.argtypes = args
-    if lib.iqpt_abi_version() != ABI_VERSION:
+    if own and lib.iqpt_abi_version() != ABI_VERSION:
         raise ImportError(f"{LIB_PATH} has ABI {lib.iqpt_abi_version()}, the bindings expect {ABI_VERSION}: "
                           "rebuild with __graft_entry__.build()")
     _lib = lib

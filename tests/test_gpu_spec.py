@@ -312,3 +312,94 @@ def test_pipelined_async_copies(require_gpu, split, expect):
         assert np.array_equal(b.cpu().numpy().view(np.uint8).reshape(-1, 4), wv)
     lin, bgra = pt.read()
     _check(pt, lin, bgra, fr)
+
+
+def _set_parity(pt, rho256):
+    from iqpt import _lib
+    lb = _lib.load()
+    lb.iqpt_debug_set_spec_parity.argtypes = [C.c_void_p, C.c_uint32]
+    _lib.check(lb.iqpt_debug_set_spec_parity(pt._h, rho256), "iqpt_debug_set_spec_parity")
+
+
+@pytest.mark.parametrize("parity", [0, 1, 480, 2000])
+@pytest.mark.parametrize("launches", [[16, 16, 16], [5, 64]])
+def test_parity_pixels(require_gpu, parity, launches):
+    """Parity pixels (round 5): round 0 traces the even slots, the walk stops at the first odd
+    slot the chain lands on, and the block's lanes share the odd slots from there on (fix-up pass). Threshold
+    0 (off: every slot), 1 (every sphere pixel, edge pixels whose camera rays often miss the sphere included:
+    many fix-ups), 480 (the default, 1.875 slots per sample) and 2000 (none). A C2 crop through both spheres
+    over several launches (history-sized windows), bit for bit."""
+    from iqpt import PathTracer, make_camera
+    ps = pixel_set(1920, 1080, 880, 1000, 470, 1, 48)
+    sc, pk = scene_for("cornell")
+    cam = make_camera(1920, 1080)
+    pt = PathTracer(1920, 1080, pixels=ps, max_depth=8)
+    pt.set_split(SPLIT_SPEC)
+    _set_parity(pt, parity)
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(1920, 1080, pixels=ps, max_depth=8)
+    for s in launches:
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    assert mode_of(pt) == 6
+    _check(pt, lin, bgra, fr)
+
+
+@pytest.mark.parametrize("rho0,plan", [(256, 0), (256, 2), (384, 4), (576, 3)])
+def test_parity_pixels_leaving_windows_and_plans(require_gpu, rho0, plan):
+    """Parity pixels whose chains leave their windows (a short first window: rho0 one slot per sample, the
+    parity threshold at 1) — the fix-up pass, then trace-all rounds from the window's end — under plans none /
+    rebuilt / 64 / 32 lanes, with a frame counter beyond 2^32; row share 3 of 8."""
+    from iqpt import PathTracer, _lib, make_camera
+    w, h = 484, 270
+    n = len(range(3, h, 8))
+    ps = pixel_set(w, h, 0, w, 3, 8, n)
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    pt.set_split(SPLIT_SPEC)
+    _set_parity(pt, 1)
+    lib = _lib.load()
+    lib.iqpt_debug_set_spec.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+    _lib.check(lib.iqpt_debug_set_spec(pt._h, rho0, 0), "iqpt_debug_set_spec")
+    lib.iqpt_debug_spec_plan.argtypes = [C.c_void_p, C.c_int]
+    _lib.check(lib.iqpt_debug_spec_plan(pt._h, plan), "iqpt_debug_spec_plan")
+    lib.iqpt_debug_set_frame.argtypes = [C.c_void_p, C.c_uint64]
+    _lib.check(lib.iqpt_debug_set_frame(pt._h, (1 << 32) + 5), "iqpt_debug_set_frame")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    fr.frame = (1 << 32) + 5
+    for s in (24, 40):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    assert mode_of(pt) == 6
+    _check(pt, lin, bgra, fr)
+
+
+@pytest.mark.parametrize("world", [8, 4])
+def test_parity_on_equals_off_on_the_share(require_gpu, world):
+    """Rank 0's whole C3 share, two 64-spp launches with parity pixels (default) and without: the same bits."""
+    from iqpt import PathTracer, make_camera
+    w, h = 1920, 1080
+    n = len(range(0, h, world))
+    ps = pixel_set(w, h, 0, w, 0, world, n)
+    sc, pk = scene_for("cornell")
+    cam = make_camera(w, h)
+    out = []
+    for parity in (480, 0):
+        pt = PathTracer(w, h, pixels=ps, max_depth=8)
+        pt.set_split(SPLIT_SPEC)
+        _set_parity(pt, parity)
+        pt.set_camera(cam)
+        pt.upload_packet(pk)
+        pt.render(64)
+        pt.render(64)
+        lin, bgra = pt.read()
+        out.append((lin.view(np.uint32).copy(), bgra.copy(), pt.read_rng(), pt.rays()))
+        pt.close()
+    assert np.array_equal(out[0][0], out[1][0]) and np.array_equal(out[0][1], out[1][1])
+    assert np.array_equal(out[0][2], out[1][2]) and out[0][3] == out[1][3]

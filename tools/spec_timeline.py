@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-block timeline of iqpt_spec_kernel on rank 0's row share of C2: for every spec
-block the s_memrealtime stamps (100 MHz) at its start, after round 0's slots, after round 0's walk and at
-its end (iqpt_debug_spec_timeline). Prints percentiles of the block start, the phases and the end, and
+block the s_memrealtime stamps (100 MHz) at its start, after round 0's slot pass, after round 0's walk (with a
+parity pixel's fix-up pass and second walk) and at its end (iqpt_debug_spec_timeline). Prints percentiles of the block start, the phases and the end, and
 the blocks that needed more than one round.
 
     spec_timeline.py [--share 8] [--specfan 1] [--plan 1] [--out f.json]
@@ -29,6 +29,9 @@ ap.add_argument("--specfan", type=int, default=1)
 ap.add_argument("--warm", type=int, default=3)
 ap.add_argument("--plan", type=int, default=1, help="iqpt_debug_spec_plan mode (0 none, 1 asynchronous)")
 ap.add_argument("--cap", type=float, default=0.0, help="iqpt_debug_set_spec_cap (0: the default)")
+ap.add_argument("--parity", type=float, default=None, help="iqpt_debug_set_spec_parity in slots per sample (0: off)")
+ap.add_argument("--prio", type=int, default=None, help="iqpt_debug_set_spec_prio step (0: off)")
+ap.add_argument("--parity-max", type=float, default=None, help="iqpt_debug_set_spec_parity_max in slots per sample")
 ap.add_argument("--out", default="")
 args = ap.parse_args()
 
@@ -48,6 +51,16 @@ _lib.check(lb.iqpt_debug_spec_plan(pt._h, args.plan), "iqpt_debug_spec_plan")
 if args.cap:
     lb.iqpt_debug_set_spec_cap.argtypes = [C.c_void_p, C.c_double]
     _lib.check(lb.iqpt_debug_set_spec_cap(pt._h, args.cap), "iqpt_debug_set_spec_cap")
+if args.parity_max is not None:
+    lb.iqpt_debug_set_spec_parity_max.argtypes = [C.c_void_p, C.c_uint32]
+    _lib.check(lb.iqpt_debug_set_spec_parity_max(pt._h, min(0xffffffff, int(round(args.parity_max * 256)))),
+               "iqpt_debug_set_spec_parity_max")
+if args.prio is not None:
+    lb.iqpt_debug_set_spec_prio.argtypes = [C.c_void_p, C.c_uint32]
+    _lib.check(lb.iqpt_debug_set_spec_prio(pt._h, args.prio), "iqpt_debug_set_spec_prio")
+if args.parity is not None:
+    lb.iqpt_debug_set_spec_parity.argtypes = [C.c_void_p, C.c_uint32]
+    _lib.check(lb.iqpt_debug_set_spec_parity(pt._h, int(round(args.parity * 256))), "iqpt_debug_set_spec_parity")
 pt.set_camera(cam)
 pt.upload_packet(pk)
 for _ in range(args.warm):
@@ -55,33 +68,45 @@ for _ in range(args.warm):
 pt.sync()
 lb.iqpt_debug_spec_timeline.argtypes = [C.c_void_p, C.c_int]
 _lib.check(lb.iqpt_debug_spec_timeline(pt._h, 1), "iqpt_debug_spec_timeline")
+info = (C.c_ulonglong * 8)()
+lb.iqpt_debug_spec_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+_lib.check(lb.iqpt_debug_spec_info(pt._h, info), "iqpt_debug_spec_info")      # clears the statistics
 pt.render(cfg.spp)
 pt.sync()
+_lib.check(lb.iqpt_debug_spec_info(pt._h, info), "iqpt_debug_spec_info")
+spec_stats = {"sphere_pixels": int(info[0]), "windows_sum": int(info[5]), "past_window_chains": int(info[7] & 0xffffffff),
+              "fixup_chains": int(info[7] >> 32)}
 cap = 1 << 16
 buf = (C.c_ulonglong * (8 * cap))()
 n = C.c_uint32(0)
 lb.iqpt_debug_read_spec_timeline.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32, C.POINTER(C.c_uint32)]
 _lib.check(lb.iqpt_debug_read_spec_timeline(pt._h, buf, cap, C.byref(n)), "iqpt_debug_read_spec_timeline")
 raw8 = np.array(buf[:8 * n.value], dtype=np.uint64).reshape(-1, 8)
-raw = raw8[:, :4]
-wave_iters = raw8[:, 4:].astype(np.int64)
-rounds = (raw[:, 3] >> np.uint64(48)).astype(np.int64)
+raw = raw8[:, :3]
+# per wave (round 5: the waves of a block run their rounds on their own): end | slot-loop iterations << 48
+wave_iters = (raw8[:, 4:] >> np.uint64(48)).astype(np.int64)
+wave_end = (raw8[:, 4:] & np.uint64(0xffffffffffff)).astype(np.float64)
+rounds = (raw8[:, 3] >> np.uint64(48)).astype(np.int64)
 iters = wave_iters.max(axis=1)                            # the block's slowest wave's slot-loop iterations
 t = (raw & np.uint64(0xffffffffffff)).astype(np.float64)
 t0 = t[:, 0].min()
 us = (t - t0) / 100.0                     # 100 MHz ticks -> us
-start, slots_end, walk_end, end = us[:, 0], us[:, 1], us[:, 2], us[:, 3]
+wave_us = (wave_end - t0) / 100.0
+# wave 0's start, its round-0 slot pass end and round-0 end; the block's end (its latest wave)
+start, slots_end, walk_end, end = us[:, 0], us[:, 1], us[:, 2], wave_us.max(axis=1)
 
 
 def pct(a):
     return {str(q): round(float(np.percentile(a, q)), 1) for q in (0, 10, 50, 90, 99, 100)}
 
 
-res = {"share": args.share, "specfan": args.specfan, "plan": args.plan, "cap": args.cap or None, "blocks": int(n.value),
+res = {"share": args.share, "specfan": args.specfan, "plan": args.plan, "cap": args.cap or None, "parity": args.parity, "parity_max": args.parity_max, "prio": args.prio,
+       "blocks": int(n.value), "spec_stats": spec_stats,
        "kernel_us": round(float(end.max()), 1),
        "start_us": pct(start), "slots_us": pct(slots_end - start), "walk_us": pct(walk_end - slots_end),
        "later_rounds_us": pct(end - walk_end), "end_us": pct(end),
        "iters_max_wave": pct(iters), "iters_spread_in_block": pct(wave_iters.max(axis=1) - wave_iters.min(axis=1)),
+       "wave_end_us": pct(wave_us.reshape(-1)), "wave_end_spread_in_block_us": pct(wave_us.max(axis=1) - wave_us.min(axis=1)),
        "rounds_hist": {str(int(k)): int(v) for k, v in zip(*np.unique(rounds, return_counts=True))},
        "slowest": [[int(i), round(float(start[i]), 1), round(float(slots_end[i] - start[i]), 1),
                     round(float(walk_end[i] - slots_end[i]), 1), round(float(end[i] - walk_end[i]), 1),
@@ -106,11 +131,18 @@ if npx.value and nb.value == n.value:
     rows = []
     for b in range(nb.value):
         first, word = blk[2 * b], blk[2 * b + 1]
-        cnt, lanes = word & 0xff, 8 << (word >> 8)
+        cnt, lanes = word & 0xff, word >> 8                  # count | lanes per pixel << 8
         qs = [order[first + i] for i in range(cnt)]
         rows.append([lanes, cnt, float(w[qs].max()), float(m[qs].max()), float(slots_end[b] - start[b]), float(iters[b])])
     a = np.array(rows)
     res["per_block"] = {"lanes_hist": {str(int(k)): int(v) for k, v in zip(*np.unique(a[:, 0], return_counts=True))}}
+    # every block: lanes, pixels, max work, max window, slot pass (us), walk + fix-up (us), end (us), rounds, the
+    # slowest wave's iterations, its waves' ends (us): for offline analysis of what sets the kernel's tail
+    res["blocks"] = [[int(a[b, 0]), int(a[b, 1]), round(float(a[b, 2]), 1), round(float(a[b, 3]), 1),
+                      round(float(slots_end[b] - start[b]), 1), round(float(walk_end[b] - slots_end[b]), 1),
+                      round(float(end[b]), 1), int(rounds[b]), int(iters[b]),
+                      [round(float(x), 1) for x in wave_us[b]], [int(x) for x in wave_iters[b]]]
+                     for b in range(nb.value)]
     # slot phase ~ alpha * max w / lanes + beta * max window + gamma (least squares)
     X = np.stack([a[:, 2] / a[:, 0], a[:, 3], np.ones(len(a))], axis=1)
     coef, *_ = np.linalg.lstsq(X, a[:, 4], rcond=None)

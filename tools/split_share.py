@@ -99,7 +99,8 @@ def run(n: int, mode: int, launches: int, warm: int, spp: int, knobs=None, chain
                      "split_pixels": info[6], "mean_window": info[4] / max(info[6], 1),
                      "mean_slots_per_sample": info[5] / 256 / max(info[6], 1), "ran_split": info[7],
                      "sphere_pixels": spec[0], "fan_tiles": spec[1], "spec_runs": spec[4], "spec_window_slots": spec[5],
-                     "spec_slots_per_sample": spec[6] / 256 / max(spec[0], 1), "spec_leftovers": spec[7]}}
+                     "spec_slots_per_sample": spec[6] / 256 / max(spec[0], 1), "spec_leftovers": spec[7] & 0xffffffff,
+                     "spec_fixup_chains": spec[7] >> 32}}
 
 
 def wave_timeline(n: int, spp: int, warm: int, knobs=None) -> dict:
