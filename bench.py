@@ -107,6 +107,10 @@ def parse():
                     help="A/B: any-hit queries for triangle-only scenes (iqpt_debug_set_anyhit; default: the library's, on)")
     ap.add_argument("--spec-parity-max", type=float, default=None,
                     help="A/B: spec parity pixels' upper bound in slots per sample (iqpt_debug_set_spec_parity_max)")
+    ap.add_argument("--spec-queue", type=int, default=None,
+                    help="A/B: spec launches in queue mode (1) or the block kernel (0) (iqpt_debug_set_spec_queue)")
+    ap.add_argument("--spec-qbpc", type=int, default=0,
+                    help="A/B: queue mode's persistent blocks per CU (0: the default)")
     ap.add_argument("--spec-prio", type=int, default=None,
                     help="A/B: spec kernel progress-fair priority step in iterations (iqpt_debug_set_spec_prio; 0 off)")
     ap.add_argument("--spec-parity", type=float, default=None,
@@ -514,6 +518,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_anyhit.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_anyhit(pt._h, args.anyhit), "iqpt_debug_set_anyhit")
+    if args.spec_queue is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec_queue.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_spec_queue(pt._h, args.spec_queue, args.spec_qbpc), "iqpt_debug_set_spec_queue")
     if args.spec_parity_max is not None:
         import ctypes as C
         lb = _lib.load()
@@ -768,7 +777,9 @@ def main():
                        **({"spec_parity": args.spec_parity} if args.spec_parity is not None else {}),
                        **({"anyhit": args.anyhit} if args.anyhit is not None else {}),
                        **({"spec_prio": args.spec_prio} if args.spec_prio is not None else {}),
-                       **({"spec_parity_max": args.spec_parity_max} if args.spec_parity_max is not None else {})},
+                       **({"spec_parity_max": args.spec_parity_max} if args.spec_parity_max is not None else {}),
+                       **({"spec_queue": args.spec_queue, "spec_qbpc": args.spec_qbpc}
+                          if args.spec_queue is not None else {})},
             "n_ranks_seen": n_ranks_seen,
             "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
             **({"gather": "stream-ordered" if stream_gather else "blocking", "gather_check": gather_check}

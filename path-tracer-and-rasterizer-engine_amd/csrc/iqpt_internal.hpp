@@ -215,8 +215,31 @@ struct kspec {
     uint32_t nblocks;                // plan blocks (the spec part of the grid)
     unsigned long long* tl;          // measurement (iqpt_debug_spec_timeline), else null: per spec block
                                      // s_memrealtime at start, after round 0's slots and walk, at the end
-                                     // (| rounds << 48)
+                                     // (| rounds << 48); queue mode: per wave start, end | iterations << 48,
+                                     // pixels | walks << 16 | fix-ups << 32
+    // queue mode (iqpt_specq_kernel): persistent waves take sphere pixels from per-XCD
+    // cursors over the plan's order (heaviest first) and trace a pool of their slots together; the walk of a pixel
+    // runs as soon as its slots are done. iqpt_spec_prep_kernel writes each pixel's window (m) and the state at
+    // every kSpecCk-th slot of it first.
+    uint32_t queue;                  // 1: queue mode
+    uint32_t* ck;                    // ck[(o ncp + c) 8 + w], w < 5: the state at slot c ck_step of the pixel at
+                                     // queue position o (order[o])
+    uint32_t ncp;                    // checkpoint records per pixel (<= kSpecQCkMax)
+    uint32_t ck_step;                // slots between two checkpoints (a multiple of kSpecCk)
+    uint32_t* cursor;                // kSpecCursors per-XCD cursors, 16 words apart (zeroed by the prep kernel)
+    uint32_t* qrec;                  // per queue position: the pixel's initial record (kSpecQRecWordsHost words)
 };
+constexpr uint32_t kSpecCk = 4;             // queue mode: slots between two checkpoints (at least; spec_ck_step)
+constexpr uint32_t kSpecQCkMax = 52;        // queue mode: checkpoints per pixel (a wave keeps them in LDS)
+constexpr uint32_t kSpecQRecWordsHost = 24; // queue mode: words per pixel record (kernels: kSpecQRecWords)
+// queue mode: the checkpoint spacing for a window cap (the smallest multiple of kSpecCk giving <= kSpecQCkMax)
+inline uint32_t spec_ck_step(uint32_t m_cap) {
+    uint32_t s = kSpecCk;
+    while (m_cap / s + 1u > kSpecQCkMax) s += kSpecCk;
+    return s;
+}
+constexpr uint32_t kSpecCursors = 8;        // queue mode: one pixel cursor per XCD
+constexpr uint32_t kSpecQBlocksPerCu = 2;   // queue mode: persistent blocks per CU (iqpt_debug_set_spec_queue)
 constexpr int kSendRing = 4;                // the multi-GPU gather's send buffers, used in turn
 constexpr int kPipeRing = 6;                // frame buffers pipelined launches write in turn once copies follow them
 constexpr int kGatherCtas = 2;              // RCCL blocks per frame gather (iqpt_debug_set_gather)
@@ -411,6 +434,11 @@ int launch_chain(void* stream, const kparams& p, uint32_t grid_blocks, int opt, 
 bool spec_variant_exists(int max_depth, int opt);
 uint32_t spec_lds(const kparams& p, const kspec& s);
 int launch_spec(void* stream, const kparams& p, const kspec& s, int opt);
+// queue mode: the prep kernel (windows, checkpoints, cursors) then the persistent kernel over `blocks` blocks
+int launch_spec_prep(void* stream, const kparams& p, const kspec& s);
+int launch_specq(void* stream, const kparams& p, const kspec& s, int opt, uint32_t blocks);
+uint32_t specq_lds(const kparams& p, const kspec& s);
+int specq_occupancy(const kparams& p, const kspec& s, int opt, int* blocks);
 // resident iqpt_spec_kernel blocks per CU for this launch
 int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks);
 // Certain-miss pixels (iqpt_sky_kernel): the p.miss pixels of `ntiles` tiles (tiles[i]),
@@ -427,6 +455,8 @@ int launch_fan(void* stream, const kparams& p, uint32_t ntiles, int opt);
 // kernel this thread launches (hipExtLaunchKernel) rather than by marker packets of their own; a launch
 // function that launches nothing leaves them bound — the caller unbinds (nullptr, nullptr).
 void bind_launch_events(void* start, void* stop);
+// the events bound to the next launch (and unbind them): a launch of several kernels binds them to its first and last
+void take_launch_events(void** start, void** stop);
 constexpr int kRenderBlock = 256;
 constexpr uint32_t kQueueChunk = 64;
 const char* render_kernel_name();

@@ -215,6 +215,15 @@ struct iqpt_ctx {
     // spec launches (iqpt_debug_set_specfan): 0 the two kernels on two streams, pipelined (the default), 1 one
     // after the other on one stream (measurement)
     int specfan_mode = 0;
+    // queue mode (iqpt_specq_kernel; iqpt_debug_set_spec_queue): persistent waves over
+    // per-XCD pixel cursors, spec_qbpc blocks per CU, behind iqpt_spec_prep_kernel (windows, checkpoints)
+    int spec_queue = 0;
+    uint32_t spec_qbpc = iqpt::kSpecQBlocksPerCu;
+    uint32_t* d_spec_ck = nullptr;       // checkpoints: spec_ck_cap words
+    size_t spec_ck_cap = 0;
+    uint32_t* d_spec_cursor = nullptr;   // kSpecCursors x 16 words
+    uint32_t spec_q_grid = 0;            // the last queue launch's blocks (timeline)
+    bool spec_q_last = false;            // the last spec launch ran in queue mode
     bool fan_pipe = true;                // FAN launches pipelined (iqpt_debug_set_pipe)
     // spec plan: the sphere pixels ordered by their last chain's work, heaviest first, the
     // heavy ones with 32 or 64 lanes; built on the host from an asynchronous read of the history (performance
@@ -1141,6 +1150,7 @@ int check_dev_err(iqpt_ctx* c) {
     return iqpt::fail(IQPT_ERR_HIP, std::string((c->dev_err & 2u)   ? "chain launch: a wave exceeded its iteration bound"
                                                 : (c->dev_err & 4u) ? "overlapped launch: an XCD's tiles were never taken"
                                                 : (c->dev_err & 8u) ? "spec launch: a chain slot was never traced"
+                                                : (c->dev_err & 16u) ? "spec queue launch: a wave found no work to hand out"
                                                                     : "overlapped launch: a per-tile wait timed out") +
                                         " (pixel state undefined until iqpt_checkpoint_load)");
 }
@@ -1355,7 +1365,8 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->stream3) (void)hipStreamDestroy(c->stream3);
     if (c->ev_pipe_end) (void)hipEventDestroy(c->ev_pipe_end);
     free_split(c);
-    for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_tl, (void*)c->d_spec_plan})
+    for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_tl, (void*)c->d_spec_plan,
+                    (void*)c->d_spec_ck, (void*)c->d_spec_cursor})
         if (b) (void)hipFree(b);
     for (void* b : {(void*)c->h_spec_rho, (void*)c->h_spec_plan})
         if (b) (void)hipHostFree(b);
@@ -1796,6 +1807,19 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
                iqpt::spec_occupancy(p, probe, opt, &occ_s) == 0 && occ_s >= 1;
         (void)hipGetLastError();
     }
+    // queue mode: its own LDS (records, checkpoints, slot counts of 6 pixels per wave) must fit too
+    bool spec_q = false;
+    if (spec && c->spec_queue) {
+        iqpt::kspec probe;
+        std::memset(&probe, 0, sizeof probe);
+        probe.m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
+        probe.ck_step = iqpt::spec_ck_step(probe.m_cap);
+        probe.ncp = probe.m_cap / probe.ck_step + 1u;
+        int occ_q = 0;
+        spec_q = iqpt::specq_lds(p, probe) <= c->lds_per_block && iqpt::specq_occupancy(p, probe, opt, &occ_q) == 0 &&
+                 occ_q >= 1;
+        (void)hipGetLastError();
+    }
     bool fan_beside_chain = chain && fan_ok && c->fan_anchored;
     if (spec) chain = fan_beside_chain = false;
     uint32_t lds_split = lds + iqpt::kRenderBlock * (16u + 24u);   // + lds_sp and the base states
@@ -2035,6 +2059,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     };
     // ---- the spec kernel's buffers, parameters, plan and history (pipelined spec launches on `stream`):
     // every enqueue of these on the spec kernel's stream `ss`
+    // queue mode's grid: spec_qbpc blocks per CU, no more waves than sphere pixels
+    auto spec_q_blocks = [&](const iqpt::kspec& k2) -> uint32_t {
+        const uint64_t want = ((uint64_t)k2.n + 3u) / 4u;
+        return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * std::max(1u, c->spec_qbpc)));
+    };
     auto spec_buffers = [&](hipStream_t ss, iqpt::kspec& ks2) -> int {
         std::memset(&ks2, 0, sizeof ks2);
         const uint32_t n = c->n_chain_pix;
@@ -2098,6 +2127,28 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.rho = c->d_spec + n;
         ks2.run_count = c->d_spec + 2 * (size_t)n;
         ks2.res = c->d_spec_res;
+        if (spec_q && n > 0) {
+            ks2.queue = 1u;
+            ks2.ck_step = iqpt::spec_ck_step(m_cap);
+            ks2.ncp = m_cap / ks2.ck_step + 1u;
+            const size_t words = (size_t)n * (ks2.ncp * 8u + iqpt::kSpecQRecWordsHost);
+            if (words > c->spec_ck_cap || !c->d_spec_cursor) {
+                IQPT_HIP(hipStreamSynchronize(c->stream));
+                if (c->d_spec_ck) (void)hipFree(c->d_spec_ck);
+                c->d_spec_ck = nullptr;
+                c->spec_ck_cap = 0;
+                if (hipMalloc(&c->d_spec_ck, words * sizeof(uint32_t)) != hipSuccess ||
+                    (!c->d_spec_cursor &&
+                     hipMalloc(&c->d_spec_cursor, iqpt::kSpecCursors * 16u * sizeof(uint32_t)) != hipSuccess)) {
+                    (void)hipGetLastError();
+                    return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec queue checkpoints");
+                }
+                c->spec_ck_cap = words;
+            }
+            ks2.ck = c->d_spec_ck;
+            ks2.qrec = c->d_spec_ck + (size_t)n * ks2.ncp * 8u;
+            ks2.cursor = c->d_spec_cursor;
+        }
         // a new pixel list: no history, and the statistics counters behind it (d_spec + 2 n) restart too
         // (after a list that shrank n they pointed into the old history)
         if (n > 0 && !c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, ((size_t)n + 2) * sizeof(uint32_t), ss));
@@ -2135,7 +2186,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             ks2.nblocks = c->spec_plan_blocks;
         }
         if (c->spec_tl_on && n > 0) {
-            const size_t nb = ks2.blocks ? ks2.nblocks : (n + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
+            // (queue mode: 4 words per wave, 16 per block = two timeline records)
+            const size_t nb = ks2.queue ? 2 * (size_t)spec_q_blocks(ks2)
+                                        : ks2.blocks ? ks2.nblocks : (n + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
             if (nb > c->spec_tl_blocks) {
                 IQPT_HIP(hipStreamSynchronize(ss));
                 if (c->d_spec_tl) (void)hipFree(c->d_spec_tl);
@@ -2320,13 +2373,27 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
         if ((st = spec_plan(c->stream, ks2)) != IQPT_OK) return st;
         const uint32_t n = ks2.n;
+        c->spec_q_last = ks2.queue != 0u;
+        // queue mode: the prep kernel (windows, checkpoints, cursors) then the persistent grid
+        auto run_spec = [&]() -> int {
+            if (!ks2.queue) return iqpt::launch_spec(c->stream, p, ks2, opt);
+            void* s0 = nullptr;
+            void* s1 = nullptr;
+            iqpt::take_launch_events(&s0, &s1);
+            iqpt::bind_launch_events(s0, nullptr);
+            int e = iqpt::launch_spec_prep(c->stream, p, ks2);
+            iqpt::bind_launch_events(nullptr, s1);
+            c->spec_q_grid = spec_q_blocks(ks2);
+            if (e == 0) e = iqpt::launch_specq(c->stream, p, ks2, opt, c->spec_q_grid);
+            return e;
+        };
         if (c->specfan_mode == 1) {
-            if (n > 0) le = iqpt::launch_spec(c->stream, p, ks2, opt);
+            if (n > 0) le = run_spec();
             if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream, pf, c->n_fan_tiles, opt);
         } else {
             if (n > 0) {
                 iqpt::bind_launch_events(e0, e1);
-                le = iqpt::launch_spec(c->stream, p, ks2, opt);
+                le = run_spec();
                 iqpt::bind_launch_events(nullptr, nullptr);
                 e1_bound = le == 0 && e1 != nullptr;
                 if (le != 0 && e0) (void)hipEventRecord(e0, c->stream);   // (unrecorded events are not read)
@@ -2650,6 +2717,8 @@ int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
     out8[1] = c->n_fan_tiles;
     out8[2] = c->n_anchor;
     out8[3] = c->n_split_tiles;
+    // the last spec launch in queue mode: its grid's blocks in the high half of word 2
+    if (c->spec_last && c->spec_q_last) out8[2] |= (unsigned long long)c->spec_q_grid << 32;
     if (c->spec_last && c->d_spec && c->spec_n >= c->n_chain_pix) {
         const uint32_t n = c->n_chain_pix;
         std::vector<uint32_t> v(2 * (size_t)n + 2);
@@ -2684,7 +2753,8 @@ int iqpt_debug_read_spec_timeline(iqpt_ctx* c, unsigned long long* out, uint32_t
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     if (!c->d_spec_tl || !c->spec_last) return IQPT_OK;
-    const size_t nspec = c->spec_plan_n == c->n_chain_pix && c->spec_plan_n && c->spec_plan_mode
+    const size_t nspec = c->spec_q_last ? 2 * (size_t)c->spec_q_grid
+                         : c->spec_plan_n == c->n_chain_pix && c->spec_plan_n && c->spec_plan_mode
                              ? c->spec_plan_blocks
                              : (c->n_chain_pix + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
     const size_t nb = std::min<size_t>(nspec, std::min<size_t>(cap_blocks, c->spec_tl_blocks));
@@ -2840,6 +2910,21 @@ int iqpt_debug_set_spec_parity(iqpt_ctx* c, uint32_t rho256) {
     int st = enter(c);
     if (st) return st;
     c->spec_parity_rho = rho256;
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): queue mode for spec launches (iqpt_specq_kernel: persistent waves taking sphere pixels
+ * from per-XCD cursors) — mode 0 the block kernel, 1 queue mode; blocks_per_cu the
+ * persistent grid (0: the default). The timeline (iqpt_debug_read_spec_timeline) then holds 4 words per wave:
+ * start, end | iterations << 48, pixels | walks << 16 | fix-ups << 32 | XCD << 48. */
+int iqpt_debug_set_spec_queue(iqpt_ctx* c, int mode, uint32_t blocks_per_cu) {
+    if (!c || mode < 0 || mode > 1 || blocks_per_cu > 16)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL, mode not 0..1 or blocks_per_cu > 16");
+    int st = enter(c);
+    if (st) return st;
+    if ((st = join_streams(c)) != IQPT_OK) return st;
+    c->spec_queue = mode;
+    c->spec_qbpc = blocks_per_cu ? blocks_per_cu : iqpt::kSpecQBlocksPerCu;
     return IQPT_OK;
 }
 

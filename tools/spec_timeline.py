@@ -32,6 +32,8 @@ ap.add_argument("--cap", type=float, default=0.0, help="iqpt_debug_set_spec_cap 
 ap.add_argument("--parity", type=float, default=None, help="iqpt_debug_set_spec_parity in slots per sample (0: off)")
 ap.add_argument("--prio", type=int, default=None, help="iqpt_debug_set_spec_prio step (0: off)")
 ap.add_argument("--parity-max", type=float, default=None, help="iqpt_debug_set_spec_parity_max in slots per sample")
+ap.add_argument("--queue", type=int, default=None, help="iqpt_debug_set_spec_queue mode (1: queue mode)")
+ap.add_argument("--qbpc", type=int, default=0, help="queue mode's blocks per CU (0: the default)")
 ap.add_argument("--out", default="")
 args = ap.parse_args()
 
@@ -51,6 +53,9 @@ _lib.check(lb.iqpt_debug_spec_plan(pt._h, args.plan), "iqpt_debug_spec_plan")
 if args.cap:
     lb.iqpt_debug_set_spec_cap.argtypes = [C.c_void_p, C.c_double]
     _lib.check(lb.iqpt_debug_set_spec_cap(pt._h, args.cap), "iqpt_debug_set_spec_cap")
+if args.queue is not None:
+    lb.iqpt_debug_set_spec_queue.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+    _lib.check(lb.iqpt_debug_set_spec_queue(pt._h, args.queue, args.qbpc), "iqpt_debug_set_spec_queue")
 if args.parity_max is not None:
     lb.iqpt_debug_set_spec_parity_max.argtypes = [C.c_void_p, C.c_uint32]
     _lib.check(lb.iqpt_debug_set_spec_parity_max(pt._h, min(0xffffffff, int(round(args.parity_max * 256)))),
@@ -82,6 +87,40 @@ n = C.c_uint32(0)
 lb.iqpt_debug_read_spec_timeline.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32, C.POINTER(C.c_uint32)]
 _lib.check(lb.iqpt_debug_read_spec_timeline(pt._h, buf, cap, C.byref(n)), "iqpt_debug_read_spec_timeline")
 raw8 = np.array(buf[:8 * n.value], dtype=np.uint64).reshape(-1, 8)
+
+
+def pct(a):
+    return {str(q): round(float(np.percentile(a, q)), 1) for q in (0, 10, 50, 90, 99, 100)}
+
+
+if (int(info[2]) >> 32) > 0:
+    # queue mode: per wave start, end | iterations << 48, pixels | walks << 16 | fix-ups << 32 | XCD << 48, time in
+    # admissions | walks << 16 | hand-outs << 32 | rays << 48 (10-ns ticks)
+    w4 = raw8.reshape(-1, 4)
+    ws = (w4[:, 0] & np.uint64(0xffffffffffff)).astype(np.float64)
+    we = (w4[:, 1] & np.uint64(0xffffffffffff)).astype(np.float64)
+    it = (w4[:, 1] >> np.uint64(48)).astype(np.int64)
+    npx_w = (w4[:, 2] & np.uint64(0xffff)).astype(np.int64)
+    nwk = ((w4[:, 2] >> np.uint64(16)) & np.uint64(0xffff)).astype(np.int64)
+    nfx = ((w4[:, 2] >> np.uint64(32)) & np.uint64(0xffff)).astype(np.int64)
+    xcd = ((w4[:, 2] >> np.uint64(48)) & np.uint64(0xff)).astype(np.int64)
+    t0 = ws.min()
+    end_w = (we - t0) / 100.0
+    res = {"share": args.share, "queue": 1, "qbpc": args.qbpc or None, "specfan": args.specfan, "plan": args.plan,
+           "parity": args.parity, "parity_max": args.parity_max, "waves": int(len(w4)), "grid_blocks": int(info[2]) >> 32,
+           "spec_stats": spec_stats, "kernel_us": round(float(end_w.max()), 1),
+           "start_us": pct((ws - t0) / 100.0), "end_us": pct(end_w),
+           "end_max_over_median": round(float(end_w.max() / max(np.median(end_w), 1e-9)), 3),
+           "iters": pct(it), "pixels_per_wave": pct(npx_w), "walks_per_wave": pct(nwk), "fixups_per_wave": pct(nfx),
+           "xcd_end_us": {str(x): round(float(end_w[xcd == x].max()), 1) for x in np.unique(xcd)},
+           "us_per_iter": pct(end_w / np.maximum(it, 1))}
+    ph = w4[:, 3]
+    for i, name in enumerate(("admit", "walk", "handout", "trace")):
+        res[f"{name}_us"] = pct(((ph >> np.uint64(16 * i)) & np.uint64(0xffff)).astype(np.float64) / 100.0)
+    print(json.dumps(res), flush=True)
+    if args.out:
+        Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
+    sys.exit(0)
 raw = raw8[:, :3]
 # per wave (round 5: the waves of a block run their rounds on their own): end | slot-loop iterations << 48
 wave_iters = (raw8[:, 4:] >> np.uint64(48)).astype(np.int64)
@@ -94,10 +133,6 @@ us = (t - t0) / 100.0                     # 100 MHz ticks -> us
 wave_us = (wave_end - t0) / 100.0
 # wave 0's start, its round-0 slot pass end and round-0 end; the block's end (its latest wave)
 start, slots_end, walk_end, end = us[:, 0], us[:, 1], us[:, 2], wave_us.max(axis=1)
-
-
-def pct(a):
-    return {str(q): round(float(np.percentile(a, q)), 1) for q in (0, 10, 50, 90, 99, 100)}
 
 
 res = {"share": args.share, "specfan": args.specfan, "plan": args.plan, "cap": args.cap or None, "parity": args.parity, "parity_max": args.parity_max, "prio": args.prio,
