@@ -215,8 +215,7 @@ struct kspec {
     uint32_t nblocks;                // plan blocks (the spec part of the grid)
     unsigned long long* tl;          // measurement (iqpt_debug_spec_timeline), else null: per spec block
                                      // s_memrealtime at start, after round 0's slots and walk, at the end
-                                     // (| rounds << 48); queue mode: per wave start, end | iterations << 48,
-                                     // pixels | walks << 16 | fix-ups << 32
+                                     // (| rounds << 48); queue mode: 8 words per wave (iqpt_debug_set_spec_queue)
     // queue mode (iqpt_specq_kernel): persistent waves take sphere pixels from per-XCD
     // cursors over the plan's order (heaviest first) and trace a pool of their slots together; the walk of a pixel
     // runs as soon as its slots are done. iqpt_spec_prep_kernel writes each pixel's window (m) and the state at
@@ -229,8 +228,8 @@ struct kspec {
     uint32_t* cursor;                // kSpecCursors per-XCD cursors, 16 words apart (zeroed by the prep kernel)
     uint32_t* qrec;                  // per queue position: the pixel's initial record (kSpecQRecWordsHost words)
 };
-constexpr uint32_t kSpecCk = 4;             // queue mode: slots between two checkpoints (at least; spec_ck_step)
-constexpr uint32_t kSpecQCkMax = 52;        // queue mode: checkpoints per pixel (a wave keeps them in LDS)
+constexpr uint32_t kSpecCk = 8;             // queue mode: slots between two checkpoints (at least; spec_ck_step)
+constexpr uint32_t kSpecQCkMax = 28;        // queue mode: checkpoints per pixel (a wave keeps them in LDS)
 constexpr uint32_t kSpecQRecWordsHost = 24; // queue mode: words per pixel record (kernels: kSpecQRecWords)
 // queue mode: the checkpoint spacing for a window cap (the smallest multiple of kSpecCk giving <= kSpecQCkMax)
 inline uint32_t spec_ck_step(uint32_t m_cap) {

@@ -3827,8 +3827,15 @@ enum : uint32_t {
     kQcm /* 16..19: mask words 0 of triangles and spheres, tile, - */, kQpx = 20, kQpy = 21
 };
 
+// the walk's jump tables: 6 levels of (window + 32) 16-bit entries, windows up to 224 slots (longer ones walk
+// their chain one sample at a time)
+__host__ __device__ inline uint32_t specq_jump_entries(uint32_t m_cap) { return (m_cap < 224u ? m_cap : 224u) + 32u; }
+__host__ __device__ inline uint32_t specq_scratch_bytes(uint32_t m_cap) {
+    const uint32_t t = (6u * specq_jump_entries(m_cap) * 2u + 15u) & ~15u;
+    return t > 64u * 16u ? t : 64u * 16u;
+}
 __host__ __device__ inline uint32_t specq_wave_bytes(uint32_t m_cap, uint32_t ncp) {
-    const uint32_t b = 64u * 16u + kSpecQRecs * kSpecQRecWords * 4u + 16u + kSpecQRecs * ncp * 20u + 64u * 2u +
+    const uint32_t b = specq_scratch_bytes(m_cap) + kSpecQRecs * kSpecQRecWords * 4u + 16u + kSpecQRecs * ncp * 20u +
                        kSpecQRecs * m_cap;
     return (b + 15u) & ~15u;
 }
@@ -3885,12 +3892,13 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
     float* lds_stk = tab_n + sp4;                                                       // [depth][thread]
     uint8_t* wb = reinterpret_cast<uint8_t*>(lds_stk + (size_t)spec_stack_depth(p.max_depth) * kSpecBlock) +
                   (size_t)(threadIdx.x >> 6) * specq_wave_bytes(s.m_cap, s.ncp);
-    float4* lc = reinterpret_cast<float4*>(wb);                                         // walk: [batch] terms
-    uint32_t* R = reinterpret_cast<uint32_t*>(lc + 64);                                 // [record][kSpecQRecWords]
+    // walk scratch: the jump tables, then (after the chain is known) the batch's mean terms
+    float4* lc = reinterpret_cast<float4*>(wb);
+    uint16_t* JT = reinterpret_cast<uint16_t*>(wb);
+    const uint32_t tb = specq_jump_entries(s.m_cap);
+    uint32_t* R = reinterpret_cast<uint32_t*>(wb + specq_scratch_bytes(s.m_cap));       // [record][kSpecQRecWords]
     uint32_t* CK = R + kSpecQRecs * kSpecQRecWords + 4u;                               // [record][ncp][5] states
-    uint16_t* lp = reinterpret_cast<uint16_t*>(CK + (size_t)kSpecQRecs * s.ncp * 5u);  // walk: [batch] slots
-    uint8_t* LN = reinterpret_cast<uint8_t*>(lp + 64);                                  // [record][slot] counts
-    (void)lp;
+    uint8_t* LN = reinterpret_cast<uint8_t*>(CK + (size_t)kSpecQRecs * s.ncp * 5u);    // [record][slot] counts
     for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kSpecBlock)
         lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
     for (uint32_t i = threadIdx.x; i < p.nsph_pairs * kSphPairFloat4; i += kSpecBlock)
@@ -3906,11 +3914,13 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
     const uint32_t xcd = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // HW_REG_XCC_ID
     const uint64_t t_start = s.tl ? __builtin_amdgcn_s_memrealtime() : 0ull;
     uint32_t n_iter = 0, n_pix = 0, n_walk = 0, n_fix = 0;   // measurement
-    uint64_t t_phase[4] = {0ull, 0ull, 0ull, 0ull};          // measurement: admissions, walks, hand-outs, traces
-    uint64_t t_mark = t_start;
+    uint32_t t_phase[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};   // measurement (10-ns ticks): admissions, walks,
+                                                                         // hand-outs, rays; the walks' wait, chain,
+                                                                         // gather + terms, fold
+    uint32_t t_mark = (uint32_t)t_start;
     auto phase = [&](int i) {
         if (s.tl) {
-            const uint64_t t = __builtin_amdgcn_s_memrealtime();
+            const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
             t_phase[i] += t - t_mark;
             t_mark = t;
         }
@@ -3923,9 +3933,7 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
     uint32_t pf_pos = lane == 0u ? atomicAdd(s.cursor + 16u * xcd, 1u) : 0u;
     // lane: the slots [jc, je) step sp of record h it traces (jc the current one), the sample's state
     bool active = false;
-    uint32_t h = 0, jc = 0, je = 0, sp = 1, cM = 0, cpx = 0, cpy = 0;
-    float4* cres = nullptr;
-    uint8_t* cln = LN;
+    uint32_t h = 0, jc = 0, je = 0, sp = 1, cq = 0;   // (cq: the record's sphere pixel; the rest is read from LDS)
     rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
     rng6 base = st;
     ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
@@ -3933,7 +3941,8 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
     uint32_t lane_rays = 0;                 // rays of the chain samples this lane gathered
     uint32_t stalls = 0;                    // iterations without a traced ray (never more than one in a row)
     auto start_slot = [&]() {
-        camera_ray<OPT>(p, cpx, cpy, st, ray);
+        const uint32_t* rh = R + h * kSpecQRecWords;
+        camera_ray<OPT>(p, rh[kQpx], rh[kQpy], st, ray);
         base = st;
         depth = 0;
     };
@@ -4003,8 +4012,17 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
             const uint32_t r = (uint32_t)__builtin_ctz(m);
             if (__any(active && h == r)) continue;
             // the colours are this wave's own stores (complete: vmcnt 0), read back from L2
+            uint32_t tw = s.tl ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
+            auto sub = [&](int i) {
+                if (s.tl) {
+                    const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
+                    t_phase[4 + i] += t - tw;
+                    tw = t;
+                }
+            };
             __builtin_amdgcn_s_waitcnt(0);
             wave_sync();
+            sub(0);
             ++n_walk;
             uint32_t* rr = R + r * kSpecQRecWords;
             const uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane((int)rr[kQq]);
@@ -4019,9 +4037,39 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
             // the slot counts of 256 slots at a time in registers (lane i: slots 4i .. 4i + 3 of the chunk): the chain
             // is followed with uniform lane reads instead of one dependent LDS load per sample
             uint32_t chunk = ~0u, word = 0u;
+            // jump tables (windows up to 224 slots): level t maps a slot to the chain's slot 2^t samples on
+            // (positions where the chain stops — an untraced slot, past the window — map to themselves), so lane i
+            // finds the batch's sample i in at most 6 lookups instead of the walker's 64 dependent steps
+            const bool jump = M + 32u <= tb;
             while (true) {
                 uint32_t c = 0, mypos = 0;
-                while (c < 64u && k + c < p.spp && jw < M) {
+                if (jump) {
+                    const uint32_t ne = M + 32u;
+                    for (uint32_t e = lane; e < ne; e += 64u) {
+                        const uint32_t n = e < M ? (uint32_t)ln[e] : 0u;
+                        JT[e] = (uint16_t)(n ? e + n : e);
+                    }
+                    wave_sync();
+                    for (uint32_t t = 0; t < 5u; ++t) {
+                        const uint16_t* Ta = JT + t * tb;
+                        uint16_t* Tn = JT + (t + 1u) * tb;
+                        for (uint32_t e = lane; e < ne; e += 64u) Tn[e] = Ta[Ta[e]];
+                        wave_sync();
+                    }
+                    uint32_t pp = jw;
+#pragma unroll
+                    for (uint32_t t = 0; t < 6u; ++t)
+                        if ((lane >> t) & 1u) pp = JT[t * tb + pp];
+                    const bool valid = pp < M && ln[pp] != 0u && k + lane < p.spp;
+                    c = (uint32_t)__popcll(__ballot(valid));   // a prefix of the lanes: stops are fixed points
+                    mypos = pp;
+                    if (c > 0u) {
+                        const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)pp, (int)(c - 1u));
+                        jw = (uint32_t)__builtin_amdgcn_readfirstlane((int)JT[last]);
+                    }
+                    wave_sync();   // (the terms below overwrite the tables)
+                }
+                while (!jump && c < 64u && k + c < p.spp && jw < M) {
                     const uint32_t ch = jw >> 8;
                     if (ch != chunk) {
                         chunk = ch;
@@ -4035,6 +4083,7 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
                     ++c;
                     jw += nj;
                 }
+                sub(1);
                 if (c == 0u) break;
                 if (lane < c) {
                     const uint32_t* src = reinterpret_cast<const uint32_t*>(res + mypos);
@@ -4049,8 +4098,9 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
                     lane_rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
                 }
                 wave_sync();
+                sub(2);
                 if (lane == 0u)
-#pragma unroll 4
+#pragma unroll 8
                     for (uint32_t i = 0; i < c; ++i) {
                         const float4 v = lc[i];
                         ax = v.x + ax * v.w;
@@ -4059,6 +4109,7 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
                     }
                 k += c;
                 wave_sync();
+                sub(3);
                 if (c < 64u) break;
             }
             if (k == p.spp) {
@@ -4166,11 +4217,7 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
                 const uint32_t* cp = CK + ((size_t)h * s.ncp + c) * 5u;
                 st = {cp[0], cp[1], cp[2], cp[3], cp[4], rr[kQd] + 2u * ja * IQ_XORWOW_WEYL};
                 xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * (ja - c * s.ck_step));
-                cM = rr[kQM];
-                cpx = rr[kQpx];
-                cpy = rr[kQpy];
-                cres = reinterpret_cast<float4*>(s.res) + (size_t)q * s.m_cap;
-                cln = LN + (size_t)h * s.m_cap;
+                cq = q;
                 active = true;
                 start_slot();
             }
@@ -4252,10 +4299,11 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
                 cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
                 cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
                 cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                cres[jc] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                reinterpret_cast<float4*>(s.res)[(size_t)cq * s.m_cap + jc] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                uint8_t* cln = LN + (size_t)h * s.m_cap;
                 cln[jc] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
                 // a parity pass (even slots): the odd slot after this one is untraced (0: the walk stops there)
-                if (sp == 2u && (jc & 1u) == 0u && jc + 1u < cM) cln[jc + 1u] = 0u;
+                if (sp == 2u && (jc & 1u) == 0u && jc + 1u < R[h * kSpecQRecWords + kQM]) cln[jc + 1u] = 0u;
                 jc += sp;
                 if (jc < je) {
                     st = base;                   // slot jc starts where slot jc - 1's camera draws ended ...
@@ -4272,15 +4320,19 @@ __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams
     }
     if (s.tl && lane == 0u) {
         const uint32_t wid = blockIdx.x * (kSpecBlock / 64u) + (threadIdx.x >> 6);
-        s.tl[4 * (size_t)wid] = t_start;
-        s.tl[4 * (size_t)wid + 1] =
+        unsigned long long ph2 = 0;
+        for (int i = 0; i < 4; ++i)
+            ph2 |= (unsigned long long)(t_phase[4 + i] < 0xffffu ? t_phase[4 + i] : 0xffffu) << (16 * i);
+        s.tl[8 * (size_t)wid + 4] = ph2;
+        s.tl[8 * (size_t)wid] = t_start;
+        s.tl[8 * (size_t)wid + 1] =
             (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) | ((unsigned long long)min(n_iter, 0xffffu) << 48);
-        s.tl[4 * (size_t)wid + 2] = (unsigned long long)n_pix | ((unsigned long long)n_walk << 16) |
+        s.tl[8 * (size_t)wid + 2] = (unsigned long long)n_pix | ((unsigned long long)n_walk << 16) |
                                     ((unsigned long long)n_fix << 32) | ((unsigned long long)xcd << 48);
         // 10-ns ticks (16 bits each) in admissions, walks, hand-outs and the slot loop's rays
         unsigned long long ph = 0;
-        for (int i = 0; i < 4; ++i) ph |= (unsigned long long)(t_phase[i] < 0xffffull ? t_phase[i] : 0xffffull) << (16 * i);
-        s.tl[4 * (size_t)wid + 3] = ph;
+        for (int i = 0; i < 4; ++i) ph |= (unsigned long long)(t_phase[i] < 0xffffu ? t_phase[i] : 0xffffu) << (16 * i);
+        s.tl[8 * (size_t)wid + 3] = ph;
     }
     unsigned long long rays = lane_rays;
 #pragma unroll

@@ -2186,8 +2186,8 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             ks2.nblocks = c->spec_plan_blocks;
         }
         if (c->spec_tl_on && n > 0) {
-            // (queue mode: 4 words per wave, 16 per block = two timeline records)
-            const size_t nb = ks2.queue ? 2 * (size_t)spec_q_blocks(ks2)
+            // (queue mode: one timeline record of 8 words per wave)
+            const size_t nb = ks2.queue ? 4 * (size_t)spec_q_blocks(ks2)
                                         : ks2.blocks ? ks2.nblocks : (n + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
             if (nb > c->spec_tl_blocks) {
                 IQPT_HIP(hipStreamSynchronize(ss));
@@ -2753,7 +2753,7 @@ int iqpt_debug_read_spec_timeline(iqpt_ctx* c, unsigned long long* out, uint32_t
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     if (!c->d_spec_tl || !c->spec_last) return IQPT_OK;
-    const size_t nspec = c->spec_q_last ? 2 * (size_t)c->spec_q_grid
+    const size_t nspec = c->spec_q_last ? 4 * (size_t)c->spec_q_grid
                          : c->spec_plan_n == c->n_chain_pix && c->spec_plan_n && c->spec_plan_mode
                              ? c->spec_plan_blocks
                              : (c->n_chain_pix + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
@@ -2915,8 +2915,9 @@ int iqpt_debug_set_spec_parity(iqpt_ctx* c, uint32_t rho256) {
 
 /* Internal (tests, A/B): queue mode for spec launches (iqpt_specq_kernel: persistent waves taking sphere pixels
  * from per-XCD cursors) — mode 0 the block kernel, 1 queue mode; blocks_per_cu the
- * persistent grid (0: the default). The timeline (iqpt_debug_read_spec_timeline) then holds 4 words per wave:
- * start, end | iterations << 48, pixels | walks << 16 | fix-ups << 32 | XCD << 48. */
+ * persistent grid (0: the default). The timeline (iqpt_debug_read_spec_timeline) then holds 8 words per wave:
+ * start, end | iterations << 48, pixels | walks << 16 | fix-ups << 32 | XCD << 48, then 10-ns ticks (16 bits
+ * each) in admissions / walks / hand-outs / rays and in the walks' wait / chain / gather / fold. */
 int iqpt_debug_set_spec_queue(iqpt_ctx* c, int mode, uint32_t blocks_per_cu) {
     if (!c || mode < 0 || mode > 1 || blocks_per_cu > 16)
         return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL, mode not 0..1 or blocks_per_cu > 16");

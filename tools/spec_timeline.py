@@ -96,7 +96,7 @@ def pct(a):
 if (int(info[2]) >> 32) > 0:
     # queue mode: per wave start, end | iterations << 48, pixels | walks << 16 | fix-ups << 32 | XCD << 48, time in
     # admissions | walks << 16 | hand-outs << 32 | rays << 48 (10-ns ticks)
-    w4 = raw8.reshape(-1, 4)
+    w4 = raw8
     ws = (w4[:, 0] & np.uint64(0xffffffffffff)).astype(np.float64)
     we = (w4[:, 1] & np.uint64(0xffffffffffff)).astype(np.float64)
     it = (w4[:, 1] >> np.uint64(48)).astype(np.int64)
@@ -117,6 +117,8 @@ if (int(info[2]) >> 32) > 0:
     ph = w4[:, 3]
     for i, name in enumerate(("admit", "walk", "handout", "trace")):
         res[f"{name}_us"] = pct(((ph >> np.uint64(16 * i)) & np.uint64(0xffff)).astype(np.float64) / 100.0)
+    for i, name in enumerate(("wait", "chain", "gather", "fold")):
+        res[f"walk_{name}_us"] = pct(((w4[:, 4] >> np.uint64(16 * i)) & np.uint64(0xffff)).astype(np.float64) / 100.0)
     print(json.dumps(res), flush=True)
     if args.out:
         Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
