@@ -261,7 +261,8 @@ int iqpt_frame_stream(iqpt_ctx* ctx, void** stream);
  *   with S >= world (S = world on a node; S > world is a rehearsal of an S-way share on fewer GPUs, in which
  *   the root places the rows of the communicator's ranks only).
  * iqpt_gather_frame_async: collective; enqueues a copy of the BGRA8 frame behind every render issued so far
- *   (it does not end overlapped or pipelined launches, like iqpt_copy_frame_device_async), the gather and,
+ *   (it does not end overlapped or pipelined launches, like iqpt_copy_frame_device_async; after a pipelined
+ *   launch no copy: the gather reads the frame buffer the launch wrote, behind its kernels), the gather and,
  *   on the root, the assembly of the W x H frame into dst_device (W*H*4 bytes; ignored elsewhere) on the
  *   communicator's stream (iqpt_comm_stream), and returns. The caller orders its reads of dst_device on that
  *   stream; every other entry point waits for the gathers in flight.

@@ -371,6 +371,8 @@ constexpr int kOptSplit = 1 << 16;     // sample-parallel chains: speculative ru
 constexpr int kOptScatter2 = 1 << 18;  // Oren–Nayar scatter with packed, branch-free transcendental pairs (iq_fp2.h)
 constexpr int kOptPrio = 1 << 17;      // VALU issue priority for waves on the launch's critical path (no effect on results)
 constexpr int kOptOverlap = 1 << 19;   // tiles bound to XCDs, launches overlap through per-tile completion counts
+constexpr int kOptAnyHit = 1 << 20;    // streamed any-hit scenes (kparams::anyhit): BVH and list loops leave at the first
+                                       // accepted triangle; its own variants, so other streamed scenes keep the registers
 constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull |
                             kOptBvh | kOptScatter2;
 constexpr uint32_t kStatsHeader = 24;        // kOptStats: 24 counters, then per-wave (start, end, iterations)

@@ -926,12 +926,12 @@ __device__ __forceinline__ void bvh_closest(const kparams& p, const ray3 r, floa
         if (hit && leaf) {
             bvh_leaf<OPT>(p, link & 0x7fffffffu, r, closest, kind, idx);
             // any-hit scenes (kparams::anyhit): an accepted triangle decides the ray, whichever it is
-            if (p.anyhit && kind == kHitTri) return;
+            if ((OPT & kOptAnyHit) && p.anyhit && kind == kHitTri) return;
         }
         i = (hit || leaf) ? i + 1 : link;
     }
     const float4* __restrict__ tris = reinterpret_cast<const float4*>(p.tris);
-    for (uint32_t a = 0; a < p.bvh_nalways && !(p.anyhit && kind == kHitTri); ++a) {
+    for (uint32_t a = 0; a < p.bvh_nalways && !((OPT & kOptAnyHit) && p.anyhit && kind == kHitTri); ++a) {
         const uint32_t k = p.bvh_always[a];
         float c2 = closest;
         int kd = kHitNone;
@@ -1684,7 +1684,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         test_triangle_pair<OPT>(q0, q1, q2, q3, q4, ray, closest, kind, hidx, 2 * j,
                                                 2 * j + 1 < p.ntri);
                     // any-hit scenes: the wave leaves once every list lane has an accepted triangle
-                    if (p.anyhit && __ballot(tri_mask != nullptr && kind != kHitTri) == 0ull) break;
+                    if ((OPT & kOptAnyHit) && p.anyhit && __ballot(tri_mask != nullptr && kind != kHitTri) == 0ull) break;
                     j = jn;
                     q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4;
                 }
@@ -4398,6 +4398,13 @@ const variant kVariants[] = {
                      IQPT_V(16, true, (O) & ~kOptLB5), IQPT_V(8, true, (O) | kOptBvhPrimary), \
                      IQPT_V(16, true, (O) | kOptBvhPrimary)
     IQPT_PROD(kOptDefault),
+    // streamed any-hit scenes (kOptAnyHit: no sphere, reference materials; C4): the first accepted triangle ends
+    // a ray's traversal. Variants of their own: the exits cost the other streamed scenes registers (C5 58.6-60.3
+    // against 56.6-56.7 ms per launch with them compiled in, r05 run 16)
+    IQPT_V(8, true, (kOptDefault | kOptAnyHit) & ~kOptLB5), IQPT_V(16, true, (kOptDefault | kOptAnyHit) & ~kOptLB5),
+    IQPT_V(8, true, kOptDefault | kOptAnyHit | kOptBvhPrimary), IQPT_V(16, true, kOptDefault | kOptAnyHit | kOptBvhPrimary),
+    IQPT_V(8, true, ((kOptDefault & ~kOptFastDiv) | kOptAnyHit) & ~kOptLB5),
+    IQPT_V(8, true, (kOptDefault & ~kOptFastDiv) | kOptAnyHit | kOptBvhPrimary),
     // pitch-only cameras (kOptCamAxis), resident scenes: 10.5 % fewer VALU instructions on C2; chosen by the
     // runtime wherever the camera qualifies (round 1 measured no gain; after kOptPrio / kOptScatter2 and
     // with overlapped launches it is -12..-14 %)
@@ -4432,6 +4439,9 @@ const variant kVariants[] = {
     IQPT_V(8, true, kOptDefault | kOptStats | kOptBvhPrimary),
     IQPT_V(8, true, (kOptDefault | kOptStats | kOptBvhPrimary) & ~kOptLB5),
     IQPT_V(8, false, kOptDefault | kOptSplit | kOptStats),
+    IQPT_V(8, true, (kOptDefault | kOptStats | kOptAnyHit) & ~kOptLB5),
+    IQPT_V(8, true, kOptDefault | kOptStats | kOptBvhPrimary | kOptAnyHit),
+    IQPT_V(8, true, (kOptDefault | kOptStats | kOptBvhPrimary | kOptAnyHit) & ~kOptLB5),
 #endif
 };
 #undef IQPT_V

@@ -1689,6 +1689,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     if (stream_batches && !iqpt::render_variant_exists(c->max_depth, true, opt) &&
         iqpt::render_variant_exists(c->max_depth, true, opt & ~iqpt::kOptLB5))
         opt &= ~iqpt::kOptLB5;
+    // streamed any-hit scenes take the variants with the first-hit exits (kOptAnyHit), where one exists
+    if (stream_batches && p.anyhit && iqpt::render_variant_exists(c->max_depth, true, opt | iqpt::kOptAnyHit))
+        opt |= iqpt::kOptAnyHit;
     // kOptCamAxis: the short camera transform, kept only where the camera qualifies (a caller's option
     // mask may ask for it; production launches add it below, where a variant exists: DESIGN.md §3.8)
     if (!cam_axis) opt &= ~iqpt::kOptCamAxis;

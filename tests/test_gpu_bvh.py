@@ -132,3 +132,39 @@ def test_camera_ray_path_switch_between_launches(require_gpu):
     w, h = 3840, 2160
     pt, _ = run_both(sc, w, h, 0, 8, pixels=pixel_set(w, h, 1800, 2000, 1000, 13, 8), launches=[1, 2, 1, 1])
     assert pt.frames() == 5
+
+
+@pytest.mark.parametrize("anyhit", [1, 0])
+def test_anyhit_variants_on_c4(require_gpu, anyhit):
+    """C4 geometry (triangles only, the reference's materials: every triangle emissive) over launches that
+    time and then use both camera-ray paths (tile lists and the BVH): with any-hit on, the launches run the
+    kOptAnyHit variants (first accepted triangle ends a ray, lists ordered by hit count), off the closest-hit
+    ones; both equal the oracle bit for bit (round 5)."""
+    import ctypes as C
+    from iqpt import _lib
+    sc = Scene()
+    sc.add_preset("mesh10k")
+    w, h = 1920, 1080
+    pk = sc.build_packet()
+    cam = make_camera(w, h)
+    ps = pixel_set(w, h, 880, 1040, 420, 9, 14)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    lb = _lib.load()
+    lb.iqpt_debug_set_anyhit.argtypes = [C.c_void_p, C.c_int]
+    _lib.check(lb.iqpt_debug_set_anyhit(pt._h, anyhit), "iqpt_debug_set_anyhit")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    for s in (2, 1, 1, 1, 3):
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    c = compare(lin, fr.lin)
+    assert c["bitexact"] == c["npix"], c
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    assert pt.rays() == int(fr.rays.sum())
+    lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    opt = C.c_int(0)
+    _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(opt)), "iqpt_debug_last_options")
+    assert bool(opt.value & (1 << 20)) == bool(anyhit), hex(opt.value)      # kOptAnyHit
