@@ -3347,7 +3347,9 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     const uint32_t px = p.x0 + col, py = p.y0 + row * p.ystep;
     if (l == 0u) {
         const uint32_t t = (row / kCullTile) * p.ntx + col / kCullTile;
-        lds_cm[g] = make_uint4(p.cull[(size_t)t * p.cull_stride], p.cull[(size_t)t * p.cull_stride + p.cull_wt], t, 0u);
+        // (w: the pixel's column and row, read when a lane starts one of its slots)
+        lds_cm[g] = make_uint4(p.cull[(size_t)t * p.cull_stride], p.cull[(size_t)t * p.cull_stride + p.cull_wt], t,
+                               px | (py << 16));
     }
     if (walker) {
         // round 0: the launch's first slot, the window from the pixel's last chain, its state
@@ -3415,9 +3417,8 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         // sample from its start state; the next one starts sp slots further (2 sp draws after this one's start:
         // the 2 camera draws then 2 (sp - 1) more).
         uint32_t gg = g, jc = j0, je = j1, sp = step;
-        uint32_t cpx = px, cpy = py;
-        float4* cres = res;
-        uint8_t* cln = ln;
+        // (the slot's pixel coordinates, result row and slot counts are read or derived from gg where they are
+        // used: registers for 5 fewer live values in the slot loop)
         bool active = live && j0 < j1;
         // fix-up pass: this lane's share [fa, fb) of the wave's pooled odd slots (pw: the prefix sums over the
         // wave's pixels of their fix-up slot counts, in the wave's own words of lds_w)
@@ -3428,7 +3429,8 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
         rng6 base = st;
         // a slot's sample starts here: its camera ray, and the state its two draws leave (the next slot's)
         auto start_slot = [&]() {
-            camera_ray<OPT>(p, cpx, cpy, st, ray);
+            const uint32_t pxy = lds_cm[gg].w;
+            camera_ray<OPT>(p, pxy & 0xffffu, pxy >> 16, st, ray);
             base = st;
             depth = 0;
         };
@@ -3448,12 +3450,6 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             fa += n_here;
             gg = h;
             sp = 2u;
-            uint32_t tcol = 0, trow = 0;
-            tile_decode(ph, p.ncols, p.nrows, &tcol, &trow);
-            cpx = p.x0 + tcol;
-            cpy = p.y0 + trow * p.ystep;
-            cres = reinterpret_cast<float4*>(s.res) + (size_t)rh[12] * s.m_cap;
-            cln = lds_n + (size_t)h * s.m_cap;
             // the pass-0 ranges of pixel h (even starts: 2 (ME_h k / L))
             const uint32_t MEh = (Mh + 1u) / 2u;
             uint32_t kk = L - 1u;
@@ -3544,7 +3540,9 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
                         cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
                         cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
                         cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                        cres[jc] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                        reinterpret_cast<float4*>(s.res)[(size_t)lds_rd[gg * 16u + 12u] * s.m_cap + jc] =
+                            make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
+                        uint8_t* cln = lds_n + (size_t)gg * s.m_cap;
                         cln[jc] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
                         // slot pass over even slots: the odd slot after this one is untraced (0: the walk stops there)
                         if (!fix && sp == 2u && jc + 1u < M) cln[jc + 1u] = 0u;
