@@ -4,10 +4,13 @@ block the s_memrealtime stamps (100 MHz) at its start, after round 0's slot pass
 parity pixel's fix-up pass and second walk) and at its end (iqpt_debug_spec_timeline). Prints percentiles of the block start, the phases and the end, and
 the blocks that needed more than one round.
 
-    spec_timeline.py [--share 8] [--specfan 1] [--plan 1] [--out f.json]
+    spec_timeline.py [--share 8] [--specfan 1] [--plan 1] [--parity R] [--parity-max R] [--queue 1 --qbpc B]
+                     [--out f.json]
 
 --specfan: 1 = the spec kernel alone on the stream (the fan kernel after it), 0 = beside the fan kernel
-on a second stream, 2 = one grid with the fan tiles."""
+on a second stream. --queue 1: queue mode (iqpt_specq_kernel, B blocks per CU): per wave its start and end,
+slot-loop iterations, pixels / walks / fix-ups, and its time in admissions, walks (wait, chain, gather, fold),
+hand-outs and rays."""
 import argparse
 import ctypes as C
 import json
