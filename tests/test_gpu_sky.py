@@ -140,7 +140,7 @@ def test_sky_kernel_ahead_of_and_behind_the_plain_kernel(require_gpu, after):
     pt.close()
 
 
-@pytest.mark.parametrize("split", ["spec", "chain"])
+@pytest.mark.parametrize("split", ["spec", "specq", "chain"])
 def test_sky_with_more_than_64_spheres(require_gpu, split):
     """a resident scene of more than 64 spheres skips the per-pixel sphere test of the split
     tiles, so every pixel of a split tile went to the spec / chain kernel's list — the certain misses too, which
@@ -162,7 +162,11 @@ def test_sky_with_more_than_64_spheres(require_gpu, split):
     ps = pixel_set(w, h, 0, w, rank, world, n)
     cam = make_camera(w, h)
     pt = PathTracer(w, h, pixels=ps, max_depth=8)
-    pt.set_split(L.SPLIT_SPEC if split == "spec" else L.SPLIT_CHAIN)
+    pt.set_split(L.SPLIT_SPEC if split in ("spec", "specq") else L.SPLIT_CHAIN)
+    if split == "specq":
+        # queue mode (iqpt_specq_kernel): the same pixel lists through persistent waves
+        lib.iqpt_debug_set_spec_queue.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
+        L.check(lib.iqpt_debug_set_spec_queue(pt.handle, 1, 0), "iqpt_debug_set_spec_queue")
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
