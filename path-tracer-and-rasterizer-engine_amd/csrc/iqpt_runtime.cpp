@@ -3069,7 +3069,7 @@ int copy_frame_async(iqpt_ctx* c, uint32_t* dst, hipEvent_t wait, hipStream_t* u
         // overlapped launches in flight: copy on the last launch's stream without joining, so the next
         // launch still overlaps this one (from here on overlapped launches alternate two frame buffers)
         if (!c->d_bgra_alt) {
-            if (hipMalloc(&c->d_bgra_alt, (size_t)c->npix * sizeof(uint32_t)) != hipSuccess) {
+            if (hipMalloc(&c->d_bgra_alt, frame_words(c) * sizeof(uint32_t)) != hipSuccess) {
                 (void)hipGetLastError();
                 c->d_bgra_alt = nullptr;
                 return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "second frame buffer for overlapped copies");
@@ -3188,22 +3188,32 @@ int iqpt_comm_init(iqpt_ctx* c, int rank, int world, const void* id, size_t byte
     c->comm_world = world;
     c->comm_stride = stride;
     c->gpar = 0;
-    // the frame buffers pipelined launches write are the gather's send buffers as they are: pad them to the rank
-    // block (the context's own buffer keeps its frame; a ring of the old size is dropped, rebuilt at the next copy)
+    // the frame buffers pipelined launches write are the gather's send buffers as they are: pad every frame
+    // buffer to the rank block. The last frame (d_bgra: the context's own buffer, the overlapped launches'
+    // second one or a ring buffer) moves into the new own buffer; the second buffer, if there is one, is
+    // re-made padded (the next overlapped launch overwrites it); a ring of the old size is dropped, rebuilt
+    // at the next copy. (The views d_bgra / d_bgra_alt may point at any of these: none is kept.)
     if (stride > c->npix) {
-        uint32_t* nb = nullptr;
-        if (hipMalloc(&nb, (size_t)stride * sizeof(uint32_t)) != hipSuccess) {
-            (void)hipGetLastError();
-            free_comm(c);
-            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "padded frame buffer");
-        }
-        IQPT_HIP(hipMemsetAsync(nb, 0, (size_t)stride * sizeof(uint32_t), c->stream));
-        IQPT_HIP(hipMemcpyAsync(nb, c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
+        const size_t pbytes = (size_t)stride * sizeof(uint32_t);
+        uint32_t* nb[2] = {};
+        const int nbuf = c->d_alt_own ? 2 : 1;
+        for (int k = 0; k < nbuf; ++k)
+            if (hipMalloc(&nb[k], pbytes) != hipSuccess) {
+                (void)hipGetLastError();
+                for (uint32_t* b : nb)
+                    if (b) (void)hipFree(b);
+                free_comm(c);
+                return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "padded frame buffer");
+            }
+        for (int k = 0; k < nbuf; ++k) IQPT_HIP(hipMemsetAsync(nb[k], 0, pbytes, c->stream));
+        IQPT_HIP(hipMemcpyAsync(nb[0], c->d_bgra, (size_t)c->npix * sizeof(uint32_t), hipMemcpyDeviceToDevice, c->stream));
         IQPT_HIP(hipStreamSynchronize(c->stream));
-        if (c->d_bgra_alt == c->d_bgra_own) c->d_bgra_alt = nb;   // (the overlapped launches' views swap)
-        if (c->d_bgra == c->d_bgra_own || c->pring_on) c->d_bgra = nb;
         (void)hipFree(c->d_bgra_own);
-        c->d_bgra_own = nb;
+        c->d_bgra_own = c->d_bgra = nb[0];
+        if (c->d_alt_own) {
+            (void)hipFree(c->d_alt_own);
+            c->d_alt_own = c->d_bgra_alt = nb[1];
+        }
         for (int i = 0; i < iqpt::kPipeRing; ++i) {
             if (c->d_pring[i]) (void)hipFree(c->d_pring[i]);
             c->d_pring[i] = nullptr;

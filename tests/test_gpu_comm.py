@@ -109,6 +109,82 @@ def test_n_rehearsals_assemble_the_whole_frame(require_gpu, n):
     assert np.array_equal(iqdist.assemble(parts, w, h, n, 4).view(np.int32).reshape(-1), frame.cpu().numpy())
 
 
+def _last_options(pt):
+    lb = iqpt.load()
+    lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    o = C.c_int(0)
+    iqpt._lib.check(lb.iqpt_debug_last_options(pt.handle, C.byref(o)), "iqpt_debug_last_options")
+    return o.value
+
+
+def _split_mode(pt):
+    lb = iqpt.load()
+    lb.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
+    info = (C.c_ulonglong * 8)()
+    iqpt._lib.check(lb.iqpt_debug_split_info(pt.handle, info), "iqpt_debug_split_info")
+    return int(info[7])
+
+
+def test_comm_init_pads_every_frame_buffer_of_a_ragged_rank(require_gpu):
+    """A ragged rank (fewer rows than the rank block) whose context already made the overlapped launches'
+    second frame buffer and the pipelined launches' ring — and whose second-buffer view points into that
+    ring — before iqpt_comm_init. The pipelined gather sends the launch's own frame buffer as it is, rank
+    block long: every frame buffer must be padded, none left dangling. Gathers after it, from overlapped
+    and from pipelined spec launches in turn, each hold their launch's frame (the oracle's), and the final
+    state is the oracle's."""
+    import oracle
+    L = iqpt._lib
+    w, h, n, r = 640, 130, 4, 3                   # rank 3 of 4: 32 rows, the rank block 33 (overlap: >= 16384 px)
+    ps = iqdist.pixel_set_for_rank(w, h, r, n)
+    pt, _, _, _ = _ctx(w, h, ps)
+    sc, pk = scene_for("cornell")                 # (the packet points into the scene's arrays: keep both)
+    cam = iqpt.make_camera(w, h)
+    fr = oracle.OracleFrame(w, h, pixels=oracle.pixel_set(w, h, 0, w, r, n, ps.nrows), max_depth=8)
+    npix = w * len(range(r, h, n))
+    assert npix < iqdist.max_rows(h, n) * w
+
+    def render(mode, s):
+        if mode == "ovl":
+            pt.set_split(L.SPLIT_OFF)
+            pt.set_overlap(L.OVERLAP_AUTO)
+        else:
+            pt.set_split(4)                       # IQPT_SPLIT_SPEC: pipelined spec + fan launches
+        pt.render(s)
+        fr.render(pk, cam, s)
+        if mode == "ovl":
+            assert _last_options(pt) & (1 << 19), hex(_last_options(pt))
+        else:
+            assert _split_mode(pt) == 6
+
+    keep = []
+    for mode, s in (("ovl", 3), ("ovl", 4), ("spec", 5), ("spec", 6), ("ovl", 3)):
+        render(mode, s)
+        b = torch.zeros(npix, dtype=torch.int32, device="cuda")
+        pt.copy_frame_device_async(b.data_ptr(), b.numel() * 4)
+        keep.append(b)                            # (the copies read the buffers comm_init replaces)
+    pt.comm_init(0, 1, iqpt.comm_unique_id())
+    frames, want = [], []
+    for mode, s in (("spec", 4), ("ovl", 5), ("spec", 3), ("ovl", 2), ("spec", 6)):
+        render(mode, s)
+        f = torch.full((h * w,), -7, dtype=torch.int32, device="cuda")
+        pt.gather_frame_async(0, f.data_ptr(), f.numel() * 4)
+        frames.append(f)
+        want.append(fr.bgra.view(np.int32).reshape(-1).copy())
+    pt.sync()
+    torch.cuda.synchronize()
+    for i, (f, wv) in enumerate(zip(frames, want)):
+        got = f.cpu().numpy().reshape(h, w)
+        assert np.array_equal(got[r::n].reshape(-1), wv), f"gather after launch {i}"
+        mask = np.ones(h, bool)
+        mask[r::n] = False
+        assert np.all(got[mask] == -7)
+    lin, bgra = pt.read()
+    assert np.array_equal(lin.view(np.uint32), fr.lin.view(np.uint32))
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    pt.close()
+
+
 def test_comm_init_rejects_a_pixel_set_it_cannot_assemble(require_gpu):
     w, h = 64, 32
     lib = iqpt.load()
