@@ -168,3 +168,36 @@ def test_anyhit_variants_on_c4(require_gpu, anyhit):
     opt = C.c_int(0)
     _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(opt)), "iqpt_debug_last_options")
     assert bool(opt.value & (1 << 20)) == bool(anyhit), hex(opt.value)      # kOptAnyHit
+
+
+@pytest.mark.parametrize("preset,w,h,ps_args,launches", [
+    ("mixed", 3840, 2160, (1700, 2100, 1000, 11, 6), [16, 3, 16]),      # C5 geometry, the bench's 16 spp
+    ("mesh10k", 1920, 1080, (860, 1060, 420, 9, 10), [8, 1, 5]),        # C4 geometry (any-hit variants)
+])
+@pytest.mark.parametrize("refill", [1, 16, 64])
+def test_stream_refill_group_sizes(require_gpu, preset, w, h, ps_args, launches, refill):
+    """Streamed-scene launches whose waves take new pixels only once `refill` lanes are idle (round 5: 16 by
+    default, neighbouring pixels together; 1 = a refill at every iteration with an idle lane; 64 = whole
+    waves): the pixels' results do not depend on when a lane takes them — bit-exact against the oracle."""
+    sc = Scene()
+    sc.add_preset(preset)
+    pk = sc.build_packet()
+    cam = make_camera(w, h)
+    ps = pixel_set(w, h, *ps_args)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    lb = _lib.load()
+    lb.iqpt_debug_set_stream_refill.argtypes = [C.c_void_p, C.c_uint32]
+    _lib.check(lb.iqpt_debug_set_stream_refill(pt._h, refill), "iqpt_debug_set_stream_refill")
+    assert lb.iqpt_debug_set_stream_refill(pt._h, 0) != 0 and lb.iqpt_debug_set_stream_refill(pt._h, 65) != 0
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    for s in launches:
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    c = compare(lin, fr.lin)
+    assert c["bitexact"] == c["npix"], c
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    assert pt.rays() == int(fr.rays.sum())
