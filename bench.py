@@ -42,13 +42,16 @@ sys.path.insert(0, str(REPO / "path-tracer-and-rasterizer-engine_amd"))
 
 FP32_PEAK_TFLOPS = 157.3        # MI355X FP32 vector peak (MI355X_MICROARCH.md); the path runs on the VALU
 HBM_PEAK_GBPS = 8000.0          # MI355X HBM3E peak, MI355X_MICROARCH.md
+STREAMED_CONFIGS = ("c4", "c5")  # scenes past the LDS: the first kTuneLaunches (4) launches time both camera-ray paths
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=None,
+                    help="untimed steps (default 3; 5 for the streamed configs c4 / c5, whose first 4 launches time "
+                         "both camera-ray paths, DESIGN.md §3.5)")
     ap.add_argument("--config", default="c2")
     ap.add_argument("--spp", type=int, default=0,
                     help="samples per pixel per step (default: the config's; a progressive pass of C5's 1024)")
@@ -123,7 +126,10 @@ def parse():
                     help="A/B: a spec plan's lanes as a fraction of the resident lanes (iqpt_debug_set_spec_cap; 0 = default)")
     ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain", "fan", "spec"],
                     help="sample-parallel chains (iqpt_set_split, DESIGN.md §3.7)")
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.warmup is None:
+        args.warmup = 5 if args.config in STREAMED_CONFIGS else 3
+    return args
 
 
 def _free_port() -> int:
@@ -787,6 +793,8 @@ def main():
                        **({"spec_prio": args.spec_prio} if args.spec_prio is not None else {}),
                        **({"spec_parity_max": args.spec_parity_max} if args.spec_parity_max is not None else {}),
                        **({"stream_refill": args.stream_refill} if args.stream_refill is not None else {}),
+                       **({"warmup_note": "W < 5: launches that time the camera-ray paths fall in the timed region"}
+                          if args.config in STREAMED_CONFIGS and args.warmup < 5 else {}),
                        **({"spec_queue": args.spec_queue, "spec_qbpc": args.spec_qbpc}
                           if args.spec_queue is not None else {})},
             "n_ranks_seen": n_ranks_seen,
