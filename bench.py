@@ -113,6 +113,8 @@ def parse():
                     help="A/B: spec parity pixels' upper bound in slots per sample (iqpt_debug_set_spec_parity_max)")
     ap.add_argument("--stream-refill", type=int, default=None,
                     help="A/B: idle lanes before a streamed-scene wave takes new pixels (iqpt_debug_set_stream_refill; 1..64)")
+    ap.add_argument("--resident-refill", type=int, default=None,
+                    help="A/B: idle lanes before a resident-scene wave takes new pixels (iqpt_debug_set_resident_refill)")
     ap.add_argument("--spec-queue", type=int, default=None,
                     help="A/B: spec launches in queue mode (1) or the block kernel (0) (iqpt_debug_set_spec_queue)")
     ap.add_argument("--spec-qbpc", type=int, default=0,
@@ -532,6 +534,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_stream_refill.argtypes = [C.c_void_p, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_stream_refill(pt._h, args.stream_refill), "iqpt_debug_set_stream_refill")
+    if args.resident_refill is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_resident_refill.argtypes = [C.c_void_p, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_resident_refill(pt._h, args.resident_refill), "iqpt_debug_set_resident_refill")
     if args.spec_queue is not None:
         import ctypes as C
         lb = _lib.load()
@@ -793,6 +800,7 @@ def main():
                        **({"spec_prio": args.spec_prio} if args.spec_prio is not None else {}),
                        **({"spec_parity_max": args.spec_parity_max} if args.spec_parity_max is not None else {}),
                        **({"stream_refill": args.stream_refill} if args.stream_refill is not None else {}),
+                       **({"resident_refill": args.resident_refill} if args.resident_refill is not None else {}),
                        **({"warmup_note": "W < 5: launches that time the camera-ray paths fall in the timed region"}
                           if args.config in STREAMED_CONFIGS and args.warmup < 5 else {}),
                        **({"spec_queue": args.spec_queue, "spec_qbpc": args.spec_qbpc}

@@ -1273,10 +1273,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     uint32_t q_next_v = 0u;            // the prefetched position (lane 0's atomic result, read when needed)
     bool have_next = false;
     // lanes idle before a refill (kOptSplit round 1: speculative runs end at different iterations, and
-    // a refill per iteration costs its dependent loads every iteration; streamed scenes: a 16-spp pixel ends
-    // at a scattered iteration, and 16 lanes taking neighbouring pixels together beat one at a time, C5 -2 %,
-    // C4 -3.5 %, r05 runs 29-30)
-    const uint32_t refill_min = (kSplit || STREAM) ? max(p.refill_min, 1u) : 1u;
+    // a refill per iteration costs its dependent loads every iteration; streamed scenes: a wave that takes
+    // a whole tile at once keeps its rays coherent through the BVHs, C5 -5 %, r05 runs 29-35)
+    const uint32_t refill_min = max(p.refill_min, 1u);
     // pixel complete: BGRA8 (:360-365), accumulator and RNG state back to HBM
     auto store_pixel = [&]() {
         const uint32_t r8 = to_u8(255.0f * iq_sqrtf(acc.x));

@@ -181,7 +181,8 @@ struct iqpt_ctx {
     float4_storage* d_res = nullptr;    // m_cap x ns_cap
     uint8_t* d_nres = nullptr;          // ns_cap x m_cap
     uint32_t split_refill_min = 16;     // idle lanes before a refill in split launches
-    uint32_t stream_refill_min = 16;    // ... in streamed launches (iqpt_debug_set_stream_refill)
+    uint32_t stream_refill_min = 64;    // ... in streamed launches: whole waves (iqpt_debug_set_stream_refill)
+    uint32_t resident_refill_min = 1;   // ... in resident plain launches (iqpt_debug_set_resident_refill)
     uint32_t split_heavy_rho = iqpt::kSplitHeavyRho;
     bool split_all_tiles = false;       // every tile in the split set (wall tiles: one slot per sample)
     // chain launches: chain-kernel waves per CU (0: kChainWavesPerCu); the last launch's mode
@@ -1703,9 +1704,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     if (stream_batches) {
         p.tri_batch = pair ? iqpt::kTriBatch / 2 : iqpt::kTriBatch;   // records
         p.sph_batch = pair ? iqpt::kSphBatch / 2 : iqpt::kSphBatch;
-        // a wave takes new pixels once this many of its lanes are idle (neighbouring pixels together)
+        // a wave takes new pixels once this many of its lanes are idle (64: a whole tile at a time, its rays
+        // coherent through the BVHs)
         p.refill_min = std::min<uint32_t>(64u, std::max<uint32_t>(1u, c->stream_refill_min));
     } else {
+        p.refill_min = std::min<uint32_t>(64u, std::max<uint32_t>(1u, c->resident_refill_min));
         p.tri_batch = tri_recs;
         p.sph_batch = sph_recs;
     }
@@ -2909,11 +2912,21 @@ int iqpt_debug_set_anyhit(iqpt_ctx* c, int on) {
 }
 
 /* Internal (tests, A/B): idle lanes a wave of a streamed-scene launch waits for before it takes new pixels
- * (1..64; 1 = every iteration with an idle lane, round 4; 16 by default). Same bits either way. */
+ * (1..64; 1 = every iteration with an idle lane, round 4; 64, a whole tile at a time, by default). Same bits
+ * either way. */
 int iqpt_debug_set_stream_refill(iqpt_ctx* c, uint32_t lanes) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     if (lanes < 1u || lanes > 64u) return iqpt::fail(IQPT_ERR_INVALID_ARG, "lanes 1..64");
     c->stream_refill_min = lanes;
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): the same for the plain kernel's launches over resident scenes (1 by default; split
+ * launches keep their own, iqpt_debug_set_split_knobs). Same bits either way. */
+int iqpt_debug_set_resident_refill(iqpt_ctx* c, uint32_t lanes) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    if (lanes < 1u || lanes > 64u) return iqpt::fail(IQPT_ERR_INVALID_ARG, "lanes 1..64");
+    c->resident_refill_min = lanes;
     return IQPT_OK;
 }
 

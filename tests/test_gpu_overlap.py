@@ -180,3 +180,36 @@ def test_async_frame_copies_keep_overlap(require_gpu, preset, w, h, crop):
     lin, bgra = pt.read()
     same((lin, bgra, pt.read_rng(), pt.rays(), pt.frames()), ref_state)
     pt.close()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("refill", [16, 64])
+def test_resident_refill_group_sizes(require_gpu, overlap, refill):
+    """Resident plain launches whose waves take new pixels only once `refill` lanes are idle
+    (iqpt_debug_set_resident_refill; 1 by default): overlapped chains of launches and single-stream ones
+    keep the oracle's bits (accumulator, BGRA8, RNG states, ray counts)."""
+    w, h = 256, 144
+    sc, pk = scene_for("cornell")              # (the packet points into the scene's arrays)
+    cam = make_camera(w, h)
+    pt = PathTracer(w, h, max_depth=8)
+    pt.set_split(_lib.SPLIT_OFF)
+    pt.set_overlap(_lib.OVERLAP_AUTO if overlap else _lib.OVERLAP_OFF)
+    lb = _lib.load()
+    lb.iqpt_debug_set_resident_refill.argtypes = [C.c_void_p, C.c_uint32]
+    _lib.check(lb.iqpt_debug_set_resident_refill(pt._h, refill), "iqpt_debug_set_resident_refill")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, max_depth=8)
+    opts = []
+    for s in (4, 9, 2, 7):
+        pt.render(s)
+        opts.append(last_options(pt))
+        fr.render(pk, cam, s)
+    assert all(bool(o & K_OPT_OVERLAP) == overlap for o in opts), opts
+    lin, bgra = pt.read()
+    c = compare(lin, fr.lin)
+    assert c["bitexact"] == c["npix"], c
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    assert pt.rays() == int(fr.rays.sum())
+    pt.close()
