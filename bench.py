@@ -113,6 +113,9 @@ def parse():
                     help="A/B: spec parity pixels' upper bound in slots per sample (iqpt_debug_set_spec_parity_max)")
     ap.add_argument("--stream-refill", type=int, default=None,
                     help="A/B: idle lanes before a streamed-scene wave takes new pixels (iqpt_debug_set_stream_refill; 1..64)")
+    ap.add_argument("--stream-xcd", type=int, default=None, choices=[0, 1, 2, 3],
+                    help="A/B: streamed scenes' tiles per XCD (iqpt_debug_set_stream_xcd: 0 one queue, 1 cost order "
+                         "dealt to the XCDs, 2 bands of tile rows dealt to the XCDs, 3 the default: 1 up to 4 spp per launch)")
     ap.add_argument("--resident-refill", type=int, default=None,
                     help="A/B: idle lanes before a resident-scene wave takes new pixels (iqpt_debug_set_resident_refill)")
     ap.add_argument("--spec-queue", type=int, default=None,
@@ -534,6 +537,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_stream_refill.argtypes = [C.c_void_p, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_stream_refill(pt._h, args.stream_refill), "iqpt_debug_set_stream_refill")
+    if args.stream_xcd is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_stream_xcd.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_stream_xcd(pt._h, args.stream_xcd), "iqpt_debug_set_stream_xcd")
     if args.resident_refill is not None:
         import ctypes as C
         lb = _lib.load()
@@ -801,6 +809,7 @@ def main():
                        **({"spec_parity_max": args.spec_parity_max} if args.spec_parity_max is not None else {}),
                        **({"stream_refill": args.stream_refill} if args.stream_refill is not None else {}),
                        **({"resident_refill": args.resident_refill} if args.resident_refill is not None else {}),
+                       **({"stream_xcd": args.stream_xcd} if args.stream_xcd is not None else {}),
                        **({"warmup_note": "W < 5: launches that time the camera-ray paths fall in the timed region"}
                           if args.config in STREAMED_CONFIGS and args.warmup < 5 else {}),
                        **({"spec_queue": args.spec_queue, "spec_qbpc": args.spec_qbpc}

@@ -1186,8 +1186,11 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     constexpr bool kSplit = (OPT & kOptSplit) && !STREAM;
     // kOptOverlap (resident, culled, not split): this XCD's tile list and queue word, per-tile waits
     constexpr bool kOverlap = (OPT & kOptOverlap) && !STREAM && !kSplit && kCull;
-    const uint32_t xcd = kOverlap ? (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) : 0u;   // HW_REG_XCC_ID
-    uint32_t* const queue_word = kOverlap ? p.queue + 16u * xcd : p.queue;
+    // streamed scenes with p.xcd_order: the same per-XCD lists and queue words (tiles dealt to the XCDs by the
+    // runtime, iqpt_debug_set_stream_xcd), without the waits
+    const bool kXcdQ = kOverlap || (STREAM && p.xcd_order != nullptr);
+    const uint32_t xcd = kXcdQ ? (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) : 0u;   // HW_REG_XCC_ID
+    uint32_t* const queue_word = kXcdQ ? p.queue + 16u * xcd : p.queue;
 
     if (!STREAM) {
         for (uint32_t i = threadIdx.x; i < tri_recs * kTriRec; i += kRenderBlock) lds_tri[i] = g_tri[i];
@@ -1260,7 +1263,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     uint64_t chunk_certain = 0;
     // ... and its certain-miss pixels (kparams::miss): iqpt_sky_kernel renders them, this kernel skips them
     uint64_t chunk_miss = 0;
-    uint32_t queue_total = kOverlap ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : (p.nqueue ? p.nqueue : p.ntiles), n_runs = 0;
+    uint32_t queue_total = kXcdQ ? p.xcd_off[xcd + 1] - p.xcd_off[xcd] : (p.nqueue ? p.nqueue : p.ntiles), n_runs = 0;
     if (kSplit) {
         // round 1, longest tasks first: the split tiles' light pixels (anchored chains with scatters, in
         // the masks' cost order), then the heavy pixels' run chunks, then the anchored (wall / sky) tiles
@@ -1346,9 +1349,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                             chunk_kind = 0;
                             t = p.anchor_order[q - p.n_split_tiles - n_runs];
                         }
-                    } else if (kOverlap) {
+                    } else if (kXcdQ) {
                         t = p.xcd_order[p.xcd_off[xcd] + q];
-                        if (p.done_target != 0u && lane == 0) {
+                        if (kOverlap && p.done_target != 0u && lane == 0) {
                             // wait until the previous launches of the chain have finished tile t: their waves
                             // ran on this XCD, so the counter and the tile's pixel state meet in its L2 (sc1
                             // polls and loads bypass this CU's L1)
@@ -2083,7 +2086,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
 
     // closest-hit query count: one atomic per wave
     if (lane == 0 && wave_rays) add_rays(p.rays, (unsigned long long)wave_rays);
-    if (kOverlap && p.ovl_err) {
+    if (kXcdQ && p.ovl_err) {
         // HIP promises no workgroup -> XCD placement: the last block to finish checks that every XCD's
         // tile list was taken to its end (a list no wave ran on would leave its tiles unrendered, silently)
         __syncthreads();

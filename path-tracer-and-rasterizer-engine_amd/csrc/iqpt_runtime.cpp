@@ -294,6 +294,14 @@ struct iqpt_ctx {
     uint32_t* d_tile_done = nullptr;    // ntiles
     uint32_t* d_xcd_order = nullptr;    // ntiles: XCD x's tiles at [xcd_off[x], xcd_off[x + 1])
     uint32_t xcd_off[9] = {};
+    // streamed scenes (iqpt_debug_set_stream_xcd): 0 one queue over the cost order; 1 the per-XCD lists above
+    // (a queue word per XCD: C5 -9 % at 1 spp per launch, where tiles are short and the one queue word is
+    // contended; +0.2..1.4 % at 16 spp and C4 +4 % at 256, where the fixed lists end unevenly, r05 runs 38-39);
+    // 2 per-XCD bands of kXcdBandRows tile rows dealt round-robin (each XCD's L2 sees a band at a time: +17 % at
+    // 16 spp, the bands are not in cost order); 3 (default) 1 up to kStreamXcdMaxSpp samples per launch, else 0
+    int stream_xcd = 3;
+    uint32_t* d_xcd_band = nullptr;     // ntiles: XCD x's bands at [xcd_band_off[x], xcd_band_off[x + 1])
+    uint32_t xcd_band_off[9] = {};
     uint32_t* d_ovl_err = nullptr;
     // stream-ordered frame copies across overlapped launches (iqpt_copy_frame_device_async): once the
     // first such copy is asked for, each overlapped launch writes the BGRA frame into the buffer the
@@ -862,6 +870,22 @@ int build_cull(iqpt_ctx* c) {
 
         IQPT_HIP(hipMemcpy(c->d_xcd_order, xo.data(), xo.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
         c->ovl_zero = true;
+        // streamed scenes' bands: rows of tiles in bands of kXcdBandRows, band b to XCD b mod 8, in tile order
+        constexpr uint32_t kXcdBandRows = 4;
+        const uint32_t ntx = c->cull_ntx, nty = (ntiles + ntx - 1) / ntx;
+        std::vector<uint32_t> xb;
+        xb.reserve(ntiles);
+        for (uint32_t x = 0; x < 8; ++x) {
+            c->xcd_band_off[x] = (uint32_t)xb.size();
+            for (uint32_t b = x; b * kXcdBandRows < nty; b += 8)
+                for (uint32_t ty = b * kXcdBandRows; ty < std::min(nty, (b + 1) * kXcdBandRows); ++ty)
+                    for (uint32_t tx = 0; tx < ntx; ++tx)
+                        if (ty * ntx + tx < ntiles) xb.push_back(ty * ntx + tx);
+        }
+        c->xcd_band_off[8] = (uint32_t)xb.size();
+        if (!c->d_xcd_band && hipMalloc(&c->d_xcd_band, (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
+            return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "XCD tile bands");
+        IQPT_HIP(hipMemcpy(c->d_xcd_band, xb.data(), xb.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     c->split_last = false;
     int st = build_split(c, order, cnt);
@@ -1359,7 +1383,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->d_rng) (void)hipFree(c->d_rng);
     if (c->d_rays) (void)hipFree(c->d_rays);
     if (c->d_queue) (void)hipFree(c->d_queue);
-    for (uint32_t* b : {c->d_tile_done, c->d_xcd_order, c->d_ovl_err})
+    for (uint32_t* b : {c->d_tile_done, c->d_xcd_order, c->d_xcd_band, c->d_ovl_err})
         if (b) (void)hipFree(b);
     if (c->ev_pre) (void)hipEventDestroy(c->ev_pre);
     if (c->ev_s2) (void)hipEventDestroy(c->ev_s2);
@@ -2010,7 +2034,19 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         opt |= iqpt::kOptCamAxis;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * occ));
-    if (!ovl && !chain && !fan && !spec) IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
+    // streamed scenes: per-XCD tile lists and queue words (iqpt_debug_set_stream_xcd), where the overlapped
+    // launches could bind tiles to XCDs (8 XCDs, enough blocks; the kernel's last block checks the placement)
+    constexpr uint32_t kStreamXcdMaxSpp = 4;
+    const int xmode = c->stream_xcd == 3 ? (spp <= kStreamXcdMaxSpp ? 1 : 0) : c->stream_xcd;
+    const bool xcdq = stream_batches && xmode != 0 && p.cull && c->d_xcd_order && c->d_xcd_band &&
+                      !split && !chain && !fan && !spec && c->num_xcc == 8 && c->num_cus >= 64 && grid >= 64;
+    if (xcdq) {
+        p.xcd_order = xmode == 1 ? c->d_xcd_order : c->d_xcd_band;
+        std::memcpy(p.xcd_off, xmode == 1 ? c->xcd_off : c->xcd_band_off, sizeof p.xcd_off);
+        p.ovl_err = c->d_ovl_err;
+    }
+    if (!ovl && !chain && !fan && !spec)
+        IQPT_HIP(hipMemsetAsync(c->d_queue, 0, (xcdq ? 16u * 8u + 1u : 4u) * sizeof(uint32_t), c->stream));
     hipEvent_t e0 = take_event(c), e1 = take_event(c), e1b = nullptr;
     // pipelined spec launches: the timing events are recorded by the spec and fan kernels' dispatches (no
     // marker packets between consecutive kernels on the two streams: -0.012 ms per step at N = 8, -0.04 with
@@ -2918,6 +2954,17 @@ int iqpt_debug_set_stream_refill(iqpt_ctx* c, uint32_t lanes) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     if (lanes < 1u || lanes > 64u) return iqpt::fail(IQPT_ERR_INVALID_ARG, "lanes 1..64");
     c->stream_refill_min = lanes;
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): how streamed-scene launches deal tiles — 0 one queue over the cost order, 1 per-XCD
+ * queues over the cost order dealt round-robin, 2 per-XCD queues over bands of tile rows dealt round-robin
+ * (spatially coherent work per XCD L2), 3 (default) 1 for launches of up to 4 samples per pixel, else 0. Same
+ * bits either way. */
+int iqpt_debug_set_stream_xcd(iqpt_ctx* c, int mode) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    if (mode < 0 || mode > 3) return iqpt::fail(IQPT_ERR_INVALID_ARG, "mode 0..3");
+    c->stream_xcd = mode;
     return IQPT_OK;
 }
 

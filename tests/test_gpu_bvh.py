@@ -201,3 +201,36 @@ def test_stream_refill_group_sizes(require_gpu, preset, w, h, ps_args, launches,
     assert np.array_equal(bgra, fr.bgra)
     assert np.array_equal(pt.read_rng(), fr.states)
     assert pt.rays() == int(fr.rays.sum())
+
+
+@pytest.mark.parametrize("preset,w,h,ps_args,launches", [
+    ("mesh10k", 1920, 1080, (0, 1920, 300, 7, 9), [2, 1]),            # C4 geometry, 17,280 pixels
+    ("mixed", 3840, 2160, (0, 3840, 900, 9, 5), [1]),                 # C5 geometry, 19,200 pixels
+])
+@pytest.mark.parametrize("mode", [1, 2])
+def test_stream_xcd_tile_lists(require_gpu, preset, w, h, ps_args, launches, mode):
+    """Streamed-scene launches whose tiles are dealt to the 8 XCDs (iqpt_debug_set_stream_xcd: 1 the cost order
+    round-robin, 2 bands of tile rows round-robin), each XCD taking its own list from its own queue word; the
+    kernel's last block checks that every list was taken. Pixel sets of more than 64 blocks, so the lists are
+    used. Bit-exact against the oracle."""
+    sc = Scene()
+    sc.add_preset(preset)
+    pk = sc.build_packet()
+    cam = make_camera(w, h)
+    ps = pixel_set(w, h, *ps_args)
+    pt = PathTracer(w, h, pixels=ps, max_depth=8)
+    lb = _lib.load()
+    lb.iqpt_debug_set_stream_xcd.argtypes = [C.c_void_p, C.c_int]
+    _lib.check(lb.iqpt_debug_set_stream_xcd(pt._h, mode), "iqpt_debug_set_stream_xcd")
+    pt.set_camera(cam)
+    pt.upload_packet(pk)
+    fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    for s in launches:
+        pt.render(s)
+        fr.render(pk, cam, s)
+    lin, bgra = pt.read()
+    c = compare(lin, fr.lin)
+    assert c["bitexact"] == c["npix"], c
+    assert np.array_equal(bgra, fr.bgra)
+    assert np.array_equal(pt.read_rng(), fr.states)
+    assert pt.rays() == int(fr.rays.sum())
