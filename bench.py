@@ -107,6 +107,9 @@ def parse():
                     help="A/B: no timing events around launches (kernel times and the roofline read 0)")
     ap.add_argument("--self-gather", action="store_true",
                     help="test: run the per-step gather path at N = 1 (a one-rank process group)")
+    ap.add_argument("--two-ray", type=int, default=None, choices=[0, 1],
+                    help="A/B: resident plain launches trace the path ray and the next sample's camera ray together "
+                         "(iqpt_debug_set_two_ray; default: the library's, on)")
     ap.add_argument("--anyhit", type=int, default=None, choices=[0, 1],
                     help="A/B: any-hit queries for triangle-only scenes (iqpt_debug_set_anyhit; default: the library's, on)")
     ap.add_argument("--spec-parity-max", type=float, default=None,
@@ -527,6 +530,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_sky.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_sky(pt._h, 0), "iqpt_debug_set_sky")
+    if args.two_ray is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_two_ray.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_two_ray(pt._h, args.two_ray), "iqpt_debug_set_two_ray")
     if args.anyhit is not None:
         import ctypes as C
         lb = _lib.load()

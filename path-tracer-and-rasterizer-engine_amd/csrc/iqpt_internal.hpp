@@ -373,6 +373,8 @@ constexpr int kOptPrio = 1 << 17;      // VALU issue priority for waves on the l
 constexpr int kOptOverlap = 1 << 19;   // tiles bound to XCDs, launches overlap through per-tile completion counts
 constexpr int kOptAnyHit = 1 << 20;    // streamed any-hit scenes (kparams::anyhit): BVH and list loops leave at the first
                                        // accepted triangle; its own variants, so other streamed scenes keep the registers
+constexpr int kOptPipe = 1 << 21;      // resident scenes: a lane traces its path's ray and its next sample's camera ray in one
+                                       // iteration; its own variants (4 waves/SIMD)
 constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos | kOptLB5 | kOptFastDiv | kOptCull |
                             kOptBvh | kOptScatter2;
 constexpr uint32_t kStatsHeader = 24;        // kOptStats: 24 counters, then per-wave (start, end, iterations)

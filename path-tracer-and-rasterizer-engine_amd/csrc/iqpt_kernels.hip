@@ -739,6 +739,121 @@ __device__ __forceinline__ void intersect_culled(const float4* tri, uint32_t ntr
     }
 }
 
+// ---- two rays per lane (kOptPipe): ray a is the lane's current path, ray b the camera
+// ray of its pixel's next sample. Each ray sees exactly the operation sequence of test_triangle_pair /
+// test_sphere_pair and the pairs in index order, so each keeps its own bits; the two tests share the
+// pair's LDS reads and their stages are interleaved, so the two dependent chains overlap.
+template <int OPT>
+__device__ __forceinline__ void test_triangle_pair2(const float4 q0, const float4 q1, const float4 q2, const float4 q3,
+                                                    const float4 q4, const ray3 ra, const ray3 rb, bool ta, bool tb,
+                                                    float& ca, int& ka, uint32_t& ia, float& cb, int& kb, uint32_t& ib,
+                                                    uint32_t k, bool second) {
+    if (ta) stat_add<OPT>(0, 2u);
+    if (tb) stat_add<OPT>(0, 2u);
+    const f2 v0x = {q0.x, q0.y}, v0y = {q0.z, q0.w}, v0z = {q1.x, q1.y};
+    const f2 e1x = {q1.z, q1.w}, e1y = {q2.x, q2.y}, e1z = {q2.z, q2.w};
+    const f2 e2x = {q3.x, q3.y}, e2y = {q3.z, q3.w}, e2z = {q4.x, q4.y};
+    const f2 pxa = ra.dy * e2z - ra.dz * e2y, pxb = rb.dy * e2z - rb.dz * e2y;
+    const f2 pya = ra.dz * e2x - ra.dx * e2z, pyb = rb.dz * e2x - rb.dx * e2z;
+    const f2 pza = ra.dx * e2y - ra.dy * e2x, pzb = rb.dx * e2y - rb.dy * e2x;
+    const f2 deta = (e1x * pxa + e1y * pya) + e1z * pza, detb = (e1x * pxb + e1y * pyb) + e1z * pzb;
+    bool a0 = ta && !(iq_fabsf(deta.x) < 0.000001f), a1 = ta && second && !(iq_fabsf(deta.y) < 0.000001f);
+    bool b0 = tb && !(iq_fabsf(detb.x) < 0.000001f), b1 = tb && second && !(iq_fabsf(detb.y) < 0.000001f);
+    if (!(a0 || a1 || b0 || b1)) return;
+    const f2 inva = {rcp_scene<OPT>(deta.x), rcp_scene<OPT>(deta.y)};
+    const f2 invb = {rcp_scene<OPT>(detb.x), rcp_scene<OPT>(detb.y)};
+    const f2 txa = ra.ox - v0x, tya = ra.oy - v0y, tza = ra.oz - v0z;
+    const f2 txb = rb.ox - v0x, tyb = rb.oy - v0y, tzb = rb.oz - v0z;
+    const f2 ua = ((txa * pxa + tya * pya) + tza * pza) * inva, ub = ((txb * pxb + tyb * pyb) + tzb * pzb) * invb;
+    a0 = a0 && !(ua.x < 0.0f || ua.x > 1.0f);
+    a1 = a1 && !(ua.y < 0.0f || ua.y > 1.0f);
+    b0 = b0 && !(ub.x < 0.0f || ub.x > 1.0f);
+    b1 = b1 && !(ub.y < 0.0f || ub.y > 1.0f);
+    if (!(a0 || a1 || b0 || b1)) return;
+    const f2 qxa = tya * e1z - tza * e1y, qxb = tyb * e1z - tzb * e1y;
+    const f2 qya = tza * e1x - txa * e1z, qyb = tzb * e1x - txb * e1z;
+    const f2 qza = txa * e1y - tya * e1x, qzb = txb * e1y - tyb * e1x;
+    const f2 va = ((ra.dx * qxa + ra.dy * qya) + ra.dz * qza) * inva;
+    const f2 vb = ((rb.dx * qxb + rb.dy * qyb) + rb.dz * qzb) * invb;
+    const f2 uva = ua + va, uvb = ub + vb;
+    a0 = a0 && !(va.x < 0.0f || uva.x > 1.0f);
+    a1 = a1 && !(va.y < 0.0f || uva.y > 1.0f);
+    b0 = b0 && !(vb.x < 0.0f || uvb.x > 1.0f);
+    b1 = b1 && !(vb.y < 0.0f || uvb.y > 1.0f);
+    if (!(a0 || a1 || b0 || b1)) return;
+    const f2 t_a = ((e2x * qxa + e2y * qya) + e2z * qza) * inva;
+    const f2 t_b = ((e2x * qxb + e2y * qyb) + e2z * qzb) * invb;
+    if (a0 && !(t_a.x < kTMin || ca < t_a.x)) { ca = t_a.x; ka = kHitTri; ia = k; }
+    if (a1 && !(t_a.y < kTMin || ca < t_a.y)) { ca = t_a.y; ka = kHitTri; ia = k + 1; }
+    if (b0 && !(t_b.x < kTMin || cb < t_b.x)) { cb = t_b.x; kb = kHitTri; ib = k; }
+    if (b1 && !(t_b.y < kTMin || cb < t_b.y)) { cb = t_b.y; kb = kHitTri; ib = k + 1; }
+}
+
+template <int OPT>
+__device__ __forceinline__ void test_sphere_pair2(const float4 s0, const float4 s1, const ray3 ra, const ray3 rb, bool ta,
+                                                  bool tb, float& ca, int& ka, uint32_t& ia, float& cb, int& kb,
+                                                  uint32_t& ib, uint32_t k, bool second) {
+    if (ta) stat_add<OPT>(1, 2u);
+    if (tb) stat_add<OPT>(1, 2u);
+    const f2 cx = {s0.x, s0.y}, cy = {s0.z, s0.w}, cz = {s1.x, s1.y}, rad = {s1.z, s1.w};
+    const f2 ocxa = cx - ra.ox, ocya = cy - ra.oy, ocza = cz - ra.oz;
+    const f2 ocxb = cx - rb.ox, ocyb = cy - rb.oy, oczb = cz - rb.oz;
+    const f2 hba = (ra.dx * ocxa + ra.dy * ocya) + ra.dz * ocza, hbb = (rb.dx * ocxb + rb.dy * ocyb) + rb.dz * oczb;
+    const f2 r2 = rad * rad;
+    const f2 cca = ((ocxa * ocxa + ocya * ocya) + ocza * ocza) - r2, ccb = ((ocxb * ocxb + ocyb * ocyb) + oczb * oczb) - r2;
+    const f2 da = hba * hba - cca, db = hbb * hbb - ccb;
+    if (ta && !(da.x < 0.0f)) sphere_roots<OPT>(hba.x, da.x, ca, ka, ia, k);
+    if (ta && second && !(da.y < 0.0f)) sphere_roots<OPT>(hba.y, da.y, ca, ka, ia, k + 1);
+    if (tb && !(db.x < 0.0f)) sphere_roots<OPT>(hbb.x, db.x, cb, kb, ib, k);
+    if (tb && second && !(db.y < 0.0f)) sphere_roots<OPT>(hbb.y, db.y, cb, kb, ib, k + 1);
+}
+
+// The closest hits of rays a and b over the LDS-resident pairs (kOptCull): ray b is always a camera ray and
+// tests the pairs of the wave's OR of its lanes' tile masks (or the uniform tile's own mask, as
+// intersect_culled); ray a tests the same pairs when every active lane's ray a is a camera ray, else every
+// pair (all_a). The loop runs over the union in index order, so each ray meets its pairs in the
+// reference's order. Called by all lanes of the wave.
+template <int OPT>
+__device__ __forceinline__ void intersect_culled2(const float4* tri, uint32_t ntri, const float4* sph, uint32_t nsph,
+                                                  const uint32_t* lane_mask, uint32_t cm_t, uint32_t cm_s, bool all_a,
+                                                  bool act_a, bool act_b, const ray3 ra, const ray3 rb, float& ca,
+                                                  int& ka, uint32_t& ia, float& cb, int& kb, uint32_t& ib, uint32_t wt,
+                                                  const uint32_t* uni_mask, unsigned long long* st = nullptr) {
+    const uint32_t tp = (ntri + 1) / 2, sp = (nsph + 1) / 2;
+    for (uint32_t w = 0; w * 32u < tp; ++w) {
+        const uint32_t mb = uni_mask ? (w == 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)cm_t) : uni_mask[w])
+                                     : wave_or(lane_mask ? (w == 0 ? cm_t : lane_mask[w]) : 0u);
+        uint32_t m = all_a ? ~0u : mb;
+        if ((OPT & kOptStats) && st) st[0] += (unsigned long long)__builtin_popcount(w * 32u + 32u <= tp ? m : (m & ((1u << (tp - w * 32u)) - 1u)));
+        while (m) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+            const uint32_t j = w * 32u + bit;
+            m &= m - 1u;
+            if (j >= tp) break;
+            const bool in_b = (mb >> bit) & 1u;
+            const float4* q = tri + (size_t)j * kTriPairFloat4;
+            test_triangle_pair2<OPT>(q[0], q[1], q[2], q[3], q[4], ra, rb, act_a, act_b && in_b, ca, ka, ia, cb, kb, ib,
+                                     2 * j, 2 * j + 1 < ntri);
+        }
+    }
+    for (uint32_t w = 0; w * 32u < sp; ++w) {
+        const uint32_t mb = uni_mask ? (w == 0 ? (uint32_t)__builtin_amdgcn_readfirstlane((int)cm_s) : uni_mask[wt + w])
+                                     : wave_or(lane_mask ? (w == 0 ? cm_s : lane_mask[wt + w]) : 0u);
+        uint32_t m = all_a ? ~0u : mb;
+        if ((OPT & kOptStats) && st) st[1] += (unsigned long long)__builtin_popcount(w * 32u + 32u <= sp ? m : (m & ((1u << (sp - w * 32u)) - 1u)));
+        while (m) {
+            const uint32_t bit = (uint32_t)__builtin_ctz(m);
+            const uint32_t j = w * 32u + bit;
+            m &= m - 1u;
+            if (j >= sp) break;
+            const bool in_b = (mb >> bit) & 1u;
+            const float4* q = sph + (size_t)j * kSphPairFloat4;
+            test_sphere_pair2<OPT>(q[0], q[1], ra, rb, act_a, act_b && in_b, ca, ka, ia, cb, kb, ib, 2 * j,
+                                   2 * j + 1 < nsph);
+        }
+    }
+}
+
 // Order-free closest-triangle update: the brute-force loop keeps the hit with the smallest t and,
 // among equal t, the one with the largest packet index (t == closest is accepted, path_tracer.cu:
 // 257-275); a BVH visits triangles in another order, so the tie is decided by index explicitly.
@@ -1153,7 +1268,7 @@ constexpr int min_waves_per_simd() {
     // kOptSplit variants are built for 4 waves/SIMD (<= 128 VGPRs): with 5 their refill and path-end
     // bookkeeping spilled 9 VGPRs to scratch, and at the low occupancy of a multi-GPU row share a scratch
     // reload's latency is not hidden
-    return (OPT & kOptSplit) ? 4
+    return ((OPT & kOptSplit) || (OPT & kOptPipe)) ? 4
                              : ((OPT & kOptLB6) ? 6 : ((OPT & kOptLB5) ? 5 : (STREAM ? 4 : 1)));
 }
 
@@ -1188,6 +1303,8 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     constexpr bool kOverlap = (OPT & kOptOverlap) && !STREAM && !kSplit && kCull;
     // streamed scenes with p.xcd_order: the same per-XCD lists and queue words (tiles dealt to the XCDs by the
     // runtime, iqpt_debug_set_stream_xcd), without the waits
+    // kOptPipe (resident, culled, reference materials): two rays per lane and iteration
+    constexpr bool kPipe = (OPT & kOptPipe) && !STREAM && !kSplit && kCull && !(OPT & kOptMaterials) && (OPT & kOptAccTable);
     const bool kXcdQ = kOverlap || (STREAM && p.xcd_order != nullptr);
     const uint32_t xcd = kXcdQ ? (__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u) : 0u;   // HW_REG_XCC_ID
     uint32_t* const queue_word = kXcdQ ? p.queue + 16u * xcd : p.queue;
@@ -1221,6 +1338,9 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
     float3 acc = make_float3(0.0f, 0.0f, 0.0f);
     ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    // kOptPipe: the camera ray of the pixel's next sample, made from the state the current path's draws left
+    ray3 ray_b = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    bool has_b = false;
     int depth = 0;
     // scatter-record stack (path_tracer.cu:243): record k of the current path at lds_stk[k][thread]
     float* lds_stk = reinterpret_cast<float*>(lds_cm + ((OPT & kOptCull) ? kRenderBlock : 0));
@@ -1488,6 +1608,13 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                         need_cam = true;           // one camera_ray call site per iteration (loop top)
                     } else {
                         camera_ray<OPT>(p, px, py, st, ray);
+                        if (kPipe) {
+                            has_b = 1u < p.spp;
+                            if (has_b) {
+                                rng6 sb = st;
+                                camera_ray<OPT>(p, px, py, sb, ray_b);
+                            }
+                        }
                     }
                 }
                 if (go && kCull && p.cull) {
@@ -1553,516 +1680,645 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             s_ready += (unsigned long long)__popcll(__ballot(active));
         }
 
-        // ------------------------------------------------ closest hit (path_tracer.cu:253-295)
-        float closest = kTMax;
-        int kind = kHitNone;
-        uint32_t hidx = 0;
-        // kOptCull: camera rays (depth 0) test only the pairs of their tile's mask; one secondary ray
-        // in the wave makes it test everything
-        const bool cull = kCull && p.cull != nullptr && !__any(active && depth != 0);
-        const uint32_t* lane_mask =
-            (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;   // null: 0
-        // kBvhPrimary: the path state the traversals never read (RNG state, accumulator, pixel, sample
-        // count, depth: 13 words) waits in this thread's slots of the unused scene-batch region of LDS
-        // (>= 13 x kRenderBlock words, checked by the runtime), so the traversals' live ranges fit the
-        // 5-wave register budget instead of spilling to scratch. The empty asm keeps the
-        // compiler from forwarding the stores into registers across the traversal.
-        uint32_t* const park = reinterpret_cast<uint32_t*>(lds_tri) + threadIdx.x;
-        if (kBvhPrimary) {
-            park[0 * kRenderBlock] = st.v0;
-            park[1 * kRenderBlock] = st.v1;
-            park[2 * kRenderBlock] = st.v2;
-            park[3 * kRenderBlock] = st.v3;
-            park[4 * kRenderBlock] = st.v4;
-            park[5 * kRenderBlock] = st.d;
-            park[6 * kRenderBlock] = __float_as_uint(acc.x);
-            park[7 * kRenderBlock] = __float_as_uint(acc.y);
-            park[8 * kRenderBlock] = __float_as_uint(acc.z);
-            park[9 * kRenderBlock] = px;
-            park[10 * kRenderBlock] = py;
-            park[11 * kRenderBlock] = done;
-            park[12 * kRenderBlock] = (uint32_t)depth;
-            asm volatile("" ::: "memory");
-        }
-        if (kBvhPrimary) {
-            // Triangles through the exact BVH, spheres through the exact sphere BVH (each falls back to
-            // the brute-force fold from global memory where its BVH is absent or the ray is outside
-            // the bounds' assumptions, bvh_ray_ok). With a sphere BVH the spheres go first and bound the
-            // triangle traversal (closest_spheres_first); otherwise triangles first, as in
-            // path_tracer.cu:257-295. Both give the reference's result.
-            if (active && sbvh_first_ok(p, ray)) {
-                if (OPT & kOptStats) {
-                    ++c_sph_rays;
-                    if (p.bvh_nodes != nullptr && bvh_ray_ok(p, ray)) ++c_tri_rays;
+        bool finished = false;             // kOptOverlap: the lane stored its pixel this iteration
+        if constexpr (kPipe) {
+            // ---- kOptPipe: the lane's path ray (a = `ray`) and the camera ray of its pixel's next
+            // sample (b = `ray_b`, made from the state the path's draws have left) are traced together. Sample k + 1
+            // starts where sample k's draws end (path_tracer.cu:338-339), so b is that sample's camera ray exactly
+            // when ray a ends the path without drawing again (an emissive triangle or the sky, path_tracer.cu:278,
+            // 307-316); then sample k + 1's first query is already done and the lane shades it in the same
+            // iteration. A scatter (material.cu:10 draws two numbers) makes b stale: it is dropped, not counted,
+            // and made again. Each ray's closest hit is the reference's (its own pairs in index order).
+            float cb = kTMax;
+            int kb = kHitNone;
+            uint32_t ib = 0;
+            float closest = kTMax;
+            int kind = kHitNone;
+            uint32_t hidx = 0;
+            {
+                uint4 cm = lds_cm[threadIdx.x];
+                const uint64_t act = __ballot(active);
+                const uint32_t first = act ? (uint32_t)__builtin_ctzll(act) : 0u;
+                const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
+                const bool uni = __ballot(active && cm.z != t0) == 0ull;
+                if (uni) {
+                    cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
+                    cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
                 }
-                closest_spheres_first<OPT>(p, ray, p.bvh_nodes != nullptr && bvh_ray_ok(p, ray), closest, kind, hidx,
-                                           (OPT & kOptStats) ? c_tri : nullptr, (OPT & kOptStats) ? c_sph : nullptr);
-            } else if (active) {
-                const bool ok = bvh_ray_ok(p, ray);
-                if (ok && p.bvh_nodes != nullptr) {
+                const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
+                const uint32_t* lane_mask = active ? p.cull + (size_t)cm.z * p.cull_stride : nullptr;
+                const bool all_a = __any(active && depth != 0);
+                intersect_culled2<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, all_a, active,
+                                       active && has_b, ray, ray_b, closest, kind, hidx, cb, kb, ib, p.cull_wt, uni_mask,
+                                       (OPT & kOptStats) ? s_tests : nullptr);
+                if (OPT & kOptStats) s_full += all_a ? 1ull : 0ull;
+            }
+            wave_rays += (uint64_t)__popcll(__ballot(active));
+            // at most two shading rounds: ray a's hit, then (ray a ended the path) ray b's
+            bool pend = active, need_a = false;
+#pragma unroll
+            for (int r = 0; r < 2; ++r) {
+                bool term = false;
+                uint32_t md_end = 0;
+                float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
+                if (pend) {
+                    if (kind == kHitSphere) {
+                        if (OPT & kOptStats) ++s_scatter_lanes;
+                        const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) +
+                                         (hidx & 1u);
+                        const float s = oren_nayar_scatter<OPT>(make_float4(q[0], q[2], q[4], q[6]), closest, ray, st);
+                        if (depth + 1 >= p.max_depth) {
+                            term = true;             // the last record is this scatter (biased, :252)
+                            md_end = 1;
+                            Lx = s;
+                            Ly = s;
+                            Lz = s;
+                        } else {
+                            lds_stk[(uint32_t)depth * kRenderBlock + threadIdx.x] = s;
+                            ++depth;
+                        }
+                    } else if (kind == kHitTri) {
+                        term = true;                 // emissive(1, 10): att 10, cos = pdf = 1
+                        Lx = 10.0f;
+                        Ly = 10.0f;
+                        Lz = 10.0f;
+                    } else {
+                        term = true;                 // sky gradient, :308-313
+                        const float a = (ray.dy + 1.0f) * 0.5f;
+                        const float one_a = 1.0f - a;
+                        Lx = one_a + a * 0.5f;
+                        Ly = one_a + a * 0.7f;
+                        Lz = one_a + a * 1.0f;
+                    }
+                }
+                if (OPT & kOptStats) {
+                    if (__ballot(pend && kind == kHitSphere)) ++s_scatter_exec;
+                    const uint64_t tm = __ballot(term);
+                    if (tm) {
+                        ++s_term_exec;
+                        s_term_lanes += (unsigned long long)__popcll(tm);
+                    }
+                }
+                bool next = false;
+                if (term) {
+                    // backward product (:321-324), clamp (:345-347), path_color = 0 + color, running mean (:356-358)
+                    float cx = Lx, cy = Ly, cz = Lz;
+                    for (int i = depth - 1; i >= 0; --i) {
+                        const float f = lds_stk[(uint32_t)i * kRenderBlock + threadIdx.x];
+                        cx = cx * f;
+                        cy = cy * f;
+                        cz = cz * f;
+                    }
+                    cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                    cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                    cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                    const float2 tv = lds_tab[done];
+                    float qx, qy, qz;
+                    mean_terms<OPT>(0.0f + cx, 0.0f + cy, 0.0f + cz, lds_tab_n[done], tv.x, p.mean_tiny, qx, qy, qz);
+                    acc.x = qx + acc.x * tv.y;
+                    acc.y = qy + acc.y * tv.y;
+                    acc.z = qz + acc.z * tv.y;
+                    ++done;
+                    depth = 0;
+                    if (done == p.spp) {
+                        store_pixel();
+                        if (kOverlap) finished = true;
+                        active = false;
+                    } else if (r == 0 && md_end == 0u && has_b) {
+                        // the path ended without drawing: ray b is the next sample's camera ray, its query done
+                        (void)xorwow_next(st);
+                        (void)xorwow_next(st);
+                        ray = ray_b;
+                        closest = cb;
+                        kind = kb;
+                        hidx = ib;
+                        next = true;
+                    } else {
+                        need_a = true;
+                    }
+                }
+                if (r == 0) wave_rays += (uint64_t)__popcll(__ballot(next));
+                pend = next;
+            }
+            // the next iteration's rays: a new path's camera ray where a path ended without taking ray b, and the
+            // camera ray of the sample after the current one (ray b is stale after any scatter or path end)
+            if (need_a && active) camera_ray<OPT>(p, px, py, st, ray);
+            has_b = active && done + 1u < p.spp;
+            if (has_b) {
+                rng6 sb = st;
+                camera_ray<OPT>(p, px, py, sb, ray_b);
+            }
+        } else {
+            // ------------------------------------------------ closest hit (path_tracer.cu:253-295)
+            float closest = kTMax;
+            int kind = kHitNone;
+            uint32_t hidx = 0;
+            // kOptCull: camera rays (depth 0) test only the pairs of their tile's mask; one secondary ray
+            // in the wave makes it test everything
+            const bool cull = kCull && p.cull != nullptr && !__any(active && depth != 0);
+            const uint32_t* lane_mask =
+                (cull && active) ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;   // null: 0
+            // kBvhPrimary: the path state the traversals never read (RNG state, accumulator, pixel, sample
+            // count, depth: 13 words) waits in this thread's slots of the unused scene-batch region of LDS
+            // (>= 13 x kRenderBlock words, checked by the runtime), so the traversals' live ranges fit the
+            // 5-wave register budget instead of spilling to scratch. The empty asm keeps the
+            // compiler from forwarding the stores into registers across the traversal.
+            uint32_t* const park = reinterpret_cast<uint32_t*>(lds_tri) + threadIdx.x;
+            if (kBvhPrimary) {
+                park[0 * kRenderBlock] = st.v0;
+                park[1 * kRenderBlock] = st.v1;
+                park[2 * kRenderBlock] = st.v2;
+                park[3 * kRenderBlock] = st.v3;
+                park[4 * kRenderBlock] = st.v4;
+                park[5 * kRenderBlock] = st.d;
+                park[6 * kRenderBlock] = __float_as_uint(acc.x);
+                park[7 * kRenderBlock] = __float_as_uint(acc.y);
+                park[8 * kRenderBlock] = __float_as_uint(acc.z);
+                park[9 * kRenderBlock] = px;
+                park[10 * kRenderBlock] = py;
+                park[11 * kRenderBlock] = done;
+                park[12 * kRenderBlock] = (uint32_t)depth;
+                asm volatile("" ::: "memory");
+            }
+            if (kBvhPrimary) {
+                // Triangles through the exact BVH, spheres through the exact sphere BVH (each falls back to
+                // the brute-force fold from global memory where its BVH is absent or the ray is outside
+                // the bounds' assumptions, bvh_ray_ok). With a sphere BVH the spheres go first and bound the
+                // triangle traversal (closest_spheres_first); otherwise triangles first, as in
+                // path_tracer.cu:257-295. Both give the reference's result.
+                if (active && sbvh_first_ok(p, ray)) {
+                    if (OPT & kOptStats) {
+                        ++c_sph_rays;
+                        if (p.bvh_nodes != nullptr && bvh_ray_ok(p, ray)) ++c_tri_rays;
+                    }
+                    closest_spheres_first<OPT>(p, ray, p.bvh_nodes != nullptr && bvh_ray_ok(p, ray), closest, kind, hidx,
+                                               (OPT & kOptStats) ? c_tri : nullptr, (OPT & kOptStats) ? c_sph : nullptr);
+                } else if (active) {
+                    const bool ok = bvh_ray_ok(p, ray);
+                    if (ok && p.bvh_nodes != nullptr) {
+                        if (OPT & kOptStats) ++c_tri_rays;
+                        bvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_tri : nullptr);
+                    } else {
+                        const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
+                        for (uint32_t j = 0; j < p.ntri_pairs; ++j) {
+                            const float4* q = gp + (size_t)j * kTriPairFloat4;
+                            test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
+                                                    2 * j + 1 < p.ntri);
+                        }
+                    }
+                    if (ok && p.sbvh_nodes != nullptr) {
+                        if (OPT & kOptStats) ++c_sph_rays;
+                        sbvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_sph : nullptr);
+                    } else {
+                        const float4* __restrict__ gs = reinterpret_cast<const float4*>(p.sph_pairs);
+                        for (uint32_t j = 0; j < p.nsph_pairs; ++j) {
+                            const float4* q = gs + (size_t)j * kSphPairFloat4;
+                            test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, 2 * j, 2 * j + 1 < p.nsph);
+                        }
+                    }
+                }
+            } else if (STREAM) {
+                // Streamed scene. Per lane and mask word: a camera ray contributes its tile's mask (kOptCull),
+                // a secondary ray that takes the BVH (kOptBvh) contributes nothing to the triangle batches,
+                // any other ray every pair; the wave ORs the words, the block skips a batch nobody needs.
+                constexpr bool kWords = kCull || kBvh;
+                const bool bvh_ray = kBvh && active && (depth != 0 || kBvhPrimary) &&
+                                     (p.bvh_nodes != nullptr || p.sbvh_nodes != nullptr) && bvh_ray_ok(p, ray);
+                const bool bvh_lane = bvh_ray && p.bvh_nodes != nullptr;
+                const uint32_t* tile_mask =
+                    (kCull && p.cull != nullptr && active && depth == 0)
+                        ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
+                const uint32_t* tri_mask = bvh_lane ? nullptr : tile_mask;
+                const bool tri_all = active && tile_mask == nullptr && !bvh_lane;
+                // the spheres through the sphere BVH (same rays as the triangle BVH) instead of the batches
+                const bool sbvh_lane = bvh_ray && p.sbvh_nodes != nullptr;
+                const bool sph_all = active && tile_mask == nullptr && !sbvh_lane;
+                const uint32_t* sph_mask = sbvh_lane ? nullptr : tile_mask;
+                // One tile for every lane that contributes mask words (and no lane that needs every pair): the
+                // wave's OR is that tile's mask, read with uniform loads instead of a DPP OR per word
+                // (camera-ray waves, the usual case); no contributing lane at all: every word is 0.
+                const uint32_t* uni_tri = nullptr;
+                const uint32_t* uni_sph = nullptr;
+                bool tri_none = false, sph_none = false;
+                uint32_t tt = 0, ts = 0;                      // the uniform tiles
+                if (kCull && p.cull != nullptr) {
+                    const uint32_t tile = lds_cm[threadIdx.x].z;
+                    const uint64_t mt = __ballot(tri_mask != nullptr), ms = __ballot(sph_mask != nullptr);
+                    if (__ballot(tri_all) == 0ull) {
+                        if (mt == 0ull) {
+                            tri_none = true;
+                        } else {
+                            tt = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(mt));
+                            if (__ballot(tri_mask != nullptr && tile != tt) == 0ull) uni_tri = p.cull + (size_t)tt * p.cull_stride;
+                        }
+                    }
+                    if (__ballot(sph_all) == 0ull) {
+                        if (ms == 0ull) {
+                            sph_none = true;
+                        } else {
+                            ts = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(ms));
+                            if (__ballot(sph_mask != nullptr && tile != ts) == 0ull) uni_sph = p.cull + (size_t)ts * p.cull_stride;
+                        }
+                    }
+                }
+                // A uniform-tile wave takes its tile's candidate pairs from the candidate list (ascending
+                // pair indices: the order of the masked batch loop, so the same closest hit), reading each
+                // pair straight from global memory with wave-uniform loads, and needs none of the batches.
+                const bool list_tri = uni_tri != nullptr && p.list != nullptr;
+                const bool list_sph = uni_sph != nullptr && p.list != nullptr;
+                if (list_tri) {
+                    const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
+                    const uint32_t a = p.list_off_tri[tt], b = p.list_off_tri[tt + 1];
+                    // software-pipelined: the next pair's records are loaded while this one is tested (C4 -1.7 %)
+                    uint32_t j = a < b ? (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[a]) : 0u;
+                    float4 q0, q1, q2, q3, q4;
+                    if (a < b) {
+                        const float4* q = gp + (size_t)j * kTriPairFloat4;
+                        q0 = q[0]; q1 = q[1]; q2 = q[2]; q3 = q[3]; q4 = q[4];
+                    }
+                    for (uint32_t e = a; e < b; ++e) {
+                        const uint32_t jn = e + 1 < b ? (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[e + 1]) : j;
+                        const float4* qn = gp + (size_t)jn * kTriPairFloat4;
+                        const float4 n0 = qn[0], n1 = qn[1], n2 = qn[2], n3 = qn[3], n4 = qn[4];
+                        if (tri_mask != nullptr)
+                            test_triangle_pair<OPT>(q0, q1, q2, q3, q4, ray, closest, kind, hidx, 2 * j,
+                                                    2 * j + 1 < p.ntri);
+                        // any-hit scenes: the wave leaves once every list lane has an accepted triangle
+                        if ((OPT & kOptAnyHit) && p.anyhit && __ballot(tri_mask != nullptr && kind != kHitTri) == 0ull) break;
+                        j = jn;
+                        q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4;
+                    }
+                    tri_none = true;                          // nothing left for the batches from this wave
+                }
+                // the whole block skips the triangle batches when every ray takes the BVH or a list
+                const bool tri_block =
+                    !kWords || __syncthreads_or((tri_all || (tri_mask != nullptr && !list_tri)) ? 1 : 0);
+                for (uint32_t base = 0; tri_block && base < tri_recs; base += p.tri_batch) {
+                    const uint32_t n = min(p.tri_batch, tri_recs - base);
+                    uint32_t wm[kWords ? 8 : 1];
+                    bool any = true;
+                    if (kWords) {
+                        // the batch's mask words (a batch is at most 256 pairs, a multiple of 32: <= 8 aligned words)
+                        any = false;
+    #pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const uint32_t w = base / 32u + (uint32_t)i;
+                            wm[i] = 0u;
+                            if ((uint32_t)i * 32u < n)
+                                wm[i] = tri_none ? 0u
+                                                 : (uni_tri ? uni_tri[w]
+                                                            : wave_or(tri_all ? ~0u : (tri_mask ? tri_mask[w] : 0u)));
+                            any = any || wm[i] != 0u;
+                        }
+                        // the barrier also orders this batch's LDS writes after the previous batch's reads
+                        if (!__syncthreads_or(any ? 1 : 0)) continue;
+                    } else {
+                        __syncthreads();
+                    }
+                    for (uint32_t i = threadIdx.x; i < n * kTriRec; i += kRenderBlock)
+                        lds_tri[i] = g_tri[(size_t)base * kTriRec + i];
+                    __syncthreads();
+                    if (active && !bvh_lane && !list_tri) {
+                        const uint32_t first = base * kTriPer;
+                        const uint32_t cnt = min(n * kTriPer, p.ntri - first);
+                        if (kWords) {
+    #pragma unroll
+                            for (int i = 0; i < 8; ++i) {
+                                uint32_t m = wm[i];
+                                while (m) {
+                                    const uint32_t j = (uint32_t)i * 32u + (uint32_t)__builtin_ctz(m);   // local pair
+                                    m &= m - 1u;
+                                    if (j >= n) break;
+                                    const float4* q = lds_tri + (size_t)j * kTriPairFloat4;
+                                    test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx,
+                                                            first + 2 * j, 2 * j + 1 < cnt);
+                                }
+                            }
+                        } else {
+                            intersect_range<OPT>(lds_tri, first, cnt, lds_sph, 0, 0, ray, closest, kind, hidx);
+                        }
+                    }
+                }
+                // secondary rays: triangles through the exact BVH (iq_bvh.hpp), before the spheres
+                if (bvh_lane) {
                     if (OPT & kOptStats) ++c_tri_rays;
                     bvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_tri : nullptr);
-                } else {
-                    const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
-                    for (uint32_t j = 0; j < p.ntri_pairs; ++j) {
-                        const float4* q = gp + (size_t)j * kTriPairFloat4;
-                        test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
-                                                2 * j + 1 < p.ntri);
+                }
+                if (list_sph) {
+                    const float4* __restrict__ gs = reinterpret_cast<const float4*>(p.sph_pairs);
+                    const uint32_t a = p.list_off_sph[ts], b = p.list_off_sph[ts + 1];
+                    for (uint32_t e = a; e < b; ++e) {
+                        const uint32_t j = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[e]);
+                        if (sph_mask != nullptr) {
+                            const float4* q = gs + (size_t)j * kSphPairFloat4;
+                            test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, 2 * j, 2 * j + 1 < p.nsph);
+                        }
+                    }
+                    sph_none = true;
+                }
+                for (uint32_t base = 0; base < sph_recs; base += p.sph_batch) {
+                    const uint32_t n = min(p.sph_batch, sph_recs - base);
+                    uint32_t wm[kWords ? 8 : 1];
+                    bool any = true;
+                    if (kWords) {
+                        any = false;
+    #pragma unroll
+                        for (int i = 0; i < 8; ++i) {
+                            const uint32_t w = p.cull_wt + base / 32u + (uint32_t)i;
+                            wm[i] = 0u;
+                            if ((uint32_t)i * 32u < n)
+                                wm[i] = sph_none ? 0u
+                                                 : (uni_sph ? uni_sph[w]
+                                                            : wave_or(sph_all ? ~0u : (sph_mask ? sph_mask[w] : 0u)));
+                            any = any || wm[i] != 0u;
+                        }
+                        if (!__syncthreads_or(any ? 1 : 0)) continue;
+                    } else {
+                        __syncthreads();
+                    }
+                    for (uint32_t i = threadIdx.x; i < n * kSphRec; i += kRenderBlock)
+                        lds_sph[i] = g_sph[(size_t)base * kSphRec + i];
+                    __syncthreads();
+                    if (active && !sbvh_lane && !list_sph) {
+                        const uint32_t first = base * kSphPer;
+                        const uint32_t cnt = min(n * kSphPer, p.nsph - first);
+                        if (kWords) {
+    #pragma unroll
+                            for (int i = 0; i < 8; ++i) {
+                                uint32_t m = wm[i];
+                                while (m) {
+                                    const uint32_t j = (uint32_t)i * 32u + (uint32_t)__builtin_ctz(m);
+                                    m &= m - 1u;
+                                    if (j >= n) break;
+                                    const float4* q = lds_sph + (size_t)j * kSphPairFloat4;
+                                    test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, first + 2 * j,
+                                                          2 * j + 1 < cnt);
+                                }
+                            }
+                        } else {
+                            intersect_range<OPT>(lds_tri, 0, 0, lds_sph, first, cnt, ray, closest, kind, hidx);
+                        }
                     }
                 }
-                if (ok && p.sbvh_nodes != nullptr) {
+                if (sbvh_lane) {
                     if (OPT & kOptStats) ++c_sph_rays;
                     sbvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_sph : nullptr);
-                } else {
-                    const float4* __restrict__ gs = reinterpret_cast<const float4*>(p.sph_pairs);
-                    for (uint32_t j = 0; j < p.nsph_pairs; ++j) {
-                        const float4* q = gs + (size_t)j * kSphPairFloat4;
-                        test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, 2 * j, 2 * j + 1 < p.nsph);
-                    }
                 }
+            } else if (kCull && p.cull != nullptr) {
+                uint4 cm = lds_cm[threadIdx.x];
+                // one tile for every active lane (the usual case: a tile's lanes start together and, on
+                // tiles whose camera rays all end on their first hit, finish together): its own mask
+                const uint64_t act = __ballot(active);
+                const uint32_t first = act ? (uint32_t)__builtin_ctzll(act) : 0u;
+                const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
+                const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
+                if (uni) {
+                    // word 0 is read from the first lane: give every lane the first active lane's words
+                    cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
+                    cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
+                }
+                const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
+                intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray,
+                                      closest, kind, hidx, p.cull_wt, uni_mask, (OPT & kOptStats) ? s_tests : nullptr);
+                if (OPT & kOptStats) s_full += cull ? 0ull : 1ull;
+            } else if (active) {
+                intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
             }
-        } else if (STREAM) {
-            // Streamed scene. Per lane and mask word: a camera ray contributes its tile's mask (kOptCull),
-            // a secondary ray that takes the BVH (kOptBvh) contributes nothing to the triangle batches,
-            // any other ray every pair; the wave ORs the words, the block skips a batch nobody needs.
-            constexpr bool kWords = kCull || kBvh;
-            const bool bvh_ray = kBvh && active && (depth != 0 || kBvhPrimary) &&
-                                 (p.bvh_nodes != nullptr || p.sbvh_nodes != nullptr) && bvh_ray_ok(p, ray);
-            const bool bvh_lane = bvh_ray && p.bvh_nodes != nullptr;
-            const uint32_t* tile_mask =
-                (kCull && p.cull != nullptr && active && depth == 0)
-                    ? p.cull + (size_t)lds_cm[threadIdx.x].z * p.cull_stride : nullptr;
-            const uint32_t* tri_mask = bvh_lane ? nullptr : tile_mask;
-            const bool tri_all = active && tile_mask == nullptr && !bvh_lane;
-            // the spheres through the sphere BVH (same rays as the triangle BVH) instead of the batches
-            const bool sbvh_lane = bvh_ray && p.sbvh_nodes != nullptr;
-            const bool sph_all = active && tile_mask == nullptr && !sbvh_lane;
-            const uint32_t* sph_mask = sbvh_lane ? nullptr : tile_mask;
-            // One tile for every lane that contributes mask words (and no lane that needs every pair): the
-            // wave's OR is that tile's mask, read with uniform loads instead of a DPP OR per word
-            // (camera-ray waves, the usual case); no contributing lane at all: every word is 0.
-            const uint32_t* uni_tri = nullptr;
-            const uint32_t* uni_sph = nullptr;
-            bool tri_none = false, sph_none = false;
-            uint32_t tt = 0, ts = 0;                      // the uniform tiles
-            if (kCull && p.cull != nullptr) {
-                const uint32_t tile = lds_cm[threadIdx.x].z;
-                const uint64_t mt = __ballot(tri_mask != nullptr), ms = __ballot(sph_mask != nullptr);
-                if (__ballot(tri_all) == 0ull) {
-                    if (mt == 0ull) {
-                        tri_none = true;
-                    } else {
-                        tt = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(mt));
-                        if (__ballot(tri_mask != nullptr && tile != tt) == 0ull) uni_tri = p.cull + (size_t)tt * p.cull_stride;
-                    }
-                }
-                if (__ballot(sph_all) == 0ull) {
-                    if (ms == 0ull) {
-                        sph_none = true;
-                    } else {
-                        ts = (uint32_t)__builtin_amdgcn_readlane((int)tile, (int)__builtin_ctzll(ms));
-                        if (__ballot(sph_mask != nullptr && tile != ts) == 0ull) uni_sph = p.cull + (size_t)ts * p.cull_stride;
-                    }
-                }
+            if (kBvhPrimary) {
+                asm volatile("" ::: "memory");
+                st.v0 = park[0 * kRenderBlock];
+                st.v1 = park[1 * kRenderBlock];
+                st.v2 = park[2 * kRenderBlock];
+                st.v3 = park[3 * kRenderBlock];
+                st.v4 = park[4 * kRenderBlock];
+                st.d = park[5 * kRenderBlock];
+                acc.x = __uint_as_float(park[6 * kRenderBlock]);
+                acc.y = __uint_as_float(park[7 * kRenderBlock]);
+                acc.z = __uint_as_float(park[8 * kRenderBlock]);
+                px = park[9 * kRenderBlock];
+                py = park[10 * kRenderBlock];
+                done = park[11 * kRenderBlock];
+                depth = (int)park[12 * kRenderBlock];
             }
-            // A uniform-tile wave takes its tile's candidate pairs from the candidate list (ascending
-            // pair indices: the order of the masked batch loop, so the same closest hit), reading each
-            // pair straight from global memory with wave-uniform loads, and needs none of the batches.
-            const bool list_tri = uni_tri != nullptr && p.list != nullptr;
-            const bool list_sph = uni_sph != nullptr && p.list != nullptr;
-            if (list_tri) {
-                const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
-                const uint32_t a = p.list_off_tri[tt], b = p.list_off_tri[tt + 1];
-                // software-pipelined: the next pair's records are loaded while this one is tested (C4 -1.7 %)
-                uint32_t j = a < b ? (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[a]) : 0u;
-                float4 q0, q1, q2, q3, q4;
-                if (a < b) {
-                    const float4* q = gp + (size_t)j * kTriPairFloat4;
-                    q0 = q[0]; q1 = q[1]; q2 = q[2]; q3 = q[3]; q4 = q[4];
-                }
-                for (uint32_t e = a; e < b; ++e) {
-                    const uint32_t jn = e + 1 < b ? (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[e + 1]) : j;
-                    const float4* qn = gp + (size_t)jn * kTriPairFloat4;
-                    const float4 n0 = qn[0], n1 = qn[1], n2 = qn[2], n3 = qn[3], n4 = qn[4];
-                    if (tri_mask != nullptr)
-                        test_triangle_pair<OPT>(q0, q1, q2, q3, q4, ray, closest, kind, hidx, 2 * j,
-                                                2 * j + 1 < p.ntri);
-                    // any-hit scenes: the wave leaves once every list lane has an accepted triangle
-                    if ((OPT & kOptAnyHit) && p.anyhit && __ballot(tri_mask != nullptr && kind != kHitTri) == 0ull) break;
-                    j = jn;
-                    q0 = n0; q1 = n1; q2 = n2; q3 = n3; q4 = n4;
-                }
-                tri_none = true;                          // nothing left for the batches from this wave
-            }
-            // the whole block skips the triangle batches when every ray takes the BVH or a list
-            const bool tri_block =
-                !kWords || __syncthreads_or((tri_all || (tri_mask != nullptr && !list_tri)) ? 1 : 0);
-            for (uint32_t base = 0; tri_block && base < tri_recs; base += p.tri_batch) {
-                const uint32_t n = min(p.tri_batch, tri_recs - base);
-                uint32_t wm[kWords ? 8 : 1];
-                bool any = true;
-                if (kWords) {
-                    // the batch's mask words (a batch is at most 256 pairs, a multiple of 32: <= 8 aligned words)
-                    any = false;
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const uint32_t w = base / 32u + (uint32_t)i;
-                        wm[i] = 0u;
-                        if ((uint32_t)i * 32u < n)
-                            wm[i] = tri_none ? 0u
-                                             : (uni_tri ? uni_tri[w]
-                                                        : wave_or(tri_all ? ~0u : (tri_mask ? tri_mask[w] : 0u)));
-                        any = any || wm[i] != 0u;
-                    }
-                    // the barrier also orders this batch's LDS writes after the previous batch's reads
-                    if (!__syncthreads_or(any ? 1 : 0)) continue;
-                } else {
-                    __syncthreads();
-                }
-                for (uint32_t i = threadIdx.x; i < n * kTriRec; i += kRenderBlock)
-                    lds_tri[i] = g_tri[(size_t)base * kTriRec + i];
-                __syncthreads();
-                if (active && !bvh_lane && !list_tri) {
-                    const uint32_t first = base * kTriPer;
-                    const uint32_t cnt = min(n * kTriPer, p.ntri - first);
-                    if (kWords) {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) {
-                            uint32_t m = wm[i];
-                            while (m) {
-                                const uint32_t j = (uint32_t)i * 32u + (uint32_t)__builtin_ctz(m);   // local pair
-                                m &= m - 1u;
-                                if (j >= n) break;
-                                const float4* q = lds_tri + (size_t)j * kTriPairFloat4;
-                                test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx,
-                                                        first + 2 * j, 2 * j + 1 < cnt);
-                            }
-                        }
-                    } else {
-                        intersect_range<OPT>(lds_tri, first, cnt, lds_sph, 0, 0, ray, closest, kind, hidx);
-                    }
-                }
-            }
-            // secondary rays: triangles through the exact BVH (iq_bvh.hpp), before the spheres
-            if (bvh_lane) {
-                if (OPT & kOptStats) ++c_tri_rays;
-                bvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_tri : nullptr);
-            }
-            if (list_sph) {
-                const float4* __restrict__ gs = reinterpret_cast<const float4*>(p.sph_pairs);
-                const uint32_t a = p.list_off_sph[ts], b = p.list_off_sph[ts + 1];
-                for (uint32_t e = a; e < b; ++e) {
-                    const uint32_t j = (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[e]);
-                    if (sph_mask != nullptr) {
-                        const float4* q = gs + (size_t)j * kSphPairFloat4;
-                        test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, 2 * j, 2 * j + 1 < p.nsph);
-                    }
-                }
-                sph_none = true;
-            }
-            for (uint32_t base = 0; base < sph_recs; base += p.sph_batch) {
-                const uint32_t n = min(p.sph_batch, sph_recs - base);
-                uint32_t wm[kWords ? 8 : 1];
-                bool any = true;
-                if (kWords) {
-                    any = false;
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const uint32_t w = p.cull_wt + base / 32u + (uint32_t)i;
-                        wm[i] = 0u;
-                        if ((uint32_t)i * 32u < n)
-                            wm[i] = sph_none ? 0u
-                                             : (uni_sph ? uni_sph[w]
-                                                        : wave_or(sph_all ? ~0u : (sph_mask ? sph_mask[w] : 0u)));
-                        any = any || wm[i] != 0u;
-                    }
-                    if (!__syncthreads_or(any ? 1 : 0)) continue;
-                } else {
-                    __syncthreads();
-                }
-                for (uint32_t i = threadIdx.x; i < n * kSphRec; i += kRenderBlock)
-                    lds_sph[i] = g_sph[(size_t)base * kSphRec + i];
-                __syncthreads();
-                if (active && !sbvh_lane && !list_sph) {
-                    const uint32_t first = base * kSphPer;
-                    const uint32_t cnt = min(n * kSphPer, p.nsph - first);
-                    if (kWords) {
-#pragma unroll
-                        for (int i = 0; i < 8; ++i) {
-                            uint32_t m = wm[i];
-                            while (m) {
-                                const uint32_t j = (uint32_t)i * 32u + (uint32_t)__builtin_ctz(m);
-                                m &= m - 1u;
-                                if (j >= n) break;
-                                const float4* q = lds_sph + (size_t)j * kSphPairFloat4;
-                                test_sphere_pair<OPT>(q[0], q[1], ray, closest, kind, hidx, first + 2 * j,
-                                                      2 * j + 1 < cnt);
-                            }
-                        }
-                    } else {
-                        intersect_range<OPT>(lds_tri, 0, 0, lds_sph, first, cnt, ray, closest, kind, hidx);
-                    }
-                }
-            }
-            if (sbvh_lane) {
-                if (OPT & kOptStats) ++c_sph_rays;
-                sbvh_closest<OPT>(p, ray, closest, kind, hidx, (OPT & kOptStats) ? c_sph : nullptr);
-            }
-        } else if (kCull && p.cull != nullptr) {
-            uint4 cm = lds_cm[threadIdx.x];
-            // one tile for every active lane (the usual case: a tile's lanes start together and, on
-            // tiles whose camera rays all end on their first hit, finish together): its own mask
-            const uint64_t act = __ballot(active);
-            const uint32_t first = act ? (uint32_t)__builtin_ctzll(act) : 0u;
-            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
-            const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
-            if (uni) {
-                // word 0 is read from the first lane: give every lane the first active lane's words
-                cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
-                cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
-            }
-            const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
-            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray,
-                                  closest, kind, hidx, p.cull_wt, uni_mask, (OPT & kOptStats) ? s_tests : nullptr);
-            if (OPT & kOptStats) s_full += cull ? 0ull : 1ull;
-        } else if (active) {
-            intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
-        }
-        if (kBvhPrimary) {
-            asm volatile("" ::: "memory");
-            st.v0 = park[0 * kRenderBlock];
-            st.v1 = park[1 * kRenderBlock];
-            st.v2 = park[2 * kRenderBlock];
-            st.v3 = park[3 * kRenderBlock];
-            st.v4 = park[4 * kRenderBlock];
-            st.d = park[5 * kRenderBlock];
-            acc.x = __uint_as_float(park[6 * kRenderBlock]);
-            acc.y = __uint_as_float(park[7 * kRenderBlock]);
-            acc.z = __uint_as_float(park[8 * kRenderBlock]);
-            px = park[9 * kRenderBlock];
-            py = park[10 * kRenderBlock];
-            done = park[11 * kRenderBlock];
-            depth = (int)park[12 * kRenderBlock];
-        }
 
-        // ------------------------------------------------ shade (path_tracer.cu:297-316)
-        bool term = false;
-        bool finished = false;             // kOptOverlap: the lane stored its pixel this iteration
-        uint32_t md_end = 0;               // the path ended on a scatter at max_depth (kOptSplit slot count)
-        float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
-        // speculative lanes' rays are counted by the stitch, for the slots on the chain only
-        wave_rays += (uint64_t)__popcll(__ballot(active) & ~spec_mask);
-        // kOptSplit: a speculative lane's first scatter keeps its base state (the RNG state of its next
-        // slot: the camera took exactly the slot's two draws) for the restore at the path's end
-        auto save_base = [&]() {
-            if (kSplit && depth == 0 && ((spec_mask >> lane) & 1ull)) {
-                lds_base[threadIdx.x] = st.v0;
-                lds_base[kRenderBlock + threadIdx.x] = st.v1;
-                lds_base[2 * kRenderBlock + threadIdx.x] = st.v2;
-                lds_base[3 * kRenderBlock + threadIdx.x] = st.v3;
-                lds_base[4 * kRenderBlock + threadIdx.x] = st.v4;
-                lds_base[5 * kRenderBlock + threadIdx.x] = st.d;
-            }
-        };
-        if (active && (OPT & kOptMaterials)) {
-            // ---- material table (§8f.3): the hit primitive's material decides the scatter
-            if (kind != kHitNone) {
-                const uint32_t mi = kind == kHitTri ? p.tri_mat[hidx] : p.sph_mat[hidx];
-                const float4_storage m0 = p.mats[2 * mi], m1 = p.mats[2 * mi + 1];
-                if (__float_as_uint(m0.w) == IQPT_MAT_EMISSIVE) {
-                    term = true;                 // emissive::scatter: strength * albedo, cos = pdf = 1
-                    Lx = m1.x * m0.x;
-                    Ly = m1.x * m0.y;
-                    Lz = m1.x * m0.z;
-                } else {
-                    float hx, hy, hz, nx, ny, nz;
-                    if (kind == kHitSphere) {
-                        float4 sphr;
-                        if (!STREAM && kPair) {
-                            const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) *
-                                                                                          kSphPairFloat4) +
-                                             (hidx & 1u);
-                            sphr = make_float4(q[0], q[2], q[4], q[6]);
+            // ------------------------------------------------ shade (path_tracer.cu:297-316)
+            bool term = false;
+            uint32_t md_end = 0;               // the path ended on a scatter at max_depth (kOptSplit slot count)
+            float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
+            // speculative lanes' rays are counted by the stitch, for the slots on the chain only
+            wave_rays += (uint64_t)__popcll(__ballot(active) & ~spec_mask);
+            // kOptSplit: a speculative lane's first scatter keeps its base state (the RNG state of its next
+            // slot: the camera took exactly the slot's two draws) for the restore at the path's end
+            auto save_base = [&]() {
+                if (kSplit && depth == 0 && ((spec_mask >> lane) & 1ull)) {
+                    lds_base[threadIdx.x] = st.v0;
+                    lds_base[kRenderBlock + threadIdx.x] = st.v1;
+                    lds_base[2 * kRenderBlock + threadIdx.x] = st.v2;
+                    lds_base[3 * kRenderBlock + threadIdx.x] = st.v3;
+                    lds_base[4 * kRenderBlock + threadIdx.x] = st.v4;
+                    lds_base[5 * kRenderBlock + threadIdx.x] = st.d;
+                }
+            };
+            if (active && (OPT & kOptMaterials)) {
+                // ---- material table (§8f.3): the hit primitive's material decides the scatter
+                if (kind != kHitNone) {
+                    const uint32_t mi = kind == kHitTri ? p.tri_mat[hidx] : p.sph_mat[hidx];
+                    const float4_storage m0 = p.mats[2 * mi], m1 = p.mats[2 * mi + 1];
+                    if (__float_as_uint(m0.w) == IQPT_MAT_EMISSIVE) {
+                        term = true;                 // emissive::scatter: strength * albedo, cos = pdf = 1
+                        Lx = m1.x * m0.x;
+                        Ly = m1.x * m0.y;
+                        Lz = m1.x * m0.z;
+                    } else {
+                        float hx, hy, hz, nx, ny, nz;
+                        if (kind == kHitSphere) {
+                            float4 sphr;
+                            if (!STREAM && kPair) {
+                                const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) *
+                                                                                              kSphPairFloat4) +
+                                                 (hidx & 1u);
+                                sphr = make_float4(q[0], q[2], q[4], q[6]);
+                            } else {
+                                sphr = g_sph_plain[hidx];
+                            }
+                            sphere_hit<OPT>(sphr, closest, ray, hx, hy, hz, nx, ny, nz);
                         } else {
-                            sphr = g_sph_plain[hidx];
+                            triangle_hit<OPT>(reinterpret_cast<const float4*>(p.tris),
+                                              reinterpret_cast<const float4*>(p.tri_shade), hidx, closest, ray, hx, hy,
+                                              hz, nx, ny, nz);
                         }
-                        sphere_hit<OPT>(sphr, closest, ray, hx, hy, hz, nx, ny, nz);
-                    } else {
-                        triangle_hit<OPT>(reinterpret_cast<const float4*>(p.tris),
-                                          reinterpret_cast<const float4*>(p.tri_shade), hidx, closest, ray, hx, hy,
-                                          hz, nx, ny, nz);
+                        float coeff, q;
+                        save_base();
+                        or_scatter_core<OPT>(hx, hy, hz, nx, ny, nz, ray, st, m1.y, m1.z, coeff, q);
+                        // m_albedo * coeff / pi, times cos / pdf (path_tracer.cu:321-324)
+                        const float sx = ((m0.x * coeff) * (1.0f / IQ_PI)) * q;
+                        const float sy = ((m0.y * coeff) * (1.0f / IQ_PI)) * q;
+                        const float sz = ((m0.z * coeff) * (1.0f / IQ_PI)) * q;
+                        if (depth + 1 >= p.max_depth) {
+                            term = true;             // the last record is this scatter (biased, :252)
+                            md_end = 1;
+                            Lx = sx;
+                            Ly = sy;
+                            Lz = sz;
+                        } else {
+                            const uint32_t b = (uint32_t)depth * 3u * kRenderBlock + threadIdx.x;
+                            lds_stk[b] = sx;
+                            lds_stk[b + kRenderBlock] = sy;
+                            lds_stk[b + 2u * kRenderBlock] = sz;
+                            ++depth;
+                        }
                     }
-                    float coeff, q;
-                    save_base();
-                    or_scatter_core<OPT>(hx, hy, hz, nx, ny, nz, ray, st, m1.y, m1.z, coeff, q);
-                    // m_albedo * coeff / pi, times cos / pdf (path_tracer.cu:321-324)
-                    const float sx = ((m0.x * coeff) * (1.0f / IQ_PI)) * q;
-                    const float sy = ((m0.y * coeff) * (1.0f / IQ_PI)) * q;
-                    const float sz = ((m0.z * coeff) * (1.0f / IQ_PI)) * q;
-                    if (depth + 1 >= p.max_depth) {
-                        term = true;             // the last record is this scatter (biased, :252)
-                        md_end = 1;
-                        Lx = sx;
-                        Ly = sy;
-                        Lz = sz;
+                } else {
+                    term = true;                     // sky gradient, :308-313
+                    const float a = (ray.dy + 1.0f) * 0.5f;
+                    const float one_a = 1.0f - a;
+                    Lx = one_a + a * 0.5f;
+                    Ly = one_a + a * 0.7f;
+                    Lz = one_a + a * 1.0f;
+                }
+            } else if (active) {
+                if (kind == kHitSphere) {
+                    if (OPT & kOptStats) ++s_scatter_lanes;
+                    float4 sphr;
+                    if (!STREAM && kPair) {
+                        // the pair record in LDS: (cx_a, cx_b, cy_a, cy_b), (cz_a, cz_b, r_a, r_b)
+                        const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) +
+                                         (hidx & 1u);
+                        sphr = make_float4(q[0], q[2], q[4], q[6]);
                     } else {
-                        const uint32_t b = (uint32_t)depth * 3u * kRenderBlock + threadIdx.x;
-                        lds_stk[b] = sx;
-                        lds_stk[b + kRenderBlock] = sy;
-                        lds_stk[b + 2u * kRenderBlock] = sz;
+                        sphr = g_sph_plain[hidx];
+                    }
+                    save_base();
+                    const float s = oren_nayar_scatter<OPT>(sphr, closest, ray, st);
+                    if (depth + 1 >= p.max_depth) {
+                        term = true;                 // the last record is this scatter (biased, :252)
+                        md_end = 1;
+                        Lx = s;
+                        Ly = s;
+                        Lz = s;
+                    } else {
+                        lds_stk[(uint32_t)depth * kRenderBlock + threadIdx.x] = s;
                         ++depth;
                     }
-                }
-            } else {
-                term = true;                     // sky gradient, :308-313
-                const float a = (ray.dy + 1.0f) * 0.5f;
-                const float one_a = 1.0f - a;
-                Lx = one_a + a * 0.5f;
-                Ly = one_a + a * 0.7f;
-                Lz = one_a + a * 1.0f;
-            }
-        } else if (active) {
-            if (kind == kHitSphere) {
-                if (OPT & kOptStats) ++s_scatter_lanes;
-                float4 sphr;
-                if (!STREAM && kPair) {
-                    // the pair record in LDS: (cx_a, cx_b, cy_a, cy_b), (cz_a, cz_b, r_a, r_b)
-                    const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) +
-                                     (hidx & 1u);
-                    sphr = make_float4(q[0], q[2], q[4], q[6]);
+                } else if (kind == kHitTri) {
+                    term = true;                     // emissive(1, 10): att 10, cos = pdf = 1
+                    Lx = 10.0f;
+                    Ly = 10.0f;
+                    Lz = 10.0f;
                 } else {
-                    sphr = g_sph_plain[hidx];
+                    term = true;                     // sky gradient, :308-313
+                    const float a = (ray.dy + 1.0f) * 0.5f;
+                    const float one_a = 1.0f - a;
+                    Lx = one_a + a * 0.5f;
+                    Ly = one_a + a * 0.7f;
+                    Lz = one_a + a * 1.0f;
                 }
-                save_base();
-                const float s = oren_nayar_scatter<OPT>(sphr, closest, ray, st);
-                if (depth + 1 >= p.max_depth) {
-                    term = true;                 // the last record is this scatter (biased, :252)
-                    md_end = 1;
-                    Lx = s;
-                    Ly = s;
-                    Lz = s;
-                } else {
-                    lds_stk[(uint32_t)depth * kRenderBlock + threadIdx.x] = s;
-                    ++depth;
+            }
+            if (OPT & kOptStats) {
+                if (__ballot(active && kind == kHitSphere)) ++s_scatter_exec;
+                const uint64_t tm = __ballot(term);
+                if (tm) {
+                    ++s_term_exec;
+                    s_term_lanes += (unsigned long long)__popcll(tm);
                 }
-            } else if (kind == kHitTri) {
-                term = true;                     // emissive(1, 10): att 10, cos = pdf = 1
-                Lx = 10.0f;
-                Ly = 10.0f;
-                Lz = 10.0f;
-            } else {
-                term = true;                     // sky gradient, :308-313
-                const float a = (ray.dy + 1.0f) * 0.5f;
-                const float one_a = 1.0f - a;
-                Lx = one_a + a * 0.5f;
-                Ly = one_a + a * 0.7f;
-                Lz = one_a + a * 1.0f;
             }
-        }
-        if (OPT & kOptStats) {
-            if (__ballot(active && kind == kHitSphere)) ++s_scatter_exec;
-            const uint64_t tm = __ballot(term);
-            if (tm) {
-                ++s_term_exec;
-                s_term_lanes += (unsigned long long)__popcll(tm);
-            }
-        }
 
-        // ------------------------------------------------ path end: product, clamp, running mean
-        if (term) {
-            // backward product over the stacked records, newest first (:321-324)
-            float cx = Lx, cy = Ly, cz = Lz;
-            // most paths end on their first ray (depth 0: no records)
-            for (int i = depth - 1; i >= 0; --i) {
-                if (OPT & kOptMaterials) {
-                    const uint32_t b = (uint32_t)i * 3u * kRenderBlock + threadIdx.x;
-                    cx = cx * lds_stk[b];
-                    cy = cy * lds_stk[b + kRenderBlock];
-                    cz = cz * lds_stk[b + 2u * kRenderBlock];
-                } else {
-                    const float r = lds_stk[(uint32_t)i * kRenderBlock + threadIdx.x];
-                    cx = cx * r;
-                    cy = cy * r;
-                    cz = cz * r;
+            // ------------------------------------------------ path end: product, clamp, running mean
+            if (term) {
+                // backward product over the stacked records, newest first (:321-324)
+                float cx = Lx, cy = Ly, cz = Lz;
+                // most paths end on their first ray (depth 0: no records)
+                for (int i = depth - 1; i >= 0; --i) {
+                    if (OPT & kOptMaterials) {
+                        const uint32_t b = (uint32_t)i * 3u * kRenderBlock + threadIdx.x;
+                        cx = cx * lds_stk[b];
+                        cy = cy * lds_stk[b + kRenderBlock];
+                        cz = cz * lds_stk[b + 2u * kRenderBlock];
+                    } else {
+                        const float r = lds_stk[(uint32_t)i * kRenderBlock + threadIdx.x];
+                        cx = cx * r;
+                        cy = cy * r;
+                        cz = cz * r;
+                    }
                 }
-            }
-            // clamp (:345-347), path_color = 0 + color (:341,348), running mean (:356-358)
-            cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-            cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-            cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-            cx = 0.0f + cx;
-            cy = 0.0f + cy;
-            cz = 0.0f + cz;
-            if (kSplit && ((spec_mask >> lane) & 1ull)) {
-                // speculative slot j of split slot sp: the clamped colour and the slots it consumed
-                // (1 + its scatters: two draws each), then the next slot of the run from the base state
-                uint4 sl = lds_sp[threadIdx.x];
-                const uint32_t nsl = (uint32_t)depth + 1u + md_end;
-                const size_t at = (size_t)sl.x * p.m_cap + sl.y;
-                reinterpret_cast<float4*>(p.res)[at] = make_float4(cx, cy, cz, __uint_as_float(nsl));
-                p.nres[at] = (uint8_t)nsl;
+                // clamp (:345-347), path_color = 0 + color (:341,348), running mean (:356-358)
+                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                cx = 0.0f + cx;
+                cy = 0.0f + cy;
+                cz = 0.0f + cz;
+                if (kSplit && ((spec_mask >> lane) & 1ull)) {
+                    // speculative slot j of split slot sp: the clamped colour and the slots it consumed
+                    // (1 + its scatters: two draws each), then the next slot of the run from the base state
+                    uint4 sl = lds_sp[threadIdx.x];
+                    const uint32_t nsl = (uint32_t)depth + 1u + md_end;
+                    const size_t at = (size_t)sl.x * p.m_cap + sl.y;
+                    reinterpret_cast<float4*>(p.res)[at] = make_float4(cx, cy, cz, __uint_as_float(nsl));
+                    p.nres[at] = (uint8_t)nsl;
+                    depth = 0;
+                    if (++sl.y == sl.z) {
+                        active = false;
+                    } else {
+                        lds_sp[threadIdx.x].y = sl.y;
+                        if (nsl > 1u) {              // the path scattered: back to the base state (its next slot)
+                            st.v0 = lds_base[threadIdx.x];
+                            st.v1 = lds_base[kRenderBlock + threadIdx.x];
+                            st.v2 = lds_base[2 * kRenderBlock + threadIdx.x];
+                            st.v3 = lds_base[3 * kRenderBlock + threadIdx.x];
+                            st.v4 = lds_base[4 * kRenderBlock + threadIdx.x];
+                            st.d = lds_base[5 * kRenderBlock + threadIdx.x];
+                        }
+                        need_cam = true;
+                    }
+                } else {
+                float keep, nf, rc = 0.0f;
+                if (use_tab) {
+                    const float2 tv = lds_tab[done];
+                    rc = tv.x;
+                    keep = tv.y;
+                    nf = lds_tab_n[done];
+                } else {
+                    const uint64_t n = p.frame0 + done + 1;
+                    // (float)n of the 64-bit frame counter; when every frame of the launch fits 32 bits
+                    // the 32-bit conversion is the same correctly rounded value (one v_cvt_f32_u32)
+                    nf = p.frames32 ? (float)(uint32_t)n : (float)n;
+                    keep = (p.frames32 ? (float)(uint32_t)(n - 1) : (float)(n - 1)) / nf;
+                }
+                if (use_tab) {
+                    float qx, qy, qz;
+                    mean_terms<OPT>(cx, cy, cz, nf, rc, p.mean_tiny, qx, qy, qz);
+                    acc.x = qx + acc.x * keep;
+                    acc.y = qy + acc.y * keep;
+                    acc.z = qz + acc.z * keep;
+                } else {
+                    acc.x = mean_term<OPT>(cx, nf) + acc.x * keep;
+                    acc.y = mean_term<OPT>(cy, nf) + acc.y * keep;
+                    acc.z = mean_term<OPT>(cz, nf) + acc.z * keep;
+                }
+                uint32_t light_sp = ~0u, light_slots = 0;
+                if (kSplit) {
+                    // a split tile's light pixel counts its slots (1 + scatters per sample) for the next
+                    // launch's heavy / light decision (iqpt_split_prep_kernel)
+                    const uint4 sl = lds_sp[threadIdx.x];
+                    if (sl.w == 2u) {
+                        light_sp = sl.x;
+                        light_slots = sl.y + (uint32_t)depth + 1u + md_end;
+                        lds_sp[threadIdx.x].y = light_slots;
+                    }
+                }
+                ++done;
                 depth = 0;
-                if (++sl.y == sl.z) {
+                if (done == p.spp) {
+                    store_pixel();
+                    if (kOverlap) finished = true;
+                    if (kSplit && light_sp != ~0u) p.sp_rho[light_sp] = (uint32_t)(((uint64_t)light_slots * 256u) / p.spp);
                     active = false;
                 } else {
-                    lds_sp[threadIdx.x].y = sl.y;
-                    if (nsl > 1u) {              // the path scattered: back to the base state (its next slot)
-                        st.v0 = lds_base[threadIdx.x];
-                        st.v1 = lds_base[kRenderBlock + threadIdx.x];
-                        st.v2 = lds_base[2 * kRenderBlock + threadIdx.x];
-                        st.v3 = lds_base[3 * kRenderBlock + threadIdx.x];
-                        st.v4 = lds_base[4 * kRenderBlock + threadIdx.x];
-                        st.d = lds_base[5 * kRenderBlock + threadIdx.x];
-                    }
-                    need_cam = true;
+                    if (kSplit) need_cam = true;   // one camera_ray call site per iteration (loop top)
+                    else camera_ray<OPT>(p, px, py, st, ray);
                 }
-            } else {
-            float keep, nf, rc = 0.0f;
-            if (use_tab) {
-                const float2 tv = lds_tab[done];
-                rc = tv.x;
-                keep = tv.y;
-                nf = lds_tab_n[done];
-            } else {
-                const uint64_t n = p.frame0 + done + 1;
-                // (float)n of the 64-bit frame counter; when every frame of the launch fits 32 bits
-                // the 32-bit conversion is the same correctly rounded value (one v_cvt_f32_u32)
-                nf = p.frames32 ? (float)(uint32_t)n : (float)n;
-                keep = (p.frames32 ? (float)(uint32_t)(n - 1) : (float)(n - 1)) / nf;
-            }
-            if (use_tab) {
-                float qx, qy, qz;
-                mean_terms<OPT>(cx, cy, cz, nf, rc, p.mean_tiny, qx, qy, qz);
-                acc.x = qx + acc.x * keep;
-                acc.y = qy + acc.y * keep;
-                acc.z = qz + acc.z * keep;
-            } else {
-                acc.x = mean_term<OPT>(cx, nf) + acc.x * keep;
-                acc.y = mean_term<OPT>(cy, nf) + acc.y * keep;
-                acc.z = mean_term<OPT>(cz, nf) + acc.z * keep;
-            }
-            uint32_t light_sp = ~0u, light_slots = 0;
-            if (kSplit) {
-                // a split tile's light pixel counts its slots (1 + scatters per sample) for the next
-                // launch's heavy / light decision (iqpt_split_prep_kernel)
-                const uint4 sl = lds_sp[threadIdx.x];
-                if (sl.w == 2u) {
-                    light_sp = sl.x;
-                    light_slots = sl.y + (uint32_t)depth + 1u + md_end;
-                    lds_sp[threadIdx.x].y = light_slots;
                 }
-            }
-            ++done;
-            depth = 0;
-            if (done == p.spp) {
-                store_pixel();
-                if (kOverlap) finished = true;
-                if (kSplit && light_sp != ~0u) p.sp_rho[light_sp] = (uint32_t)(((uint64_t)light_slots * 256u) / p.spp);
-                active = false;
-            } else {
-                if (kSplit) need_cam = true;   // one camera_ray call site per iteration (loop top)
-                else camera_ray<OPT>(p, px, py, st, ray);
-            }
             }
         }
         if (kOverlap && p.tile_done) {
@@ -4425,6 +4681,16 @@ const variant kVariants[] = {
     IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptPrio | kOptOverlap),
     IQPT_V(16, false, kOptDefault | kOptCamAxis | kOptPrio | kOptOverlap),
     IQPT_V(8, false, kOptDefault | kOptMaterials | kOptCamAxis | kOptPrio | kOptOverlap),
+    // two rays per lane (kOptPipe): resident scenes under the reference's materials
+    IQPT_V(8, false, kOptDefault | kOptPrio | kOptPipe), IQPT_V(16, false, kOptDefault | kOptPrio | kOptPipe),
+    IQPT_V(8, false, kOptDefault | kOptPrio | kOptOverlap | kOptPipe),
+    IQPT_V(16, false, kOptDefault | kOptPrio | kOptOverlap | kOptPipe),
+    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptPrio | kOptPipe),
+    IQPT_V(16, false, kOptDefault | kOptCamAxis | kOptPrio | kOptPipe),
+    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptPrio | kOptOverlap | kOptPipe),
+    IQPT_V(16, false, kOptDefault | kOptCamAxis | kOptPrio | kOptOverlap | kOptPipe),
+    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptPrio | kOptPipe),
+    IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptPrio | kOptOverlap | kOptPipe),
     // sample-parallel chains (kOptSplit), resident scenes
     IQPT_V(8, false, kOptDefault | kOptSplit | kOptPrio), IQPT_V(16, false, kOptDefault | kOptSplit | kOptPrio),
     IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptSplit | kOptPrio),
@@ -4436,6 +4702,9 @@ const variant kVariants[] = {
     // kOptStats counts the primitive and node tests each query executes (the executed-work roofline)
     IQPT_V(8, false, kOptDefault | kOptStats),
     IQPT_V(8, false, kOptDefault | kOptPrio | kOptStats),
+    IQPT_V(8, false, kOptDefault | kOptPrio | kOptStats | kOptPipe),
+    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptPrio | kOptOverlap | kOptStats),
+    IQPT_V(8, false, kOptDefault | kOptCamAxis | kOptPrio | kOptOverlap | kOptStats | kOptPipe),
     IQPT_V(8, false, (kOptDefault & ~kOptFastDiv) | kOptStats),
     IQPT_V(8, true, (kOptDefault | kOptStats) & ~kOptLB5),
     IQPT_V(8, true, kOptDefault | kOptStats | kOptBvhPrimary),

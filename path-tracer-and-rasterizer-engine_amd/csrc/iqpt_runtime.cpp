@@ -210,6 +210,7 @@ struct iqpt_ctx {
     uint32_t spec_parity_rho = iqpt::kSpecParityRho;   // parity pixels' threshold (iqpt_debug_set_spec_parity; 0 off)
     uint32_t spec_parity_hi = iqpt::kSpecParityHi;     // ... and upper bound (iqpt_debug_set_spec_parity_max)
     bool anyhit_on = true;                  // any-hit queries in triangle-only scenes (iqpt_debug_set_anyhit)
+    bool pipe_on = true;                    // two rays per lane in resident plain launches (kOptPipe, iqpt_debug_set_two_ray)
     uint32_t spec_prio_q = 0;               // spec kernel progress-fair priority step (iqpt_debug_set_spec_prio; 0 off)
     uint32_t spec_margin_div = 16;          // window margin: 1/16 of the extra slots, at least 4 (iqpt_debug_set_spec;
                                             // against 1/4, 5 % of the chains take a second round instead of 0.6 %,
@@ -725,24 +726,20 @@ int build_cull(iqpt_ctx* c) {
     // a pixel of the next tile, so waves hold two tiles and their LDS batches test the union of both tiles'
     // candidates: C4 +66 % per launch whether the pixels are folded in the refill or by a kernel of their own
     // (profiles/r03/ab_certain.json, ab_streamed_certain_fold_rejected.json)
-    // per tile: candidate triangle pairs and sphere pairs (the queue order's cost, the lists' sizes, and the
-    // certain kernel's budget below); d_cnt is freed with the lists
-    uint32_t* d_cnt = nullptr;
-    IQPT_HIP(hipMalloc(&d_cnt, 2 * (size_t)ntiles * sizeof(uint32_t)));
+    // per tile: candidate triangle pairs and sphere pairs (the queue order's cost and the lists' sizes), read
+    // back at once: the device buffer is freed before any later step can return early
     std::vector<uint32_t> cnt(2 * (size_t)ntiles);
     {
+        uint32_t* d_cnt = nullptr;
+        IQPT_HIP(hipMalloc(&d_cnt, 2 * (size_t)ntiles * sizeof(uint32_t)));
         const int lcnt = iqpt::launch_tile_count(c->stream, c->d_cull, ntiles, c->cull_wt, c->cull_stride, d_cnt,
                                                  d_cnt + ntiles);
         hipError_t e = lcnt ? (hipError_t)lcnt : hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * sizeof(uint32_t),
                                                                 hipMemcpyDeviceToHost, c->stream);
         if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
-        if (e != hipSuccess) {
-            (void)hipFree(d_cnt);
-            return iqpt::hip_fail(e, "tile counts");
-        }
+        (void)hipFree(d_cnt);
+        if (e != hipSuccess) return iqpt::hip_fail(e, "tile counts");
     }
-    uint64_t cand = 0;
-    for (size_t t = 0; t < cnt.size(); ++t) cand += cnt[t];
     c->certain_valid = false;
     c->sky_active = false;
     c->h_miss.clear();
@@ -756,7 +753,6 @@ int build_cull(iqpt_ctx* c) {
     c->n_sky_pixels = 0;
     // (resident scenes: streamed ones with certain pixels and the sky kernel — their BVH-primary variants, which
     // have no LDS batches — measured slower on C4 in round 5, 135 -> 161 ms)
-    (void)cand;
     if (!c->d_mats && ntiles > 0 && resident_bytes <= iqpt::kLdsResidentBytes) {
         // per tile: the certain-hit mask (2 words), then after all tiles the certain-miss masks (2 words each)
         if (hipMalloc(&c->d_certain, 4 * (size_t)ntiles * sizeof(uint32_t)) != hipSuccess)
@@ -847,7 +843,6 @@ int build_cull(iqpt_ctx* c) {
             c->list_total = total;
         }
     }
-    (void)hipFree(d_cnt);
     std::vector<uint32_t> order(ntiles);
     for (uint32_t t = 0; t < ntiles; ++t) order[t] = t;
     std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
@@ -1965,6 +1960,12 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // Tiles are bound to the 8 XCDs (HW_REG_XCC_ID): only on a device that exposes 8 (not a partition
     // mode) and with at least 64 blocks, so that the observed round-robin dispatch puts blocks on every
     // XCD (HIP promises no placement; the kernel's last block checks it and raises an error bit if not)
+    // kOptPipe: plain launches over resident scenes under the reference's materials take the
+    // two-rays-per-lane variants where they are built (a caller's fixed option set keeps its own bits)
+    if (!c->opt_fixed && c->pipe_on && !stream_batches && !split && !chain && !fan && !spec && tune_slot < 0 &&
+        p.cull != nullptr && p.acc_tab && !(opt & iqpt::kOptMaterials) &&
+        iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptPipe))
+        opt |= iqpt::kOptPipe;
     bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && !chain && !fan && !spec &&
                p.cull != nullptr &&
                tune_slot < 0 && c->d_tile_done && c->d_xcd_order && c->num_xcc == 8 && c->num_cus >= 64 &&
@@ -2944,6 +2945,17 @@ int iqpt_debug_set_anyhit(iqpt_ctx* c, int on) {
     if (st) return st;
     c->anyhit_on = on != 0;
     c->cull_valid = false;               // the candidate lists' order follows the setting
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): resident plain launches under the reference's materials trace the lane's path ray and
+ * its pixel's next camera ray together (kOptPipe, 1, the default) or one ray per iteration (0). Same bits either
+ * way. */
+int iqpt_debug_set_two_ray(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->pipe_on = on != 0;
     return IQPT_OK;
 }
 

@@ -91,10 +91,13 @@ def build_lib(force: bool = False, stats: bool = False, flags: tuple[str, ...] =
     extra = (["-DIQPT_STATS_VARIANTS"] if stats else []) + list(flags)
     for s in srcs:
         o = bdir / (s.name + ".o")
-        cmds.append([HIPCC, *HIP_FLAGS, *extra, "-x", "hip", "-c", str(s), "-o", str(o)])
+        # an object is rebuilt when its source, a header or this recipe is newer (force: always)
+        if force or not _newer(o, [s] + _headers() + [Path(__file__)]):
+            cmds.append([HIPCC, *HIP_FLAGS, *extra, "-x", "hip", "-c", str(s), "-o", str(o)])
         objs.append(o)
-    with ThreadPoolExecutor(max_workers=min(4, len(cmds))) as ex:
-        list(ex.map(_run, cmds))
+    if cmds:
+        with ThreadPoolExecutor(max_workers=min(4, len(cmds))) as ex:
+            list(ex.map(_run, cmds))
     tmp = target.with_suffix(".so.tmp")
     _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp)])
     os.replace(tmp, target)
