@@ -380,6 +380,8 @@ constexpr int kOptDefault = kOptCamConst | kOptAccTable | kOptPair | kOptSinCos 
 constexpr uint32_t kStatsHeader = 24;        // kOptStats: 24 counters, then per-wave (start, end, iterations)
 constexpr uint32_t kStatsWaveSlots = 65536;
 constexpr uint32_t kStatsQueueSlots = 65536;   // kOptStats: then the s_memrealtime at which queue position q was taken
+constexpr uint32_t kStatsPhaseWords = 4;       // kOptStats: then per wave slot the shader-clock cycles (s_memtime) spent in
+                                               // the closest hits, the shading, the next rays and the rest of the loop
 constexpr uint32_t kAccTableMax = 1024;  // spp per launch covered by the LDS table (8 KiB)
 
 // Launch wrappers (iqpt_kernels.hip). Return a hipError_t as int.

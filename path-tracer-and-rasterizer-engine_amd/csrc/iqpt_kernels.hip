@@ -1665,12 +1665,23 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
     // kOptBvhPrimary: every ray goes through the BVHs, no LDS batches, so no workgroup barriers: the
     // waves iterate independently, as in the resident kernel
     constexpr bool kBatches = STREAM && !kBvhPrimary;
+    // kOptStats: shader-clock cycles per phase of the loop (closest hits, shading, next rays, the rest)
+    unsigned long long s_ph[4] = {0ull, 0ull, 0ull, 0ull};
+    unsigned long long s_t = (OPT & kOptStats) ? __builtin_amdgcn_s_memtime() : 0ull;
+    auto phase = [&](int i) {
+        if (OPT & kOptStats) {
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            s_ph[i] += t - s_t;
+            s_t = t;
+        }
+    };
     while (true) {
         if (kBatches) {
             if (!__syncthreads_or(active ? 1 : 0)) break;
         } else {
             if (!__any(active)) break;
         }
+        phase(3);
         if (kSplit && need_cam) {
             camera_ray<OPT>(p, px, py, st, ray);
             need_cam = false;
@@ -1713,6 +1724,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                                        (OPT & kOptStats) ? s_tests : nullptr);
                 if (OPT & kOptStats) s_full += all_a ? 1ull : 0ull;
             }
+            phase(0);
             wave_rays += (uint64_t)__popcll(__ballot(active));
             // at most two shading rounds: ray a's hit, then (ray a ended the path) ray b's
             bool pend = active, need_a = false;
@@ -1800,6 +1812,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 if (r == 0) wave_rays += (uint64_t)__popcll(__ballot(next));
                 pend = next;
             }
+            phase(1);
             // the next iteration's rays: a new path's camera ray where a path ended without taking ray b, and the
             // camera ray of the sample after the current one (ray b is stale after any scatter or path end)
             if (need_a && active) camera_ray<OPT>(p, px, py, st, ray);
@@ -1808,6 +1821,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 rng6 sb = st;
                 camera_ray<OPT>(p, px, py, sb, ray_b);
             }
+            phase(2);
         } else {
             // ------------------------------------------------ closest hit (path_tracer.cu:253-295)
             float closest = kTMax;
@@ -2084,6 +2098,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
             } else if (active) {
                 intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
             }
+            phase(0);
             if (kBvhPrimary) {
                 asm volatile("" ::: "memory");
                 st.v0 = park[0 * kRenderBlock];
@@ -2320,6 +2335,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 }
                 }
             }
+            phase(1);
         }
         if (kOverlap && p.tile_done) {
             // pixels completed this iteration: once their stores are done (vmcnt 0), one counter add per tile
@@ -2397,6 +2413,12 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     (t_start & 0xffffffffffffull) |
                     ((unsigned long long)(blockIdx.x * (kRenderBlock / 64) + threadIdx.x / 64) << 48);
                 p.stats[kStatsHeader + 3 * slot + 1] = __builtin_amdgcn_s_memrealtime();
+                unsigned long long* ph = p.stats + kStatsHeader + 3 * (size_t)kStatsWaveSlots + kStatsQueueSlots +
+                                         (size_t)kStatsPhaseWords * slot;
+                ph[0] = s_ph[0];
+                ph[1] = s_ph[1];
+                ph[2] = s_ph[2];
+                ph[3] = s_ph[3];
                 // iterations | (split: speculative lanes; else first queue position (24 b) | chunks (8 b)) << 32
                 p.stats[kStatsHeader + 3 * slot + 2] =
                     s_iter | ((kSplit ? s_spec_lanes

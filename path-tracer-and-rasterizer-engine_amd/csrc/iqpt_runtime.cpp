@@ -3613,7 +3613,8 @@ int iqpt_debug_set_kernel_options(iqpt_ctx* c, int opt) {
     int st = enter(c);
     if (st) return st;
     if ((opt & iqpt::kOptStats) && !c->d_stats) {
-        const size_t words = iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots + iqpt::kStatsQueueSlots;
+        const size_t words = iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots + iqpt::kStatsQueueSlots +
+                             iqpt::kStatsPhaseWords * (size_t)iqpt::kStatsWaveSlots;
         if (hipMalloc(&c->d_stats, words * sizeof(unsigned long long)) != hipSuccess)
             return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "stats");
         IQPT_HIP(hipMemset(c->d_stats, 0, words * sizeof(unsigned long long)));
@@ -3784,6 +3785,21 @@ int iqpt_debug_read_queue_times(iqpt_ctx* c, unsigned long long* out) {
     if (!c->d_stats) return iqpt::fail(IQPT_ERR_INVALID_ARG, "no stats buffer (kOptStats not set)");
     IQPT_HIP(hipMemcpy(out, c->d_stats + iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots,
                        iqpt::kStatsQueueSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    return IQPT_OK;
+}
+
+/* Internal (tools/wave_timeline.py): per wave slot of the last kOptStats launch, the shader-clock cycles spent in the
+ * closest hits, the shading, the next rays and the rest of the loop (kStatsPhaseWords each, same slots as
+ * iqpt_debug_read_wave_times). Call before iqpt_debug_read_stats. */
+int iqpt_debug_read_wave_phases(iqpt_ctx* c, unsigned long long* out, uint32_t cap) {
+    if (!c || !out) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
+    int st = enter(c);
+    if (st) return st;
+    IQPT_HIP(hipStreamSynchronize(c->stream));
+    if (!c->d_stats) return iqpt::fail(IQPT_ERR_INVALID_ARG, "no stats buffer (kOptStats not set)");
+    const size_t m = std::min<size_t>(cap, iqpt::kStatsWaveSlots);
+    IQPT_HIP(hipMemcpy(out, c->d_stats + iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots + iqpt::kStatsQueueSlots,
+                       iqpt::kStatsPhaseWords * m * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     return IQPT_OK;
 }
 

@@ -6,8 +6,11 @@ Pass B: SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE
 (each in its own run with --kernel-trace only). SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* count
 quad-cycles; WAIT_ANY (parked on s_waitcnt / barrier) + WAIT_INST_ANY (ready, not issued) +
 ACTIVE_INST_ANY ~= WAVE_CYCLES (MI355X_MICROARCH.md, rocprofv3 PMC slots). GRBM_GUI_ACTIVE is summed
-over the 8 XCDs: kernel cycles = GRBM_GUI_ACTIVE / 8. valu_busy_frac = VALU-active cycles per SIMD
-over the kernel's cycles (1024 SIMDs).
+over the 8 XCDs: kernel cycles = GRBM_GUI_ACTIVE / 8. valu_busy_frac = the SIMDs' VALU issue cycles over the
+kernel's cycles (1024 SIMDs): a wave64 VALU instruction holds a SIMD-32 for 2 cycles, a transcendental one for 4
+(MI355X_MICROARCH.md, constants table), so this cannot exceed 1. valu_active_per_simd is the older measure,
+SQ_ACTIVE_INST_VALU summed over waves per SIMD-cycle: waves' VALU instructions in flight overlap, so it can exceed
+1 (round 5's sky kernel read 1.025) and is not a utilisation.
 
 usage: pmc_mix.py <passA.csv> <passB.csv> <config> <wave_iterations_per_launch> <out.json> [label] [kernel]
 
@@ -59,7 +62,8 @@ def main():
         "per_iteration": {k: round(v / iters, 2) for k, v in a.items() if k.startswith("SQ_INSTS")},
         "kernel_ms_profiled": round(dur * 1e3, 4),
         "clock_ghz": round(kcycles / dur / 1e9, 3),
-        "valu_busy_frac": round(b["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / kcycles, 3),
+        "valu_busy_frac": round((2.0 * a["SQ_INSTS_VALU"] + 2.0 * a.get("SQ_INSTS_VALU_TRANS_F32", 0.0)) / SIMDS / kcycles, 3),
+        "valu_active_per_simd": round(b["SQ_ACTIVE_INST_VALU"] * 4 / SIMDS / kcycles, 3),
         "wave_time_split": {"issuing": round(b["SQ_ACTIVE_INST_ANY"] / wave, 3),
                             "ready_not_issued": round(b["SQ_WAIT_INST_ANY"] / wave, 3),
                             "parked_on_waitcnt": round(b["SQ_WAIT_ANY"] / wave, 3)},

@@ -37,6 +37,7 @@ ap.add_argument("--prio", type=int, default=None, help="iqpt_debug_set_spec_prio
 ap.add_argument("--parity-max", type=float, default=None, help="iqpt_debug_set_spec_parity_max in slots per sample")
 ap.add_argument("--queue", type=int, default=None, help="iqpt_debug_set_spec_queue mode (1: queue mode)")
 ap.add_argument("--qbpc", type=int, default=0, help="queue mode's blocks per CU (0: the default)")
+ap.add_argument("--two-ray", type=int, default=None, help="iqpt_debug_set_two_ray (kOptPipe: 1 on, 0 off)")
 ap.add_argument("--out", default="")
 args = ap.parse_args()
 
@@ -69,6 +70,9 @@ if args.prio is not None:
 if args.parity is not None:
     lb.iqpt_debug_set_spec_parity.argtypes = [C.c_void_p, C.c_uint32]
     _lib.check(lb.iqpt_debug_set_spec_parity(pt._h, int(round(args.parity * 256))), "iqpt_debug_set_spec_parity")
+if args.two_ray is not None:
+    lb.iqpt_debug_set_two_ray.argtypes = [C.c_void_p, C.c_int]
+    _lib.check(lb.iqpt_debug_set_two_ray(pt._h, args.two_ray), "iqpt_debug_set_two_ray")
 pt.set_camera(cam)
 pt.upload_packet(pk)
 for _ in range(args.warm):
@@ -140,7 +144,7 @@ wave_us = (wave_end - t0) / 100.0
 start, slots_end, walk_end, end = us[:, 0], us[:, 1], us[:, 2], wave_us.max(axis=1)
 
 
-res = {"share": args.share, "specfan": args.specfan, "plan": args.plan, "cap": args.cap or None, "parity": args.parity, "parity_max": args.parity_max, "prio": args.prio,
+res = {"share": args.share, "two_ray": args.two_ray, "specfan": args.specfan, "plan": args.plan, "cap": args.cap or None, "parity": args.parity, "parity_max": args.parity_max, "prio": args.prio,
        "blocks": int(n.value), "spec_stats": spec_stats,
        "kernel_us": round(float(end.max()), 1),
        "start_us": pct(start), "slots_us": pct(slots_end - start), "walk_us": pct(walk_end - slots_end),
