@@ -112,8 +112,6 @@ def parse():
                          "(iqpt_debug_set_two_ray; default: the library's, on)")
     ap.add_argument("--anyhit", type=int, default=None, choices=[0, 1],
                     help="A/B: any-hit queries for triangle-only scenes (iqpt_debug_set_anyhit; default: the library's, on)")
-    ap.add_argument("--spec-parity-max", type=float, default=None,
-                    help="A/B: spec parity pixels' upper bound in slots per sample (iqpt_debug_set_spec_parity_max)")
     ap.add_argument("--stream-refill", type=int, default=None,
                     help="A/B: idle lanes before a streamed-scene wave takes new pixels (iqpt_debug_set_stream_refill; 1..64)")
     ap.add_argument("--stream-xcd", type=int, default=None, choices=[0, 1, 2, 3],
@@ -121,18 +119,10 @@ def parse():
                          "dealt to the XCDs, 2 bands of tile rows dealt to the XCDs, 3 the default: 1 up to 4 spp per launch)")
     ap.add_argument("--resident-refill", type=int, default=None,
                     help="A/B: idle lanes before a resident-scene wave takes new pixels (iqpt_debug_set_resident_refill)")
-    ap.add_argument("--spec-queue", type=int, default=None,
-                    help="A/B: spec launches in queue mode (1) or the block kernel (0) (iqpt_debug_set_spec_queue)")
-    ap.add_argument("--spec-qbpc", type=int, default=0,
-                    help="A/B: queue mode's persistent blocks per CU (0: the default)")
-    ap.add_argument("--spec-prio", type=int, default=None,
-                    help="A/B: spec kernel progress-fair priority step in iterations (iqpt_debug_set_spec_prio; 0 off)")
     ap.add_argument("--spec-parity", type=float, default=None,
                     help="A/B: spec parity pixels' threshold in slots per sample (iqpt_debug_set_spec_parity; 0 = every "
                          "slot traced, the round-4 kernel; default: the library's 1.875)")
-    ap.add_argument("--spec-cap", type=float, default=0.0,
-                    help="A/B: a spec plan's lanes as a fraction of the resident lanes (iqpt_debug_set_spec_cap; 0 = default)")
-    ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "chain", "fan", "spec"],
+    ap.add_argument("--split", default="auto", choices=["auto", "on", "off", "spec"],
                     help="sample-parallel chains (iqpt_set_split, DESIGN.md §3.7)")
     args = ap.parse_args()
     if args.warmup is None:
@@ -293,8 +283,7 @@ def certain_pixels(pt, _lib) -> int:
 
 # the kernels a launch mode runs (iqpt_debug_split_info's launch mode)
 LAUNCH_KERNELS = {"plain": "iqpt_render_kernel", "spec": "iqpt_spec_kernel + iqpt_fan_kernel",
-                  "fan": "iqpt_render_kernel + iqpt_fan_kernel", "chain": "iqpt_chain_kernel + iqpt_render_kernel",
-                  "chain+fan": "iqpt_chain_kernel + iqpt_fan_kernel", "split": "iqpt_render_kernel (split rounds)",
+                  "split": "iqpt_render_kernel (split rounds)",
                   "split+fan": "iqpt_render_kernel (split rounds) + iqpt_fan_kernel"}
 
 
@@ -501,7 +490,6 @@ def main():
     pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, seed=seed, max_depth=cfg.max_depth, device=device)
     setup["create_and_rng_init_ms"] = (time.perf_counter() - t0) * 1e3
     pt.set_split({"auto": _lib.SPLIT_AUTO, "on": _lib.SPLIT_ON, "off": _lib.SPLIT_OFF,
-                  "chain": _lib.SPLIT_CHAIN, "fan": _lib.SPLIT_FAN,
                   "spec": _lib.SPLIT_SPEC}[args.split])
     if args.kernel_options:
         import ctypes as C
@@ -555,32 +543,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_resident_refill.argtypes = [C.c_void_p, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_resident_refill(pt._h, args.resident_refill), "iqpt_debug_set_resident_refill")
-    if args.spec_queue is not None:
-        import ctypes as C
-        lb = _lib.load()
-        lb.iqpt_debug_set_spec_queue.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
-        _lib.check(lb.iqpt_debug_set_spec_queue(pt._h, args.spec_queue, args.spec_qbpc), "iqpt_debug_set_spec_queue")
-    if args.spec_parity_max is not None:
-        import ctypes as C
-        lb = _lib.load()
-        lb.iqpt_debug_set_spec_parity_max.argtypes = [C.c_void_p, C.c_uint32]
-        _lib.check(lb.iqpt_debug_set_spec_parity_max(pt._h, min(0xffffffff, int(round(args.spec_parity_max * 256)))),
-                   "iqpt_debug_set_spec_parity_max")
-    if args.spec_prio is not None:
-        import ctypes as C
-        lb = _lib.load()
-        lb.iqpt_debug_set_spec_prio.argtypes = [C.c_void_p, C.c_uint32]
-        _lib.check(lb.iqpt_debug_set_spec_prio(pt._h, args.spec_prio), "iqpt_debug_set_spec_prio")
     if args.spec_parity is not None:
         import ctypes as C
         lb = _lib.load()
         lb.iqpt_debug_set_spec_parity.argtypes = [C.c_void_p, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_spec_parity(pt._h, int(round(args.spec_parity * 256))), "iqpt_debug_set_spec_parity")
-    if args.spec_cap:
-        import ctypes as C
-        lb = _lib.load()
-        lb.iqpt_debug_set_spec_cap.argtypes = [C.c_void_p, C.c_double]
-        _lib.check(lb.iqpt_debug_set_spec_cap(pt._h, args.spec_cap), "iqpt_debug_set_spec_cap")
     pt.set_camera(cam)
     t0 = time.perf_counter()
     pt.upload_packet(pk)
@@ -701,7 +668,8 @@ def main():
     _lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
     _o = C.c_int(0)
     _lib.check(_lb.iqpt_debug_last_options(pt.handle, C.byref(_o)), "iqpt_debug_last_options")
-    last_opt = _o.value                                # the render-kernel option set of the last launch
+    last_opt = _o.value & ~(1 << 30)                   # the render-kernel option set of the last launch
+    xcd_lists = bool(_o.value & (1 << 30))             # ... whose tiles were dealt to per-XCD lists
     certain_px = certain_pixels(pt, _lib) if args.certain != "off" else 0
     sky_px = sky_pixels(pt, _lib) if (args.certain != "off" and args.sky != "off") else 0
 
@@ -809,21 +777,19 @@ def main():
                        # the plain kernel's option bits of the last launch (iqpt_internal.hpp kOpt*): for streamed
                        # scenes bit 12 (kOptBvhPrimary) says whether camera rays took the BVH or the tile lists
                        "kernel_option_bits": hex(last_opt),
+                       "xcd_tile_lists": xcd_lists,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
-                       **({"spec_cap": args.spec_cap} if args.spec_cap else {}),
                        **({"spec_parity": args.spec_parity} if args.spec_parity is not None else {}),
                        **({"anyhit": args.anyhit} if args.anyhit is not None else {}),
-                       **({"spec_prio": args.spec_prio} if args.spec_prio is not None else {}),
-                       **({"spec_parity_max": args.spec_parity_max} if args.spec_parity_max is not None else {}),
                        **({"stream_refill": args.stream_refill} if args.stream_refill is not None else {}),
                        **({"resident_refill": args.resident_refill} if args.resident_refill is not None else {}),
                        **({"stream_xcd": args.stream_xcd} if args.stream_xcd is not None else {}),
                        **({"warmup_note": "W < 5: launches that time the camera-ray paths fall in the timed region"}
-                          if args.config in STREAMED_CONFIGS and args.warmup < 5 else {}),
-                       **({"spec_queue": args.spec_queue, "spec_qbpc": args.spec_qbpc}
-                          if args.spec_queue is not None else {})},
+                          if args.config in STREAMED_CONFIGS and args.warmup < 5 else {})},
             "n_ranks_seen": n_ranks_seen,
             "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4")),
+            # the libiqpt that ran (its ABI; an A/B --lib may be an older build)
+            "lib": {"path": str(_lib.LIB_PATH.name) if not args.lib else args.lib, "abi": _lib.LOADED_ABI},
             **({"gather": "stream-ordered" if stream_gather else "blocking", "gather_check": gather_check}
                if strong_multi else {}),
             "msamples_per_s": round(samples / elapsed / 1e6, 3),

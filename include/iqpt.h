@@ -43,7 +43,9 @@
 extern "C" {
 #endif
 
-#define IQPT_ABI_VERSION 5
+/* 6 (round 6): IQPT_SPLIT_CHAIN and IQPT_SPLIT_FAN are refused with IQPT_ERR_UNSUPPORTED (their kernels were
+ * archived); the other entry points are unchanged from 5. */
+#define IQPT_ABI_VERSION 6
 
 typedef enum iqpt_status {
     IQPT_OK = 0,
@@ -182,19 +184,16 @@ int iqpt_sync(iqpt_ctx* ctx);
 #define IQPT_SPLIT_AUTO (-1)
 #define IQPT_SPLIT_OFF 0
 #define IQPT_SPLIT_ON 1
-/* CHAIN: the same set of pixels, each evaluated by a group of lanes at consecutive
- * stream offsets and folded in sample order as the results arrive, in a kernel that runs beside the
- * plain kernel over the other tiles (one launch pair, no stitch pass). */
+/* CHAIN and FAN were launch modes of rounds 2-5, archived in round 6 (AUTO never chose
+ * FAN, and CHAIN only where SPEC did not fit): iqpt_set_split refuses them with IQPT_ERR_UNSUPPORTED. */
 #define IQPT_SPLIT_CHAIN 2
-/* FAN: the tiles whose camera rays cannot reach a sphere (every sample one ray and two
- * draws, so sample k starts 2k draws into the pixel's stream) spread each pixel's samples over four
- * waves and fold them in order; the other tiles run in the plain kernel beside them, on a second stream,
- * pipelined across launches (no join per launch). Chain launches run their anchored tiles this way too. */
 #define IQPT_SPLIT_FAN 3
 /* SPEC: the pixels whose own camera rays may reach a sphere (the only ones whose samples
  * take more than two draws) have every slot of a window evaluated in parallel and their chains walked in
- * order afterwards; every other pixel runs as in FAN, on a second stream, the two kernels pipelined across
- * launches. AUTO picks it for small shares (fewer than 4 owned pixels per resident lane: C3 at N >= 2). */
+ * order afterwards; every other pixel's samples are spread over the four waves of a tile's block of the fan
+ * kernel (every sample one ray and two draws, so sample k starts 2k draws into the pixel's stream) and
+ * folded in order, on a second stream, the two kernels pipelined across launches. AUTO picks it for small
+ * shares (fewer than 4 owned pixels per resident lane: C3 at N >= 2). */
 #define IQPT_SPLIT_SPEC 4
 int iqpt_set_split(iqpt_ctx* ctx, int mode);
 

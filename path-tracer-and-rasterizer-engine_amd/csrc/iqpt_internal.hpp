@@ -161,14 +161,14 @@ struct kparams {
     uint32_t done_target;            // k: launches of the chain before this one (0: no wait)
     const uint32_t* xcd_order;
     uint32_t xcd_off[9];
-    uint32_t* ovl_err;               // bit 0: a wait exceeded spin_limit, bit 1: a chain wave exceeded iter_limit,
-                                     // bit 2: an XCD's tile list was never taken (no workgroup ran there)
-    // forward-progress bounds (never reached by a real launch; iqpt_debug_set_limits lowers them so that
-    // tests can force each one): s_sleep polls of one per-tile wait, loop iterations of one chain wave
+    uint32_t* ovl_err;               // bit 0: a wait exceeded spin_limit, bit 2: an XCD's tile list was never taken
+                                     // (no workgroup ran there)
+    // forward-progress bound (never reached by a real launch; iqpt_debug_set_limits lowers it so that tests can
+    // force it): s_sleep polls of one per-tile wait; iter_limit bounded the archived chain kernel's loop (unused)
     uint32_t spin_limit, iter_limit;
     // iqpt_fan_kernel: the lanes of fan tile b that it renders (bit i: pixel i of the tile); null = all.
-    // Chain launches give the fan kernel every pixel whose camera rays provably miss every sphere, also
-    // inside tiles with sphere candidates (the other pixels of those tiles are the chain kernel's).
+    // Spec launches give the fan kernel every pixel whose camera rays provably miss every sphere, also
+    // inside tiles with sphere candidates (the other pixels of those tiles are the spec kernel's).
     const uint64_t* fan_lanes;
     // queue length of the plain kernel's tile queue (tile_order[0 .. nqueue)); 0: every tile (ntiles).
     // Chain launches give the plain kernel the anchored tiles only.
@@ -185,7 +185,7 @@ constexpr uint32_t kRaySlots = 64;
 constexpr uint32_t kRaySlotStride = 16;      // unsigned long longs
 constexpr int kSphNodeFloat4 = 3;
 constexpr uint32_t kOverlapSpinLimit = 1u << 23;   // s_sleep(20) polls before a wait gives up (~seconds)
-constexpr uint32_t kChainIterLimit = 1u << 22;     // chain-kernel loop iterations before a wave gives up
+constexpr uint32_t kChainIterLimit = 1u << 22;     // (the archived chain kernel's loop bound; iqpt_debug_set_limits)
 // two launch parities x (8 XCD queue words + the finished-block count), 64 B apart
 constexpr uint32_t kOverlapQueueWords = 2 * 9 * 16;
 
@@ -208,37 +208,13 @@ struct kspec {
     // one (pooled over the block's lanes); 0: every slot of every window
     uint32_t parity_rho;
     uint32_t parity_hi;              // ... and at most parity_hi / 256 slots per sample
-    uint32_t prio_q;                 // progress-fair priority: a wave's level drops by one per prio_q slot-loop
-                                     // iterations (0: level 3 throughout)
     const uint32_t* order;           // a plan (else null): sphere pixel q at each position, heaviest first
     const uint32_t* blocks;          // per plan block: first position, count | log2(lanes / 8) << 8
     uint32_t nblocks;                // plan blocks (the spec part of the grid)
     unsigned long long* tl;          // measurement (iqpt_debug_spec_timeline), else null: per spec block
                                      // s_memrealtime at start, after round 0's slots and walk, at the end
-                                     // (| rounds << 48); queue mode: 8 words per wave (iqpt_debug_set_spec_queue)
-    // queue mode (iqpt_specq_kernel): persistent waves take sphere pixels from per-XCD
-    // cursors over the plan's order (heaviest first) and trace a pool of their slots together; the walk of a pixel
-    // runs as soon as its slots are done. iqpt_spec_prep_kernel writes each pixel's window (m) and the state at
-    // every kSpecCk-th slot of it first.
-    uint32_t queue;                  // 1: queue mode
-    uint32_t* ck;                    // ck[(o ncp + c) 8 + w], w < 5: the state at slot c ck_step of the pixel at
-                                     // queue position o (order[o])
-    uint32_t ncp;                    // checkpoint records per pixel (<= kSpecQCkMax)
-    uint32_t ck_step;                // slots between two checkpoints (a multiple of kSpecCk)
-    uint32_t* cursor;                // kSpecCursors per-XCD cursors, 16 words apart (zeroed by the prep kernel)
-    uint32_t* qrec;                  // per queue position: the pixel's initial record (kSpecQRecWordsHost words)
+                                     // (| rounds << 48)
 };
-constexpr uint32_t kSpecCk = 8;             // queue mode: slots between two checkpoints (at least; spec_ck_step)
-constexpr uint32_t kSpecQCkMax = 28;        // queue mode: checkpoints per pixel (a wave keeps them in LDS)
-constexpr uint32_t kSpecQRecWordsHost = 24; // queue mode: words per pixel record (kernels: kSpecQRecWords)
-// queue mode: the checkpoint spacing for a window cap (the smallest multiple of kSpecCk giving <= kSpecQCkMax)
-inline uint32_t spec_ck_step(uint32_t m_cap) {
-    uint32_t s = kSpecCk;
-    while (m_cap / s + 1u > kSpecQCkMax) s += kSpecCk;
-    return s;
-}
-constexpr uint32_t kSpecCursors = 8;        // queue mode: one pixel cursor per XCD
-constexpr uint32_t kSpecQBlocksPerCu = 2;   // queue mode: persistent blocks per CU (iqpt_debug_set_spec_queue)
 constexpr int kSendRing = 4;                // the multi-GPU gather's send buffers, used in turn
 constexpr int kPipeRing = 6;                // frame buffers pipelined launches write in turn once copies follow them
 constexpr int kGatherCtas = 2;              // RCCL blocks per frame gather (iqpt_debug_set_gather)
@@ -426,24 +402,11 @@ int render_occupancy(int max_depth, bool stream_batches, int opt, uint32_t lds_b
 int launch_split_prep(void* stream, const ksplit& s);
 int launch_split_stitch(void* stream, const ksplit& s, bool fastdiv);
 bool render_variant_exists(int max_depth, bool stream_batches, int opt);
-// Chain-parallel pixels (iqpt_chain_kernel): the split set's pixels, each evaluated by
-// kChainLanes lanes at consecutive even stream offsets and folded in sample order; reads p.sp_pix /
-// p.ns_cap and takes pixels from p.queue[1]. Resident scenes, reference materials, max_depth <= 16.
-// lanes: lanes per pixel, 4, 8 or 16.
-bool chain_variant_exists(int max_depth, int opt, uint32_t lanes);
-uint32_t chain_lds(const kparams& p, uint32_t lanes);
-int chain_occupancy(int max_depth, int opt, uint32_t lanes, uint32_t lds, int* blocks_per_cu);
-int launch_chain(void* stream, const kparams& p, uint32_t grid_blocks, int opt, uint32_t lanes);
 // Slot-parallel sphere pixels: resident scene, reference materials, max_depth <= 16,
 // spp <= kAccTableMax.
 bool spec_variant_exists(int max_depth, int opt);
 uint32_t spec_lds(const kparams& p, const kspec& s);
 int launch_spec(void* stream, const kparams& p, const kspec& s, int opt);
-// queue mode: the prep kernel (windows, checkpoints, cursors) then the persistent kernel over `blocks` blocks
-int launch_spec_prep(void* stream, const kparams& p, const kspec& s);
-int launch_specq(void* stream, const kparams& p, const kspec& s, int opt, uint32_t blocks);
-uint32_t specq_lds(const kparams& p, const kspec& s);
-int specq_occupancy(const kparams& p, const kspec& s, int opt, int* blocks);
 // resident iqpt_spec_kernel blocks per CU for this launch
 int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks);
 // Certain-miss pixels (iqpt_sky_kernel): the p.miss pixels of `ntiles` tiles (tiles[i]),

@@ -3011,326 +3011,6 @@ __global__ __launch_bounds__(kStitchBlock) void iqpt_split_stitch_kernel(const k
 }
 
 // ------------------------------------------------------------------------------------------------
-// Chain-parallel pixels (iqpt_chain_kernel). A pixel's samples are one XORWOW stream
-// (path_tracer.cu:339): sample k starts where sample k-1's draws ended, 2 draws for the camera jitter
-// (camera.cu:24-25) plus 2 per Oren-Nayar scatter (material.cu:10). Everything a sample does from even
-// stream offset 2j depends on j alone, so LANES (4 or 8) lanes of a wave evaluate one pixel's samples at
-// consecutive "slots" j (lane i: slots i, i + LANES, ...) speculatively, each from the state
-// 2j draws into the pixel's stream, and one lane per group (the walker) follows the chain
-// 0 -> j + n_j -> ... through a ring of results in LDS, applying the running mean in sample order.
-// The chain needs slot ptr next; a lane may start slot c only while c < ptr + 2 LANES (the ring
-// entry it overwrites is behind the chain), so the lane holding slot ptr always gets to it and the
-// chain always advances. When the pixel's samples are complete, the state at the chain's end is the
-// start state of slot ptr (stored when the slot started, or stepped there by its lane). Same bits as
-// the anchored kernel: the same per-sample code, the same mean terms, the chain's own slots counted
-// as rays. The pixels come from the split set (tiles whose camera rays may scatter, under the
-// reference's materials); the other tiles run anchored in iqpt_render_kernel beside this kernel.
-constexpr uint32_t kChainBlock = 64;                   // one wave per block
-constexpr int kChainWaves = 4;                         // __launch_bounds__ waves per SIMD
-constexpr uint32_t kChainRingMul = 2;                  // ring entries per lane
-
-template <int MAXD, int OPT, int LANES>
-__global__ __launch_bounds__(kChainBlock, kChainWaves) void iqpt_chain_kernel(const kparams p) {
-    constexpr uint32_t kL = LANES;              // lanes per pixel
-    constexpr uint32_t kG = 64 / kL;            // pixels per wave
-    constexpr uint32_t kR = kChainRingMul * kL; // slots in flight per pixel (ring entries, a multiple of kL)
-    extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    constexpr bool kCull = (OPT & kOptCull) && (OPT & kOptPair);
-    float4* lds_tri = lds;
-    float4* lds_sph = lds + (size_t)p.ntri_pairs * kTriPairFloat4;
-    float2* lds_tab = reinterpret_cast<float2*>(lds_sph + (size_t)p.nsph_pairs * kSphPairFloat4);
-    float* lds_tab_n = reinterpret_cast<float*>(lds_tab + ((p.spp + 1u) & ~1u));
-    uint4* lds_cm = reinterpret_cast<uint4*>(lds_tab_n + ((p.spp + 3u) & ~3u));
-    float4* ring_res = reinterpret_cast<float4*>(lds_cm + kChainBlock);        // [group][ring]
-    uint32_t* ring_tag = reinterpret_cast<uint32_t*>(ring_res + kG * kR);
-    uint32_t* ring_st = ring_tag + kG * kR;                     // 5 planes [group][ring]
-    // per group: 0 pixel (~0u none), 1 px, 2 py, 3 d0, 4 generation, 5 limit, 6 finishing, 7 ptr, 8 tile
-    uint32_t* grp = ring_st + 5 * kG * kR;
-    float* lds_stk = reinterpret_cast<float*>(grp + 16 * kG);         // [depth][lane]
-
-    for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kChainBlock)
-        lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
-    for (uint32_t i = threadIdx.x; i < p.nsph_pairs * kSphPairFloat4; i += kChainBlock)
-        lds_sph[i] = reinterpret_cast<const float4*>(p.sph_pairs)[i];
-    for (uint32_t s = threadIdx.x; s < p.spp; s += kChainBlock) {
-        const uint64_t n = p.frame0 + s + 1;
-        lds_tab[s] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
-        lds_tab_n[s] = (float)n;
-    }
-    for (uint32_t i = threadIdx.x; i < kG * kR; i += kChainBlock) ring_tag[i] = ~0u;
-    for (uint32_t i = threadIdx.x; i < 16 * kG; i += kChainBlock) grp[i] = (i % 16u) == 0u ? ~0u : 0u;
-    __syncthreads();
-    if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);     // the longest chains of the launch
-
-    const uint32_t lane = threadIdx.x;
-    const uint32_t g = lane / kL, li = lane % kL;
-    const bool walker = li == 0u;
-    uint32_t* const G = grp + 16 * g;
-    // walker registers: the pixel's chain
-    uint32_t w_pix = ~0u, w_ptr = 0u, w_k = 0u;
-    bool w_done = false, w_fin = false;
-    float ax = 0.0f, ay = 0.0f, az = 0.0f;
-    unsigned long long w_rays = 0;
-    // lane registers: the slot being traced (or the next one) and its start state (v0..v4; d follows)
-    bool active = false;
-    int depth = 0;
-    ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
-    uint32_t b0 = 0u, b1 = 0u, b2 = 0u, b3 = 0u, b4 = 0u, cslot = 0u, gen_seen = 0u;
-    uint32_t guard = 0u;               // iterations: a bound every wave reaches (never expected to bind)
-
-    while (true) {
-        if (++guard > p.iter_limit) {
-            if (lane == 0 && p.ovl_err) atomicOr(p.ovl_err, 2u);
-            break;
-        }
-        // ---- A. walkers: finish a complete chain, take a pixel, follow the chain
-        if (walker) {
-            if (w_fin) {
-                // the state at the chain's end: slot ptr's start state (phase B made sure it is stored)
-                const uint32_t e = g * kR + w_ptr % kR;
-                const uint32_t pix = w_pix;
-                const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
-                const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
-                const uint32_t bb = to_u8(255.0f * iq_sqrtf(az));
-                p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = bb | (g8 << 8) | (r8 << 16) | (255u << 24);
-                reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
-                p.rng[pix] = ring_st[e];
-                p.rng[(size_t)p.npix + pix] = ring_st[kG * kR + e];
-                p.rng[2 * (size_t)p.npix + pix] = ring_st[2 * kG * kR + e];
-                p.rng[3 * (size_t)p.npix + pix] = ring_st[3 * kG * kR + e];
-                p.rng[4 * (size_t)p.npix + pix] = ring_st[4 * kG * kR + e];
-                p.rng[5 * (size_t)p.npix + pix] = G[3] + 2u * w_ptr * IQ_XORWOW_WEYL;
-                w_pix = ~0u;
-                w_fin = false;
-                G[0] = ~0u;
-                G[6] = 0u;
-            }
-            if (w_pix == ~0u && !w_done) {
-                uint32_t pix = ~0u;
-                while (true) {
-                    const uint32_t q = atomicAdd(p.queue + 1, 1u);
-                    if (q >= p.ns_cap) {
-                        w_done = true;
-                        break;
-                    }
-                    pix = p.sp_pix[q];
-                    if (pix != ~0u) break;
-                }
-                if (!w_done) {
-                    // the pixel's accumulator, RNG state and tile mask words in one round of loads; the
-                    // group's lanes read them from G (no second round trip in phase B)
-                    w_pix = pix;
-                    w_ptr = 0u;
-                    w_k = 0u;
-                    uint32_t col, row;
-                    tile_decode(pix, p.ncols, p.nrows, &col, &row);
-                    const uint32_t t = (row / kCullTile) * p.ntx + col / kCullTile;
-                    const float* a = reinterpret_cast<const float*>(p.lin + pix);
-                    ax = a[0];
-                    ay = a[1];
-                    az = a[2];
-                    const uint32_t r0 = p.rng[pix], r1 = p.rng[(size_t)p.npix + pix], r2 = p.rng[2 * (size_t)p.npix + pix],
-                                   r3 = p.rng[3 * (size_t)p.npix + pix], r4 = p.rng[4 * (size_t)p.npix + pix],
-                                   r5 = p.rng[5 * (size_t)p.npix + pix];
-                    uint32_t cm0 = 0u, cm1 = 0u;
-                    if (kCull && p.cull) {
-                        cm0 = p.cull[(size_t)t * p.cull_stride];
-                        cm1 = p.cull[(size_t)t * p.cull_stride + p.cull_wt];
-                    }
-                    G[0] = pix;
-                    G[1] = p.x0 + col;
-                    G[2] = p.y0 + row * p.ystep;
-                    G[3] = r5;
-                    G[4] = G[4] + 1u;
-                    G[6] = 0u;
-                    G[7] = 0u;
-                    G[8] = t;
-                    G[9] = r0;
-                    G[10] = r1;
-                    G[11] = r2;
-                    G[12] = r3;
-                    G[13] = r4;
-                    G[14] = cm0;
-                    G[15] = cm1;
-                    for (uint32_t i = 0; i < kR; ++i) ring_tag[g * kR + i] = ~0u;
-                }
-            }
-            if (w_pix != ~0u) {
-                // fold the finished slots on the chain, in sample order (path_tracer.cu:356-358)
-                while (w_k < p.spp) {
-                    const uint32_t e = g * kR + w_ptr % kR;
-                    if (ring_tag[e] != w_ptr) break;
-                    const float4 r = ring_res[e];
-                    const uint32_t nsl = __float_as_uint(r.w);
-                    if (nsl == 0u) break;
-                    const float2 tv = lds_tab[w_k];
-                    float qx, qy, qz;
-                    mean_terms<OPT>(r.x, r.y, r.z, lds_tab_n[w_k], tv.x, p.mean_tiny, qx, qy, qz);
-                    ax = qx + ax * tv.y;
-                    ay = qy + ay * tv.y;
-                    az = qz + az * tv.y;
-                    w_rays += (nsl - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : nsl;
-                    w_ptr += nsl;
-                    ++w_k;
-                }
-                G[7] = w_ptr;
-                const uint32_t rem = p.spp - w_k;
-                const uint32_t ahead = min(kR, max(kL, rem + rem / 2u + 1u));
-                G[5] = w_ptr + ahead;
-                if (w_k == p.spp) {
-                    G[6] = 1u;
-                    w_fin = true;
-                }
-            }
-        }
-        __syncthreads();
-        // ---- B. lanes: a new pixel, a chain's end, slot starts
-        const uint32_t gpix = G[0];
-        const uint32_t gen = G[4];
-        if (gpix != ~0u && gen != gen_seen) {
-            gen_seen = gen;
-            active = false;
-            cslot = li;
-            b0 = G[9];
-            b1 = G[10];
-            b2 = G[11];
-            b3 = G[12];
-            b4 = G[13];
-            xorwow_skip_v(b0, b1, b2, b3, b4, 2u * li);
-            if (kCull && p.cull) lds_cm[lane] = make_uint4(G[14], G[15], G[8], 0u);
-        }
-        // a slot still being traced that the chain has passed was not on it (the walker folds only
-        // finished slots): it is dead, so stop tracing it
-        if (gpix != ~0u && active && G[6] == 0u && cslot < G[7]) active = false;
-        if (gpix != ~0u && G[6] != 0u) {
-            // the chain is complete: drop the speculative slots; the lane of slot ptr provides its state
-            active = false;
-            const uint32_t ptr = G[7];
-            const uint32_t e = g * kR + ptr % kR;
-            if (li == ptr % kL && ring_tag[e] != ptr) {
-                // not started: cslot <= ptr (slots start in order), so step forward
-                xorwow_skip_v(b0, b1, b2, b3, b4, 2u * (ptr - cslot));
-                cslot = ptr;
-                ring_st[e] = b0;
-                ring_st[kG * kR + e] = b1;
-                ring_st[2 * kG * kR + e] = b2;
-                ring_st[3 * kG * kR + e] = b3;
-                ring_st[4 * kG * kR + e] = b4;
-                ring_tag[e] = ptr;
-            }
-        } else if (gpix != ~0u && !active && cslot < G[5]) {
-            const uint32_t ptr = G[7];
-            // slots behind the chain (inside a folded sample's scatter draws) are dead: step past them to
-            // this lane's first slot at or after ptr instead of tracing them (2 kL draws per slot skipped)
-            while (cslot < ptr) {
-                xorwow_skip_v(b0, b1, b2, b3, b4, 2u * kL);
-                cslot += kL;
-            }
-        }
-        if (gpix != ~0u && G[6] == 0u && !active && cslot < G[5]) {
-            // start slot cslot: the state 2 cslot draws into the pixel's stream
-            const uint32_t e = g * kR + cslot % kR;
-            ring_st[e] = b0;
-            ring_st[kG * kR + e] = b1;
-            ring_st[2 * kG * kR + e] = b2;
-            ring_st[3 * kG * kR + e] = b3;
-            ring_st[4 * kG * kR + e] = b4;
-            ring_tag[e] = cslot;
-            ring_res[e].w = 0.0f;
-            st = {b0, b1, b2, b3, b4, G[3] + 2u * cslot * IQ_XORWOW_WEYL};
-            camera_ray<OPT>(p, G[1], G[2], st, ray);
-            depth = 0;
-            active = true;
-        }
-        const bool more = walker && !w_done;
-        if (!__any(active) && !__any(more) && !__any(w_fin)) break;
-        __syncthreads();
-        if (!__any(active)) continue;
-
-        // ---- C. one bounce of every traced slot (the anchored kernel's closest hit and shading)
-        float closest = kTMax;
-        int kind = kHitNone;
-        uint32_t hidx = 0;
-        if (kCull && p.cull != nullptr) {
-            const bool cull = !__any(active && depth != 0);
-            const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)lds_cm[lane].z * p.cull_stride : nullptr;
-            uint4 cm = lds_cm[lane];
-            const uint64_t act = __ballot(active);
-            const uint32_t first = (uint32_t)__builtin_ctzll(act);
-            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
-            const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
-            if (uni) {
-                cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
-                cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
-            }
-            const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
-            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray, closest,
-                                  kind, hidx, p.cull_wt, uni_mask);
-        } else if (active) {
-            intersect_range<OPT>(lds_tri, 0, p.ntri, lds_sph, 0, p.nsph, ray, closest, kind, hidx);
-        }
-        if (active) {
-            bool term = false;
-            uint32_t md_end = 0;
-            float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
-            if (kind == kHitSphere) {
-                const float* q = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
-                const float4 sphr = make_float4(q[0], q[2], q[4], q[6]);
-                const float s = oren_nayar_scatter<OPT>(sphr, closest, ray, st);
-                if (depth + 1 >= p.max_depth) {
-                    term = true;
-                    md_end = 1;
-                    Lx = s;
-                    Ly = s;
-                    Lz = s;
-                } else {
-                    lds_stk[(uint32_t)depth * kChainBlock + lane] = s;
-                    ++depth;
-                }
-            } else if (kind == kHitTri) {
-                term = true;
-                Lx = 10.0f;
-                Ly = 10.0f;
-                Lz = 10.0f;
-            } else {
-                term = true;
-                const float a = (ray.dy + 1.0f) * 0.5f;
-                const float one_a = 1.0f - a;
-                Lx = one_a + a * 0.5f;
-                Ly = one_a + a * 0.7f;
-                Lz = one_a + a * 1.0f;
-            }
-            if (term) {
-                float cx = Lx, cy = Ly, cz = Lz;
-                for (int i = depth - 1; i >= 0; --i) {
-                    const float r = lds_stk[(uint32_t)i * kChainBlock + lane];
-                    cx = cx * r;
-                    cy = cy * r;
-                    cz = cz * r;
-                }
-                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                cx = 0.0f + cx;
-                cy = 0.0f + cy;
-                cz = 0.0f + cz;
-                // slots consumed: 1 + the scatters (two draws each)
-                const uint32_t nsl = (uint32_t)depth + 1u + md_end;
-                ring_res[g * kR + cslot % kR] = make_float4(cx, cy, cz, __uint_as_float(nsl));
-                xorwow_skip_v(b0, b1, b2, b3, b4, 2u * kL);
-                cslot += kL;
-                active = false;
-            }
-        }
-        __syncthreads();
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) w_rays += __shfl_xor(w_rays, off);
-    if (lane == 0 && w_rays) add_rays(p.rays, w_rays);
-}
-
-// ------------------------------------------------------------------------------------------------
 // Sample-parallel anchored tiles (iqpt_fan_kernel). A tile whose camera rays cannot
 // reach a sphere (no sphere bit in its §3.3 mask) under the reference's materials (every triangle
 // emissive, path_tracer.cu:248-249, 278) ends every path on its first ray: an emissive hit or the sky
@@ -3668,7 +3348,6 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
     const bool rec_w = s.tl != nullptr && (threadIdx.x & 63u) == 0u;
     uint64_t t_rec[3] = {rec ? __builtin_amdgcn_s_memrealtime() : 0ull, 0ull, 0ull};
     uint32_t rounds = 0, iters = 0;                          // measurement: this wave's slot-loop iterations
-    uint32_t it_done = 0;                                     // this wave's slot-loop iterations so far (priority)
     uint32_t lane_rays = 0;                                  // rays of the chain samples this lane gathered
     __syncthreads();
 
@@ -3747,18 +3426,6 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             if (active) start_slot();
             while (__any(active)) {
                 if (rec_w) ++iters;
-                // progress-fair VALU priority (s.prio_q, round 5): every spec block is resident from the start and
-                // the SIMDs arbitrate by priority, then age, so at one priority the youngest blocks (dispatched
-                // last) only issue when older waves stall and end last; a wave's priority falls from 3 by one
-                // level per prio_q iterations it has run, so a wave that lags keeps the higher level
-                if ((OPT & kOptPrio) && s.prio_q) {
-                    const uint32_t lvl = it_done / s.prio_q;
-                    if (lvl == 0u) __builtin_amdgcn_s_setprio(3);
-                    else if (lvl == 1u) __builtin_amdgcn_s_setprio(2);
-                    else if (lvl == 2u) __builtin_amdgcn_s_setprio(1);
-                    else __builtin_amdgcn_s_setprio(0);
-                }
-                ++it_done;
                 // closest hit (path_tracer.cu:253-295): camera rays over their tile's mask pairs in index order
                 float closest = kTMax;
                 int kind = kHitNone;
@@ -3905,7 +3572,6 @@ __device__ __forceinline__ void spec_body(const kparams& p, const kspec& s, uint
             // a fix-up pass) ends the wave's pixels: the highest priority
             __builtin_amdgcn_s_waitcnt(0);
             wave_sync();
-            if ((OPT & kOptPrio) && s.prio_q) __builtin_amdgcn_s_setprio(3);
             if (rec && rounds == 0u && pass == 0u) t_rec[1] = __builtin_amdgcn_s_memrealtime();
             walk();
             if (pass == 1u) break;
@@ -4079,555 +3745,6 @@ __global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p)
 template <int MAXD, int OPT>
 __global__ __launch_bounds__(kSpecBlock, 4) void iqpt_spec_kernel(const kparams p, const kspec s) {
     spec_body<MAXD, OPT>(p, s, blockIdx.x);
-}
-
-// ------------------------------------------------------------------------------------------------
-// Queue mode. The block-per-pixel-set kernel above ends when its heaviest blocks'
-// slot loops and walks do (every spec block is resident at once, so no ordering moves work between them).
-// Here persistent waves share the work while it runs:
-//  * a wave holds up to kSpecQRecs sphere pixels (records in LDS) and takes the next one from its XCD's
-//    cursor over the plan's order (heaviest first; another XCD's once its own list is done) whenever fewer
-//    than 64 of its pixels' slots are left to hand out;
-//  * each iteration, its idle lanes take the next slots of its pixels (one or two consecutive slots of one
-//    pixel each; the start state from the pixel's checkpoints in LDS, a few draws on) and every lane traces
-//    one ray, so no lane waits for a longer range of its pixel;
-//  * a pixel whose slots are all traced is walked at once (the walk of spec_body: the chain in sample order
-//    through its LDS slot counts, colours gathered by the wave, the running mean folded in order), then
-//    finished, or given its odd slots from where the chain landed on one (parity pixels), or a new window
-//    (a chain past its window);
-// so the waves end together, at the last pixels' walks. Same per-slot code, same walk: the same bits.
-// iqpt_spec_prep_kernel runs first: each pixel's window (from its last chain, as spec_body) and the state
-// at every s.ck_step-th slot of it (one lane per pixel stepping its stream), and the cursors zeroed.
-constexpr uint32_t kSpecQRecs = 6;        // sphere pixels a wave holds at once
-constexpr uint32_t kSpecQRecWords = 24;   // words per record (96 B)
-static_assert(kSpecQRecWords == kSpecQRecWordsHost, "queue records");
-constexpr uint32_t kSpecQRun = 2;         // slots one lane takes at once while its pixels have many left
-enum : uint32_t {
-    kQq = 0, kQpix, kQjs, kQM, kQstart, kQstep, kQcnt, kQnext, kQax, kQay, kQaz, kQk, kQjw, kQflags, kQnc, kQd,
-    kQcm /* 16..19: mask words 0 of triangles and spheres, tile, - */, kQpx = 20, kQpy = 21
-};
-
-// the walk's jump tables: 6 levels of (window + 32) 16-bit entries, windows up to 224 slots (longer ones walk
-// their chain one sample at a time)
-__host__ __device__ inline uint32_t specq_jump_entries(uint32_t m_cap) { return (m_cap < 224u ? m_cap : 224u) + 32u; }
-__host__ __device__ inline uint32_t specq_scratch_bytes(uint32_t m_cap) {
-    const uint32_t t = (6u * specq_jump_entries(m_cap) * 2u + 15u) & ~15u;
-    return t > 64u * 16u ? t : 64u * 16u;
-}
-__host__ __device__ inline uint32_t specq_wave_bytes(uint32_t m_cap, uint32_t ncp) {
-    const uint32_t b = specq_scratch_bytes(m_cap) + kSpecQRecs * kSpecQRecWords * 4u + 16u + kSpecQRecs * ncp * 20u +
-                       kSpecQRecs * m_cap;
-    return (b + 15u) & ~15u;
-}
-__host__ __device__ inline uint32_t specq_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, int max_depth, uint32_t spp,
-                                                    uint32_t m_cap, uint32_t ncp) {
-    const uint32_t sp4 = (spp + 3u) & ~3u;
-    return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + sp4 * 12u +
-           spec_stack_depth(max_depth) * kSpecBlock * 4u + (kSpecBlock / 64u) * specq_wave_bytes(m_cap, ncp);
-}
-
-__global__ __launch_bounds__(256) void iqpt_spec_prep_kernel(const kparams p, const kspec s) {
-    // one lane per queue position o (sphere pixel q = order[o]): the record image a wave copies into LDS when it
-    // takes position o, and the checkpoints, both at position o, so that taking a pixel is one round trip
-    const uint32_t o = blockIdx.x * 256u + threadIdx.x;
-    if (blockIdx.x == 0 && threadIdx.x < kSpecCursors * 16u) s.cursor[threadIdx.x] = 0u;
-    if (o >= s.n) return;
-    const uint32_t q = s.order ? s.order[o] : o;
-    const uint32_t pix = s.pix[q];
-    const uint32_t r0 = s.rho[q] ? s.rho[q] : s.rho0;
-    const uint32_t M = spec_window(r0, p.spp, s.m_cap, s.margin_div);
-    s.m[q] = M;
-    // parity pixel: the even slots first (spec_body's rd[14])
-    const bool parity = s.parity_rho != 0u && r0 >= s.parity_rho && r0 <= s.parity_hi;
-    const uint32_t nc = min(s.ncp, M / s.ck_step + 1u);   // slots 0, ck_step, ... up to M
-    uint32_t col = 0, row = 0;
-    tile_decode(pix, p.ncols, p.nrows, &col, &row);
-    const uint32_t t = (row / kCullTile) * p.ntx + col / kCullTile;
-    const float4 a = reinterpret_cast<const float4*>(p.lin)[pix];
-    uint4* rec = reinterpret_cast<uint4*>(s.qrec + (size_t)o * kSpecQRecWords);
-    rec[0] = make_uint4(q, pix, 0u, M);                                                  // q, pix, js, M
-    rec[1] = make_uint4(0u, parity ? 2u : 1u, parity ? (M + 1u) / 2u : M, 0u);           // start, step, cnt, next
-    rec[2] = make_uint4(__float_as_uint(a.x), __float_as_uint(a.y), __float_as_uint(a.z), 0u);   // acc, k
-    rec[3] = make_uint4(0u, 0u, nc, p.rng[5 * (size_t)p.npix + pix]);                    // jw, flags, nc, d
-    rec[4] = make_uint4(p.cull[(size_t)t * p.cull_stride], p.cull[(size_t)t * p.cull_stride + p.cull_wt], t, 0u);
-    rec[5] = make_uint4(p.x0 + col, p.y0 + row * p.ystep, 0u, 0u);                       // px, py
-    uint32_t v0 = p.rng[pix], v1 = p.rng[(size_t)p.npix + pix], v2 = p.rng[2 * (size_t)p.npix + pix],
-             v3 = p.rng[3 * (size_t)p.npix + pix], v4 = p.rng[4 * (size_t)p.npix + pix];
-    uint4* ck = reinterpret_cast<uint4*>(s.ck + (size_t)o * s.ncp * 8u);
-    for (uint32_t c = 0; c < nc; ++c) {
-        ck[2 * c] = make_uint4(v0, v1, v2, v3);
-        ck[2 * c + 1] = make_uint4(v4, 0u, 0u, 0u);
-        if (c + 1u < nc) xorwow_skip_v(v0, v1, v2, v3, v4, 2u * s.ck_step);
-    }
-}
-
-template <int MAXD, int OPT>
-__global__ __launch_bounds__(kSpecBlock, 4) void iqpt_specq_kernel(const kparams p, const kspec s) {
-    extern __shared__ __attribute__((aligned(16))) float4 lds[];
-    const uint32_t sp4 = (p.spp + 3u) & ~3u;
-    float4* lds_tri = lds;
-    float4* lds_sph = lds_tri + (size_t)p.ntri_pairs * kTriPairFloat4;
-    float2* tab = reinterpret_cast<float2*>(lds_sph + (size_t)p.nsph_pairs * kSphPairFloat4);
-    float* tab_n = reinterpret_cast<float*>(tab + sp4);
-    float* lds_stk = tab_n + sp4;                                                       // [depth][thread]
-    uint8_t* wb = reinterpret_cast<uint8_t*>(lds_stk + (size_t)spec_stack_depth(p.max_depth) * kSpecBlock) +
-                  (size_t)(threadIdx.x >> 6) * specq_wave_bytes(s.m_cap, s.ncp);
-    // walk scratch: the jump tables, then (after the chain is known) the batch's mean terms
-    float4* lc = reinterpret_cast<float4*>(wb);
-    uint16_t* JT = reinterpret_cast<uint16_t*>(wb);
-    const uint32_t tb = specq_jump_entries(s.m_cap);
-    uint32_t* R = reinterpret_cast<uint32_t*>(wb + specq_scratch_bytes(s.m_cap));       // [record][kSpecQRecWords]
-    uint32_t* CK = R + kSpecQRecs * kSpecQRecWords + 4u;                               // [record][ncp][5] states
-    uint8_t* LN = reinterpret_cast<uint8_t*>(CK + (size_t)kSpecQRecs * s.ncp * 5u);    // [record][slot] counts
-    for (uint32_t i = threadIdx.x; i < p.ntri_pairs * kTriPairFloat4; i += kSpecBlock)
-        lds_tri[i] = reinterpret_cast<const float4*>(p.tri_pairs)[i];
-    for (uint32_t i = threadIdx.x; i < p.nsph_pairs * kSphPairFloat4; i += kSpecBlock)
-        lds_sph[i] = reinterpret_cast<const float4*>(p.sph_pairs)[i];
-    for (uint32_t k = threadIdx.x; k < p.spp; k += kSpecBlock) {
-        const uint64_t n = p.frame0 + k + 1;
-        tab[k] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
-        tab_n[k] = (float)n;
-    }
-    __syncthreads();   // the last block-wide step: the waves are independent from here
-    if (OPT & kOptPrio) __builtin_amdgcn_s_setprio(3);
-    const uint32_t lane = __lane_id();
-    const uint32_t xcd = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 7u;   // HW_REG_XCC_ID
-    const uint64_t t_start = s.tl ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    uint32_t n_iter = 0, n_pix = 0, n_walk = 0, n_fix = 0;   // measurement
-    uint32_t t_phase[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};   // measurement (10-ns ticks): admissions, walks,
-                                                                         // hand-outs, rays; the walks' wait, chain,
-                                                                         // gather + terms, fold
-    uint32_t t_mark = (uint32_t)t_start;
-    auto phase = [&](int i) {
-        if (s.tl) {
-            const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
-            t_phase[i] += t - t_mark;
-            t_mark = t;
-        }
-    };
-
-    // wave-uniform: records in use, records with slots left to hand out, cursors tried past this XCD's own
-    uint32_t used = 0, open = 0, xs = 0;
-    bool exhausted = false;
-    // lane 0: the next position of cursor xs, taken ahead of the admission that uses it
-    uint32_t pf_pos = lane == 0u ? atomicAdd(s.cursor + 16u * xcd, 1u) : 0u;
-    // lane: the slots [jc, je) step sp of record h it traces (jc the current one), the sample's state
-    bool active = false;
-    uint32_t h = 0, jc = 0, je = 0, sp = 1, cq = 0;   // (cq: the record's sphere pixel; the rest is read from LDS)
-    rng6 st = {0u, 0u, 0u, 0u, 0u, 0u};
-    rng6 base = st;
-    ray3 ray = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
-    int depth = 0;
-    uint32_t lane_rays = 0;                 // rays of the chain samples this lane gathered
-    uint32_t stalls = 0;                    // iterations without a traced ray (never more than one in a row)
-    auto start_slot = [&]() {
-        const uint32_t* rh = R + h * kSpecQRecWords;
-        camera_ray<OPT>(p, rh[kQpx], rh[kQpy], st, ray);
-        base = st;
-        depth = 0;
-    };
-
-    while (true) {
-        phase(3);
-        // ---- (a) take pixels while fewer than 64 slots are left to hand out
-        uint32_t avail = 0;
-        for (uint32_t m = open; m; m &= m - 1u) {
-            const uint32_t* rr = R + (uint32_t)__builtin_ctz(m) * kSpecQRecWords;
-            avail += rr[kQcnt] - rr[kQnext];
-        }
-        while (!exhausted && used != (1u << kSpecQRecs) - 1u && avail < 64u) {
-            // the position taken from cursor xs at the last admission (its atomic's latency hidden behind the work
-            // since), else, past that list's end, the next cursors in turn; then the next position is taken ahead
-            uint32_t o = ~0u;
-            if (lane == 0u) {
-                uint64_t oo = (uint64_t)((xcd + xs) & (kSpecCursors - 1u)) + (uint64_t)kSpecCursors * pf_pos;
-                while (oo >= s.n) {
-                    if (++xs >= kSpecCursors) break;
-                    pf_pos = atomicAdd(s.cursor + 16u * ((xcd + xs) & (kSpecCursors - 1u)), 1u);
-                    oo = (uint64_t)((xcd + xs) & (kSpecCursors - 1u)) + (uint64_t)kSpecCursors * pf_pos;
-                }
-                if (xs < kSpecCursors) {
-                    o = (uint32_t)oo;
-                    pf_pos = atomicAdd(s.cursor + 16u * ((xcd + xs) & (kSpecCursors - 1u)), 1u);
-                }
-            }
-            o = (uint32_t)__builtin_amdgcn_readfirstlane((int)o);
-            xs = (uint32_t)__builtin_amdgcn_readfirstlane((int)xs);
-            if (o == ~0u) {
-                exhausted = true;
-                break;
-            }
-            const uint32_t r = (uint32_t)__builtin_ctz(~used);
-            uint32_t* rr = R + r * kSpecQRecWords;
-            // the record image (iqpt_spec_prep_kernel) and the checkpoints of position o, one round trip
-            {
-                const uint32_t* img = s.qrec + (size_t)o * kSpecQRecWords;
-                const uint4* src = reinterpret_cast<const uint4*>(s.ck + (size_t)o * s.ncp * 8u);
-                const uint32_t w = lane < kSpecQRecWords ? img[lane] : 0u;
-                uint32_t* dst = CK + (size_t)r * s.ncp * 5u;
-                // every checkpoint record of the position (those past the pixel's nc are never read): the loads
-                // do not wait for the record's
-                for (uint32_t i = lane; i < 2u * s.ncp; i += 64u) {
-                    const uint4 v = src[i];
-                    if (i & 1u) dst[(i >> 1) * 5u + 4u] = v.x;
-                    else {
-                        dst[(i >> 1) * 5u] = v.x;
-                        dst[(i >> 1) * 5u + 1u] = v.y;
-                        dst[(i >> 1) * 5u + 2u] = v.z;
-                        dst[(i >> 1) * 5u + 3u] = v.w;
-                    }
-                }
-                if (lane < kSpecQRecWords) rr[lane] = w;
-                avail += (uint32_t)__builtin_amdgcn_readlane((int)w, (int)kQcnt);
-            }
-            used |= 1u << r;
-            open |= 1u << r;
-            ++n_pix;
-            wave_sync();
-        }
-
-        phase(0);
-        // ---- (b) walk the pixels whose slots are all traced (no slot handed out, none in flight)
-        for (uint32_t m = used & ~open; m; m &= m - 1u) {
-            const uint32_t r = (uint32_t)__builtin_ctz(m);
-            if (__any(active && h == r)) continue;
-            // the colours are this wave's own stores (complete: vmcnt 0), read back from L2
-            uint32_t tw = s.tl ? (uint32_t)__builtin_amdgcn_s_memrealtime() : 0u;
-            auto sub = [&](int i) {
-                if (s.tl) {
-                    const uint32_t t = (uint32_t)__builtin_amdgcn_s_memrealtime();
-                    t_phase[4 + i] += t - tw;
-                    tw = t;
-                }
-            };
-            __builtin_amdgcn_s_waitcnt(0);
-            wave_sync();
-            sub(0);
-            ++n_walk;
-            uint32_t* rr = R + r * kSpecQRecWords;
-            const uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane((int)rr[kQq]);
-            const uint32_t M = (uint32_t)__builtin_amdgcn_readfirstlane((int)rr[kQM]);
-            const uint32_t js = (uint32_t)__builtin_amdgcn_readfirstlane((int)rr[kQjs]);
-            uint32_t jw = (uint32_t)__builtin_amdgcn_readfirstlane((int)rr[kQjw]);
-            uint32_t k = (uint32_t)__builtin_amdgcn_readfirstlane((int)rr[kQk]);
-            float ax = __uint_as_float(rr[kQax]), ay = __uint_as_float(rr[kQay]), az = __uint_as_float(rr[kQaz]);
-            const uint8_t* ln = LN + (size_t)r * s.m_cap;
-            const uint32_t* lnw = reinterpret_cast<const uint32_t*>(ln);
-            const float4* res = reinterpret_cast<const float4*>(s.res) + (size_t)q * s.m_cap;
-            // the slot counts of 256 slots at a time in registers (lane i: slots 4i .. 4i + 3 of the chunk): the chain
-            // is followed with uniform lane reads instead of one dependent LDS load per sample
-            uint32_t chunk = ~0u, word = 0u;
-            // jump tables (windows up to 224 slots): level t maps a slot to the chain's slot 2^t samples on
-            // (positions where the chain stops — an untraced slot, past the window — map to themselves), so lane i
-            // finds the batch's sample i in at most 6 lookups instead of the walker's 64 dependent steps
-            const bool jump = M + 32u <= tb;
-            while (true) {
-                uint32_t c = 0, mypos = 0;
-                if (jump) {
-                    const uint32_t ne = M + 32u;
-                    for (uint32_t e = lane; e < ne; e += 64u) {
-                        const uint32_t n = e < M ? (uint32_t)ln[e] : 0u;
-                        JT[e] = (uint16_t)(n ? e + n : e);
-                    }
-                    wave_sync();
-                    for (uint32_t t = 0; t < 5u; ++t) {
-                        const uint16_t* Ta = JT + t * tb;
-                        uint16_t* Tn = JT + (t + 1u) * tb;
-                        for (uint32_t e = lane; e < ne; e += 64u) Tn[e] = Ta[Ta[e]];
-                        wave_sync();
-                    }
-                    uint32_t pp = jw;
-#pragma unroll
-                    for (uint32_t t = 0; t < 6u; ++t)
-                        if ((lane >> t) & 1u) pp = JT[t * tb + pp];
-                    const bool valid = pp < M && ln[pp] != 0u && k + lane < p.spp;
-                    c = (uint32_t)__popcll(__ballot(valid));   // a prefix of the lanes: stops are fixed points
-                    mypos = pp;
-                    if (c > 0u) {
-                        const uint32_t last = (uint32_t)__builtin_amdgcn_readlane((int)pp, (int)(c - 1u));
-                        jw = (uint32_t)__builtin_amdgcn_readfirstlane((int)JT[last]);
-                    }
-                    wave_sync();   // (the terms below overwrite the tables)
-                }
-                while (!jump && c < 64u && k + c < p.spp && jw < M) {
-                    const uint32_t ch = jw >> 8;
-                    if (ch != chunk) {
-                        chunk = ch;
-                        const uint32_t wi = ch * 64u + lane;
-                        word = wi * 4u < s.m_cap ? lnw[wi] : 0u;
-                    }
-                    const uint32_t nj =
-                        ((uint32_t)__builtin_amdgcn_readlane((int)word, (int)((jw >> 2) & 63u)) >> (8u * (jw & 3u))) & 0xffu;
-                    if (nj == 0u) break;
-                    if (lane == c) mypos = jw;
-                    ++c;
-                    jw += nj;
-                }
-                sub(1);
-                if (c == 0u) break;
-                if (lane < c) {
-                    const uint32_t* src = reinterpret_cast<const uint32_t*>(res + mypos);
-                    const float cx = __uint_as_float(__hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    const float cy = __uint_as_float(__hip_atomic_load(src + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    const float cz = __uint_as_float(__hip_atomic_load(src + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-                    const float2 tv = tab[k + lane];
-                    float qx, qy, qz;
-                    mean_terms<OPT>(cx, cy, cz, tab_n[k + lane], tv.x, p.mean_tiny, qx, qy, qz);
-                    lc[lane] = make_float4(qx, qy, qz, tv.y);
-                    const uint32_t n = ln[mypos];
-                    lane_rays += (n - 1u == (uint32_t)p.max_depth) ? (uint32_t)p.max_depth : n;
-                }
-                wave_sync();
-                sub(2);
-                if (lane == 0u)
-#pragma unroll 8
-                    for (uint32_t i = 0; i < c; ++i) {
-                        const float4 v = lc[i];
-                        ax = v.x + ax * v.w;
-                        ay = v.y + ay * v.w;
-                        az = v.z + az * v.w;
-                    }
-                k += c;
-                wave_sync();
-                sub(3);
-                if (c < 64u) break;
-            }
-            if (k == p.spp) {
-                // finished: the state at the chain's end, slot js + jw, from the checkpoint at or below it
-                if (lane == 0u) {
-                    const uint32_t pix = rr[kQpix];
-                    const uint32_t ja = js + jw;
-                    const uint32_t c = min(ja / s.ck_step, rr[kQnc] - 1u);
-                    const uint32_t* cp = CK + ((size_t)r * s.ncp + c) * 5u;
-                    uint32_t v0 = cp[0], v1 = cp[1], v2 = cp[2], v3 = cp[3], v4 = cp[4];
-                    xorwow_skip_v(v0, v1, v2, v3, v4, 2u * (ja - c * s.ck_step));
-                    const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
-                    const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
-                    const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
-                    p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
-                    reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
-                    p.rng[pix] = v0;
-                    p.rng[(size_t)p.npix + pix] = v1;
-                    p.rng[2 * (size_t)p.npix + pix] = v2;
-                    p.rng[3 * (size_t)p.npix + pix] = v3;
-                    p.rng[4 * (size_t)p.npix + pix] = v4;
-                    p.rng[5 * (size_t)p.npix + pix] = rr[kQd] + 2u * ja * IQ_XORWOW_WEYL;
-                    s.rho[q] = (uint32_t)(((uint64_t)ja * 256u) / p.spp);
-                }
-                used &= ~(1u << r);
-            } else {
-                if (lane == 0u) {
-                    rr[kQax] = __float_as_uint(ax);
-                    rr[kQay] = __float_as_uint(ay);
-                    rr[kQaz] = __float_as_uint(az);
-                    rr[kQk] = k;
-                    rr[kQnext] = 0u;
-                    if (jw < M && (rr[kQflags] & 1u) == 0u) {
-                        // a parity pixel's chain landed on an odd slot (untraced, count 0): the odd slots from
-                        // there to the window's end (the even ones are traced, so the next walk reaches the end)
-                        atomicAdd(s.run_count, 1u);
-                        rr[kQflags] |= 1u;
-                        rr[kQjw] = jw;
-                        rr[kQstart] = jw;
-                        rr[kQstep] = 2u;
-                        rr[kQcnt] = (M - jw + 1u) / 2u;
-                    } else if (jw < M) {
-                        // (not expected: every slot from jw on is traced) every slot from jw
-                        rr[kQjw] = jw;
-                        rr[kQstart] = jw;
-                        rr[kQstep] = 1u;
-                        rr[kQcnt] = M - jw;
-                    } else {
-                        // the chain left its window: a new one from its end, sized for the remaining samples,
-                        // every slot traced (spec_body's rounds)
-                        atomicAdd(s.run_count + 1, 1u);
-                        rr[kQjs] = js + jw;
-                        const uint32_t rem = p.spp - k;
-                        const uint32_t M2 = min(s.m_cap, max(16u, 3u * rem + 4u));
-                        rr[kQM] = M2;
-                        rr[kQjw] = 0u;
-                        rr[kQstart] = 0u;
-                        rr[kQstep] = 1u;
-                        rr[kQcnt] = M2;
-                    }
-                }
-                if (jw < M) ++n_fix;
-                open |= 1u << r;
-            }
-            wave_sync();
-        }
-
-        phase(1);
-        // ---- (c) hand the next slots of the wave's pixels to its idle lanes, oldest record first
-        const uint64_t idle = __ballot(!active);
-        bool fresh = false;
-        if (idle != 0ull && open != 0u) {
-            const uint32_t nid = (uint32_t)__popcll(idle), rank = prefix_below(idle);
-            uint32_t b = 0;
-            for (uint32_t m = open; m && b < nid; m &= m - 1u) {
-                const uint32_t r = (uint32_t)__builtin_ctz(m);
-                uint32_t* rr = R + r * kSpecQRecWords;
-                const uint32_t nx = rr[kQnext], cn = rr[kQcnt];
-                const uint32_t av = cn - nx;
-                const uint32_t run = av >= 2u * 64u ? kSpecQRun : 1u;
-                const uint32_t nl = min(nid - b, (av + run - 1u) / run);
-                const uint32_t take = min(av, nl * run);
-                if (!active && rank >= b && rank < b + nl) {
-                    const uint32_t i0 = nx + (rank - b) * run;
-                    const uint32_t ni = min(run, nx + take - i0);
-                    const uint32_t st0 = rr[kQstart], stp = rr[kQstep];
-                    h = r;
-                    jc = st0 + stp * i0;
-                    je = jc + stp * ni;
-                    sp = stp;
-                    fresh = true;
-                }
-                wave_sync();
-                if (lane == 0u) rr[kQnext] = nx + take;
-                if (nx + take == cn) open &= ~(1u << r);
-                b += nl;
-            }
-            wave_sync();
-            if (fresh) {
-                // the slot's state: the record's checkpoint at or below it, stepped on (2 draws per slot)
-                const uint32_t* rr = R + h * kSpecQRecWords;
-                const uint32_t q = rr[kQq], js = rr[kQjs];
-                const uint32_t ja = js + jc;
-                const uint32_t c = min(ja / s.ck_step, rr[kQnc] - 1u);
-                const uint32_t* cp = CK + ((size_t)h * s.ncp + c) * 5u;
-                st = {cp[0], cp[1], cp[2], cp[3], cp[4], rr[kQd] + 2u * ja * IQ_XORWOW_WEYL};
-                xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * (ja - c * s.ck_step));
-                cq = q;
-                active = true;
-                start_slot();
-            }
-        }
-        phase(2);
-        if (!__any(active)) {
-            if (used == 0u && exhausted) break;
-            // nothing traced this iteration: a taken pixel's first slots are handed out on the next (never
-            // twice in a row; the bound keeps a wave from spinning forever on a broken invariant)
-            if (++stalls > 4u) {
-                atomicOr(p.ovl_err, 16u);
-                break;
-            }
-            continue;
-        }
-        stalls = 0;
-
-        // ---- (d) one ray per active lane (spec_body's slot loop)
-        ++n_iter;
-        float closest = kTMax;
-        int kind = kHitNone;
-        uint32_t hidx = 0;
-        {
-            const bool cull = !__any(active && depth != 0);
-            uint4 cm = *reinterpret_cast<const uint4*>(R + h * kSpecQRecWords + kQcm);
-            const uint32_t* lane_mask = (cull && active) ? p.cull + (size_t)cm.z * p.cull_stride : nullptr;
-            const uint64_t act = __ballot(active);
-            const uint32_t first = (uint32_t)__builtin_ctzll(act);
-            const uint32_t t0 = (uint32_t)__builtin_amdgcn_readlane((int)cm.z, (int)first);
-            const bool uni = cull && __ballot(active && cm.z != t0) == 0ull;
-            if (uni) {
-                cm.x = (uint32_t)__builtin_amdgcn_readlane((int)cm.x, (int)first);
-                cm.y = (uint32_t)__builtin_amdgcn_readlane((int)cm.y, (int)first);
-            }
-            const uint32_t* uni_mask = uni ? p.cull + (size_t)t0 * p.cull_stride : nullptr;
-            intersect_culled<OPT>(lds_tri, p.ntri, lds_sph, p.nsph, lane_mask, cm.x, cm.y, !cull, active, ray, closest,
-                                  kind, hidx, p.cull_wt, uni_mask);
-        }
-        if (active) {
-            // shade (path_tracer.cu:297-316) under the reference's materials
-            bool term = false;
-            uint32_t md_end = 0;
-            float Lx = 0.0f, Ly = 0.0f, Lz = 0.0f;
-            if (kind == kHitSphere) {
-                const float* sq = reinterpret_cast<const float*>(lds_sph + (size_t)(hidx >> 1) * kSphPairFloat4) + (hidx & 1u);
-                const float sc = oren_nayar_scatter<OPT>(make_float4(sq[0], sq[2], sq[4], sq[6]), closest, ray, st);
-                if (depth + 1 >= p.max_depth) {
-                    term = true;                 // the last record is this scatter (biased, :252)
-                    md_end = 1;
-                    Lx = sc;
-                    Ly = sc;
-                    Lz = sc;
-                } else {
-                    lds_stk[(uint32_t)depth * kSpecBlock + threadIdx.x] = sc;
-                    ++depth;
-                }
-            } else if (kind == kHitTri) {
-                term = true;                     // emissive(1, 10)
-                Lx = 10.0f;
-                Ly = 10.0f;
-                Lz = 10.0f;
-            } else {
-                term = true;                     // sky gradient, :308-313
-                const float a = (ray.dy + 1.0f) * 0.5f;
-                const float one_a = 1.0f - a;
-                Lx = one_a + a * 0.5f;
-                Ly = one_a + a * 0.7f;
-                Lz = one_a + a * 1.0f;
-            }
-            if (term) {
-                // backward product (:321-324), clamp (:345-347), 0 + colour (:341, 348)
-                float cx = Lx, cy = Ly, cz = Lz;
-                for (int i = depth - 1; i >= 0; --i) {
-                    const float rr = lds_stk[(uint32_t)i * kSpecBlock + threadIdx.x];
-                    cx = cx * rr;
-                    cy = cy * rr;
-                    cz = cz * rr;
-                }
-                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
-                reinterpret_cast<float4*>(s.res)[(size_t)cq * s.m_cap + jc] = make_float4(0.0f + cx, 0.0f + cy, 0.0f + cz, 0.0f);
-                uint8_t* cln = LN + (size_t)h * s.m_cap;
-                cln[jc] = (uint8_t)((uint32_t)depth + 1u + md_end);   // slots: 1 + its scatters
-                // a parity pass (even slots): the odd slot after this one is untraced (0: the walk stops there)
-                if (sp == 2u && (jc & 1u) == 0u && jc + 1u < R[h * kSpecQRecWords + kQM]) cln[jc + 1u] = 0u;
-                jc += sp;
-                if (jc < je) {
-                    st = base;                   // slot jc starts where slot jc - 1's camera draws ended ...
-                    if (sp == 2u) {              // ... or two draws after that
-                        (void)xorwow_next(st);
-                        (void)xorwow_next(st);
-                    }
-                    start_slot();
-                } else {
-                    active = false;
-                }
-            }
-        }
-    }
-    if (s.tl && lane == 0u) {
-        const uint32_t wid = blockIdx.x * (kSpecBlock / 64u) + (threadIdx.x >> 6);
-        unsigned long long ph2 = 0;
-        for (int i = 0; i < 4; ++i)
-            ph2 |= (unsigned long long)(t_phase[4 + i] < 0xffffu ? t_phase[4 + i] : 0xffffu) << (16 * i);
-        s.tl[8 * (size_t)wid + 4] = ph2;
-        s.tl[8 * (size_t)wid] = t_start;
-        s.tl[8 * (size_t)wid + 1] =
-            (__builtin_amdgcn_s_memrealtime() & 0xffffffffffffull) | ((unsigned long long)min(n_iter, 0xffffu) << 48);
-        s.tl[8 * (size_t)wid + 2] = (unsigned long long)n_pix | ((unsigned long long)n_walk << 16) |
-                                    ((unsigned long long)n_fix << 32) | ((unsigned long long)xcd << 48);
-        // 10-ns ticks (16 bits each) in admissions, walks, hand-outs and the slot loop's rays
-        unsigned long long ph = 0;
-        for (int i = 0; i < 4; ++i) ph |= (unsigned long long)(t_phase[i] < 0xffffu ? t_phase[i] : 0xffffu) << (16 * i);
-        s.tl[8 * (size_t)wid + 3] = ph;
-    }
-    unsigned long long rays = lane_rays;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) rays += __shfl_xor(rays, off);
-    if (lane == 0u && rays) add_rays(p.rays, rays);
-}
-
-// LDS bytes of the chain kernel for a launch (scene pairs, mean table, mask slots, ring, group words,
-// scatter stack)
-__host__ __device__ inline uint32_t chain_lds_bytes(uint32_t ntri_pairs, uint32_t nsph_pairs, uint32_t spp, int max_depth,
-                                                    uint32_t lanes) {
-    const uint32_t groups = 64u / lanes, ring = kChainRingMul * lanes;
-    return ntri_pairs * kTriPairFloat4 * 16u + nsph_pairs * kSphPairFloat4 * 16u + ((spp + 1u) & ~1u) * 8u +
-           ((spp + 3u) & ~3u) * 4u + kChainBlock * 16u + groups * ring * (16u + 4u + 20u) + 16u * groups * 4u +
-           (uint32_t)(max_depth > 1 ? max_depth : 1) * kChainBlock * 4u;
 }
 
 // Events bound to the next kernel launch (bind_launch_events): recorded by the dispatch itself
@@ -4883,40 +4000,6 @@ int launch_split_stitch(void* stream, const ksplit& s, bool fastdiv) {
 }
 
 
-// kOptChain launches (iqpt_chain_kernel): the resident production option sets, reference materials
-namespace {
-template <int MAXD, int OPT, int L>
-int chain_launch_t(hipStream_t stream, const kparams& p, uint32_t grid, uint32_t lds) {
-    hipLaunchKernelGGL((iqpt_chain_kernel<MAXD, OPT, L>), dim3(grid), dim3(kChainBlock), lds, stream, p);
-    return (int)hipGetLastError();
-}
-template <int MAXD, int OPT, int L>
-int chain_occ_t(uint32_t lds, int* blocks) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_chain_kernel<MAXD, OPT, L>, kChainBlock, lds);
-}
-struct chain_variant {
-    int maxd, opt, lanes;
-    int (*launch)(hipStream_t, const kparams&, uint32_t, uint32_t);
-    int (*occ)(uint32_t, int*);
-};
-#define IQPT_CV(M, O, L) {M, O, L, chain_launch_t<M, O, L>, chain_occ_t<M, O, L>}
-#define IQPT_CV4(O) IQPT_CV(8, O, 8), IQPT_CV(16, O, 8), IQPT_CV(8, O, 4), IQPT_CV(16, O, 4), IQPT_CV(8, O, 16), \
-                    IQPT_CV(16, O, 16)
-const chain_variant kChainVariants[] = {
-    IQPT_CV4(kOptDefault | kOptPrio),
-    IQPT_CV4((kOptDefault & ~kOptFastDiv) | kOptPrio),
-    IQPT_CV4(kOptDefault | kOptCamAxis | kOptPrio),
-};
-#undef IQPT_CV4
-#undef IQPT_CV
-const chain_variant* find_chain(int max_depth, int opt, uint32_t lanes) {
-    const int maxd = max_depth <= 8 ? 8 : 16;
-    for (const chain_variant& v : kChainVariants)
-        if (v.maxd == maxd && v.opt == (opt | kOptPrio) && v.lanes == (int)lanes) return &v;
-    return nullptr;
-}
-}  // namespace
-
 // iqpt_fan_kernel launches: the option bits it depends on are the camera form and the division forms
 namespace {
 template <int OPT>
@@ -5047,85 +4130,6 @@ int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks) {
     const spec_variant* v = find_spec(p.max_depth, opt);
     if (!v) return (int)hipErrorInvalidDeviceFunction;
     return v->occ(spec_lds(p, s), blocks);
-}
-
-// queue mode (iqpt_specq_kernel): the spec kernel's variants
-namespace {
-template <int MAXD, int OPT>
-int specq_launch_t(hipStream_t stream, const kparams& p, const kspec& s, uint32_t lds, uint32_t blocks) {
-    dispatch(iqpt_specq_kernel<MAXD, OPT>, dim3(blocks), dim3(kSpecBlock), lds, stream, p, s);
-    return (int)hipGetLastError();
-}
-template <int MAXD, int OPT>
-int specq_occ_t(uint32_t lds, int* blocks) {
-    return (int)hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, iqpt_specq_kernel<MAXD, OPT>, kSpecBlock, lds);
-}
-struct specq_variant {
-    int maxd, opt;
-    int (*launch)(hipStream_t, const kparams&, const kspec&, uint32_t, uint32_t);
-    int (*occ)(uint32_t, int*);
-};
-#define IQPT_QV(M, O) {M, O, specq_launch_t<M, O>, specq_occ_t<M, O>}
-#define IQPT_QV2(O) IQPT_QV(8, O), IQPT_QV(16, O)
-const specq_variant kSpecQVariants[] = {
-    IQPT_QV2(kOptDefault | kOptPrio),
-    IQPT_QV2((kOptDefault & ~kOptFastDiv) | kOptPrio),
-    IQPT_QV2(kOptDefault | kOptCamAxis | kOptPrio),
-};
-#undef IQPT_QV2
-#undef IQPT_QV
-const specq_variant* find_specq(int max_depth, int opt) {
-    const int maxd = max_depth <= 8 ? 8 : 16;
-    for (const specq_variant& v : kSpecQVariants)
-        if (v.maxd == maxd && v.opt == ((opt | kOptPrio) & ~(kOptOverlap | kOptSplit))) return &v;
-    return nullptr;
-}
-}  // namespace
-
-uint32_t specq_lds(const kparams& p, const kspec& s) {
-    return specq_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.max_depth, p.spp, s.m_cap, s.ncp);
-}
-
-int launch_spec_prep(void* stream, const kparams& p, const kspec& s) {
-    if (s.n == 0) return 0;
-    dispatch(iqpt_spec_prep_kernel, dim3((s.n + 255u) / 256u), dim3(256), 0u, (hipStream_t)stream, p, s);
-    return (int)hipGetLastError();
-}
-
-int launch_specq(void* stream, const kparams& p, const kspec& s, int opt, uint32_t blocks) {
-    const specq_variant* v = find_specq(p.max_depth, opt);
-    if (!v || p.max_depth > 16 || p.cull == nullptr || p.spp > kAccTableMax || s.m_cap > 65535u || s.ncp > kSpecQCkMax ||
-        s.ck_step == 0u || s.ck == nullptr || s.cursor == nullptr || s.qrec == nullptr)
-        return (int)hipErrorInvalidDeviceFunction;
-    if (s.n == 0 || blocks == 0) return 0;
-    return v->launch((hipStream_t)stream, p, s, specq_lds(p, s), blocks);
-}
-
-int specq_occupancy(const kparams& p, const kspec& s, int opt, int* blocks) {
-    const specq_variant* v = find_specq(p.max_depth, opt);
-    if (!v) return (int)hipErrorInvalidDeviceFunction;
-    return v->occ(specq_lds(p, s), blocks);
-}
-
-bool chain_variant_exists(int max_depth, int opt, uint32_t lanes) {
-    return max_depth <= 16 && find_chain(max_depth, opt, lanes) != nullptr;
-}
-
-uint32_t chain_lds(const kparams& p, uint32_t lanes) {
-    return chain_lds_bytes(p.ntri_pairs, p.nsph_pairs, p.spp, p.max_depth, lanes);
-}
-
-int chain_occupancy(int max_depth, int opt, uint32_t lanes, uint32_t lds, int* blocks) {
-    const chain_variant* v = find_chain(max_depth, opt, lanes);
-    if (!v) return (int)hipErrorInvalidDeviceFunction;
-    return v->occ(lds, blocks);
-}
-
-int launch_chain(void* stream, const kparams& p, uint32_t grid, int opt, uint32_t lanes) {
-    const chain_variant* v = find_chain(p.max_depth, opt, lanes);
-    if (!v || p.max_depth > 16 || p.spp > kAccTableMax) return (int)hipErrorInvalidDeviceFunction;
-    if (grid == 0) return 0;
-    return v->launch((hipStream_t)stream, p, grid, chain_lds(p, lanes));
 }
 
 }  // namespace iqpt

@@ -41,16 +41,11 @@ static_assert((kTriBatch / 2) * kTriPairFloat4 * 16 + (kSphBatch / 2) * kSphPair
 constexpr int kTuneLaunches = 4;     // timed launches before the camera-ray path is chosen (A, B, A, B)
 // kOptSplit auto mode: split when the owned pixels are fewer than this many per resident lane
 constexpr double kSplitAutoPixelsPerLane = 1.2;
-// chain launches: AUTO takes them below this many owned pixels per resident lane of the
-// plain kernel (C3 shares: N = 4 has 1.6, N = 8 0.8; N = 2, 3.2, is faster plain); chain-kernel waves per
-// CU by default (profiles/r02/split_share_v12_lanes.json: 16 beats 8 at N <= 4, equal at N = 8)
-constexpr double kChainAutoPixelsPerLane = 2.0;
 // spec launches: AUTO takes them below this many owned pixels per resident lane of the
 // plain kernel (C3 shares: N = 8 has 0.8, N = 4 1.6, N = 2 3.2; pipelined spec launches 0.27 / 0.47 / 0.87 ms
 // per step through the gather against plain 0.95 / 1.0 / 0.91; N = 1, 6.3, stays plain; profiles/r03/
 // split_share_run37.json, r03_share_v11.json, run49_share{2,4,8}_2.json)
 constexpr double kSpecAutoPixelsPerLane = 4.0;
-constexpr uint32_t kChainWavesPerCu = 16;
 constexpr size_t kSplitResBudget = size_t(8) << 30;   // speculative results (bytes)
 
 std::once_flag g_tables_once;
@@ -167,6 +162,7 @@ struct iqpt_ctx {
     bool tune_primary = false;
     hipEvent_t tune_ev[2 * 4] = {};
     int last_opt = -1;           // option set of the last render launch (iqpt_debug_last_options)
+    bool last_xcd_lists = false; // the last launch dealt its tiles to per-XCD lists (overlapped or streamed)
     // kOptSplit, sample-parallel chains: mode (IQPT_SPLIT_*), the split set built with
     // the masks (tiles whose camera rays may scatter), per-slot buffers sized for the launch
     int split_mode = IQPT_SPLIT_AUTO;
@@ -185,15 +181,10 @@ struct iqpt_ctx {
     uint32_t resident_refill_min = 1;   // ... in resident plain launches (iqpt_debug_set_resident_refill)
     uint32_t split_heavy_rho = iqpt::kSplitHeavyRho;
     bool split_all_tiles = false;       // every tile in the split set (wall tiles: one slot per sample)
-    // chain launches: chain-kernel waves per CU (0: kChainWavesPerCu); the last launch's mode
-    uint32_t chain_waves = 0;
-    uint32_t chain_lanes = 8;           // lanes per pixel (4 or 8)
-    bool chain_last = false;
     bool fan_last = false;              // the last launch ran the anchored tiles in iqpt_fan_kernel
-    bool fan_anchored = true;           // chain / fan launches: anchored tiles in the fan kernel (else plain)
-    // chain launches with the fan kernel: the pixels of split tiles whose own camera-ray
-    // bundle may reach a sphere (the chain kernel's pixel list), and the fan kernel's tiles with the lanes
-    // it owns (anchored tiles whole; split tiles without their sphere pixels)
+    // spec launches with the fan kernel: the pixels of split tiles whose own camera-ray
+    // bundle may reach a sphere (the spec kernel's pixel list, "chain pixels"), and the fan kernel's tiles with
+    // the lanes it owns (anchored tiles whole; split tiles without their sphere pixels)
     uint32_t* d_chain_pix = nullptr;
     uint32_t n_chain_pix = 0;
     uint32_t* d_fan_tiles = nullptr;
@@ -208,32 +199,21 @@ struct iqpt_ctx {
     bool spec_last = false;
     uint32_t spec_rho0 = iqpt::kSpecRho0;   // window of a pixel without history (iqpt_debug_set_spec)
     uint32_t spec_parity_rho = iqpt::kSpecParityRho;   // parity pixels' threshold (iqpt_debug_set_spec_parity; 0 off)
-    uint32_t spec_parity_hi = iqpt::kSpecParityHi;     // ... and upper bound (iqpt_debug_set_spec_parity_max)
+    uint32_t spec_parity_hi = iqpt::kSpecParityHi;     // ... and upper bound
     bool anyhit_on = true;                  // any-hit queries in triangle-only scenes (iqpt_debug_set_anyhit)
     bool pipe_on = true;                    // two rays per lane in resident plain launches (kOptPipe, iqpt_debug_set_two_ray)
-    uint32_t spec_prio_q = 0;               // spec kernel progress-fair priority step (iqpt_debug_set_spec_prio; 0 off)
     uint32_t spec_margin_div = 16;          // window margin: 1/16 of the extra slots, at least 4 (iqpt_debug_set_spec;
                                             // against 1/4, 5 % of the chains take a second round instead of 0.6 %,
                                             // yet -4 % per launch at N = 2 / 4 / 8, profiles/r03/spec_margins.json)
     // spec launches (iqpt_debug_set_specfan): 0 the two kernels on two streams, pipelined (the default), 1 one
     // after the other on one stream (measurement)
     int specfan_mode = 0;
-    // queue mode (iqpt_specq_kernel; iqpt_debug_set_spec_queue): persistent waves over
-    // per-XCD pixel cursors, spec_qbpc blocks per CU, behind iqpt_spec_prep_kernel (windows, checkpoints)
-    int spec_queue = 0;
-    uint32_t spec_qbpc = iqpt::kSpecQBlocksPerCu;
-    uint32_t* d_spec_ck = nullptr;       // checkpoints: spec_ck_cap words
-    size_t spec_ck_cap = 0;
-    uint32_t* d_spec_cursor = nullptr;   // kSpecCursors x 16 words
-    uint32_t spec_q_grid = 0;            // the last queue launch's blocks (timeline)
-    bool spec_q_last = false;            // the last spec launch ran in queue mode
-    bool fan_pipe = true;                // FAN launches pipelined (iqpt_debug_set_pipe)
     // spec plan: the sphere pixels ordered by their last chain's work, heaviest first, the
     // heavy ones with 32 or 64 lanes; built on the host from an asynchronous read of the history (performance
     // only: every plan gives the same bits). iqpt_debug_spec_plan: 0 off, 1 asynchronous (default), 2..5
     // synchronous before every launch (tests; 3, 4: every pixel 32 / 64 lanes, 5: mixed)
     int spec_plan_mode = 1;
-    double spec_cap = 0.97;                 // a plan's lanes: this fraction of the resident lanes (iqpt_debug_set_spec_cap)
+    double spec_cap = 0.97;                 // a plan's lanes: this fraction of the resident lanes
     uint32_t* h_spec_rho = nullptr;      // pinned: the history read back (spec_n)
     uint32_t* h_spec_plan = nullptr;     // pinned: staging of the plan (3 spec_n)
     hipEvent_t ev_spec_rho = nullptr, ev_spec_plan = nullptr;
@@ -250,7 +230,7 @@ struct iqpt_ctx {
     // go on `stream3` behind both kernels; from the first such copy on, launches write the two frame buffers
     // in turn and a launch waits only for the copy that read its buffer two launches earlier.
     bool pipe = false;                   // the last launch was pipelined and nothing has joined since
-    int pipe_kind = 0;                   // ... a spec launch (1) or a fan launch (2)
+    int pipe_kind = 0;                   // ... a spec launch (1)
     hipStream_t stream3 = nullptr;
     hipEvent_t ev_pipe_end = nullptr;    // on `stream`, recorded by a copy behind a pipelined launch
     // the events the last pipelined launch's kernels recorded at their ends on `stream` / `stream2` (timing
@@ -277,8 +257,6 @@ struct iqpt_ctx {
     unsigned long long* d_spec_tl = nullptr;   // iqpt_debug_spec_timeline: per spec block timestamps
     size_t spec_tl_blocks = 0;
     bool spec_tl_on = false;
-    uint32_t chain_par = 0;             // the queue-counter set of the next chain launch
-    bool chain_q_ready[2] = {false, false};   // that set is zeroed (in stream order)
     size_t res_slots = 0;               // m_cap x ns_cap allocated (res, nres)
     double tune_work[4] = {0.0, 0.0, 0.0, 0.0};
     // kOptOverlap: consecutive render launches alternate between `stream` and
@@ -1168,11 +1146,8 @@ int check_dev_err(iqpt_ctx* c) {
         c->dev_err = err;
     }
     if (!c->dev_err) return IQPT_OK;
-    return iqpt::fail(IQPT_ERR_HIP, std::string((c->dev_err & 2u)   ? "chain launch: a wave exceeded its iteration bound"
-                                                : (c->dev_err & 4u) ? "overlapped launch: an XCD's tiles were never taken"
-                                                : (c->dev_err & 8u) ? "spec launch: a chain slot was never traced"
-                                                : (c->dev_err & 16u) ? "spec queue launch: a wave found no work to hand out"
-                                                                    : "overlapped launch: a per-tile wait timed out") +
+    return iqpt::fail(IQPT_ERR_HIP, std::string((c->dev_err & 4u) ? "launch: an XCD's tile list was never taken"
+                                                                   : "overlapped launch: a per-tile wait timed out") +
                                         " (pixel state undefined until iqpt_checkpoint_load)");
 }
 
@@ -1387,7 +1362,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->ev_pipe_end) (void)hipEventDestroy(c->ev_pipe_end);
     free_split(c);
     for (void* b : {(void*)c->d_spec, (void*)c->d_spec_res, (void*)c->d_spec_tl, (void*)c->d_spec_plan,
-                    (void*)c->d_spec_ck, (void*)c->d_spec_cursor})
+})
         if (b) (void)hipFree(b);
     for (void* b : {(void*)c->h_spec_rho, (void*)c->h_spec_plan})
         if (b) (void)hipHostFree(b);
@@ -1800,27 +1775,22 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // kOptSplit: resident scenes with a split set, when the mode asks for it (auto:
     // fewer owned pixels than kSplitAutoPixelsPerLane per resident lane, i.e. too few pixel chains to
     // fill and drain the chip evenly)
-    // chain launches: the split set's pixels in iqpt_chain_kernel, the other tiles in the
-    // plain kernel beside it (resident scenes, reference materials)
-    bool chain = false;
+    // (round 6: the chain kernel, DESIGN.md §3.9, and FAN launches, §3.10, left the library for the branch
+    // round6-ab-archive; AUTO never chose FAN, and chain launches only where spec launches did not fit)
     bool auto_spec = false;             // AUTO: the share is small enough for spec launches (if they apply)
-    if ((c->split_mode == IQPT_SPLIT_CHAIN || c->split_mode == IQPT_SPLIT_AUTO) && !stream_batches && p.cull &&
-        c->n_split_tiles > 0 && tune_slot < 0 && !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax &&
-        iqpt::chain_variant_exists(c->max_depth, opt, c->chain_lanes)) {
+    if (c->split_mode == IQPT_SPLIT_AUTO && !stream_batches && p.cull && c->n_split_tiles > 0 && tune_slot < 0 &&
+        !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax) {
         int occ_p = 0;
         if (iqpt::render_occupancy(c->max_depth, false, opt, lds, &occ_p) != 0) occ_p = 0;
         const double lanes = (double)c->num_cus * std::max(occ_p, 1) * iqpt::kRenderBlock;
-        chain = c->split_mode == IQPT_SPLIT_CHAIN || (double)c->npix < iqpt::kChainAutoPixelsPerLane * lanes;
-        auto_spec = c->split_mode == IQPT_SPLIT_AUTO && (double)c->npix < iqpt::kSpecAutoPixelsPerLane * lanes;
+        auto_spec = (double)c->npix < iqpt::kSpecAutoPixelsPerLane * lanes;
     }
-    // fan launches: the anchored tiles (no sphere candidate) in iqpt_fan_kernel, the split
-    // set's tiles in the plain kernel beside it
+    // the fan kernel: the anchored tiles (no sphere candidate) of spec and split launches
     const bool fan_ok = !stream_batches && p.cull && (c->n_anchor > 0 || c->n_fan_tiles > 0) && tune_slot < 0 &&
                         !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax && c->cull_wt <= 16 &&
                         iqpt::fan_variant_exists(opt);
-    const bool fan = !chain && fan_ok && c->split_mode == IQPT_SPLIT_FAN;
     // spec launches: sphere pixels slot-parallel, every other pixel in the fan kernel
-    bool spec = (!chain || auto_spec) && fan_ok && (c->split_mode == IQPT_SPLIT_SPEC || auto_spec) && c->n_split_tiles > 0 &&
+    bool spec = fan_ok && (c->split_mode == IQPT_SPLIT_SPEC || auto_spec) && c->n_split_tiles > 0 &&
                 iqpt::spec_variant_exists(c->max_depth, opt) &&
                 (size_t)c->n_chain_pix * ((iqpt::kSplitMCapMul * spp + 15u) & ~15u) * 16u <= iqpt::kSplitResBudget;
     if (spec) {
@@ -1835,25 +1805,9 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
                iqpt::spec_occupancy(p, probe, opt, &occ_s) == 0 && occ_s >= 1;
         (void)hipGetLastError();
     }
-    // queue mode: its own LDS (records, checkpoints, slot counts of 6 pixels per wave) must fit too
-    bool spec_q = false;
-    if (spec && c->spec_queue) {
-        iqpt::kspec probe;
-        std::memset(&probe, 0, sizeof probe);
-        probe.m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
-        probe.ck_step = iqpt::spec_ck_step(probe.m_cap);
-        probe.ncp = probe.m_cap / probe.ck_step + 1u;
-        int occ_q = 0;
-        spec_q = iqpt::specq_lds(p, probe) <= c->lds_per_block && iqpt::specq_occupancy(p, probe, opt, &occ_q) == 0 &&
-                 occ_q >= 1;
-        (void)hipGetLastError();
-    }
-    bool fan_beside_chain = chain && fan_ok && c->fan_anchored;
-    if (spec) chain = fan_beside_chain = false;
     uint32_t lds_split = lds + iqpt::kRenderBlock * (16u + 24u);   // + lds_sp and the base states
     bool split = false;
-    if (!chain && !fan && !spec && c->split_mode != IQPT_SPLIT_OFF && c->split_mode != IQPT_SPLIT_CHAIN &&
-        c->split_mode != IQPT_SPLIT_FAN && c->split_mode != IQPT_SPLIT_SPEC && !stream_batches && p.cull &&
+    if (!spec && c->split_mode != IQPT_SPLIT_OFF && c->split_mode != IQPT_SPLIT_SPEC && !stream_batches && p.cull &&
         c->n_split_tiles > 0 &&
         tune_slot < 0 && iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptSplit)) {
         int occ_s = 0;
@@ -1862,11 +1816,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         split = occ_s > 0 && (c->split_mode == IQPT_SPLIT_ON || (double)c->npix < iqpt::kSplitAutoPixelsPerLane * lanes);
     }
     // pipelined spec launches continue without a join (the launch below orders itself); the others never overlap
-    const bool fan_pipe = fan && !chain && !spec && c->fan_pipe;   // pipelined FAN launch
-    const bool pipe_next = c->pipe && ((spec && c->specfan_mode == 0 && c->pipe_kind == 1) || (fan_pipe && c->pipe_kind == 2));
-    if ((split || chain || fan || spec) && !pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
+    const bool pipe_next = c->pipe && spec && c->specfan_mode == 0 && c->pipe_kind == 1;
+    if ((split || spec) && !pipe_next && (st = join_streams(c)) != IQPT_OK) return st;
     // split launches with the anchored tiles in the fan kernel beside the four split passes
-    const bool fan_split = split && fan_ok && c->fan_anchored;
+    const bool fan_split = split && fan_ok;
     const size_t ns_cap = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
     const uint32_t m_cap = (iqpt::kSplitMCapMul * spp + 15u) & ~15u;
     const uint32_t g_max = (m_cap + iqpt::kSplitRunLen - 1) / iqpt::kSplitRunLen;
@@ -1962,11 +1915,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // XCD (HIP promises no placement; the kernel's last block checks it and raises an error bit if not)
     // kOptPipe: plain launches over resident scenes under the reference's materials take the
     // two-rays-per-lane variants where they are built (a caller's fixed option set keeps its own bits)
-    if (!c->opt_fixed && c->pipe_on && !stream_batches && !split && !chain && !fan && !spec && tune_slot < 0 &&
+    if (!c->opt_fixed && c->pipe_on && !stream_batches && !split && !spec && tune_slot < 0 &&
         p.cull != nullptr && p.acc_tab && !(opt & iqpt::kOptMaterials) &&
         iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptPipe))
         opt |= iqpt::kOptPipe;
-    bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && !chain && !fan && !spec &&
+    bool ovl = c->overlap_mode != IQPT_OVERLAP_OFF && !stream_batches && !split && !spec &&
                p.cull != nullptr &&
                tune_slot < 0 && c->d_tile_done && c->d_xcd_order && c->num_xcc == 8 && c->num_cus >= 64 &&
                (uint64_t)c->npix >= 64ull * iqpt::kRenderBlock &&
@@ -1978,12 +1931,12 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // two launches in flight: each keeps one block slot per CU free for the other (occ - 1 per CU), so the
     // earlier launch, which the later one waits for, can always run
     if (ovl && occ < 2) ovl = false;
-    if ((ovl || chain || fan || fan_split || spec) && !c->stream2) {
+    if ((ovl || fan_split || spec) && !c->stream2) {
         if (hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming) != hipSuccess ||
             hipEventCreateWithFlags(&c->ev_s2, hipEventDisableTiming) != hipSuccess) {
             (void)hipGetLastError();
-            if (chain || fan || fan_split || spec) return iqpt::fail(IQPT_ERR_HIP, "second stream for the chain / fan kernel");
+            if (fan_split || spec) return iqpt::fail(IQPT_ERR_HIP, "second stream for the spec / fan kernel");
             ovl = false;
             c->overlap_mode = IQPT_OVERLAP_OFF;
         }
@@ -2011,7 +1964,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         p.xcd_order = c->d_xcd_order;
         std::memcpy(p.xcd_off, c->xcd_off, sizeof p.xcd_off);
         p.ovl_err = c->d_ovl_err;
-        c->chain_q_ready[0] = c->chain_q_ready[1] = false;   // the overlapped launches' words (chain sets)
         if (c->copy_seq > c->pwaited) {    // copies behind earlier pipelined launches may still read d_bgra
             IQPT_HIP(hipStreamWaitEvent(ls, c->pev[c->copy_seq % iqpt::kPipeRing], 0));
             c->pwaited = c->copy_seq;
@@ -2026,11 +1978,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         occ -= 1;
     }
     // pitch-only cameras take the short camera transform (exact, kOptCamAxis) wherever that variant is
-    // built: resident plain, overlapped and chain launches (C2 -14 % overlapped, C3 shares -3..-12 %,
+    // built: resident plain, overlapped and spec launches (C2 -14 % overlapped, C3 shares -3..-12 %,
     // profiles/r02/ab_camaxis_overlap.json, split_share_v17_camaxis.json)
     if (!c->opt_fixed && cam_axis && !stream_batches && !split &&
         iqpt::render_variant_exists(c->max_depth, false, opt | iqpt::kOptCamAxis) &&
-        (!chain || iqpt::chain_variant_exists(c->max_depth, opt | iqpt::kOptCamAxis, c->chain_lanes)) &&
         (!spec || iqpt::spec_variant_exists(c->max_depth, opt | iqpt::kOptCamAxis)))
         opt |= iqpt::kOptCamAxis;
     const uint64_t want = ((uint64_t)c->npix + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
@@ -2040,13 +1991,13 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     constexpr uint32_t kStreamXcdMaxSpp = 4;
     const int xmode = c->stream_xcd == 3 ? (spp <= kStreamXcdMaxSpp ? 1 : 0) : c->stream_xcd;
     const bool xcdq = stream_batches && xmode != 0 && p.cull && c->d_xcd_order && c->d_xcd_band &&
-                      !split && !chain && !fan && !spec && c->num_xcc == 8 && c->num_cus >= 64 && grid >= 64;
+                      !split && !spec && c->num_xcc == 8 && c->num_cus >= 64 && grid >= 64;
     if (xcdq) {
         p.xcd_order = xmode == 1 ? c->d_xcd_order : c->d_xcd_band;
         std::memcpy(p.xcd_off, xmode == 1 ? c->xcd_off : c->xcd_band_off, sizeof p.xcd_off);
         p.ovl_err = c->d_ovl_err;
     }
-    if (!ovl && !chain && !fan && !spec)
+    if (!ovl && !spec)
         IQPT_HIP(hipMemsetAsync(c->d_queue, 0, (xcdq ? 16u * 8u + 1u : 4u) * sizeof(uint32_t), c->stream));
     hipEvent_t e0 = take_event(c), e1 = take_event(c), e1b = nullptr;
     // pipelined spec launches: the timing events are recorded by the spec and fan kernels' dispatches (no
@@ -2105,11 +2056,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     };
     // ---- the spec kernel's buffers, parameters, plan and history (pipelined spec launches on `stream`):
     // every enqueue of these on the spec kernel's stream `ss`
-    // queue mode's grid: spec_qbpc blocks per CU, no more waves than sphere pixels
-    auto spec_q_blocks = [&](const iqpt::kspec& k2) -> uint32_t {
-        const uint64_t want = ((uint64_t)k2.n + 3u) / 4u;
-        return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want, (uint64_t)c->num_cus * std::max(1u, c->spec_qbpc)));
-    };
     auto spec_buffers = [&](hipStream_t ss, iqpt::kspec& ks2) -> int {
         std::memset(&ks2, 0, sizeof ks2);
         const uint32_t n = c->n_chain_pix;
@@ -2167,34 +2113,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         ks2.margin_div = c->spec_margin_div;
         ks2.parity_rho = c->spec_parity_rho;
         ks2.parity_hi = c->spec_parity_hi;
-        ks2.prio_q = c->spec_prio_q;
         ks2.pix = c->d_chain_pix;
         ks2.m = c->d_spec;
         ks2.rho = c->d_spec + n;
         ks2.run_count = c->d_spec + 2 * (size_t)n;
         ks2.res = c->d_spec_res;
-        if (spec_q && n > 0) {
-            ks2.queue = 1u;
-            ks2.ck_step = iqpt::spec_ck_step(m_cap);
-            ks2.ncp = m_cap / ks2.ck_step + 1u;
-            const size_t words = (size_t)n * (ks2.ncp * 8u + iqpt::kSpecQRecWordsHost);
-            if (words > c->spec_ck_cap || !c->d_spec_cursor) {
-                IQPT_HIP(hipStreamSynchronize(c->stream));
-                if (c->d_spec_ck) (void)hipFree(c->d_spec_ck);
-                c->d_spec_ck = nullptr;
-                c->spec_ck_cap = 0;
-                if (hipMalloc(&c->d_spec_ck, words * sizeof(uint32_t)) != hipSuccess ||
-                    (!c->d_spec_cursor &&
-                     hipMalloc(&c->d_spec_cursor, iqpt::kSpecCursors * 16u * sizeof(uint32_t)) != hipSuccess)) {
-                    (void)hipGetLastError();
-                    return iqpt::fail(IQPT_ERR_OUT_OF_MEMORY, "spec queue checkpoints");
-                }
-                c->spec_ck_cap = words;
-            }
-            ks2.ck = c->d_spec_ck;
-            ks2.qrec = c->d_spec_ck + (size_t)n * ks2.ncp * 8u;
-            ks2.cursor = c->d_spec_cursor;
-        }
         // a new pixel list: no history, and the statistics counters behind it (d_spec + 2 n) restart too
         // (after a list that shrank n they pointed into the old history)
         if (n > 0 && !c->spec_rho_valid) IQPT_HIP(hipMemsetAsync(ks2.rho, 0, ((size_t)n + 2) * sizeof(uint32_t), ss));
@@ -2232,9 +2155,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             ks2.nblocks = c->spec_plan_blocks;
         }
         if (c->spec_tl_on && n > 0) {
-            // (queue mode: one timeline record of 8 words per wave)
-            const size_t nb = ks2.queue ? 4 * (size_t)spec_q_blocks(ks2)
-                                        : ks2.blocks ? ks2.nblocks : (n + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
+            const size_t nb = ks2.blocks ? ks2.nblocks : (n + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
             if (nb > c->spec_tl_blocks) {
                 IQPT_HIP(hipStreamSynchronize(ss));
                 if (c->d_spec_tl) (void)hipFree(c->d_spec_tl);
@@ -2266,7 +2187,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     // kernel on the launch's stream; the plain kernel skips them. Consecutive sky kernels order themselves
     // through ev_sky (overlapped launches alternate streams); their pixels are disjoint from the plain kernel's.
     const bool sky = c->sky_on && c->certain_on && c->certain_valid && c->n_sky_tiles > 0 && p.certain != nullptr &&
-                     !stream_batches && !split && !chain && !fan && !spec && tune_slot < 0 &&
+                     !stream_batches && !split && !spec && tune_slot < 0 &&
                      !(opt & iqpt::kOptMaterials) && spp <= iqpt::kAccTableMax && iqpt::sky_variant_exists(opt);
     // overlapped launches may put the sky kernel behind the plain kernel on the launch's stream
     // (iqpt_debug_set_sky_order), so the plain kernel, whose sphere tiles carry the launch's longest chains,
@@ -2313,93 +2234,6 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         c->ovl_epoch += 1;
         c->next_on_main = !c->next_on_main;
         if (le != 0) c->ovl_zero = true;     // a failed launch breaks the chain's counts: restart it
-    } else if (fan_pipe) {
-        // pipelined FAN launch: the split tiles in the plain kernel on stream (queue[0], zeroed there), the
-        // anchored tiles in the fan kernel on stream2
-        if ((st = pipe_begin()) != IQPT_OK) return st;
-        IQPT_HIP(hipMemsetAsync(c->d_queue, 0, 4 * sizeof(uint32_t), c->stream));
-        p.queue = c->d_queue;
-        p.ovl_err = c->d_ovl_err;
-        if (c->n_split_tiles > 0) {
-            iqpt::kparams ps = p;
-            ps.tile_order = c->d_split + c->n_anchor;
-            ps.nqueue = c->n_split_tiles;
-            const uint64_t want_s = ((uint64_t)c->n_split_tiles * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
-            const uint32_t grid_s = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_s, (uint64_t)c->num_cus * occ));
-            le = iqpt::launch_render(c->stream, ps, grid_s, lds, stream_batches, opt);
-        }
-        if (le == 0 && c->n_anchor > 0) {
-            p.tile_order = c->d_split;
-            p.nqueue = c->n_anchor;
-            le = iqpt::launch_fan(c->stream2, p, c->n_anchor, opt);
-        }
-        if ((st = pipe_end(2)) != IQPT_OK) return st;
-    } else if (chain || fan) {
-        // chain: the split set's pixels in iqpt_chain_kernel (pixels from queue[1]) on stream; fan: the split
-        // set's tiles in the plain kernel (queue[0]) on stream. Beside it on stream2 the anchored tiles, in
-        // iqpt_fan_kernel (one block per tile) or the plain kernel (queue[0]); stream waits for stream2
-        // before the end event.
-        // the chain kernel's pixels: every pixel of the split tiles, or (with the fan kernel beside it) those
-        // whose own bundle may reach a sphere
-        const size_t ns = fan_beside_chain ? c->n_chain_pix : (size_t)c->n_split_tiles * iqpt::kQueueChunk;
-        p.sp_pix = fan_beside_chain ? c->d_chain_pix : c->d_split + c->n_anchor + c->n_split_tiles;
-        p.ns_cap = (uint32_t)ns;
-        const uint32_t lanes = c->chain_lanes;
-        const uint32_t lds_c = iqpt::chain_lds(p, lanes);
-        int occ_c = 0;
-        if (iqpt::chain_occupancy(c->max_depth, opt, lanes, lds_c, &occ_c) != 0 || occ_c < 1) occ_c = 1;
-        const uint32_t per_cu = std::min<uint32_t>((uint32_t)occ_c, c->chain_waves ? c->chain_waves : iqpt::kChainWavesPerCu);
-        const uint64_t px_per_wave = 64u / lanes;
-        const uint64_t want_c = (ns + px_per_wave - 1) / px_per_wave;
-        const uint32_t grid_c = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_c, (uint64_t)c->num_cus * per_cu));
-        p.ovl_err = c->d_ovl_err;
-        // The chain kernel (the launch's critical path) goes first on the context stream; the anchored
-        // kernel (shorter) follows on stream2 behind a cross-queue event, whose latency it absorbs. The
-        // queue counters alternate between two sets in the overlapped launches' words: this launch's set
-        // was zeroed behind the previous chain launch's anchored kernel, off the critical path.
-        uint32_t* const qset = c->d_queue + 4 + c->chain_par * (iqpt::kOverlapQueueWords / 2);
-        if (!c->chain_q_ready[c->chain_par]) IQPT_HIP(hipMemsetAsync(qset, 0, 4 * sizeof(uint32_t), c->stream));
-        p.queue = qset;
-        IQPT_HIP(hipEventRecord(c->ev_pre, c->stream));
-        IQPT_HIP(hipStreamWaitEvent(c->stream2, c->ev_pre, 0));
-        if (chain) {
-            if (ns > 0) le = iqpt::launch_chain(c->stream, p, grid_c, opt, lanes);
-        } else if (c->n_split_tiles > 0) {
-            iqpt::kparams ps = p;
-            ps.tile_order = c->d_split + c->n_anchor;
-            ps.nqueue = c->n_split_tiles;
-            const uint64_t want_s = ((uint64_t)c->n_split_tiles * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
-            const uint32_t grid_s = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_s, (uint64_t)c->num_cus * occ));
-            le = iqpt::launch_render(c->stream, ps, grid_s, lds, stream_batches, opt);
-        }
-        if (le == 0 && fan_beside_chain && c->sky_active) {
-            // the certain-miss pixels the fan lists left out, ahead of the fan kernel
-            iqpt::kparams pm = p;
-            pm.miss = c->d_certain + 2 * (size_t)c->cull_ntx * c->cull_nty;
-            le = iqpt::launch_sky(c->stream2, pm, c->d_sky_tiles, c->n_sky_tiles, opt);
-        }
-        if (le == 0 && fan_beside_chain && c->n_fan_tiles > 0) {
-            p.tile_order = c->d_fan_tiles;
-            p.fan_lanes = c->d_fan_lanes;
-            le = iqpt::launch_fan(c->stream2, p, c->n_fan_tiles, opt);
-        } else if (le == 0 && c->n_anchor > 0) {
-            p.tile_order = c->d_split;
-            p.nqueue = c->n_anchor;
-            if (fan) {
-                le = iqpt::launch_fan(c->stream2, p, c->n_anchor, opt);
-            } else {
-                const uint64_t want_p = ((uint64_t)c->n_anchor * iqpt::kQueueChunk + iqpt::kRenderBlock - 1) / iqpt::kRenderBlock;
-                const uint32_t grid_p = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(want_p, (uint64_t)c->num_cus * occ));
-                le = iqpt::launch_render(c->stream2, p, grid_p, lds, stream_batches, opt);
-            }
-        }
-        const uint32_t nxt = c->chain_par ^ 1u;
-        IQPT_HIP(hipMemsetAsync(c->d_queue + 4 + nxt * (iqpt::kOverlapQueueWords / 2), 0, 4 * sizeof(uint32_t), c->stream2));
-        c->chain_q_ready[nxt] = true;
-        c->chain_q_ready[c->chain_par] = false;
-        c->chain_par = nxt;
-        IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
-        IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
     } else if (spec) {
         // every pixel without a sphere in reach in the fan kernel on stream2; the sphere pixels in
         // iqpt_spec_kernel on stream (slots, then the walk)
@@ -2419,20 +2253,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         }
         if ((st = spec_plan(c->stream, ks2)) != IQPT_OK) return st;
         const uint32_t n = ks2.n;
-        c->spec_q_last = ks2.queue != 0u;
-        // queue mode: the prep kernel (windows, checkpoints, cursors) then the persistent grid
-        auto run_spec = [&]() -> int {
-            if (!ks2.queue) return iqpt::launch_spec(c->stream, p, ks2, opt);
-            void* s0 = nullptr;
-            void* s1 = nullptr;
-            iqpt::take_launch_events(&s0, &s1);
-            iqpt::bind_launch_events(s0, nullptr);
-            int e = iqpt::launch_spec_prep(c->stream, p, ks2);
-            iqpt::bind_launch_events(nullptr, s1);
-            c->spec_q_grid = spec_q_blocks(ks2);
-            if (e == 0) e = iqpt::launch_specq(c->stream, p, ks2, opt, c->spec_q_grid);
-            return e;
-        };
+        auto run_spec = [&]() -> int { return iqpt::launch_spec(c->stream, p, ks2, opt); };
         if (c->specfan_mode == 1) {
             if (n > 0) le = run_spec();
             if (le == 0 && c->n_fan_tiles > 0) le = iqpt::launch_fan(c->stream, pf, c->n_fan_tiles, opt);
@@ -2484,11 +2305,11 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
         le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
     }
     c->split_last = split;
-    c->chain_last = chain;
-    c->fan_last = fan || fan_beside_chain || fan_split || spec;
+    c->fan_last = fan_split || spec;
     c->spec_last = spec;
     c->last_ls = ls;
     c->last_ovl = ovl;
+    c->last_xcd_lists = (ovl || xcdq) && !spec && !split;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1 && !e1_bound) (void)hipEventRecord(e1, ls);
     if (e0 && e1) c->timed.push_back({e0, e1, e1b});
@@ -2763,8 +2584,6 @@ int iqpt_debug_spec_info(iqpt_ctx* c, unsigned long long* out8) {
     out8[1] = c->n_fan_tiles;
     out8[2] = c->n_anchor;
     out8[3] = c->n_split_tiles;
-    // the last spec launch in queue mode: its grid's blocks in the high half of word 2
-    if (c->spec_last && c->spec_q_last) out8[2] |= (unsigned long long)c->spec_q_grid << 32;
     if (c->spec_last && c->d_spec && c->spec_n >= c->n_chain_pix) {
         const uint32_t n = c->n_chain_pix;
         std::vector<uint32_t> v(2 * (size_t)n + 2);
@@ -2799,8 +2618,7 @@ int iqpt_debug_read_spec_timeline(iqpt_ctx* c, unsigned long long* out, uint32_t
     if (st) return st;
     IQPT_HIP(hipStreamSynchronize(c->stream));
     if (!c->d_spec_tl || !c->spec_last) return IQPT_OK;
-    const size_t nspec = c->spec_q_last ? 4 * (size_t)c->spec_q_grid
-                         : c->spec_plan_n == c->n_chain_pix && c->spec_plan_n && c->spec_plan_mode
+    const size_t nspec = c->spec_plan_n == c->n_chain_pix && c->spec_plan_n && c->spec_plan_mode
                              ? c->spec_plan_blocks
                              : (c->n_chain_pix + iqpt::kSpecPixPerBlock - 1) / iqpt::kSpecPixPerBlock;
     const size_t nb = std::min<size_t>(nspec, std::min<size_t>(cap_blocks, c->spec_tl_blocks));
@@ -2918,25 +2736,6 @@ int iqpt_debug_certain_tiles(iqpt_ctx* c, uint32_t* n, uint32_t* ntiles, uint32_
     return IQPT_OK;
 }
 
-/* Internal (A/B): FAN launches pipelined (1, the default) or joined after every launch (0). */
-int iqpt_debug_set_pipe(iqpt_ctx* c, int fan_pipe) {
-    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    int st = enter(c);
-    if (st) return st;
-    c->fan_pipe = fan_pipe != 0;
-    return IQPT_OK;
-}
-
-/* Internal (A/B): the spec kernel's progress-fair VALU priority — a wave's priority falls from 3 by one level per
- * `q` slot-loop iterations it has run (0: 3 throughout, the round-4 behaviour). Same bits either way. */
-int iqpt_debug_set_spec_prio(iqpt_ctx* c, uint32_t q) {
-    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    int st = enter(c);
-    if (st) return st;
-    c->spec_prio_q = q;
-    return IQPT_OK;
-}
-
 /* Internal (tests, A/B): any-hit queries for triangle-only scenes under the reference's materials (1, the
  * default) or the closest-hit search (0). Same bits either way. */
 int iqpt_debug_set_anyhit(iqpt_ctx* c, int on) {
@@ -3000,31 +2799,6 @@ int iqpt_debug_set_spec_parity(iqpt_ctx* c, uint32_t rho256) {
     return IQPT_OK;
 }
 
-/* Internal (tests, A/B): queue mode for spec launches (iqpt_specq_kernel: persistent waves taking sphere pixels
- * from per-XCD cursors) — mode 0 the block kernel, 1 queue mode; blocks_per_cu the
- * persistent grid (0: the default). The timeline (iqpt_debug_read_spec_timeline) then holds 8 words per wave:
- * start, end | iterations << 48, pixels | walks << 16 | fix-ups << 32 | XCD << 48, then 10-ns ticks (16 bits
- * each) in admissions / walks / hand-outs / rays and in the walks' wait / chain / gather / fold. */
-int iqpt_debug_set_spec_queue(iqpt_ctx* c, int mode, uint32_t blocks_per_cu) {
-    if (!c || mode < 0 || mode > 1 || blocks_per_cu > 16)
-        return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL, mode not 0..1 or blocks_per_cu > 16");
-    int st = enter(c);
-    if (st) return st;
-    if ((st = join_streams(c)) != IQPT_OK) return st;
-    c->spec_queue = mode;
-    c->spec_qbpc = blocks_per_cu ? blocks_per_cu : iqpt::kSpecQBlocksPerCu;
-    return IQPT_OK;
-}
-
-/* Internal (tests, A/B): the parity pixels' upper bound (slots per sample x 256 of the last chain; 0xffffffff: none). */
-int iqpt_debug_set_spec_parity_max(iqpt_ctx* c, uint32_t rho256) {
-    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    int st = enter(c);
-    if (st) return st;
-    c->spec_parity_hi = rho256;
-    return IQPT_OK;
-}
-
 /* Internal (A/B, measurement): how spec launches run the fan tiles beside the sphere pixels — 0 two kernels on
  * two streams, pipelined across launches (the default), 1 two kernels one after the other on one stream. (Round
  * 4's mode 2, spec and fan blocks in one grid, measured slower and is archived: branch round4-ab-archive.)
@@ -3049,25 +2823,6 @@ int iqpt_debug_set_spec(iqpt_ctx* c, uint32_t rho0, uint32_t margin_div) {
     return IQPT_OK;
 }
 
-/* Internal (A/B): the fraction of the spec kernel's resident lanes a plan may fill in one block-wave
- * (0.97 by default; a plan only orders work: same bits). The next plan uses it. */
-int iqpt_debug_set_spec_cap(iqpt_ctx* c, double frac) {
-    if (!c || !(frac > 0.0 && frac <= 64.0)) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL or fraction not in (0, 64]");
-    c->spec_cap = frac;
-    c->spec_plan_n = 0;
-    return IQPT_OK;
-}
-
-/* Internal (A/B): chain launches run the anchored tiles in iqpt_fan_kernel (1, the default) or in the
- * plain kernel (0). */
-int iqpt_debug_set_fan(iqpt_ctx* c, int on) {
-    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    c->fan_anchored = on != 0;
-    return IQPT_OK;
-}
-
-/* Internal (tests): lower the kernels' forward-progress bounds (0 keeps a bound's default) and bias the
- * per-tile wait targets of overlapped launches, so that tests can force each error path. */
 /* Internal (tests): after joining the context's streams, fills the LDS of every CU with non-zero garbage (blocks of
  * the largest per-block allocation, eight per CU) on the context's stream, ahead of the next launch, which then
  * starts joined behind it: a kernel that reads LDS before writing it gives other bits than the oracle. */
@@ -3082,6 +2837,9 @@ int iqpt_debug_poison_lds(iqpt_ctx* c, uint32_t pattern) {
     return IQPT_OK;
 }
 
+/* Internal (tests): lower the kernels' forward-progress bound (0 keeps the default) and bias the per-tile wait targets
+ * of overlapped launches, so that tests can force the error path. iter_limit bounded the archived chain kernel's loop
+ * (kept in the signature, unused). */
 int iqpt_debug_set_limits(iqpt_ctx* c, uint32_t spin_limit, uint32_t iter_limit, uint32_t wait_bias) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     c->spin_limit = spin_limit ? spin_limit : iqpt::kOverlapSpinLimit;
@@ -3527,11 +3285,9 @@ int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
     out8[1] = c->n_anchor;
     const size_t ns = (size_t)c->n_split_tiles * iqpt::kQueueChunk;
     out8[2] = ns;
-    // launch mode: 1 split, 2 chain (anchored tiles plain), 3 fan (split tiles plain), 4 chain + fan, 5 split + fan,
-    // 6 spec (sphere pixels slot-parallel, the rest fan)
-    out8[7] = c->spec_last ? 6
-                           : (c->split_last ? (c->fan_last ? 5 : 1)
-                                            : (c->chain_last ? (c->fan_last ? 4 : 2) : (c->fan_last ? 3 : 0)));
+    // launch mode: 0 plain, 1 split, 5 split + fan, 6 spec (sphere pixels slot-parallel, the rest fan); 2-4 were the
+    // chain and FAN launches (archived in round 6)
+    out8[7] = c->spec_last ? 6 : (c->split_last ? (c->fan_last ? 5 : 1) : 0);
     if (!c->d_split || ns == 0) return IQPT_OK;
     uint32_t left = 0;
     IQPT_HIP(hipMemcpy(&left, c->d_queue + 2, sizeof left, hipMemcpyDeviceToHost));
@@ -3544,36 +3300,6 @@ int iqpt_debug_split_info(iqpt_ctx* c, unsigned long long* out8) {
         out8[5] += v[2 * ns + i];
         out8[6] += 1;
     }
-    return IQPT_OK;
-}
-
-// kOptSplit tuning knobs (tools/split_share.py): the heavy threshold (slots per sample x 256 of a
-// pixel's last launch; 0 keeps the default) and the idle lanes a wave waits for before it refills
-// (1..64). Results do not depend on either.
-int iqpt_debug_set_split_knobs(iqpt_ctx* c, uint32_t heavy_rho, uint32_t refill_min) {
-    if (!c || (refill_min & 0xffffu) == 0 || (refill_min & 0xffffu) > 64)
-        return iqpt::fail(IQPT_ERR_INVALID_ARG, "refill_min 1..64");
-    // bit 16 of refill_min: every tile joins the split set (rebuilt with the masks)
-    const bool all = (refill_min >> 16) & 1u;
-    if (all != c->split_all_tiles) {
-        c->split_all_tiles = all;
-        c->cull_valid = false;
-    }
-    refill_min &= 0xffffu;
-    if (heavy_rho) c->split_heavy_rho = heavy_rho;
-    c->split_refill_min = refill_min;
-    return IQPT_OK;
-}
-
-// Chain launches (tools/split_share.py): chain-kernel waves per CU (0: the default). Results do not depend on it.
-// Bits 8..15 of waves_per_cu: lanes per pixel (4 or 8; 0 keeps the current value).
-int iqpt_debug_set_chain_waves(iqpt_ctx* c, uint32_t waves_per_cu) {
-    const uint32_t lanes = (waves_per_cu >> 8) & 0xffu;
-    waves_per_cu &= 0xffu;
-    if (!c || waves_per_cu > 64 || (lanes != 0 && lanes != 4 && lanes != 8 && lanes != 16))
-        return iqpt::fail(IQPT_ERR_INVALID_ARG, "waves_per_cu 0..64, lanes 0, 4, 8 or 16");
-    c->chain_waves = waves_per_cu;
-    if (lanes) c->chain_lanes = lanes;
     return IQPT_OK;
 }
 
@@ -3593,9 +3319,10 @@ int iqpt_set_overlap(iqpt_ctx* c, int mode) {
 }
 int iqpt_set_split(iqpt_ctx* c, int mode) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
-    if (mode != IQPT_SPLIT_AUTO && mode != IQPT_SPLIT_OFF && mode != IQPT_SPLIT_ON && mode != IQPT_SPLIT_CHAIN &&
-        mode != IQPT_SPLIT_FAN && mode != IQPT_SPLIT_SPEC)
-        return iqpt::fail(IQPT_ERR_INVALID_ARG, "split mode must be IQPT_SPLIT_AUTO, _OFF, _ON, _CHAIN, _FAN or _SPEC");
+    if (mode == IQPT_SPLIT_CHAIN || mode == IQPT_SPLIT_FAN)
+        return iqpt::fail(IQPT_ERR_UNSUPPORTED, "CHAIN and FAN launches were archived in round 6 (branch round6-ab-archive)");
+    if (mode != IQPT_SPLIT_AUTO && mode != IQPT_SPLIT_OFF && mode != IQPT_SPLIT_ON && mode != IQPT_SPLIT_SPEC)
+        return iqpt::fail(IQPT_ERR_INVALID_ARG, "split mode must be IQPT_SPLIT_AUTO, _OFF, _ON or _SPEC");
     c->split_mode = mode;
     return IQPT_OK;
 }
@@ -3765,26 +3492,12 @@ int iqpt_debug_set_frame(iqpt_ctx* c, uint64_t frame) {
     return IQPT_OK;
 }
 
-/* Internal (tests): the kernel option set of the context's last render launch (-1 before any). */
+/* Internal (tests): the kernel option set of the context's last render launch (-1 before any), with bit 30 set when
+ * that launch dealt its tiles to per-XCD lists and queue words (overlapped launches; streamed launches,
+ * iqpt_debug_set_stream_xcd): the kernels fall back to one queue silently otherwise. */
 int iqpt_debug_last_options(iqpt_ctx* c, int* opt) {
     if (!c || !opt) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    *opt = c->last_opt;
-    return IQPT_OK;
-}
-
-/* Internal (tools/ab_kernel.py): the per-wave timeline of the last kOptStats launch: up to `cap`
- * (start, end, iterations) triples (s_memrealtime ticks, 100 MHz); *n = waves recorded. Call before
- * iqpt_debug_read_stats (which clears the buffer). */
-// kOptStats: the s_memrealtime (100 MHz) at which each queue position was taken, 0 for positions not
-// taken (out: kStatsQueueSlots words).
-int iqpt_debug_read_queue_times(iqpt_ctx* c, unsigned long long* out) {
-    if (!c || !out) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    int st = enter(c);
-    if (st) return st;
-    IQPT_HIP(hipStreamSynchronize(c->stream));
-    if (!c->d_stats) return iqpt::fail(IQPT_ERR_INVALID_ARG, "no stats buffer (kOptStats not set)");
-    IQPT_HIP(hipMemcpy(out, c->d_stats + iqpt::kStatsHeader + 3 * (size_t)iqpt::kStatsWaveSlots,
-                       iqpt::kStatsQueueSlots * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    *opt = c->last_opt < 0 ? c->last_opt : (c->last_opt | (c->last_xcd_lists ? (1 << 30) : 0));
     return IQPT_OK;
 }
 

@@ -20,7 +20,8 @@ MESH_TRIANGLES = 0
 MESH_SPHERES = 1
 DEFAULT_SEED = 1984
 DEFAULT_MAX_DEPTH = 5
-SPLIT_AUTO, SPLIT_OFF, SPLIT_ON, SPLIT_CHAIN, SPLIT_FAN, SPLIT_SPEC = -1, 0, 1, 2, 3, 4   # IQPT_SPLIT_* (iqpt_set_split)
+SPLIT_AUTO, SPLIT_OFF, SPLIT_ON, SPLIT_CHAIN, SPLIT_FAN, SPLIT_SPEC = -1, 0, 1, 2, 3, 4   # IQPT_SPLIT_* (iqpt_set_split;
+# CHAIN and FAN are refused with IQPT_ERR_UNSUPPORTED since round 6)
 OVERLAP_OFF, OVERLAP_AUTO = 0, 1               # IQPT_OVERLAP_* (iqpt_set_overlap)
 COMM_ID_BYTES = 128                            # IQPT_COMM_ID_BYTES (iqpt_comm_unique_id)
 GATHER_ACCUM = 1                               # IQPT_GATHER_ACCUM / IQPT_GATHER_FRAME (iqpt_gather_read_select)
@@ -144,7 +145,8 @@ SIGNATURES = [
 _lib = None
 
 
-ABI_VERSION = 5      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
+ABI_VERSION = 6      # IQPT_ABI_VERSION of include/iqpt.h these bindings mirror
+LOADED_ABI = None    # the ABI of the library load() bound (an A/B library may be older; bench.py reports it)
 
 
 def load() -> C.CDLL:
@@ -155,10 +157,15 @@ def load() -> C.CDLL:
     if not LIB_PATH.exists():
         raise ImportError(f"{LIB_PATH} is missing: run __graft_entry__.build() "
                           "(the HIP extension is required; there is no CPU fallback)")
+    global LOADED_ABI
     lib = C.CDLL(str(LIB_PATH))
     # an A/B library of an earlier round (bench.py --lib, another path) may lack the newest entry points: those
-    # are left unbound there; the package's own library must export every one
+    # are left unbound there; the package's own library must export every one. A library of a newer ABI than
+    # these bindings is refused whatever its path (its signatures may differ from the ones bound here).
     own = LIB_PATH.resolve() == (_PKG / "libiqpt.so").resolve()
+    abi = lib.iqpt_abi_version() if getattr(lib, "iqpt_abi_version", None) is not None else None
+    if abi is not None and abi > ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {abi}, newer than these bindings' {ABI_VERSION}")
     for name, res, args in SIGNATURES:
         fn = getattr(lib, name, None)
         if fn is None:
@@ -167,9 +174,10 @@ def load() -> C.CDLL:
             continue
         fn.restype = res
         fn.argtypes = args
-    if own and lib.iqpt_abi_version() != ABI_VERSION:
-        raise ImportError(f"{LIB_PATH} has ABI {lib.iqpt_abi_version()}, the bindings expect {ABI_VERSION}: "
+    if own and abi != ABI_VERSION:
+        raise ImportError(f"{LIB_PATH} has ABI {abi}, the bindings expect {ABI_VERSION}: "
                           "rebuild with __graft_entry__.build()")
+    LOADED_ABI = abi
     _lib = lib
     return lib
 

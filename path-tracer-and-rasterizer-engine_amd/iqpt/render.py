@@ -167,8 +167,8 @@ class PathTracer:
         return int(s.value or 0)
 
     def set_split(self, mode: int):
-        """Sample-parallel launches: _lib.SPLIT_AUTO (default), SPLIT_OFF, SPLIT_ON, SPLIT_CHAIN or SPLIT_FAN
-        (iqpt_set_split)."""
+        """Sample-parallel launches: _lib.SPLIT_AUTO (default), SPLIT_OFF, SPLIT_ON or SPLIT_SPEC (iqpt_set_split;
+        SPLIT_CHAIN and SPLIT_FAN are refused since round 6, their kernels archived)."""
         check(self._lib.iqpt_set_split(self._h, mode), "iqpt_set_split")
 
     def set_overlap(self, mode: int):
@@ -176,15 +176,13 @@ class PathTracer:
         check(self._lib.iqpt_set_overlap(self._h, mode), "iqpt_set_overlap")
 
     def launch_mode(self) -> str:
-        """How the last launch ran: "plain", "split" (speculative runs + stitch), "chain" (chain kernel beside
-        the plain kernel), "fan" (fan kernel beside the plain kernel), "chain+fan", "split+fan" or "spec", from
-        iqpt_debug_split_info. Synchronises."""
+        """How the last launch ran: "plain", "split" (speculative runs + stitch), "split+fan" (with the anchored
+        tiles in the fan kernel) or "spec", from iqpt_debug_split_info. Synchronises."""
         import ctypes as C
         self._lib.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
         info = (C.c_ulonglong * 8)()
         check(self._lib.iqpt_debug_split_info(self._h, info), "iqpt_debug_split_info")
-        return {1: "split", 2: "chain", 3: "fan", 4: "chain+fan", 5: "split+fan", 6: "spec",
-                }.get(int(info[7]), "plain")
+        return {1: "split", 5: "split+fan", 6: "spec"}.get(int(info[7]), "plain")
 
     def kernel_span(self) -> float:
         """First start to last end (ms) of the launches of the last kernel_time() call (iqpt_kernel_span)."""

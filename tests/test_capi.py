@@ -31,7 +31,9 @@ def test_every_declared_symbol_is_exported_and_bound():
 
 def test_abi_version_and_error_strings():
     lib = iqpt.load()
-    assert lib.iqpt_abi_version() == 5      # 2: packet material table; 3: split mode, prepare, frame copy; 4: RCCL gather; 5: gather_read_select
+    # 2: packet material table; 3: split mode, prepare, frame copy; 4: RCCL gather; 5: gather_read_select;
+    # 6: CHAIN / FAN launch modes refused (archived)
+    assert lib.iqpt_abi_version() == 6
     assert lib.iqpt_error_string(0) == b"IQPT_OK"
     assert lib.iqpt_error_string(4) == b"IQPT_ERR_NO_DEVICE"
     assert lib.iqpt_error_string(99) == b"IQPT_ERR_UNKNOWN"

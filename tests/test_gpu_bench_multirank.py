@@ -41,13 +41,13 @@ def test_two_rank_strong_frame_equals_one_rank(require_gpu, tmp_path, gather):
 
 
 @pytest.mark.parametrize("share,split,mode", [(2, "auto", "spec"), (2, "off", "plain"), (4, "auto", "spec"),
-                                              (4, "chain", "chain+fan"), (8, "auto", "spec")])
+                                              (8, "auto", "spec")])
 def test_stream_ordered_gather_on_one_gpu(require_gpu, tmp_path, share, split, mode):
     """The RCCL path the driver's N-GPU runs take, on one GPU: a one-rank nccl process group, rank 0's
     rows of an N-way split, the stream-ordered frame copy + gather every step, 8 hardware queues: the
     pipelined spec launches AUTO takes (copies on a third stream behind both kernels), overlapped plain
     launches at N = 2 (copies on the last launch's stream; the RCCL kernels share the CUs with launches
-    that wait per tile for the one before) and chain launches."""
+    that wait per tile for the one before)."""
     res, _ = _bench(tmp_path, 1, f"self{share}{split}", ("--self-gather", "--share-of", str(share), "--split", split))
     assert res["gather"] == "stream-ordered" and res["gather_check"] is True
     assert res["hw_queues"] == 8 and res["n_ranks_seen"] == 1

@@ -207,12 +207,14 @@ def test_stream_refill_group_sizes(require_gpu, preset, w, h, ps_args, launches,
     ("mesh10k", 1920, 1080, (0, 1920, 300, 7, 9), [2, 1]),            # C4 geometry, 17,280 pixels
     ("mixed", 3840, 2160, (0, 3840, 900, 9, 5), [1]),                 # C5 geometry, 19,200 pixels
 ])
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [1, 2, 3])
 def test_stream_xcd_tile_lists(require_gpu, preset, w, h, ps_args, launches, mode):
     """Streamed-scene launches whose tiles are dealt to the 8 XCDs (iqpt_debug_set_stream_xcd: 1 the cost order
-    round-robin, 2 bands of tile rows round-robin), each XCD taking its own list from its own queue word; the
-    kernel's last block checks that every list was taken. Pixel sets of more than 64 blocks, so the lists are
-    used. Bit-exact against the oracle."""
+    round-robin, 2 bands of tile rows round-robin, 3 the default: 1 for launches of up to 4 samples), each XCD
+    taking its own list from its own queue word; the kernel's last block checks that every list was taken. Pixel
+    sets of more than 64 blocks, so the lists are used — and the launches must report that they were (bit 30 of
+    iqpt_debug_last_options; the runtime falls back to one queue silently on other devices or grids).
+    Bit-exact against the oracle."""
     sc = Scene()
     sc.add_preset(preset)
     pk = sc.build_packet()
@@ -225,9 +227,13 @@ def test_stream_xcd_tile_lists(require_gpu, preset, w, h, ps_args, launches, mod
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)
+    lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
     for s in launches:
         pt.render(s)
         fr.render(pk, cam, s)
+        o = C.c_int(0)
+        _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(o)), "iqpt_debug_last_options")
+        assert o.value & (1 << 30), hex(o.value)     # every launch here has <= 4 spp: per-XCD lists in mode 3 too
     lin, bgra = pt.read()
     c = compare(lin, fr.lin)
     assert c["bitexact"] == c["npix"], c

@@ -24,10 +24,9 @@ def _poison(pt, pattern):
     _lib.check(lb.iqpt_debug_poison_lds(pt._h, pattern), "iqpt_debug_poison_lds")
 
 
-@pytest.mark.parametrize("world,split,queue", [(8, SPLIT_SPEC, 0), (4, SPLIT_SPEC, 0), (8, SPLIT_SPEC, 1),
-                                               (4, SPLIT_SPEC, 1), (1, SPLIT_OFF, 0)])
-def test_launches_after_lds_garbage(require_gpu, world, split, queue):
-    """(queue: spec launches through the queue kernel, iqpt_debug_set_spec_queue.)"""
+@pytest.mark.parametrize("world,split", [(8, SPLIT_SPEC), (4, SPLIT_SPEC), (1, SPLIT_OFF)])
+def test_launches_after_lds_garbage(require_gpu, world, split):
+    """(world 1: a crop in the plain kernel, two rays per lane; else rank world - 1's share in spec launches.)"""
     from iqpt import PathTracer, make_camera
     w, h = 1920, 1080
     rank = world - 1
@@ -40,11 +39,6 @@ def test_launches_after_lds_garbage(require_gpu, world, split, queue):
     cam = make_camera(w, h)
     pt = PathTracer(w, h, pixels=ps, max_depth=8)
     pt.set_split(split)
-    if queue:
-        from iqpt import _lib
-        lb = _lib.load()
-        lb.iqpt_debug_set_spec_queue.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
-        _lib.check(lb.iqpt_debug_set_spec_queue(pt._h, 1, 0), "iqpt_debug_set_spec_queue")
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)

@@ -140,13 +140,13 @@ def test_sky_kernel_ahead_of_and_behind_the_plain_kernel(require_gpu, after):
     pt.close()
 
 
-@pytest.mark.parametrize("split", ["spec", "specq", "chain"])
+@pytest.mark.parametrize("split", ["spec"])
 def test_sky_with_more_than_64_spheres(require_gpu, split):
     """a resident scene of more than 64 spheres skips the per-pixel sphere test of the split
     tiles, so every pixel of a split tile went to the spec / chain kernel's list — the certain misses too, which
     the sky kernel also renders on the other stream. The Cornell box plus 70 small spheres (a grid above the
     floor, resident in LDS), a row share, spec and chain launches with the sky kernel on: bit for bit against
-    the oracle, and the sky kernel still has pixels."""
+    the oracle, and the sky kernel still has pixels. (Round 6 archived the chain kernel and queue mode.)"""
     from iqpt import PathTracer, make_camera
     L, lib = _lib()
     from iqpt.scene import Scene
@@ -162,11 +162,7 @@ def test_sky_with_more_than_64_spheres(require_gpu, split):
     ps = pixel_set(w, h, 0, w, rank, world, n)
     cam = make_camera(w, h)
     pt = PathTracer(w, h, pixels=ps, max_depth=8)
-    pt.set_split(L.SPLIT_SPEC if split in ("spec", "specq") else L.SPLIT_CHAIN)
-    if split == "specq":
-        # queue mode (iqpt_specq_kernel): the same pixel lists through persistent waves
-        lib.iqpt_debug_set_spec_queue.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
-        L.check(lib.iqpt_debug_set_spec_queue(pt.handle, 1, 0), "iqpt_debug_set_spec_queue")
+    pt.set_split(L.SPLIT_SPEC)
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)

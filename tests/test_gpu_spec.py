@@ -18,46 +18,14 @@ from helpers import compare, gpu_render, oracle_render, pixel_set, scene_for
 pytestmark = pytest.mark.gpu
 RMSE_TOL = 1e-5
 SPLIT_OFF, SPLIT_SPEC = 0, 4
-_QUEUE = [0]      # the spec kernel of this test run: 0 the block kernel, 1 queue mode (iqpt_specq_kernel)
-
-
-@pytest.fixture(autouse=True, params=[0, 1], ids=["block", "queue"])
-def spec_queue(request, monkeypatch):
-    """Every test here runs twice: spec launches through the block kernel and through queue mode (round 5:
-    persistent waves taking sphere pixels from per-XCD cursors and sharing their slots), set on every context
-    the test makes (after its set_split)."""
-    from iqpt import PathTracer, _lib
-    q = request.param
-    orig = PathTracer.set_split
-
-    def set_split(self, mode):
-        orig(self, mode)
-        lb = _lib.load()
-        lb.iqpt_debug_set_spec_queue.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
-        _lib.check(lb.iqpt_debug_set_spec_queue(self._h, q, 0), "iqpt_debug_set_spec_queue")
-
-    monkeypatch.setattr(PathTracer, "set_split", set_split)
-    _QUEUE[0] = q
-    yield q
-    _QUEUE[0] = 0
-
-
 def mode_of(pt, queue_fits=True) -> int:
-    """The last launch's mode (6: spec); in queue runs a spec launch must have run the queue kernel (when its
-    LDS fits the device's per-block limit: queue_fits)."""
+    """The last launch's mode (6: spec). (queue_fits: kept for the callers; round 6 archived queue mode.)"""
     from iqpt import _lib
     lb = _lib.load()
     lb.iqpt_debug_split_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
     info = (C.c_ulonglong * 8)()
     _lib.check(lb.iqpt_debug_split_info(pt._h, info), "iqpt_debug_split_info")
-    mode = int(info[7])
-    if mode == 6:
-        lb.iqpt_debug_spec_info.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
-        si = (C.c_ulonglong * 8)()
-        _lib.check(lb.iqpt_debug_spec_info(pt._h, si), "iqpt_debug_spec_info")
-        q = (int(si[2]) >> 32) > 0
-        assert q == bool(_QUEUE[0]) or (not queue_fits and not q), (int(si[2]) >> 32, _QUEUE[0])
-    return mode
+    return int(info[7])
 
 
 def _check(pt, lin, bgra, fr):
@@ -303,9 +271,9 @@ def test_spec_plan_async_c3_share8(require_gpu):
     assert outs[0][3] == outs[1][3]
 
 
-@pytest.mark.parametrize("split,expect", [(SPLIT_SPEC, 6), (3, 3)])
+@pytest.mark.parametrize("split,expect", [(SPLIT_SPEC, 6)])
 def test_pipelined_async_copies(require_gpu, split, expect):
-    """Pipelined spec and FAN launches (the fan stream runs ahead, no join per launch) with a stream-ordered
+    """Pipelined spec launches (the fan stream runs ahead, no join per launch) with a stream-ordered
     frame copy after every launch, as the multi-GPU gather issues them: copy k holds exactly launch k's frame
     (the launches write two frame buffers in turn), a reset in the middle joins the streams, and the final
     state is the oracle's bit for bit."""

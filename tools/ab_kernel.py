@@ -154,10 +154,6 @@ def main():
             raw = np.array(wt[:3 * nw.value], dtype=np.uint64).reshape(-1, 3)
             if args.timeline_npy:
                 np.save(args.timeline_npy, raw)
-                qt = (C.c_ulonglong * 65536)()
-                lib.iqpt_debug_read_queue_times.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
-                if lib.iqpt_debug_read_queue_times(pt.handle, qt) == 0:
-                    np.save(args.timeline_npy.replace(".npy", "_queue.npy"), np.array(qt[:], dtype=np.uint64))
             a = (raw & np.uint64(0xffffffffffff)).astype(np.float64)    # 48-bit times (wave id above)
             a[:, 2] = (raw[:, 2] & np.uint64(0xffffffff)).astype(np.float64)
             t0 = a[:, 0].min()

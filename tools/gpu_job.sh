@@ -1,13 +1,12 @@
-# r06 run 6: plain-kernel wave timelines with per-phase cycles (two rays on / off; full frame overlapped, sphere crop)
+# r06 run 7: after the prune (chain kernel, FAN launch mode, spec queue mode archived): the whole -m gpu suite,
+# smoke, the default line
 mkdir -p gpurun_out
 O=gpurun_out
-R=r06_06
+R=r06_07
 export TMPDIR=/tmp
-for t in 1 0; do
-  timeout -k 10 300 python3 tools/wave_timeline.py --two-ray $t --out $O/${R}_wt_full_t$t.json > $O/${R}_wt_full_t$t.log 2>&1 || { tail -20 $O/${R}_wt_full_t$t.log; exit 1; }
-  timeout -k 10 300 python3 tools/wave_timeline.py --two-ray $t --overlap 0 --crop 760,1160,480,96 --out $O/${R}_wt_crop_t$t.json > $O/${R}_wt_crop_t$t.log 2>&1 || { tail -20 $O/${R}_wt_crop_t$t.log; exit 1; }
-done
-for f in $O/${R}_wt_*.json; do python3 -c "
-import json; d=json.load(open('$f'))
-t=d['longest_5pct']
-print('$f', d['kernel_ms'], 'iters', t['iters']['50'], 'us/iter', t['us_per_iter']['50'], {k: v['50'] for k, v in t['cycles_per_iter'].items()})"; done
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/${R}_tests.log 2>&1 || { tail -40 $O/${R}_tests.log; exit 1; }
+tail -1 $O/${R}_tests.log
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/${R}_smoke.log 2>&1 || { tail -20 $O/${R}_smoke.log; exit 1; }
+tail -1 $O/${R}_smoke.log
+timeout -k 10 300 python3 bench.py --no-cpu-baseline > $O/${R}_default.json 2> $O/${R}_default.err || { tail -20 $O/${R}_default.err; exit 1; }
+python3 -c "import json; d=json.loads(open('$O/${R}_default.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['config']['kernel_option_bits'], d['bitexact_frac_vs_oracle'], d['lib'])"

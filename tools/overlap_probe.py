@@ -3,7 +3,7 @@
 render the same pixel set alternately without host synchronisation, against one context rendering the
 same number of launches back to back. Wall time per launch; no correctness claim (independent frames).
 
-    overlap_probe.py [--config c2] [--share N] [--mode plain|chain|fan|auto] [--out f.json]
+    overlap_probe.py [--config c2] [--share N] [--mode plain|spec|auto] [--out f.json]
 
 --share N: rank 0's rows of an N-way C3 split (one GPU's share); the ratio then says how much of a
 share launch is tail (latency) rather than throughput."""
@@ -23,11 +23,11 @@ from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c2")
 ap.add_argument("--share", type=int, default=1)
-ap.add_argument("--mode", default="plain", choices=["plain", "chain", "fan", "auto"])
+ap.add_argument("--mode", default="plain", choices=["plain", "spec", "auto"])
 ap.add_argument("--launches", type=int, default=20)
 ap.add_argument("--out", default="")
 args = ap.parse_args()
-mode = {"plain": _lib.SPLIT_OFF, "chain": _lib.SPLIT_CHAIN, "fan": _lib.SPLIT_FAN, "auto": _lib.SPLIT_AUTO}[args.mode]
+mode = {"plain": _lib.SPLIT_OFF, "spec": _lib.SPLIT_SPEC, "auto": _lib.SPLIT_AUTO}[args.mode]
 
 cfg = CONFIGS[args.config]
 n = args.launches

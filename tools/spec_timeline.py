@@ -4,13 +4,10 @@ block the s_memrealtime stamps (100 MHz) at its start, after round 0's slot pass
 parity pixel's fix-up pass and second walk) and at its end (iqpt_debug_spec_timeline). Prints percentiles of the block start, the phases and the end, and
 the blocks that needed more than one round.
 
-    spec_timeline.py [--share 8] [--specfan 1] [--plan 1] [--parity R] [--parity-max R] [--queue 1 --qbpc B]
-                     [--out f.json]
+    spec_timeline.py [--share 8] [--specfan 1] [--plan 1] [--parity R] [--out f.json]
 
 --specfan: 1 = the spec kernel alone on the stream (the fan kernel after it), 0 = beside the fan kernel
-on a second stream. --queue 1: queue mode (iqpt_specq_kernel, B blocks per CU): per wave its start and end,
-slot-loop iterations, pixels / walks / fix-ups, and its time in admissions, walks (wait, chain, gather, fold),
-hand-outs and rays."""
+on a second stream. (Round 6 archived queue mode and the plan-cap / priority / parity-bound knobs.)"""
 import argparse
 import ctypes as C
 import json
@@ -31,12 +28,7 @@ ap.add_argument("--share", type=int, default=8)
 ap.add_argument("--specfan", type=int, default=1)
 ap.add_argument("--warm", type=int, default=3)
 ap.add_argument("--plan", type=int, default=1, help="iqpt_debug_spec_plan mode (0 none, 1 asynchronous)")
-ap.add_argument("--cap", type=float, default=0.0, help="iqpt_debug_set_spec_cap (0: the default)")
 ap.add_argument("--parity", type=float, default=None, help="iqpt_debug_set_spec_parity in slots per sample (0: off)")
-ap.add_argument("--prio", type=int, default=None, help="iqpt_debug_set_spec_prio step (0: off)")
-ap.add_argument("--parity-max", type=float, default=None, help="iqpt_debug_set_spec_parity_max in slots per sample")
-ap.add_argument("--queue", type=int, default=None, help="iqpt_debug_set_spec_queue mode (1: queue mode)")
-ap.add_argument("--qbpc", type=int, default=0, help="queue mode's blocks per CU (0: the default)")
 ap.add_argument("--two-ray", type=int, default=None, help="iqpt_debug_set_two_ray (kOptPipe: 1 on, 0 off)")
 ap.add_argument("--out", default="")
 args = ap.parse_args()
@@ -54,19 +46,6 @@ lb.iqpt_debug_set_specfan.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
 _lib.check(lb.iqpt_debug_set_specfan(pt._h, args.specfan, 0xffffffff), "iqpt_debug_set_specfan")
 lb.iqpt_debug_spec_plan.argtypes = [C.c_void_p, C.c_int]
 _lib.check(lb.iqpt_debug_spec_plan(pt._h, args.plan), "iqpt_debug_spec_plan")
-if args.cap:
-    lb.iqpt_debug_set_spec_cap.argtypes = [C.c_void_p, C.c_double]
-    _lib.check(lb.iqpt_debug_set_spec_cap(pt._h, args.cap), "iqpt_debug_set_spec_cap")
-if args.queue is not None:
-    lb.iqpt_debug_set_spec_queue.argtypes = [C.c_void_p, C.c_int, C.c_uint32]
-    _lib.check(lb.iqpt_debug_set_spec_queue(pt._h, args.queue, args.qbpc), "iqpt_debug_set_spec_queue")
-if args.parity_max is not None:
-    lb.iqpt_debug_set_spec_parity_max.argtypes = [C.c_void_p, C.c_uint32]
-    _lib.check(lb.iqpt_debug_set_spec_parity_max(pt._h, min(0xffffffff, int(round(args.parity_max * 256)))),
-               "iqpt_debug_set_spec_parity_max")
-if args.prio is not None:
-    lb.iqpt_debug_set_spec_prio.argtypes = [C.c_void_p, C.c_uint32]
-    _lib.check(lb.iqpt_debug_set_spec_prio(pt._h, args.prio), "iqpt_debug_set_spec_prio")
 if args.parity is not None:
     lb.iqpt_debug_set_spec_parity.argtypes = [C.c_void_p, C.c_uint32]
     _lib.check(lb.iqpt_debug_set_spec_parity(pt._h, int(round(args.parity * 256))), "iqpt_debug_set_spec_parity")
@@ -100,36 +79,6 @@ def pct(a):
     return {str(q): round(float(np.percentile(a, q)), 1) for q in (0, 10, 50, 90, 99, 100)}
 
 
-if (int(info[2]) >> 32) > 0:
-    # queue mode: per wave start, end | iterations << 48, pixels | walks << 16 | fix-ups << 32 | XCD << 48, time in
-    # admissions | walks << 16 | hand-outs << 32 | rays << 48 (10-ns ticks)
-    w4 = raw8
-    ws = (w4[:, 0] & np.uint64(0xffffffffffff)).astype(np.float64)
-    we = (w4[:, 1] & np.uint64(0xffffffffffff)).astype(np.float64)
-    it = (w4[:, 1] >> np.uint64(48)).astype(np.int64)
-    npx_w = (w4[:, 2] & np.uint64(0xffff)).astype(np.int64)
-    nwk = ((w4[:, 2] >> np.uint64(16)) & np.uint64(0xffff)).astype(np.int64)
-    nfx = ((w4[:, 2] >> np.uint64(32)) & np.uint64(0xffff)).astype(np.int64)
-    xcd = ((w4[:, 2] >> np.uint64(48)) & np.uint64(0xff)).astype(np.int64)
-    t0 = ws.min()
-    end_w = (we - t0) / 100.0
-    res = {"share": args.share, "queue": 1, "qbpc": args.qbpc or None, "specfan": args.specfan, "plan": args.plan,
-           "parity": args.parity, "parity_max": args.parity_max, "waves": int(len(w4)), "grid_blocks": int(info[2]) >> 32,
-           "spec_stats": spec_stats, "kernel_us": round(float(end_w.max()), 1),
-           "start_us": pct((ws - t0) / 100.0), "end_us": pct(end_w),
-           "end_max_over_median": round(float(end_w.max() / max(np.median(end_w), 1e-9)), 3),
-           "iters": pct(it), "pixels_per_wave": pct(npx_w), "walks_per_wave": pct(nwk), "fixups_per_wave": pct(nfx),
-           "xcd_end_us": {str(x): round(float(end_w[xcd == x].max()), 1) for x in np.unique(xcd)},
-           "us_per_iter": pct(end_w / np.maximum(it, 1))}
-    ph = w4[:, 3]
-    for i, name in enumerate(("admit", "walk", "handout", "trace")):
-        res[f"{name}_us"] = pct(((ph >> np.uint64(16 * i)) & np.uint64(0xffff)).astype(np.float64) / 100.0)
-    for i, name in enumerate(("wait", "chain", "gather", "fold")):
-        res[f"walk_{name}_us"] = pct(((w4[:, 4] >> np.uint64(16 * i)) & np.uint64(0xffff)).astype(np.float64) / 100.0)
-    print(json.dumps(res), flush=True)
-    if args.out:
-        Path(args.out).write_text(json.dumps(res, indent=1) + "\n")
-    sys.exit(0)
 raw = raw8[:, :3]
 # per wave (round 5: the waves of a block run their rounds on their own): end | slot-loop iterations << 48
 wave_iters = (raw8[:, 4:] >> np.uint64(48)).astype(np.int64)
@@ -144,7 +93,7 @@ wave_us = (wave_end - t0) / 100.0
 start, slots_end, walk_end, end = us[:, 0], us[:, 1], us[:, 2], wave_us.max(axis=1)
 
 
-res = {"share": args.share, "two_ray": args.two_ray, "specfan": args.specfan, "plan": args.plan, "cap": args.cap or None, "parity": args.parity, "parity_max": args.parity_max, "prio": args.prio,
+res = {"share": args.share, "two_ray": args.two_ray, "specfan": args.specfan, "plan": args.plan, "parity": args.parity,
        "blocks": int(n.value), "spec_stats": spec_stats,
        "kernel_us": round(float(end.max()), 1),
        "start_us": pct(start), "slots_us": pct(slots_end - start), "walk_us": pct(walk_end - slots_end),

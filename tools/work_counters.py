@@ -62,7 +62,7 @@ def main():
         pt.render(spp)
     o = C.c_int()
     _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(o)), "last options")
-    prod_opt = o.value
+    prod_opt = o.value & ~(1 << 30)                  # (bit 30: per-XCD tile lists, not an option)
     pt.close()
     # 2) the stats build of that option set (the 5-wave bound is not part of the algorithm)
     stats_opt = prod_opt | K_STATS
