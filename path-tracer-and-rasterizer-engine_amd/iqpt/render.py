@@ -140,10 +140,15 @@ class PathTracer:
     def gather_read(self, root: int, what: str = "both"):
         """Collective, synchronous (every rank calls it with the same `what`): on `root` the whole frame's
         (lin [W*H,4] float32, bgra [W*H,4] uint8), row-major, with None for a plane not asked for ("accum",
-        "frame" or "both"; iqpt_gather_read_select); None on every other rank."""
+        "frame" or "both"; iqpt_gather_read_select). Every other rank gets None (not a tuple: its host buffers
+        are not touched). The root is told apart by the rank given to comm_init(), which must come first: a
+        communicator set up another way raises here, instead of a root passing no buffers."""
         sel = {"accum": _lib.GATHER_ACCUM, "frame": _lib.GATHER_FRAME,
                "both": _lib.GATHER_ACCUM | _lib.GATHER_FRAME}[what]
-        is_root = root == getattr(self, "_comm_rank", None)
+        rank = getattr(self, "_comm_rank", None)
+        if rank is None:
+            raise RuntimeError("gather_read: call comm_init() on this PathTracer first (its rank decides the root)")
+        is_root = root == rank
         lin = (np.empty((self.width * self.height, 4), dtype=np.float32)
                if is_root and sel & _lib.GATHER_ACCUM else None)
         bgra = (np.empty((self.width * self.height, 4), dtype=np.uint8)

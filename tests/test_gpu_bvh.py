@@ -176,9 +176,9 @@ def test_anyhit_variants_on_c4(require_gpu, anyhit):
 ])
 @pytest.mark.parametrize("refill", [1, 16, 64])
 def test_stream_refill_group_sizes(require_gpu, preset, w, h, ps_args, launches, refill):
-    """Streamed-scene launches whose waves take new pixels only once `refill` lanes are idle (round 5: 16 by
-    default, neighbouring pixels together; 1 = a refill at every iteration with an idle lane; 64 = whole
-    waves): the pixels' results do not depend on when a lane takes them — bit-exact against the oracle."""
+    """Streamed-scene launches whose waves take new pixels only once `refill` lanes are idle (64, whole waves, by
+    default since round 5: a tile's pixels together; 1 = a refill at every iteration with an idle lane): the
+    pixels' results do not depend on when a lane takes them — bit-exact against the oracle."""
     sc = Scene()
     sc.add_preset(preset)
     pk = sc.build_packet()
