@@ -56,7 +56,7 @@ def parse():
     ap.add_argument("--spp", type=int, default=0,
                     help="samples per pixel per step (default: the config's; a progressive pass of C5's 1024)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=30.0,
+    ap.add_argument("--cpu-seconds", type=float, default=60.0,
                     help="wall time of the CPU-baseline sample (a bounded sample: the default run stays within "
                          "minutes; BASELINE.md §3's 60-s runs: --cpu-seconds 60)")
     ap.add_argument("--verify-rows", type=int, default=16)
@@ -186,8 +186,15 @@ def cpu_baseline(cfg, pk, cam, seconds: float) -> dict:
     scene: full-frame 1-spp passes until `seconds` of wall time (Mrays/s does not depend on spp)."""
     sys.path.insert(0, str(REPO / "oracle"))
     import oracle  # cpu_baseline leg only
+    from iqpt import _build
     threads = baseline_threads()
-    fr = oracle.OracleFrame(cfg.width, cfg.height, max_depth=cfg.max_depth)
+    # BASELINE.md §3: -O3 -march=native, built here for this host's CPU; the parity build (no -march) if that fails
+    try:
+        _, build = _build.build_oracle_native()
+        flavour = "native"
+    except (RuntimeError, OSError) as e:
+        build, flavour = f"the parity build liboracle.so (-march=native build failed: {str(e)[:120]})", "b"
+    fr = oracle.OracleFrame(cfg.width, cfg.height, max_depth=cfg.max_depth, flavour=flavour)
     rays = 0
     passes = 0
     t0 = time.perf_counter()
@@ -197,8 +204,12 @@ def cpu_baseline(cfg, pk, cam, seconds: float) -> dict:
         dt = time.perf_counter() - t0
         if dt >= seconds:
             break
+    info = cpu_info()
     return {"value": rays / dt / 1e6, "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "per_core": rays / dt / 1e6 / threads, **cpu_info(),
+            "per_core": rays / dt / 1e6 / threads, **info, "build": build, "seconds": round(dt, 1),
+            # the GPU box runs a command on its per-GPU CPU share (OMP_NUM_THREADS = 16 of the host's CPUs): the
+            # host-wide figure is that share's rate scaled linearly to every visible CPU, stated, not measured
+            "all_cpus_linear_estimate": round(rays / dt / 1e6 / threads * (info.get("cpus_visible") or threads), 1),
             "sample": f"{passes} full {cfg.width}x{cfg.height} 1-spp passes of {cfg.preset} "
                       f"(max_depth {cfg.max_depth}) in {dt:.1f} s, {rays} rays, {threads} OpenMP threads"}
 
@@ -238,34 +249,50 @@ def load_json(path: str, cfg_name: str):
 BYTES_PER_PIXEL_LAUNCH = 84     # RNG 24 read + 24 written, accumulator 16 + 16, BGRA8 4
 
 
+def _by_sha(cands, accept):
+    """The candidate profiles `accept` takes, the newest one of THESE kernel sources (kernel_sha16 equal to the
+    build's) first, else the newest of any (reported as stale). Returns (profile, path, same_sources) or None."""
+    from iqpt._build import kernel_source_sha16
+    want = kernel_source_sha16()
+    ok = [(d, c) for c in cands for d in [accept(c)] if d]
+    for d, c in ok:
+        if d.get("kernel_sha16") == want:
+            return d, c, True
+    return (ok[0][0], ok[0][1], False) if ok else None
+
+
+def _rel(c: Path) -> str:
+    c = c.resolve()
+    return str(c.relative_to(REPO)) if c.is_relative_to(REPO) else str(c)
+
+
 def find_pmc(cfg_name: str, spp: int, explicit: str):
     """The PMC traffic profile of THIS launch shape: same config and same samples per launch (traffic
     per launch grows with spp only through the kernel's own re-reads, but a 1-spp profile divided by a
-    16-spp kernel time is meaningless). Returns (profile, path) or (None, why)."""
+    16-spp kernel time is meaningless), of these kernel sources where one exists. Returns (profile, path,
+    same_sources) or (None, why, None)."""
     cands = [Path(explicit)] if explicit else sorted(
         (REPO / "profiles").glob(f"r0*/pmc_traffic_{cfg_name}*.json"), key=lambda q: (q.parent.name, q.name), reverse=True)
-    why = "no PMC profile of this config"
-    for c in cands:
+    why = ["no PMC profile of this config"]
+
+    def accept(c):
         d = load_json(str(c), cfg_name)
-        if not d:
-            continue
-        if d.get("spp_per_launch") != spp:
-            why = f"{c.relative_to(REPO)} was taken at {d.get('spp_per_launch')} spp per launch, this run launches {spp}"
-            continue
-        return d, str(c.relative_to(REPO))
-    return None, why
+        if d and d.get("spp_per_launch") != spp:
+            why[0] = f"{_rel(c)} was taken at {d.get('spp_per_launch')} spp per launch, this run launches {spp}"
+            return None
+        return d
+    got = _by_sha(cands, accept)
+    return (got[0], _rel(got[1]), got[2]) if got else (None, why[0], None)
 
 
 def find_mix(cfg_name: str, explicit: str):
-    """The PMC instruction-mix profile (tools/pmc_mix.py) of this config's current kernel: the explicit
-    file, else the newest round's profiles/r0*/<config>_pmc_mix*.json. Returns (profile, path)."""
+    """The PMC instruction-mix profile (tools/pmc_mix.py) of this config's kernel: the explicit file, else the
+    newest profiles/r0*/<config>_pmc_mix*.json of these kernel sources, else the newest of any. Returns
+    (profile, path, same_sources)."""
     cands = [Path(explicit)] if explicit else sorted(
         (REPO / "profiles").glob(f"r0*/{cfg_name}_pmc_mix*.json"), key=lambda q: (q.parent.name, q.name), reverse=True)
-    for c in cands:
-        d = load_json(str(c), cfg_name)
-        if d:
-            return d, str(c.resolve().relative_to(REPO)) if c.resolve().is_relative_to(REPO) else str(c)
-    return None, None
+    got = _by_sha(cands, lambda c: load_json(str(c), cfg_name))
+    return (got[0], _rel(got[1]), got[2]) if got else (None, None, None)
 
 
 def certain_pixels(pt, _lib) -> int:
@@ -290,25 +317,23 @@ LAUNCH_KERNELS = {"plain": "iqpt_render_kernel", "spec": "iqpt_spec_kernel + iqp
 def mix_for_launch(cfg_name: str, launch_mode: str, split_ways: int, explicit: str):
     """The instruction-mix profile of the kernels this launch mode ran: the plain kernel's for a full-frame
     plain line; for a spec line the spec and fan kernels' own at this share (profiles/r0*/pmc_mix_{spec,fan}_n<N>.json,
-    taken at the same C3 share); else none (no profile of those kernels). Returns (busy, split, source)."""
+    taken at the same C3 share); else none (no profile of those kernels). Returns (busy, split, source, same_sources)."""
     if explicit or (launch_mode == "plain" and split_ways == 1):
-        mix, src = find_mix(cfg_name, explicit)
-        return ((mix or {}).get("valu_busy_frac"), (mix or {}).get("wave_time_split"), src)
+        mix, src, same = find_mix(cfg_name, explicit)
+        return ((mix or {}).get("valu_busy_frac"), (mix or {}).get("wave_time_split"), src, same)
     if launch_mode == "spec":
         name = f"c3_share{split_ways}"
         got = {}
         for k in ("spec", "fan"):
             cands = sorted((REPO / "profiles").glob(f"r0*/pmc_mix_{k}_n{split_ways}*.json"),
                            key=lambda q: (q.parent.name, q.name), reverse=True)
-            for c in cands:
-                d = load_json(str(c), name)
-                if d:
-                    got[k] = (d.get("valu_busy_frac"), d.get("wave_time_split"), str(c.relative_to(REPO)))
-                    break
+            g = _by_sha(cands, lambda c: load_json(str(c), name))
+            if g:
+                got[k] = (g[0].get("valu_busy_frac"), g[0].get("wave_time_split"), _rel(g[1]), g[2])
         if len(got) == 2:
             return ({k: v[0] for k, v in got.items()}, {k: v[1] for k, v in got.items()},
-                    {k: v[2] for k, v in got.items()})
-    return None, None, None
+                    {k: v[2] for k, v in got.items()}, all(v[3] for v in got.values()))
+    return None, None, None, None
 
 
 def sky_pixels(pt, _lib) -> int:
@@ -335,15 +360,18 @@ def roofline(cfg, args, world, rays_per_launch, kern_avg_ms, launch_mode: str, s
     ref_tflops = f_ray * rays_per_launch / t / 1e12 if t > 0 else 0.0
     # PMC bytes only for the launch shape they were measured on (one GPU's full frame at this spp); the
     # algorithmic bytes (84 B per owned pixel per launch) for every line, rank 0's share at N > 1
-    pmc, pmc_src = find_pmc(cfg.name, spp, args.pmc_json) if world == 1 and not args.share_of else (None, "N > 1: per-rank PMC not collected")
+    pmc, pmc_src, pmc_same = (find_pmc(cfg.name, spp, args.pmc_json) if world == 1 and not args.share_of
+                              else (None, "N > 1: per-rank PMC not collected", None))
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
-    busy, wsplit, mix_src = mix_for_launch(cfg.name, launch_mode, split_ways, args.pmc_mix_json)
+    busy, wsplit, mix_src, mix_same = mix_for_launch(cfg.name, launch_mode, split_ways, args.pmc_mix_json)
     work_path, work_why = (args.work_json, None) if args.work_json else newest_work(cfg.name)
     work = load_json(work_path, cfg.name) if work_path else None
     out = {"bound": "valu", "unit": "TFLOP/s", "peak": FP32_PEAK_TFLOPS,
            "kernel": LAUNCH_KERNELS.get(launch_mode, launch_mode), "launch_mode": launch_mode,
            "kernel_avg_ms": round(kern_avg_ms, 4), "traffic": traffic,
-           "valu_busy_frac": busy, "wave_time_split": wsplit, "mix_source": mix_src}
+           "valu_busy_frac": busy, "wave_time_split": wsplit, "mix_source": mix_src,
+           # whether the PMC profiles were taken on these kernel sources (their kernel_sha16 = the build's)
+           "traffic_same_kernel_sources": pmc_same, "mix_same_kernel_sources": mix_same}
     ex = work["flops_per_ray"] * rays_per_launch / t / 1e12 if (work and work.get("flops_per_ray") and t > 0) else None
     if work_why:
         out["executed_work"] = {"missing": work_why}

@@ -23,6 +23,9 @@ from iqpt._lib import Camera, PacketDesc, PixelSet  # noqa: E402  (ctypes layout
 LIB = _HERE / "liboracle.so"
 LIB_GLIBC = _HERE / "liboracle_glibc.so"
 LIB_FMA = _HERE / "liboracle_fma.so"     # informational flavour: FMA contraction on, glibc libm
+# bench.py's CPU baseline: flavour B built on the host that runs it with -O3 -march=native (iqpt._build.
+# build_oracle_native), so it matches that host's CPU
+LIB_NATIVE = _HERE / "_native" / "liboracle_native.so"
 
 _cache: dict[str, C.CDLL] = {}
 _FP = C.POINTER(C.c_float)
@@ -30,9 +33,10 @@ _UP = C.POINTER(C.c_uint32)
 
 
 def load(glibc: bool = False, flavour: str | None = None) -> C.CDLL:
-    """flavour: None / "b" (the parity target), "glibc", "fma" (see DESIGN.md §4)."""
+    """flavour: None / "b" (the parity target), "glibc", "fma" (see DESIGN.md §4), "native" (flavour B with
+    -march=native, built on this host: bench.py's CPU baseline)."""
     flavour = flavour or ("glibc" if glibc else "b")
-    path = {"b": LIB, "glibc": LIB_GLIBC, "fma": LIB_FMA}[flavour]
+    path = {"b": LIB, "glibc": LIB_GLIBC, "fma": LIB_FMA, "native": LIB_NATIVE}[flavour]
     key = str(path)
     if key in _cache:
         return _cache[key]

@@ -142,6 +142,24 @@ def build_oracle(force: bool = False) -> list[Path]:
     return built
 
 
+ORACLE_NATIVE_FLAGS = ["-O3", "-march=native", "-std=gnu11", "-fPIC", "-shared", "-fopenmp", *FP_FLAGS,
+                       "-fno-builtin-sinf"]
+
+
+def build_oracle_native() -> tuple[Path, str]:
+    """TEST INFRASTRUCTURE (bench.py's CPU baseline only): flavour B of the oracle compiled for THIS host's CPU
+    (-O3 -march=native, contraction off as every flavour-B build), into oracle/_native/. Built where
+    the baseline runs (the GPU box's CPU is not this container's), a few seconds with gcc. Returns (path, the
+    command line as a string)."""
+    src = ORACLE_DIR / "iqpt_oracle.c"
+    dst = ORACLE_DIR / "_native" / "liboracle_native.so"
+    dst.parent.mkdir(parents=True, exist_ok=True)
+    cmd = [CC, *ORACLE_NATIVE_FLAGS, f"-I{INCLUDE}", f"-I{CSRC}", str(src), "-o", str(dst.with_suffix(".so.tmp")), "-lm"]
+    _run(cmd)
+    os.replace(dst.with_suffix(".so.tmp"), dst)
+    return dst, " ".join([Path(CC).name, *ORACLE_NATIVE_FLAGS, "-lm"])
+
+
 def build_all(force: bool = False) -> None:
     build_lib(force)
     build_tools(force)

@@ -47,3 +47,15 @@ def test_fma_flavour_is_close_but_not_within_bits(preset, w, h, spp, depth, crop
     # handful of path decisions; the mean colour stays close
     assert c["rmse"] < 1e-3, c
     assert c["bitexact"] < c["npix"], "the FMA build must actually contract (vfmadd in liboracle_fma.so)"
+
+
+@pytest.mark.parametrize("preset,w,h,spp,depth,crop", CASES)
+def test_native_baseline_build_is_flavour_b(preset, w, h, spp, depth, crop):
+    """bench.py's CPU baseline runs flavour B built with -O3 -march=native on the host that runs it:
+    with contraction off the vector ISA changes no bit, so the baseline times the same computation the GPU does."""
+    from iqpt import _build
+    _build.build_oracle_native()
+    fr = _frames(preset, w, h, spp, depth, crop, ("b", "native"))
+    assert (fr["b"].lin.view("u4") == fr["native"].lin.view("u4")).all()
+    assert (fr["b"].bgra == fr["native"].bgra).all()
+    assert (fr["b"].states == fr["native"].states).all()

@@ -21,6 +21,10 @@ import csv
 import json
 import sys
 from collections import defaultdict
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "path-tracer-and-rasterizer-engine_amd"))
+from iqpt._build import kernel_source_sha16  # noqa: E402  (the kernels the profile describes; bench.py keys on it)
 
 SIMDS = 256 * 4
 
@@ -57,6 +61,7 @@ def main():
     res = {
         "config": config,
         "kernel": label or KERNEL,
+        "kernel_sha16": kernel_source_sha16(),
         "wave_iterations_per_launch": iters,
         "counters": {**a, **b},
         "per_iteration": {k: round(v / iters, 2) for k, v in a.items() if k.startswith("SQ_INSTS")},

@@ -24,6 +24,10 @@ import csv
 import json
 import sys
 from collections import defaultdict
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parent.parent / "path-tracer-and-rasterizer-engine_amd"))
+from iqpt._build import kernel_source_sha16  # noqa: E402  (the kernels the profile describes; bench.py keys on it)
 
 
 def per_kernel(path, counter, kernel="iqpt_render_kernel"):
@@ -54,6 +58,7 @@ def main():
     w_avg = sum(v["write_bytes"] for v in parts.values())
     first = parts[kernels[0]]
     res = {"config": config, "spp_per_launch": int(spp), "kernel": "+".join(kernels),
+           "kernel_sha16": kernel_source_sha16(),
            "dispatches_fetch": first["dispatches_fetch"], "dispatches_write": first["dispatches_write"],
            "last_dispatches_only": last or None,
            "fetch_bytes_raw": f_avg, "write_bytes": w_avg, "fetch_bytes_corrected": 2 * f_avg,
