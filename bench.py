@@ -112,6 +112,9 @@ def parse():
                          "(iqpt_debug_set_two_ray; default: the library's, on)")
     ap.add_argument("--anyhit", type=int, default=None, choices=[0, 1],
                     help="A/B: any-hit queries for triangle-only scenes (iqpt_debug_set_anyhit; default: the library's, on)")
+    ap.add_argument("--pixel-masks", type=int, default=None, choices=[0, 1],
+                    help="A/B: per-pixel candidate masks over streamed tile lists (iqpt_debug_set_pixel_masks; default: "
+                         "the library's, on)")
     ap.add_argument("--stream-refill", type=int, default=None,
                     help="A/B: idle lanes before a streamed-scene wave takes new pixels (iqpt_debug_set_stream_refill; 1..64)")
     ap.add_argument("--stream-xcd", type=int, default=None, choices=[0, 1, 2, 3],
@@ -556,6 +559,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_anyhit.argtypes = [C.c_void_p, C.c_int]
         _lib.check(lb.iqpt_debug_set_anyhit(pt._h, args.anyhit), "iqpt_debug_set_anyhit")
+    if args.pixel_masks is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_pixel_masks.argtypes = [C.c_void_p, C.c_int]
+        _lib.check(lb.iqpt_debug_set_pixel_masks(pt._h, args.pixel_masks), "iqpt_debug_set_pixel_masks")
     if args.stream_refill is not None:
         import ctypes as C
         lb = _lib.load()
@@ -809,6 +817,7 @@ def main():
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
                        **({"spec_parity": args.spec_parity} if args.spec_parity is not None else {}),
                        **({"anyhit": args.anyhit} if args.anyhit is not None else {}),
+                       **({"pixel_masks": args.pixel_masks} if args.pixel_masks is not None else {}),
                        **({"stream_refill": args.stream_refill} if args.stream_refill is not None else {}),
                        **({"resident_refill": args.resident_refill} if args.resident_refill is not None else {}),
                        **({"stream_xcd": args.stream_xcd} if args.stream_xcd is not None else {}),

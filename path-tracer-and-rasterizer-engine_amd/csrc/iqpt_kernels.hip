@@ -1551,11 +1551,14 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     st.d = p.sp_st[5 * (size_t)p.ns_cap + sp];
                     lds_sp[threadIdx.x] = make_uint4(sp, 0u, 0u, 0u);
                 }
+                uint32_t loc = 0;                                   // the pixel's place in its tile (kparams::pmask)
                 if (go) {
                     uint32_t col, row;
                     tile_decode(pix, p.ncols, p.nrows, &col, &row);
                     px = p.x0 + col;
                     py = p.y0 + row * p.ystep;
+                    if (STREAM)
+                        loc = (row % kCullTile) * min(kCullTile, p.ncols - (col / kCullTile) * kCullTile) + col % kCullTile;
                     if (spec) {
                         // state from the run planes (above)
                     } else if (kSplit && chunk_kind == 2) {
@@ -1621,7 +1624,7 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                     // the tile and word 0 of its triangle / sphere masks, kept in this lane's LDS slot for
                     // the pixel's lifetime (the global load latency is paid once per pixel, not per ray)
                     lds_cm[threadIdx.x] = make_uint4(p.cull[(size_t)tile * p.cull_stride],
-                                                     p.cull[(size_t)tile * p.cull_stride + p.cull_wt], tile, 0u);
+                                                     p.cull[(size_t)tile * p.cull_stride + p.cull_wt], tile, loc);
                 }
                 if (go) active = true;
             }
@@ -1940,9 +1943,31 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 // pair straight from global memory with wave-uniform loads, and needs none of the batches.
                 const bool list_tri = uni_tri != nullptr && p.list != nullptr;
                 const bool list_sph = uni_sph != nullptr && p.list != nullptr;
-                if (list_tri) {
+                const uint32_t la = list_tri ? p.list_off_tri[tt] : 0u, lb = list_tri ? p.list_off_tri[tt + 1] : 0u;
+                if (list_tri && p.pmask != nullptr && lb - la <= 32u * kPixMaskWords) {
+                    // per-pixel candidates (kparams::pmask): each lane walks the entries its own bundle may meet, in
+                    // list order; the wave leaves when no lane has one left (or, any-hit, every lane left has its hit)
                     const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
-                    const uint32_t a = p.list_off_tri[tt], b = p.list_off_tri[tt + 1];
+                    const uint32_t* pm = p.pmask + (size_t)tt * kPixMaskWords * 64u + lds_cm[threadIdx.x].w;
+                    const uint32_t nw = (lb - la + 31u) / 32u;
+                    uint32_t wi = 0, cur = tri_mask != nullptr ? pm[0] : 0u;
+                    while (true) {
+                        while (cur == 0u && tri_mask != nullptr && wi + 1u < nw) cur = pm[(size_t)(++wi) * 64u];
+                        const bool want = cur != 0u && !((OPT & kOptAnyHit) && p.anyhit && kind == kHitTri);
+                        if (!__any(want)) break;
+                        if (want) {
+                            const uint32_t e = wi * 32u + (uint32_t)__builtin_ctz(cur);
+                            cur &= cur - 1u;
+                            const uint32_t j = p.list[la + e];
+                            const float4* q = gp + (size_t)j * kTriPairFloat4;
+                            test_triangle_pair<OPT>(q[0], q[1], q[2], q[3], q[4], ray, closest, kind, hidx, 2 * j,
+                                                    2 * j + 1 < p.ntri);
+                        }
+                    }
+                    tri_none = true;
+                } else if (list_tri) {
+                    const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
+                    const uint32_t a = la, b = lb;
                     // software-pipelined: the next pair's records are loaded while this one is tested (C4 -1.7 %)
                     uint32_t j = a < b ? (uint32_t)__builtin_amdgcn_readfirstlane((int)p.list[a]) : 0u;
                     float4 q0, q1, q2, q3, q4;
@@ -2762,6 +2787,60 @@ __global__ __launch_bounds__(64) void iqpt_tile_list_order_kernel(const kbin b, 
         uint32_t r = 0;
         for (uint32_t q = 0; q < n; ++q) r += (sc[q] > s || (sc[q] == s && q < e)) ? 1u : 0u;
         list[a0 + r] = ix[e];
+    }
+}
+
+// Per-pixel candidate masks over a tile's triangle list (round 6, kparams::pmask). A pixel's camera rays (its own
+// jitter square) meet far fewer of the tile's candidates than the whole tile does — a streamed scene's silhouette
+// and pole tiles hold long lists that every miss ray of the tile tests to the end. One wave per tile, lane = pixel in
+// the tile's storage order; bit e of the lane's word w is set unless iq_interval.h proves that the reference's tests
+// reject both triangles of list entry 32 w + e for every camera ray of the pixel (tri_culled, the tests the tile
+// masks are built with). Skipping a cleared entry changes no result: the entry is rejected by that ray anyway, and
+// the set entries keep the list's order. Tiles with more than 32 kPixMaskWords entries are left without masks.
+__global__ __launch_bounds__(64) void iqpt_pixel_mask_kernel(const kbin b, const uint32_t* off_tri, const uint32_t* list,
+                                                             uint32_t* pmask) {
+    const uint32_t t = blockIdx.x, lane = threadIdx.x;
+    const uint32_t a = off_tri[t], n = off_tri[t + 1] - a;
+    if (n > 32u * kPixMaskWords) return;
+    const uint32_t tx = t % b.ntx, ty = t / b.ntx;
+    const uint32_t tw = min(kCullTile, b.ncols - tx * kCullTile), th = min(kCullTile, b.nrows - ty * kCullTile);
+    const bool inside = lane < tw * th;
+    iqiv::bundle bd;
+    bd.ok = false;
+    if (inside) {
+        iqiv::camera_in ci;
+        ci.width = b.width;
+        ci.height = b.height;
+        ci.rcp_width = 0.0f;
+        ci.rcp_height = 0.0f;
+        ci.inv_proj = b.inv_proj;
+        ci.inv_view = b.inv_view;
+        ci.cam_const = (int)b.cam_const;
+        ci.near_rw = b.cam_near_rw;
+        ci.far_rw = b.cam_far_rw;
+        const uint32_t x = b.x0 + tx * kCullTile + lane % tw, y = b.y0 + (ty * kCullTile + lane / tw) * b.ystep;
+        bd = iqiv::camera_bundle(ci, x, x, y, y);
+    }
+    uint32_t* out = pmask + (size_t)t * kPixMaskWords * 64u + lane;
+    for (uint32_t w = 0; w * 32u < n; ++w) {
+        uint32_t bits = 0u;
+        for (uint32_t i = 0; i < 32u && inside; ++i) {
+            const uint32_t e = w * 32u + i;
+            if (e >= n) break;
+            const uint32_t j = list[a + e];
+            bool culled = bd.ok;
+            for (uint32_t h = 0; h < 2u && culled; ++h) {
+                const uint32_t k = 2u * j + h;
+                if (k >= b.ntri) break;
+                const float4_storage* tr = b.tris + (size_t)k * kTriFloat4;
+                const float v0[3] = {tr[0].x, tr[0].y, tr[0].z};
+                const float e1[3] = {tr[0].w, tr[1].x, tr[1].y};
+                const float e2[3] = {tr[1].z, tr[1].w, tr[2].x};
+                culled = iqiv::tri_culled(bd, v0, e1, e2);
+            }
+            if (!culled) bits |= 1u << i;
+        }
+        out[(size_t)w * 64u] = bits;
     }
 }
 
@@ -3944,6 +4023,13 @@ int launch_tile_list_order(void* stream, const kbin& b, const uint32_t* off_tri,
     const uint32_t ntiles = b.ntx * b.nty;
     if (ntiles == 0) return 0;
     hipLaunchKernelGGL(iqpt_tile_list_order_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, b, off_tri, list);
+    return (int)hipGetLastError();
+}
+
+int launch_pixel_mask(void* stream, const kbin& b, const uint32_t* off_tri, const uint32_t* list, uint32_t* pmask) {
+    const uint32_t ntiles = b.ntx * b.nty;
+    if (ntiles == 0) return 0;
+    hipLaunchKernelGGL(iqpt_pixel_mask_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, b, off_tri, list, pmask);
     return (int)hipGetLastError();
 }
 

@@ -145,6 +145,9 @@ struct iqpt_ctx {
     uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
     uint32_t* d_list = nullptr;         // candidate lists of the masks, then their offsets (tri, sph)
     uint64_t list_total = 0;
+    uint32_t* d_pmask = nullptr;        // per-pixel candidate masks over the triangle lists (kparams::pmask)
+    bool pmask_on = true;               // iqpt_debug_set_pixel_masks (A/B: 0 walks the whole tile list)
+    uint32_t pmask_tiles = 0;           // tiles with masks (a triangle list of 1 .. 32 kPixMaskWords entries)
     size_t cull_cap = 0;       // words allocated
     bool cull_valid = false;
     uint32_t cull_ntx = 0, cull_nty = 0, cull_wt = 0, cull_stride = 0;
@@ -787,6 +790,9 @@ int build_cull(iqpt_ctx* c) {
     // worth building where the masks are long; skipped when they would exceed the list budget
     if (c->d_list) (void)hipFree(c->d_list);
     c->d_list = nullptr;
+    if (c->d_pmask) (void)hipFree(c->d_pmask);
+    c->d_pmask = nullptr;
+    c->pmask_tiles = 0;
     const bool want_lists = c->cull_stride > 8;
     uint64_t total = 0;
     std::vector<uint32_t> off(2 * ((size_t)ntiles + 1));
@@ -819,6 +825,18 @@ int build_cull(iqpt_ctx* c) {
             c->d_list = nullptr;
         } else {
             c->list_total = total;
+            // per-pixel masks over the triangle lists (a miss ray near a silhouette walks only the entries its
+            // own pixel may meet); without them (allocation or launch failure) the kernel walks whole lists
+            const size_t pm_words = (size_t)ntiles * iqpt::kPixMaskWords * 64u;
+            if (c->pmask_on && hipMalloc(&c->d_pmask, pm_words * sizeof(uint32_t)) == hipSuccess &&
+                !(iqpt::launch_pixel_mask(c->stream, b, d_off, c->d_list, c->d_pmask) == 0 &&
+                  hipStreamSynchronize(c->stream) == hipSuccess)) {
+                (void)hipFree(c->d_pmask);
+                c->d_pmask = nullptr;
+            }
+            if (c->d_pmask)
+                for (uint32_t t = 0; t < ntiles; ++t)
+                    c->pmask_tiles += (cnt[t] > 0 && cnt[t] <= 32u * iqpt::kPixMaskWords) ? 1u : 0u;
         }
     }
     std::vector<uint32_t> order(ntiles);
@@ -1375,6 +1393,7 @@ int iqpt_destroy(iqpt_ctx* c) {
     if (c->ev_sky) (void)hipEventDestroy(c->ev_sky);
     if (c->d_tile_order) (void)hipFree(c->d_tile_order);
     if (c->d_list) (void)hipFree(c->d_list);
+    if (c->d_pmask) (void)hipFree(c->d_pmask);
     for (auto& tl : c->timed)
         for (hipEvent_t ev : {tl.e0, tl.e1, tl.e1b})
             if (ev) (void)hipEventDestroy(ev);
@@ -1728,6 +1747,7 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             p.list = c->d_list;
             p.list_off_tri = c->d_list + c->list_total;
             p.list_off_sph = p.list_off_tri + (c->cull_ntx * c->cull_nty + 1);
+            p.pmask = c->d_pmask;
         }
     }
     p.ntx = (c->ncols + iqpt::kCullTile - 1) / iqpt::kCullTile;
@@ -2744,6 +2764,24 @@ int iqpt_debug_set_anyhit(iqpt_ctx* c, int on) {
     if (st) return st;
     c->anyhit_on = on != 0;
     c->cull_valid = false;               // the candidate lists' order follows the setting
+    return IQPT_OK;
+}
+
+/* Internal (tests, A/B): per-pixel candidate masks over the streamed kernel's tile lists (1, the default) or the
+ * whole list for every lane (0). Same bits either way. */
+int iqpt_debug_set_pixel_masks(iqpt_ctx* c, int on) {
+    if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
+    int st = enter(c);
+    if (st) return st;
+    c->pmask_on = on != 0;
+    c->cull_valid = false;
+    return IQPT_OK;
+}
+
+/* Internal (tests): tiles whose triangle lists have per-pixel masks (0: none built). */
+int iqpt_debug_pixel_mask_info(iqpt_ctx* c, uint32_t* tiles) {
+    if (!c || !tiles) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx or tiles is NULL");
+    *tiles = c->pmask_tiles;
     return IQPT_OK;
 }
 
