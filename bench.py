@@ -112,9 +112,9 @@ def parse():
                          "(iqpt_debug_set_two_ray; default: the library's, on)")
     ap.add_argument("--anyhit", type=int, default=None, choices=[0, 1],
                     help="A/B: any-hit queries for triangle-only scenes (iqpt_debug_set_anyhit; default: the library's, on)")
-    ap.add_argument("--pixel-masks", type=int, default=None, choices=[0, 1],
-                    help="A/B: per-pixel candidate masks over streamed tile lists (iqpt_debug_set_pixel_masks; default: "
-                         "the library's, on)")
+    ap.add_argument("--pixel-masks", type=int, default=None, choices=[0, 1, 2],
+                    help="A/B: per-pixel candidate masks over streamed tile lists (iqpt_debug_set_pixel_masks: 0 none, "
+                         "1 in the plain kernel, 2 the library's default: + iqpt_anyhit_kernel for any-hit scenes)")
     ap.add_argument("--stream-refill", type=int, default=None,
                     help="A/B: idle lanes before a streamed-scene wave takes new pixels (iqpt_debug_set_stream_refill; 1..64)")
     ap.add_argument("--stream-xcd", type=int, default=None, choices=[0, 1, 2, 3],
@@ -312,7 +312,8 @@ def certain_pixels(pt, _lib) -> int:
 
 
 # the kernels a launch mode runs (iqpt_debug_split_info's launch mode)
-LAUNCH_KERNELS = {"plain": "iqpt_render_kernel", "spec": "iqpt_spec_kernel + iqpt_fan_kernel",
+LAUNCH_KERNELS = {"plain": "iqpt_render_kernel", "anyhit": "iqpt_anyhit_kernel",
+                  "spec": "iqpt_spec_kernel + iqpt_fan_kernel",
                   "split": "iqpt_render_kernel (split rounds)",
                   "split+fan": "iqpt_render_kernel (split rounds) + iqpt_fan_kernel"}
 
@@ -321,7 +322,7 @@ def mix_for_launch(cfg_name: str, launch_mode: str, split_ways: int, explicit: s
     """The instruction-mix profile of the kernels this launch mode ran: the plain kernel's for a full-frame
     plain line; for a spec line the spec and fan kernels' own at this share (profiles/r0*/pmc_mix_{spec,fan}_n<N>.json,
     taken at the same C3 share); else none (no profile of those kernels). Returns (busy, split, source, same_sources)."""
-    if explicit or (launch_mode == "plain" and split_ways == 1):
+    if explicit or (launch_mode in ("plain", "anyhit") and split_ways == 1):
         mix, src, same = find_mix(cfg_name, explicit)
         return ((mix or {}).get("valu_busy_frac"), (mix or {}).get("wave_time_split"), src, same)
     if launch_mode == "spec":
@@ -704,8 +705,10 @@ def main():
     _lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
     _o = C.c_int(0)
     _lib.check(_lb.iqpt_debug_last_options(pt.handle, C.byref(_o)), "iqpt_debug_last_options")
-    last_opt = _o.value & ~(1 << 30)                   # the render-kernel option set of the last launch
+    last_opt = _o.value & ~((1 << 30) | (1 << 29))    # the render-kernel option set of the last launch
     xcd_lists = bool(_o.value & (1 << 30))             # ... whose tiles were dealt to per-XCD lists
+    if _o.value >= 0 and _o.value & (1 << 29):         # ... rendered by iqpt_anyhit_kernel instead (C4)
+        launch_mode = "anyhit"
     certain_px = certain_pixels(pt, _lib) if args.certain != "off" else 0
     sky_px = sky_pixels(pt, _lib) if (args.certain != "off" and args.sky != "off") else 0
 

@@ -100,10 +100,11 @@ struct kparams {
     const uint32_t* list_off_tri;
     const uint32_t* list_off_sph;
     // per-pixel candidate masks over the tile's triangle list (round 6, iqpt_pixel_mask_kernel): bit e of word w of
-    // pixel i (tile storage order) of tile t, at pmask[(t * kPixMaskWords + w) * 64 + i], is set unless the pixel's
-    // own bundle culls both triangles of list entry 32 w + e; tiles whose list is longer than 32 kPixMaskWords
-    // entries have none (the wave-uniform list loop). null = none
+    // pixel i (tile storage order) of tile t, at pmask[pmask_off[t] + 64 w + i], is set unless the pixel's own bundle
+    // culls both triangles of list entry 32 w + e; tiles whose list is longer than kPixMaskMax entries have none (the
+    // wave-uniform list loop). null = none
     const uint32_t* pmask;
+    const uint32_t* pmask_off;
     // kOptMaterials (packet material table): material index per triangle / sphere, the material
     // records (2 x float4 each: (albedo.rgb, type bits), (strength | sigma, A, B, 0)) and the
     // triangle shading records (kTriShadeFloat4 per triangle)
@@ -298,7 +299,8 @@ struct kbin {
     uint32_t* cull;                  // ntx * nty * stride words
 };
 constexpr uint32_t kCullTile = 8;
-constexpr uint32_t kPixMaskWords = 8;   // kparams::pmask: lists of up to 256 entries
+constexpr uint32_t kPixMaskMax = 1024;   // kparams::pmask: masks for triangle lists of up to this many entries
+constexpr uint32_t kAnyMaxEntries = 512; // iqpt_anyhit_kernel: lists of up to this many (16 mask words in registers)
 
 // Pixel state (accumulator, BGRA, RNG planes) is stored TILE-MAJOR over the owned set: 8x8 tiles
 // of (column, owned row) in row-major tile order, pixels row-major inside a tile; tiles of the last
@@ -391,7 +393,8 @@ int launch_tile_list(void* stream, const uint32_t* cull, uint32_t ntiles, uint32
 // Any-hit scenes: each tile's triangle candidate list reordered by how many of the tile's central rays a pair hits
 // (any order gives the same bits there; the candidate-list loop leaves sooner)
 int launch_tile_list_order(void* stream, const kbin& b, const uint32_t* off_tri, uint32_t* list);
-int launch_pixel_mask(void* stream, const kbin& b, const uint32_t* off_tri, const uint32_t* list, uint32_t* pmask);
+int launch_pixel_mask(void* stream, const kbin& b, const uint32_t* off_tri, const uint32_t* list,
+                      const uint32_t* pmask_off, uint32_t* pmask);
 // Device probe of the camera transforms (iqpt_debug_camera_rays): general and kOptCamAxis forms.
 int launch_camera_probe(void* stream, const kparams& p, const float* ndc, float* gen, float* axis, uint32_t n,
                         bool do_axis);
@@ -419,6 +422,8 @@ int spec_occupancy(const kparams& p, const kspec& s, int opt, int* blocks);
 // Certain-miss pixels (iqpt_sky_kernel): the p.miss pixels of `ntiles` tiles (tiles[i]),
 // lane = pixel, one wave per tile; resident scenes, reference materials, spp <= kAccTableMax.
 bool sky_variant_exists(int opt);
+bool anyhit_variant_exists(int opt);
+int launch_anyhit(void* stream, const kparams& p, int opt);
 int launch_sky(void* stream, const kparams& p, const uint32_t* tiles, uint32_t ntiles, int opt);
 // Sample-parallel anchored tiles (iqpt_fan_kernel): one block per tile of
 // p.tile_order[0 .. ntiles) — tiles without sphere candidates, reference materials, resident scene

@@ -1944,11 +1944,11 @@ __global__ __launch_bounds__(kRenderBlock, (min_waves_per_simd<OPT, STREAM>())) 
                 const bool list_tri = uni_tri != nullptr && p.list != nullptr;
                 const bool list_sph = uni_sph != nullptr && p.list != nullptr;
                 const uint32_t la = list_tri ? p.list_off_tri[tt] : 0u, lb = list_tri ? p.list_off_tri[tt + 1] : 0u;
-                if (list_tri && p.pmask != nullptr && lb - la <= 32u * kPixMaskWords) {
+                if (list_tri && p.pmask != nullptr && lb - la <= kPixMaskMax) {
                     // per-pixel candidates (kparams::pmask): each lane walks the entries its own bundle may meet, in
                     // list order; the wave leaves when no lane has one left (or, any-hit, every lane left has its hit)
                     const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
-                    const uint32_t* pm = p.pmask + (size_t)tt * kPixMaskWords * 64u + lds_cm[threadIdx.x].w;
+                    const uint32_t* pm = p.pmask + p.pmask_off[tt] + lds_cm[threadIdx.x].w;
                     const uint32_t nw = (lb - la + 31u) / 32u;
                     uint32_t wi = 0, cur = tri_mask != nullptr ? pm[0] : 0u;
                     while (true) {
@@ -2796,12 +2796,13 @@ __global__ __launch_bounds__(64) void iqpt_tile_list_order_kernel(const kbin b, 
 // the tile's storage order; bit e of the lane's word w is set unless iq_interval.h proves that the reference's tests
 // reject both triangles of list entry 32 w + e for every camera ray of the pixel (tri_culled, the tests the tile
 // masks are built with). Skipping a cleared entry changes no result: the entry is rejected by that ray anyway, and
-// the set entries keep the list's order. Tiles with more than 32 kPixMaskWords entries are left without masks.
+// the set entries keep the list's order. Tiles with more than kPixMaskMax entries are left without masks; a tile's
+// words start at pmask_off[t] (64 per 32 entries, compact over the tiles).
 __global__ __launch_bounds__(64) void iqpt_pixel_mask_kernel(const kbin b, const uint32_t* off_tri, const uint32_t* list,
-                                                             uint32_t* pmask) {
+                                                             const uint32_t* pmask_off, uint32_t* pmask) {
     const uint32_t t = blockIdx.x, lane = threadIdx.x;
     const uint32_t a = off_tri[t], n = off_tri[t + 1] - a;
-    if (n > 32u * kPixMaskWords) return;
+    if (n > kPixMaskMax) return;
     const uint32_t tx = t % b.ntx, ty = t / b.ntx;
     const uint32_t tw = min(kCullTile, b.ncols - tx * kCullTile), th = min(kCullTile, b.nrows - ty * kCullTile);
     const bool inside = lane < tw * th;
@@ -2821,7 +2822,7 @@ __global__ __launch_bounds__(64) void iqpt_pixel_mask_kernel(const kbin b, const
         const uint32_t x = b.x0 + tx * kCullTile + lane % tw, y = b.y0 + (ty * kCullTile + lane / tw) * b.ystep;
         bd = iqiv::camera_bundle(ci, x, x, y, y);
     }
-    uint32_t* out = pmask + (size_t)t * kPixMaskWords * 64u + lane;
+    uint32_t* out = pmask + pmask_off[t] + lane;
     for (uint32_t w = 0; w * 32u < n; ++w) {
         uint32_t bits = 0u;
         for (uint32_t i = 0; i < 32u && inside; ++i) {
@@ -3816,6 +3817,110 @@ __global__ __launch_bounds__(kSkyBlock) void iqpt_sky_kernel(const kparams p, co
     if (lane == 0 && nm) add_rays(p.rays, (unsigned long long)nm * p.spp);
 }
 
+// ------------------------------------------------------------------------------------------------
+// Any-hit scenes (kparams::anyhit: no sphere, every triangle emissive, the reference's materials) whose every tile
+// list has per-pixel masks (kparams::pmask), round 6. A sample of such a scene is one camera ray (the camera's two
+// jitter draws, camera.cu:24-25) that either meets some triangle — emissive, colour (10, 10, 10) clamped to (1, 1, 1)
+// (path_tracer.cu:278, 341-348), whichever triangle it is — or misses everything and takes the sky gradient
+// (:307-316). Lane = pixel, one wave per tile (in the cost order), four tiles per block: the tile's candidate list
+// in LDS, the lane's mask words in registers for all of its samples; per sample the lane tests its own candidates in
+// list order with the reference's Möller–Trumbore (test_triangle_pair) until one accepts the ray. The plain kernel's
+// operations for these paths — camera ray, tests, clamp, running mean with the launch table — so the same bits,
+// without its queue, refill, batches and path bookkeeping, and with no pixel waiting on another tile's list.
+constexpr uint32_t kAnyBlock = 256;
+
+template <int OPT>
+__global__ __launch_bounds__(kAnyBlock) void iqpt_anyhit_kernel(const kparams p) {
+    extern __shared__ __attribute__((aligned(16))) float4 lds[];
+    float2* tab = reinterpret_cast<float2*>(lds);
+    float* tab_n = reinterpret_cast<float*>(tab + ((p.spp + 1u) & ~1u));
+    uint32_t* lists = reinterpret_cast<uint32_t*>(tab_n + ((p.spp + 3u) & ~3u));
+    for (uint32_t k = threadIdx.x; k < p.spp; k += kAnyBlock) {
+        const uint64_t n = p.frame0 + k + 1;
+        tab[k] = make_float2(1.0f / (float)n, (float)(n - 1) / (float)n);
+        tab_n[k] = (float)n;
+    }
+    const uint32_t wv = threadIdx.x / 64u, lane = __lane_id();
+    const uint32_t q = blockIdx.x * (kAnyBlock / 64u) + wv;
+    const bool live = q < p.ntiles;
+    const uint32_t t = live ? (p.tile_order ? p.tile_order[q] : q) : 0u;
+    const uint32_t la = live ? p.list_off_tri[t] : 0u, n = live ? p.list_off_tri[t + 1] - la : 0u;
+    uint32_t* wl = lists + wv * kAnyMaxEntries;
+    for (uint32_t e = lane; e < n; e += 64u) wl[e] = p.list[la + e];
+    __syncthreads();
+    if (!live) return;
+    const uint32_t tx = t % p.ntx, ty = t / p.ntx;
+    const uint32_t th = min(kCullTile, p.nrows - ty * kCullTile), tw = min(kCullTile, p.ncols - tx * kCullTile);
+    if (lane < tw * th) {
+        const uint32_t pix = ty * kCullTile * p.ncols + tx * kCullTile * th + lane;   // tile-major storage
+        uint32_t col, row;
+        tile_decode(pix, p.ncols, p.nrows, &col, &row);
+        const uint32_t px = p.x0 + col, py = p.y0 + row * p.ystep;
+        rng6 st = {p.rng[pix], p.rng[(size_t)p.npix + pix], p.rng[2 * (size_t)p.npix + pix],
+                   p.rng[3 * (size_t)p.npix + pix], p.rng[4 * (size_t)p.npix + pix], p.rng[5 * (size_t)p.npix + pix]};
+        const float4 a0 = reinterpret_cast<const float4*>(p.lin)[pix];
+        float ax = a0.x, ay = a0.y, az = a0.z;
+        constexpr uint32_t kW = kAnyMaxEntries / 32u;
+        uint32_t wm[kW];
+        const uint32_t* pm = p.pmask + p.pmask_off[t] + lane;
+#pragma unroll
+        for (uint32_t w = 0; w < kW; ++w) wm[w] = w * 32u < n ? pm[(size_t)w * 64u] : 0u;
+        const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
+        for (uint32_t k = 0; k < p.spp; ++k) {
+            ray3 ray;
+            camera_ray<OPT>(p, px, py, st, ray);
+            float closest = kTMax;
+            int kind = kHitNone;
+            uint32_t hidx = 0;
+#pragma unroll
+            for (uint32_t w = 0; w < kW; ++w) {
+                uint32_t m = wm[w];
+                while (m != 0u && kind != kHitTri) {
+                    const uint32_t j = wl[w * 32u + (uint32_t)__builtin_ctz(m)];
+                    m &= m - 1u;
+                    const float4* qq = gp + (size_t)j * kTriPairFloat4;
+                    test_triangle_pair<OPT>(qq[0], qq[1], qq[2], qq[3], qq[4], ray, closest, kind, hidx, 2 * j,
+                                            2 * j + 1 < p.ntri);
+                }
+            }
+            float cx, cy, cz;
+            if (kind == kHitTri) {
+                cx = 1.0f;                                       // emissive (1, 10): 10 clamped (:345-347)
+                cy = 1.0f;
+                cz = 1.0f;
+            } else {
+                const float a = (ray.dy + 1.0f) * 0.5f;          // sky gradient (:308-313)
+                const float one_a = 1.0f - a;
+                cx = one_a + a * 0.5f;
+                cy = one_a + a * 0.7f;
+                cz = one_a + a * 1.0f;
+                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+            }
+            const float2 tv = tab[k];
+            float qx, qy, qz;
+            mean_terms<OPT>(0.0f + cx, 0.0f + cy, 0.0f + cz, tab_n[k], tv.x, p.mean_tiny, qx, qy, qz);
+            ax = qx + ax * tv.y;
+            ay = qy + ay * tv.y;
+            az = qz + az * tv.y;
+        }
+        const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
+        const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
+        const uint32_t b8 = to_u8(255.0f * iq_sqrtf(az));
+        p.bgra[tile_to_compact(pix, p.ncols, p.nrows)] = b8 | (g8 << 8) | (r8 << 16) | (255u << 24);
+        reinterpret_cast<float4*>(p.lin)[pix] = make_float4(ax, ay, az, 0.0f);
+        p.rng[pix] = st.v0;
+        p.rng[(size_t)p.npix + pix] = st.v1;
+        p.rng[2 * (size_t)p.npix + pix] = st.v2;
+        p.rng[3 * (size_t)p.npix + pix] = st.v3;
+        p.rng[4 * (size_t)p.npix + pix] = st.v4;
+        p.rng[5 * (size_t)p.npix + pix] = st.d;
+    }
+    // one closest-hit query per sample (the hit or the miss ends the path at crt_depth 1)
+    if (lane == 0) add_rays(p.rays, (unsigned long long)(tw * th) * p.spp);
+}
+
 template <int OPT>
 __global__ __launch_bounds__(kFanBlock, 2) void iqpt_fan_kernel(const kparams p) {
     fan_body<OPT>(p, blockIdx.x);
@@ -4026,10 +4131,12 @@ int launch_tile_list_order(void* stream, const kbin& b, const uint32_t* off_tri,
     return (int)hipGetLastError();
 }
 
-int launch_pixel_mask(void* stream, const kbin& b, const uint32_t* off_tri, const uint32_t* list, uint32_t* pmask) {
+int launch_pixel_mask(void* stream, const kbin& b, const uint32_t* off_tri, const uint32_t* list,
+                      const uint32_t* pmask_off, uint32_t* pmask) {
     const uint32_t ntiles = b.ntx * b.nty;
     if (ntiles == 0) return 0;
-    hipLaunchKernelGGL(iqpt_pixel_mask_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, b, off_tri, list, pmask);
+    hipLaunchKernelGGL(iqpt_pixel_mask_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, b, off_tri, list,
+                       pmask_off, pmask);
     return (int)hipGetLastError();
 }
 
@@ -4152,6 +4259,44 @@ int launch_sky(void* stream, const kparams& p, const uint32_t* tiles, uint32_t n
     if (!v || p.spp > kAccTableMax || p.miss == nullptr || tiles == nullptr) return (int)hipErrorInvalidDeviceFunction;
     if (ntiles == 0 || p.spp == 0) return 0;
     return v->launch((hipStream_t)stream, p, tiles, ntiles, ((p.spp + 1u) & ~1u) * 8u + ((p.spp + 3u) & ~3u) * 4u);
+}
+
+// iqpt_anyhit_kernel launches: keyed like the sky kernel (camera form, division forms)
+namespace {
+template <int OPT>
+int anyhit_launch_t(hipStream_t stream, const kparams& p, uint32_t lds) {
+    dispatch(iqpt_anyhit_kernel<OPT>, dim3((p.ntiles + kAnyBlock / 64u - 1u) / (kAnyBlock / 64u)), dim3(kAnyBlock),
+             lds, stream, p);
+    return (int)hipGetLastError();
+}
+struct anyhit_variant {
+    int key;
+    int (*launch)(hipStream_t, const kparams&, uint32_t);
+};
+const anyhit_variant kAnyVariants[] = {
+    {kOptFastDiv, anyhit_launch_t<kOptDefault>},
+    {0, anyhit_launch_t<kOptDefault & ~kOptFastDiv>},
+    {kOptFastDiv | kOptCamAxis, anyhit_launch_t<kOptDefault | kOptCamAxis>},
+};
+const anyhit_variant* find_anyhit(int opt) {
+    if ((opt & (kOptAccTable | kOptCamConst | kOptPair)) != (kOptAccTable | kOptCamConst | kOptPair) ||
+        (opt & (kOptMaterials | kOptStats)))
+        return nullptr;
+    for (const anyhit_variant& v : kAnyVariants)
+        if (v.key == (opt & kFanKeyBits)) return &v;
+    return nullptr;
+}
+}  // namespace
+
+bool anyhit_variant_exists(int opt) { return find_anyhit(opt) != nullptr; }
+
+int launch_anyhit(void* stream, const kparams& p, int opt) {
+    const anyhit_variant* v = find_anyhit(opt);
+    if (!v || p.spp > kAccTableMax || !p.list || !p.list_off_tri || !p.pmask || !p.pmask_off || !p.anyhit)
+        return (int)hipErrorInvalidDeviceFunction;
+    if (p.ntiles == 0 || p.spp == 0) return 0;
+    return v->launch((hipStream_t)stream, p,
+                     ((p.spp + 1u) & ~1u) * 8u + ((p.spp + 3u) & ~3u) * 4u + (kAnyBlock / 64u) * kAnyMaxEntries * 4u);
 }
 
 uint32_t fan_lds(const kparams& p) { return fan_lds_bytes(p.ntri_pairs, p.spp); }

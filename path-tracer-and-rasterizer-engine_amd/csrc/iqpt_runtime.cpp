@@ -145,9 +145,12 @@ struct iqpt_ctx {
     uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
     uint32_t* d_list = nullptr;         // candidate lists of the masks, then their offsets (tri, sph)
     uint64_t list_total = 0;
-    uint32_t* d_pmask = nullptr;        // per-pixel candidate masks over the triangle lists (kparams::pmask)
-    bool pmask_on = true;               // iqpt_debug_set_pixel_masks (A/B: 0 walks the whole tile list)
-    uint32_t pmask_tiles = 0;           // tiles with masks (a triangle list of 1 .. 32 kPixMaskWords entries)
+    uint32_t* d_pmask = nullptr;        // per-tile word offsets (ntiles + 1), then the per-pixel candidate masks (kparams::pmask)
+    int pmask_mode = 2;                 // iqpt_debug_set_pixel_masks: 0 none, 1 in the plain kernel, 2 + iqpt_anyhit_kernel
+    uint32_t pmask_tiles = 0;           // tiles with masks (a triangle list of 1 .. kPixMaskMax entries)
+    bool pmask_all = false;             // every list within kAnyMaxEntries and no tile with a sphere candidate
+    uint32_t list_max = 0;              // the longest triangle list
+    bool last_anyk = false;             // the last launch ran iqpt_anyhit_kernel
     size_t cull_cap = 0;       // words allocated
     bool cull_valid = false;
     uint32_t cull_ntx = 0, cull_nty = 0, cull_wt = 0, cull_stride = 0;
@@ -793,6 +796,8 @@ int build_cull(iqpt_ctx* c) {
     if (c->d_pmask) (void)hipFree(c->d_pmask);
     c->d_pmask = nullptr;
     c->pmask_tiles = 0;
+    c->pmask_all = false;
+    c->list_max = 0;
     const bool want_lists = c->cull_stride > 8;
     uint64_t total = 0;
     std::vector<uint32_t> off(2 * ((size_t)ntiles + 1));
@@ -827,16 +832,32 @@ int build_cull(iqpt_ctx* c) {
             c->list_total = total;
             // per-pixel masks over the triangle lists (a miss ray near a silhouette walks only the entries its
             // own pixel may meet); without them (allocation or launch failure) the kernel walks whole lists
-            const size_t pm_words = (size_t)ntiles * iqpt::kPixMaskWords * 64u;
-            if (c->pmask_on && hipMalloc(&c->d_pmask, pm_words * sizeof(uint32_t)) == hipSuccess &&
-                !(iqpt::launch_pixel_mask(c->stream, b, d_off, c->d_list, c->d_pmask) == 0 &&
+            // compact: 64 words per 32 entries of each tile with at most kPixMaskMax entries, after the offsets
+            std::vector<uint32_t> pm_off((size_t)ntiles + 1);
+            uint64_t pm_words = 0;
+            for (uint32_t t = 0; t < ntiles; ++t) {
+                pm_off[t] = (uint32_t)pm_words;          // (used only when every offset fits: `fits` below)
+                if (cnt[t] <= iqpt::kPixMaskMax) pm_words += 64u * (((uint64_t)cnt[t] + 31u) / 32u);
+            }
+            pm_off[ntiles] = (uint32_t)pm_words;
+            const bool fits = (uint64_t)ntiles + 1 + pm_words < 0xffffffffull;
+            if (c->pmask_mode != 0 && fits &&
+                hipMalloc(&c->d_pmask, ((size_t)ntiles + 1 + pm_words) * sizeof(uint32_t)) == hipSuccess &&
+                !(hipMemcpyAsync(c->d_pmask, pm_off.data(), pm_off.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                                 c->stream) == hipSuccess &&
+                  iqpt::launch_pixel_mask(c->stream, b, d_off, c->d_list, c->d_pmask, c->d_pmask + ntiles + 1) == 0 &&
                   hipStreamSynchronize(c->stream) == hipSuccess)) {
                 (void)hipFree(c->d_pmask);
                 c->d_pmask = nullptr;
             }
-            if (c->d_pmask)
-                for (uint32_t t = 0; t < ntiles; ++t)
-                    c->pmask_tiles += (cnt[t] > 0 && cnt[t] <= 32u * iqpt::kPixMaskWords) ? 1u : 0u;
+            if (c->d_pmask) {
+                c->pmask_all = true;
+                for (uint32_t t = 0; t < ntiles; ++t) {
+                    c->list_max = std::max(c->list_max, cnt[t]);
+                    c->pmask_tiles += (cnt[t] > 0 && cnt[t] <= iqpt::kPixMaskMax) ? 1u : 0u;
+                    c->pmask_all = c->pmask_all && cnt[t] <= iqpt::kAnyMaxEntries && cnt[ntiles + t] == 0;
+                }
+            }
         }
     }
     std::vector<uint32_t> order(ntiles);
@@ -1747,7 +1768,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             p.list = c->d_list;
             p.list_off_tri = c->d_list + c->list_total;
             p.list_off_sph = p.list_off_tri + (c->cull_ntx * c->cull_nty + 1);
-            p.pmask = c->d_pmask;
+            if (c->d_pmask) {
+                p.pmask_off = c->d_pmask;
+                p.pmask = c->d_pmask + (c->cull_ntx * c->cull_nty + 1);
+            }
         }
     }
     p.ntx = (c->ncols + iqpt::kCullTile - 1) / iqpt::kCullTile;
@@ -1758,13 +1782,18 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     p.rays = c->d_rays;
     p.queue = c->d_queue;
     p.stats = c->d_stats;
+    // any-hit scenes whose every tile list has per-pixel masks: iqpt_anyhit_kernel renders the launch (one camera
+    // ray per sample, the lane's own candidates; no BVH-primary tuning, no queue)
+    const bool anyk = c->pmask_mode == 2 && !c->opt_fixed && stream_batches && p.anyhit && (opt & iqpt::kOptAnyHit) &&
+                      p.pmask != nullptr && c->pmask_all && p.list != nullptr && spp > 0 && spp <= iqpt::kAccTableMax &&
+                      iqpt::anyhit_variant_exists(opt);
     // kOptBvhPrimary: decided by timing (see iqpt_ctx::tune_stage); its batch-free variants keep the
     // 5-wave bound the batched streamed variants drop
     const int prim_opt = (opt | iqpt::kOptBvhPrimary) |
                          (iqpt::render_variant_exists(c->max_depth, true, opt | iqpt::kOptBvhPrimary | iqpt::kOptLB5)
                               ? iqpt::kOptLB5 : 0);
     int tune_slot = -1;
-    if (!c->opt_fixed && stream_batches && p.bvh_nodes && p.cull && (opt & iqpt::kOptBvh) &&
+    if (!c->opt_fixed && !anyk && stream_batches && p.bvh_nodes && p.cull && (opt & iqpt::kOptBvh) &&
         iqpt::render_variant_exists(c->max_depth, true, prim_opt)) {
         if (c->tune_stage == iqpt::kTuneLaunches) {
             // per variant the fastest of its timed launches, per sample-pixel of work
@@ -2321,15 +2350,18 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             IQPT_HIP(hipEventRecord(c->ev_s2, c->stream2));
             IQPT_HIP(hipStreamWaitEvent(c->stream, c->ev_s2, 0));
         }
+    } else if (anyk) {
+        le = iqpt::launch_anyhit(c->stream, p, opt);
     } else {
         le = iqpt::launch_render(c->stream, p, grid, lds, stream_batches, opt);
     }
+    c->last_anyk = anyk;
     c->split_last = split;
     c->fan_last = fan_split || spec;
     c->spec_last = spec;
     c->last_ls = ls;
     c->last_ovl = ovl;
-    c->last_xcd_lists = (ovl || xcdq) && !spec && !split;
+    c->last_xcd_lists = (ovl || xcdq) && !spec && !split && !anyk;
     if (tune_slot >= 0) (void)hipEventRecord(c->tune_ev[2 * tune_slot + 1], c->stream);
     if (e1 && !e1_bound) (void)hipEventRecord(e1, ls);
     if (e0 && e1) c->timed.push_back({e0, e1, e1b});
@@ -2767,21 +2799,27 @@ int iqpt_debug_set_anyhit(iqpt_ctx* c, int on) {
     return IQPT_OK;
 }
 
-/* Internal (tests, A/B): per-pixel candidate masks over the streamed kernel's tile lists (1, the default) or the
- * whole list for every lane (0). Same bits either way. */
+/* Internal (tests, A/B): per-pixel candidate masks over the streamed kernel's tile lists: 2 (the default) with
+ * iqpt_anyhit_kernel for any-hit scenes whose every tile has them, 1 in the plain kernel only, 0 none (the whole
+ * list for every lane). Same bits either way. */
 int iqpt_debug_set_pixel_masks(iqpt_ctx* c, int on) {
     if (!c) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx is NULL");
     int st = enter(c);
     if (st) return st;
-    c->pmask_on = on != 0;
+    if (on < 0 || on > 2) return iqpt::fail(IQPT_ERR_INVALID_ARG, "pixel mask mode must be 0, 1 or 2");
+    c->pmask_mode = on;
     c->cull_valid = false;
     return IQPT_OK;
 }
 
-/* Internal (tests): tiles whose triangle lists have per-pixel masks (0: none built). */
-int iqpt_debug_pixel_mask_info(iqpt_ctx* c, uint32_t* tiles) {
-    if (!c || !tiles) return iqpt::fail(IQPT_ERR_INVALID_ARG, "ctx or tiles is NULL");
+/* Internal (tests, tools): tiles whose triangle lists have per-pixel masks (0: none built), whether every tile has
+ * them and no tile has a sphere candidate (iqpt_anyhit_kernel's condition besides an any-hit scene), and the longest
+ * triangle list (null: not wanted). */
+int iqpt_debug_pixel_mask_info(iqpt_ctx* c, uint32_t* tiles, int* all, uint32_t* list_max) {
+    if (!c || !tiles || !all) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
     *tiles = c->pmask_tiles;
+    *all = c->pmask_all ? 1 : 0;
+    if (list_max) *list_max = c->list_max;
     return IQPT_OK;
 }
 
@@ -3532,10 +3570,12 @@ int iqpt_debug_set_frame(iqpt_ctx* c, uint64_t frame) {
 
 /* Internal (tests): the kernel option set of the context's last render launch (-1 before any), with bit 30 set when
  * that launch dealt its tiles to per-XCD lists and queue words (overlapped launches; streamed launches,
- * iqpt_debug_set_stream_xcd): the kernels fall back to one queue silently otherwise. */
+ * iqpt_debug_set_stream_xcd): the kernels fall back to one queue silently otherwise; bit 29 when it ran
+ * iqpt_anyhit_kernel instead of the plain kernel (any-hit scenes with per-pixel masks on every tile). */
 int iqpt_debug_last_options(iqpt_ctx* c, int* opt) {
     if (!c || !opt) return iqpt::fail(IQPT_ERR_INVALID_ARG, "NULL argument");
-    *opt = c->last_opt < 0 ? c->last_opt : (c->last_opt | (c->last_xcd_lists ? (1 << 30) : 0));
+    *opt = c->last_opt < 0 ? c->last_opt
+                           : (c->last_opt | (c->last_xcd_lists ? (1 << 30) : 0) | (c->last_anyk ? (1 << 29) : 0));
     return IQPT_OK;
 }
 

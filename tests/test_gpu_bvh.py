@@ -224,6 +224,9 @@ def test_stream_xcd_tile_lists(require_gpu, preset, w, h, ps_args, launches, mod
     lb = _lib.load()
     lb.iqpt_debug_set_stream_xcd.argtypes = [C.c_void_p, C.c_int]
     _lib.check(lb.iqpt_debug_set_stream_xcd(pt._h, mode), "iqpt_debug_set_stream_xcd")
+    # (the plain kernel's lists: C4's any-hit scene would otherwise take iqpt_anyhit_kernel, which has no queue)
+    lb.iqpt_debug_set_pixel_masks.argtypes = [C.c_void_p, C.c_int]
+    _lib.check(lb.iqpt_debug_set_pixel_masks(pt._h, 1), "iqpt_debug_set_pixel_masks")
     pt.set_camera(cam)
     pt.upload_packet(pk)
     fr = oracle.OracleFrame(w, h, pixels=ps, max_depth=8)

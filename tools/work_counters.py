@@ -62,7 +62,9 @@ def main():
         pt.render(spp)
     o = C.c_int()
     _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(o)), "last options")
-    prod_opt = o.value & ~(1 << 30)                  # (bit 30: per-XCD tile lists, not an option)
+    # (bit 30: per-XCD tile lists, bit 29: iqpt_anyhit_kernel, not options; the instrumented plain kernel runs the
+    # same per-pixel candidate walk, so its test counts are the any-hit kernel's)
+    prod_opt = o.value & ~((1 << 30) | (1 << 29))
     pt.close()
     # 2) the stats build of that option set (the 5-wave bound is not part of the algorithm)
     stats_opt = prod_opt | K_STATS
