@@ -757,13 +757,19 @@ __device__ __forceinline__ void test_triangle_pair2(const float4 q0, const float
     const f2 pya = ra.dz * e2x - ra.dx * e2z, pyb = rb.dz * e2x - rb.dx * e2z;
     const f2 pza = ra.dx * e2y - ra.dy * e2x, pzb = rb.dx * e2y - rb.dy * e2x;
     const f2 deta = (e1x * pxa + e1y * pya) + e1z * pza, detb = (e1x * pxb + e1y * pyb) + e1z * pzb;
+    // T = O - v0 ahead of the determinant test, held there (the empty asm): the pair's v0 and edge records are
+    // read from LDS together, one wait instead of a second one after the test (the test rarely rejects a wall)
+    f2 txa = ra.ox - v0x, tya = ra.oy - v0y, tza = ra.oz - v0z;
+    f2 txb = rb.ox - v0x, tyb = rb.oy - v0y, tzb = rb.oz - v0z;
+#ifndef IQPT_PAIR2_PIN
+#define IQPT_PAIR2_PIN 1
+#endif
+    if (IQPT_PAIR2_PIN) asm volatile("" : "+v"(txa), "+v"(tya), "+v"(tza), "+v"(txb), "+v"(tyb), "+v"(tzb));
     bool a0 = ta && !(iq_fabsf(deta.x) < 0.000001f), a1 = ta && second && !(iq_fabsf(deta.y) < 0.000001f);
     bool b0 = tb && !(iq_fabsf(detb.x) < 0.000001f), b1 = tb && second && !(iq_fabsf(detb.y) < 0.000001f);
     if (!(a0 || a1 || b0 || b1)) return;
     const f2 inva = {rcp_scene<OPT>(deta.x), rcp_scene<OPT>(deta.y)};
     const f2 invb = {rcp_scene<OPT>(detb.x), rcp_scene<OPT>(detb.y)};
-    const f2 txa = ra.ox - v0x, tya = ra.oy - v0y, tza = ra.oz - v0z;
-    const f2 txb = rb.ox - v0x, tyb = rb.oy - v0y, tzb = rb.oz - v0z;
     const f2 ua = ((txa * pxa + tya * pya) + tza * pza) * inva, ub = ((txb * pxb + tyb * pyb) + tzb * pzb) * invb;
     a0 = a0 && !(ua.x < 0.0f || ua.x > 1.0f);
     a1 = a1 && !(ua.y < 0.0f || ua.y > 1.0f);
