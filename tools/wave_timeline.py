@@ -25,6 +25,8 @@ from iqpt.scene import CONFIGS, Scene, make_camera  # noqa: E402
 K_STATS, K_PIPE, K_OVERLAP, K_CAMAXIS, K_PRIO = 1 << 7, 1 << 21, 1 << 19, 1 << 14, 1 << 17
 
 ap = argparse.ArgumentParser()
+ap.add_argument("--config", default="c2")
+ap.add_argument("--spp", type=int, default=0, help="samples per launch (default: the config's)")
 ap.add_argument("--two-ray", type=int, default=1)
 ap.add_argument("--overlap", type=int, default=1)
 ap.add_argument("--crop", default="", help="x0,x1,y0,rows: a pixel set instead of the full frame")
@@ -38,7 +40,8 @@ lb.iqpt_debug_set_kernel_options.argtypes = [C.c_void_p, C.c_int]
 lb.iqpt_debug_default_options.restype = C.c_int
 lb.iqpt_debug_read_stats.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong)]
 lb.iqpt_debug_read_wave_times.argtypes = [C.c_void_p, C.POINTER(C.c_ulonglong), C.c_uint32, C.POINTER(C.c_uint32)]
-cfg = CONFIGS["c2"]
+cfg = CONFIGS[args.config]
+spp = args.spp or cfg.spp
 sc = Scene()
 sc.add_preset(cfg.preset)
 pk = sc.build_packet()
@@ -50,18 +53,27 @@ if args.crop:
 pt = iqpt.PathTracer(cfg.width, cfg.height, pixels=ps, max_depth=cfg.max_depth)
 pt.set_split(_lib.SPLIT_OFF)
 pt.set_overlap(_lib.OVERLAP_AUTO if args.overlap else _lib.OVERLAP_OFF)
-opt = lb.iqpt_debug_default_options() | K_PRIO | K_STATS | (K_PIPE if args.two_ray else 0)
-if args.overlap:
-    opt |= K_OVERLAP | K_CAMAXIS        # the production overlapped form (its stats variants are built)
-_lib.check(lb.iqpt_debug_set_kernel_options(pt._h, opt), "kernel options")
 pt.set_camera(cam)
 pt.upload_packet(pk)
+if args.config == "c2":
+    opt = lb.iqpt_debug_default_options() | K_PRIO | K_STATS | (K_PIPE if args.two_ray else 0)
+    if args.overlap:
+        opt |= K_OVERLAP | K_CAMAXIS        # the production overlapped form (its stats variants are built)
+else:
+    # other configs: the production launch's own option set (its first launches tune the camera-ray path), + stats
+    lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+    for _ in range(6):
+        pt.render(spp)
+    o = C.c_int(0)
+    _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(o)), "last options")
+    opt = (o.value & ~((1 << 30) | (1 << 29))) | K_STATS
+_lib.check(lb.iqpt_debug_set_kernel_options(pt._h, opt), "kernel options")
 for _ in range(args.warm):
-    pt.render(cfg.spp)
+    pt.render(spp)
 pt.sync()
 s = (C.c_ulonglong * 24)()
 lb.iqpt_debug_read_stats(pt._h, s)                  # clears the counters and the wave slots
-pt.render(cfg.spp)
+pt.render(spp)
 pt.sync()
 cap = 1 << 16
 wt = (C.c_ulonglong * (3 * cap))()
@@ -90,7 +102,7 @@ def pct(x):
 
 order = np.argsort(-iters)
 top = order[:max(1, int(0.05 * busy.sum()))]           # the longest 5 % of the waves: the chains that set the launch
-res = {"two_ray": args.two_ray, "overlap": args.overlap, "crop": args.crop or None, "options": hex(opt),
+res = {"config": args.config, "spp": spp, "two_ray": args.two_ray, "overlap": args.overlap, "crop": args.crop or None, "options": hex(opt),
        "kernel_ms": round(t / max(k, 1), 4), "waves": int(busy.sum()),
        "launch_iterations": v[0], "active_lanes_per_iteration": round(v[1] / max(v[0], 1), 2),
        "exec_population": round(v[1] / max(v[0], 1) / 64.0, 3),
