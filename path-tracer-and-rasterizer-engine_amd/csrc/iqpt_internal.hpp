@@ -105,6 +105,10 @@ struct kparams {
     // wave-uniform list loop). null = none
     const uint32_t* pmask;
     const uint32_t* pmask_off;
+    // per tile (2 words): the pixels one of whose tile's candidate triangles accepts every camera ray of the pixel
+    // (iq_interval.h tri_certain), for iqpt_anyhit_kernel (any-hit scenes: such a pixel ends every sample on its
+    // camera ray with the emissive colour)
+    const uint32_t* pmask_certain;
     // kOptMaterials (packet material table): material index per triangle / sphere, the material
     // records (2 x float4 each: (albedo.rgb, type bits), (strength | sigma, A, B, 0)) and the
     // triangle shading records (kTriShadeFloat4 per triangle)
@@ -394,7 +398,7 @@ int launch_tile_list(void* stream, const uint32_t* cull, uint32_t ntiles, uint32
 // (any order gives the same bits there; the candidate-list loop leaves sooner)
 int launch_tile_list_order(void* stream, const kbin& b, const uint32_t* off_tri, uint32_t* list);
 int launch_pixel_mask(void* stream, const kbin& b, const uint32_t* off_tri, const uint32_t* list,
-                      const uint32_t* pmask_off, uint32_t* pmask);
+                      const uint32_t* pmask_off, uint32_t* pmask, uint32_t* certain);
 // Device probe of the camera transforms (iqpt_debug_camera_rays): general and kOptCamAxis forms.
 int launch_camera_probe(void* stream, const kparams& p, const float* ndc, float* gen, float* axis, uint32_t n,
                         bool do_axis);

@@ -2803,12 +2803,21 @@ __global__ __launch_bounds__(64) void iqpt_tile_list_order_kernel(const kbin b, 
 // reject both triangles of list entry 32 w + e for every camera ray of the pixel (tri_culled, the tests the tile
 // masks are built with). Skipping a cleared entry changes no result: the entry is rejected by that ray anyway, and
 // the set entries keep the list's order. Tiles with more than kPixMaskMax entries are left without masks; a tile's
-// words start at pmask_off[t] (64 per 32 entries, compact over the tiles).
+// words start at pmask_off[t] (64 per 32 entries, compact over the tiles). Also per pixel: whether one of its
+// candidates accepts every camera ray of the pixel (tri_certain; certain[2 t], certain[2 t + 1]: the tile's 64-bit
+// mask), for iqpt_anyhit_kernel.
 __global__ __launch_bounds__(64) void iqpt_pixel_mask_kernel(const kbin b, const uint32_t* off_tri, const uint32_t* list,
-                                                             const uint32_t* pmask_off, uint32_t* pmask) {
+                                                             const uint32_t* pmask_off, uint32_t* pmask,
+                                                             uint32_t* certain) {
     const uint32_t t = blockIdx.x, lane = threadIdx.x;
     const uint32_t a = off_tri[t], n = off_tri[t + 1] - a;
-    if (n > kPixMaskMax) return;
+    if (n > kPixMaskMax) {
+        if (lane == 0) {
+            certain[2 * (size_t)t] = 0u;
+            certain[2 * (size_t)t + 1] = 0u;
+        }
+        return;
+    }
     const uint32_t tx = t % b.ntx, ty = t / b.ntx;
     const uint32_t tw = min(kCullTile, b.ncols - tx * kCullTile), th = min(kCullTile, b.nrows - ty * kCullTile);
     const bool inside = lane < tw * th;
@@ -2829,6 +2838,7 @@ __global__ __launch_bounds__(64) void iqpt_pixel_mask_kernel(const kbin b, const
         bd = iqiv::camera_bundle(ci, x, x, y, y);
     }
     uint32_t* out = pmask + pmask_off[t] + lane;
+    bool sure = false;
     for (uint32_t w = 0; w * 32u < n; ++w) {
         uint32_t bits = 0u;
         for (uint32_t i = 0; i < 32u && inside; ++i) {
@@ -2844,10 +2854,16 @@ __global__ __launch_bounds__(64) void iqpt_pixel_mask_kernel(const kbin b, const
                 const float e1[3] = {tr[0].w, tr[1].x, tr[1].y};
                 const float e2[3] = {tr[1].z, tr[1].w, tr[2].x};
                 culled = iqiv::tri_culled(bd, v0, e1, e2);
+                if (!culled && !sure) sure = iqiv::tri_certain(bd, v0, e1, e2);
             }
             if (!culled) bits |= 1u << i;
         }
         out[(size_t)w * 64u] = bits;
+    }
+    const uint64_t sm = __ballot(sure);
+    if (lane == 0) {
+        certain[2 * (size_t)t] = (uint32_t)sm;
+        certain[2 * (size_t)t + 1] = (uint32_t)(sm >> 32);
     }
 }
 
@@ -3834,6 +3850,10 @@ __global__ __launch_bounds__(kSkyBlock) void iqpt_sky_kernel(const kparams p, co
 // operations for these paths — camera ray, tests, clamp, running mean with the launch table — so the same bits,
 // without its queue, refill, batches and path bookkeeping, and with no pixel waiting on another tile's list.
 constexpr uint32_t kAnyBlock = 256;
+#ifndef IQPT_ANY_BATCH
+#define IQPT_ANY_BATCH 2
+#endif
+constexpr uint32_t kAnyBatch = IQPT_ANY_BATCH;          // samples traced together per lane
 
 template <int OPT>
 __global__ __launch_bounds__(kAnyBlock) void iqpt_anyhit_kernel(const kparams p) {
@@ -3866,50 +3886,88 @@ __global__ __launch_bounds__(kAnyBlock) void iqpt_anyhit_kernel(const kparams p)
                    p.rng[3 * (size_t)p.npix + pix], p.rng[4 * (size_t)p.npix + pix], p.rng[5 * (size_t)p.npix + pix]};
         const float4 a0 = reinterpret_cast<const float4*>(p.lin)[pix];
         float ax = a0.x, ay = a0.y, az = a0.z;
+        // a certain pixel: every sample takes the camera's two draws and ends on a triangle, colour (1, 1, 1), whose
+        // mean term c / n is the table's RN(1 / n) (the plain kernel's certain fold)
+        const bool sure = (p.pmask_certain[2 * (size_t)t + lane / 32u] >> (lane % 32u)) & 1u;
+        const uint32_t nk = sure ? 0u : p.spp;
+        if (sure) {
+            xorwow_skip_v(st.v0, st.v1, st.v2, st.v3, st.v4, 2u * p.spp);
+            st.d += 2u * p.spp * IQ_XORWOW_WEYL;
+            for (uint32_t k = 0; k < p.spp; ++k) {
+                const float2 tv = tab[k];
+                ax = tv.x + ax * tv.y;
+                ay = tv.x + ay * tv.y;
+                az = tv.x + az * tv.y;
+            }
+        }
         constexpr uint32_t kW = kAnyMaxEntries / 32u;
         uint32_t wm[kW];
         const uint32_t* pm = p.pmask + p.pmask_off[t] + lane;
 #pragma unroll
         for (uint32_t w = 0; w < kW; ++w) wm[w] = w * 32u < n ? pm[(size_t)w * 64u] : 0u;
         const float4* __restrict__ gp = reinterpret_cast<const float4*>(p.tri_pairs);
-        for (uint32_t k = 0; k < p.spp; ++k) {
-            ray3 ray;
-            camera_ray<OPT>(p, px, py, st, ray);
-            float closest = kTMax;
-            int kind = kHitNone;
-            uint32_t hidx = 0;
+        // kAnyBatch samples at a time: a sample's draws are its camera's two, whatever it meets, so the batch's rays
+        // are made in sample order up front; each candidate pair is loaded once for the batch and tested against
+        // every ray of it not yet accepted (the rays' own operations, so the same bits); the colours fold in order
+        for (uint32_t k0 = 0; k0 < nk; k0 += kAnyBatch) {
+            ray3 rs[kAnyBatch];
+            float cl[kAnyBatch];
+            int kd[kAnyBatch];
+            uint32_t live = 0u;                                  // bit r: ray r not yet accepted
+#pragma unroll
+            for (uint32_t r = 0; r < kAnyBatch; ++r) {
+                cl[r] = kTMax;
+                kd[r] = kHitNone;
+                if (k0 + r < nk) {
+                    camera_ray<OPT>(p, px, py, st, rs[r]);
+                    live |= 1u << r;
+                } else {
+                    rs[r] = rs[0];
+                }
+            }
 #pragma unroll
             for (uint32_t w = 0; w < kW; ++w) {
                 uint32_t m = wm[w];
-                while (m != 0u && kind != kHitTri) {
+                while (m != 0u && live != 0u) {
                     const uint32_t j = wl[w * 32u + (uint32_t)__builtin_ctz(m)];
                     m &= m - 1u;
                     const float4* qq = gp + (size_t)j * kTriPairFloat4;
-                    test_triangle_pair<OPT>(qq[0], qq[1], qq[2], qq[3], qq[4], ray, closest, kind, hidx, 2 * j,
-                                            2 * j + 1 < p.ntri);
+                    const float4 q0 = qq[0], q1 = qq[1], q2 = qq[2], q3 = qq[3], q4 = qq[4];
+#pragma unroll
+                    for (uint32_t r = 0; r < kAnyBatch; ++r)
+                        if ((live >> r) & 1u) {
+                            uint32_t hidx = 0;
+                            test_triangle_pair<OPT>(q0, q1, q2, q3, q4, rs[r], cl[r], kd[r], hidx, 2 * j,
+                                                    2 * j + 1 < p.ntri);
+                            if (kd[r] == kHitTri) live &= ~(1u << r);
+                        }
                 }
             }
-            float cx, cy, cz;
-            if (kind == kHitTri) {
-                cx = 1.0f;                                       // emissive (1, 10): 10 clamped (:345-347)
-                cy = 1.0f;
-                cz = 1.0f;
-            } else {
-                const float a = (ray.dy + 1.0f) * 0.5f;          // sky gradient (:308-313)
-                const float one_a = 1.0f - a;
-                cx = one_a + a * 0.5f;
-                cy = one_a + a * 0.7f;
-                cz = one_a + a * 1.0f;
-                cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
-                cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
-                cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+#pragma unroll
+            for (uint32_t r = 0; r < kAnyBatch; ++r) {
+                if (k0 + r >= nk) break;
+                float cx, cy, cz;
+                if (kd[r] == kHitTri) {
+                    cx = 1.0f;                                   // emissive (1, 10): 10 clamped (:345-347)
+                    cy = 1.0f;
+                    cz = 1.0f;
+                } else {
+                    const float a = (rs[r].dy + 1.0f) * 0.5f;    // sky gradient (:308-313)
+                    const float one_a = 1.0f - a;
+                    cx = one_a + a * 0.5f;
+                    cy = one_a + a * 0.7f;
+                    cz = one_a + a * 1.0f;
+                    cx = cx > 1.0f ? 1.0f : (cx < 0.0f ? 0.0f : cx);
+                    cy = cy > 1.0f ? 1.0f : (cy < 0.0f ? 0.0f : cy);
+                    cz = cz > 1.0f ? 1.0f : (cz < 0.0f ? 0.0f : cz);
+                }
+                const float2 tv = tab[k0 + r];
+                float qx, qy, qz;
+                mean_terms<OPT>(0.0f + cx, 0.0f + cy, 0.0f + cz, tab_n[k0 + r], tv.x, p.mean_tiny, qx, qy, qz);
+                ax = qx + ax * tv.y;
+                ay = qy + ay * tv.y;
+                az = qz + az * tv.y;
             }
-            const float2 tv = tab[k];
-            float qx, qy, qz;
-            mean_terms<OPT>(0.0f + cx, 0.0f + cy, 0.0f + cz, tab_n[k], tv.x, p.mean_tiny, qx, qy, qz);
-            ax = qx + ax * tv.y;
-            ay = qy + ay * tv.y;
-            az = qz + az * tv.y;
         }
         const uint32_t r8 = to_u8(255.0f * iq_sqrtf(ax));
         const uint32_t g8 = to_u8(255.0f * iq_sqrtf(ay));
@@ -4138,11 +4196,11 @@ int launch_tile_list_order(void* stream, const kbin& b, const uint32_t* off_tri,
 }
 
 int launch_pixel_mask(void* stream, const kbin& b, const uint32_t* off_tri, const uint32_t* list,
-                      const uint32_t* pmask_off, uint32_t* pmask) {
+                      const uint32_t* pmask_off, uint32_t* pmask, uint32_t* certain) {
     const uint32_t ntiles = b.ntx * b.nty;
     if (ntiles == 0) return 0;
     hipLaunchKernelGGL(iqpt_pixel_mask_kernel, dim3(ntiles), dim3(64), 0, (hipStream_t)stream, b, off_tri, list,
-                       pmask_off, pmask);
+                       pmask_off, pmask, certain);
     return (int)hipGetLastError();
 }
 
@@ -4298,7 +4356,8 @@ bool anyhit_variant_exists(int opt) { return find_anyhit(opt) != nullptr; }
 
 int launch_anyhit(void* stream, const kparams& p, int opt) {
     const anyhit_variant* v = find_anyhit(opt);
-    if (!v || p.spp > kAccTableMax || !p.list || !p.list_off_tri || !p.pmask || !p.pmask_off || !p.anyhit)
+    if (!v || p.spp > kAccTableMax || !p.list || !p.list_off_tri || !p.pmask || !p.pmask_off || !p.pmask_certain ||
+        !p.anyhit)
         return (int)hipErrorInvalidDeviceFunction;
     if (p.ntiles == 0 || p.spp == 0) return 0;
     return v->launch((hipStream_t)stream, p,

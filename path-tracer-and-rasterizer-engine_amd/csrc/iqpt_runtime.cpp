@@ -145,9 +145,11 @@ struct iqpt_ctx {
     uint32_t* d_tile_order = nullptr;   // work-queue order over tiles, built with the masks
     uint32_t* d_list = nullptr;         // candidate lists of the masks, then their offsets (tri, sph)
     uint64_t list_total = 0;
-    uint32_t* d_pmask = nullptr;        // per-tile word offsets (ntiles + 1), then the per-pixel candidate masks (kparams::pmask)
+    uint32_t* d_pmask = nullptr;        // per-tile word offsets (ntiles + 1), the per-pixel candidate masks (kparams::pmask),
+                                        // then 2 words per tile of certain pixels (kparams::pmask_certain)
     int pmask_mode = 2;                 // iqpt_debug_set_pixel_masks: 0 none, 1 in the plain kernel, 2 + iqpt_anyhit_kernel
     uint32_t pmask_tiles = 0;           // tiles with masks (a triangle list of 1 .. kPixMaskMax entries)
+    uint64_t pmask_words = 0;           // mask words after the offsets
     bool pmask_all = false;             // every list within kAnyMaxEntries and no tile with a sphere candidate
     uint32_t list_max = 0;              // the longest triangle list
     bool last_anyk = false;             // the last launch ran iqpt_anyhit_kernel
@@ -842,15 +844,18 @@ int build_cull(iqpt_ctx* c) {
             pm_off[ntiles] = (uint32_t)pm_words;
             const bool fits = (uint64_t)ntiles + 1 + pm_words < 0xffffffffull;
             if (c->pmask_mode != 0 && fits &&
-                hipMalloc(&c->d_pmask, ((size_t)ntiles + 1 + pm_words) * sizeof(uint32_t)) == hipSuccess &&
+                hipMalloc(&c->d_pmask, ((size_t)ntiles + 1 + pm_words + 2 * (size_t)ntiles) * sizeof(uint32_t)) ==
+                    hipSuccess &&
                 !(hipMemcpyAsync(c->d_pmask, pm_off.data(), pm_off.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
                                  c->stream) == hipSuccess &&
-                  iqpt::launch_pixel_mask(c->stream, b, d_off, c->d_list, c->d_pmask, c->d_pmask + ntiles + 1) == 0 &&
+                  iqpt::launch_pixel_mask(c->stream, b, d_off, c->d_list, c->d_pmask, c->d_pmask + ntiles + 1,
+                                          c->d_pmask + ntiles + 1 + pm_words) == 0 &&
                   hipStreamSynchronize(c->stream) == hipSuccess)) {
                 (void)hipFree(c->d_pmask);
                 c->d_pmask = nullptr;
             }
             if (c->d_pmask) {
+                c->pmask_words = pm_words;
                 c->pmask_all = true;
                 for (uint32_t t = 0; t < ntiles; ++t) {
                     c->list_max = std::max(c->list_max, cnt[t]);
@@ -1769,8 +1774,10 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
             p.list_off_tri = c->d_list + c->list_total;
             p.list_off_sph = p.list_off_tri + (c->cull_ntx * c->cull_nty + 1);
             if (c->d_pmask) {
+                const uint32_t nt = c->cull_ntx * c->cull_nty;
                 p.pmask_off = c->d_pmask;
-                p.pmask = c->d_pmask + (c->cull_ntx * c->cull_nty + 1);
+                p.pmask = c->d_pmask + (nt + 1);
+                p.pmask_certain = c->d_pmask + (nt + 1) + c->pmask_words;
             }
         }
     }
