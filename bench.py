@@ -122,6 +122,8 @@ def parse():
                          "dealt to the XCDs, 2 bands of tile rows dealt to the XCDs, 3 the default: 1 up to 4 spp per launch)")
     ap.add_argument("--resident-refill", type=int, default=None,
                     help="A/B: idle lanes before a resident-scene wave takes new pixels (iqpt_debug_set_resident_refill)")
+    ap.add_argument("--spec-margin", type=int, default=None,
+                    help="A/B: spec windows' margin, 1 / this of the extra slots (iqpt_debug_set_spec; default 16)")
     ap.add_argument("--spec-parity", type=float, default=None,
                     help="A/B: spec parity pixels' threshold in slots per sample (iqpt_debug_set_spec_parity; 0 = every "
                          "slot traced, the round-4 kernel; default: the library's 1.875)")
@@ -580,6 +582,11 @@ def main():
         lb = _lib.load()
         lb.iqpt_debug_set_resident_refill.argtypes = [C.c_void_p, C.c_uint32]
         _lib.check(lb.iqpt_debug_set_resident_refill(pt._h, args.resident_refill), "iqpt_debug_set_resident_refill")
+    if args.spec_margin is not None:
+        import ctypes as C
+        lb = _lib.load()
+        lb.iqpt_debug_set_spec.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32]
+        _lib.check(lb.iqpt_debug_set_spec(pt._h, 0, args.spec_margin), "iqpt_debug_set_spec")
     if args.spec_parity is not None:
         import ctypes as C
         lb = _lib.load()
@@ -819,6 +826,7 @@ def main():
                        "xcd_tile_lists": xcd_lists,
                        **({"kernel_options": args.kernel_options} if args.kernel_options else {}),
                        **({"spec_parity": args.spec_parity} if args.spec_parity is not None else {}),
+                       **({"spec_margin": args.spec_margin} if args.spec_margin is not None else {}),
                        **({"anyhit": args.anyhit} if args.anyhit is not None else {}),
                        **({"pixel_masks": args.pixel_masks} if args.pixel_masks is not None else {}),
                        **({"stream_refill": args.stream_refill} if args.stream_refill is not None else {}),
