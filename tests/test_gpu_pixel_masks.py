@@ -64,11 +64,12 @@ def check_oracle(out, scene, cam, w, h, ps, launches, depth=8):
 
 
 @pytest.mark.parametrize("mode,anyhit", [(2, 1), (1, 1), (2, 0)])
-@pytest.mark.parametrize("y0,ystep,rows,every", [(150, 97, 9, None), (180, 1, 24, True), (520, 1, 16, True)])
+@pytest.mark.parametrize("y0,ystep,rows,every", [(150, 97, 9, None), (180, 1, 24, True), (520, 1, 16, True),
+                                                  (500, 3, 16, None)])
 def test_bands_match_oracle(require_gpu, mode, anyhit, y0, ystep, rows, every):
     """Full-width bands through the ball's silhouettes: rows 97 apart (tiles of owned rows span the frame: long
-    lists) and contiguous bands through the upper cap and the middle (every tile masked: iqpt_anyhit_kernel in
-    mode 2); launches of 2 and 1 samples."""
+    lists), contiguous bands through the upper cap and the middle (every tile masked: iqpt_anyhit_kernel in
+    mode 2) and every third row (a 3-way row split's share); launches of 2 and 1 samples."""
     w, h = 1920, 1080
     ps = pixel_set(w, h, 0, w, y0, ystep, rows)
     launches = [2, 1]

@@ -1,14 +1,18 @@
-# r06 run 27: the final tree's C3 share steps with the library's gather (N = 8 / 4 / 2, x2), C5 at 1 spp per step
+# r06 run 28: pixel-mask tests with a 3-way row share (every third row)
 mkdir -p gpurun_out
 O=gpurun_out
-R=r06_27
+R=r06_28
 export TMPDIR=/tmp
-pr() { python3 -c "import json,sys; d=json.loads(open('$1').read().strip().splitlines()[-1]); r=d['roofline']; print('$2', d['value'], d['ms_per_step'], r.get('kernel_avg_ms'), d['bitexact_frac_vs_oracle'], d['config'].get('launch_mode'))"; }
-for i in 1 2; do
-for s in 8 4 2; do
-timeout -k 10 200 python3 bench.py --no-cpu-baseline --steps 20 --warmup 5 --share-of $s --self-gather > $O/${R}_s${s}g_$i.json 2> $O/${R}_e.err || { tail -20 $O/${R}_e.err; exit 1; }
-pr $O/${R}_s${s}g_$i.json s${s}g_$i
-done
-done
-timeout -k 10 200 python3 bench.py --config c5 --spp 1 --steps 10 --no-cpu-baseline > $O/${R}_c5s1.json 2> $O/${R}_e.err || { tail -20 $O/${R}_e.err; exit 1; }
-pr $O/${R}_c5s1.json c5_spp1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_pixel_masks.py -m gpu -v --timeout 300 --timeout-method thread > $O/${R}_tests.log 2>&1 || { tail -40 $O/${R}_tests.log; exit 1; }
+grep -c PASSED $O/${R}_tests.log; tail -1 $O/${R}_tests.log
+timeout -k 10 120 python3 - <<'PY'
+import sys, ctypes as C
+sys.path.insert(0, "path-tracer-and-rasterizer-engine_amd")
+from iqpt import PathTracer, Scene, _lib, make_camera, pixel_set
+sc = Scene(); sc.add_preset("mesh10k"); pk = sc.build_packet()
+pt = PathTracer(1920, 1080, pixels=pixel_set(1920, 1080, 0, 1920, 500, 3, 16), max_depth=8)
+pt.set_camera(make_camera(1920, 1080)); pt.upload_packet(pk); pt.render(2); pt.sync()
+lb = _lib.load(); lb.iqpt_debug_last_options.argtypes = [C.c_void_p, C.POINTER(C.c_int)]
+o = C.c_int(0); _lib.check(lb.iqpt_debug_last_options(pt._h, C.byref(o)), "last")
+print("ystep 3 band: iqpt_anyhit_kernel", bool(o.value & (1 << 29)))
+PY
