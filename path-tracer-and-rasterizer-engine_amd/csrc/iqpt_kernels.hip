@@ -4043,6 +4043,9 @@ const variant kVariants[] = {
                      IQPT_V(16, true, (O) & ~kOptLB5), IQPT_V(8, true, (O) | kOptBvhPrimary), \
                      IQPT_V(16, true, (O) | kOptBvhPrimary)
     IQPT_PROD(kOptDefault),
+    // BVH-primary at 4 waves per SIMD (128 VGPRs, no spills): the runtime's choice above 4 samples per launch
+    // (C5 16 spp -5 %, 1 spp +7 % against the 5-wave form, r06 run 36)
+    IQPT_V(8, true, (kOptDefault | kOptBvhPrimary) & ~kOptLB5), IQPT_V(16, true, (kOptDefault | kOptBvhPrimary) & ~kOptLB5),
     // streamed any-hit scenes (kOptAnyHit: no sphere, reference materials; C4): the first accepted triangle ends
     // a ray's traversal. Variants of their own: the exits cost the other streamed scenes registers (C5 58.6-60.3
     // against 56.6-56.7 ms per launch with them compiled in, r05 run 16)

@@ -1794,10 +1794,16 @@ int render_launch(iqpt_ctx* c, uint32_t spp) {
     const bool anyk = c->pmask_mode == 2 && !c->opt_fixed && stream_batches && p.anyhit && (opt & iqpt::kOptAnyHit) &&
                       p.pmask != nullptr && c->pmask_all && p.list != nullptr && spp > 0 && spp <= iqpt::kAccTableMax &&
                       iqpt::anyhit_variant_exists(opt);
-    // kOptBvhPrimary: decided by timing (see iqpt_ctx::tune_stage); its batch-free variants keep the
-    // 5-wave bound the batched streamed variants drop
-    const int prim_opt = (opt | iqpt::kOptBvhPrimary) |
-                         (iqpt::render_variant_exists(c->max_depth, true, opt | iqpt::kOptBvhPrimary | iqpt::kOptLB5)
+    // kOptBvhPrimary: decided by timing (see iqpt_ctx::tune_stage). Its batch-free variants keep the 5-wave bound
+    // the batched streamed variants drop for launches of up to kPrimaryLB5MaxSpp samples, and run at 4 waves
+    // per SIMD (no spills) above that where that variant is built: C5 16 spp 54.0-54.3 -> 51.5 ms, 1 spp 3.17 ->
+    // 3.39 ms (r06 run 36)
+    constexpr uint32_t kPrimaryLB5MaxSpp = 4;
+    const bool prim_lb5 = spp <= kPrimaryLB5MaxSpp ||
+                          !iqpt::render_variant_exists(c->max_depth, true, (opt | iqpt::kOptBvhPrimary) & ~iqpt::kOptLB5);
+    const int prim_opt = ((opt | iqpt::kOptBvhPrimary) & ~iqpt::kOptLB5) |
+                         (prim_lb5 && iqpt::render_variant_exists(c->max_depth, true,
+                                                                  opt | iqpt::kOptBvhPrimary | iqpt::kOptLB5)
                               ? iqpt::kOptLB5 : 0);
     int tune_slot = -1;
     if (!c->opt_fixed && !anyk && stream_batches && p.bvh_nodes && p.cull && (opt & iqpt::kOptBvh) &&

@@ -1,8 +1,8 @@
-# r06 run 22: PMC traffic and instruction mixes of the final kernels (kernel_sha16 997f65c619e1d78a): C2, the share-8
+# r06 run 38: PMC traffic and instruction mixes of the final kernels (kernel_sha16 3a8d33396bae8753): C2, the share-8
 # step, C4 (iqpt_anyhit_kernel), C5
 mkdir -p gpurun_out
 O=gpurun_out
-R=r06_22
+R=r06_38
 export TMPDIR=/tmp
 pmc() {  # name, counters, bench args
   timeout -s KILL 150 rocprofv3 --pmc $2 --kernel-trace --output-format csv -d $O/${R}_$1 -o run -- $B $3 > $O/${R}_$1.log 2>&1 || { tail -20 $O/${R}_$1.log; exit 1; }
