@@ -48,9 +48,12 @@ STREAMED_CONFIGS = ("c4", "c5")  # scenes past the LDS: the first kTuneLaunches 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100,
+                    help="timed steps (default 100: the timed region starts and ends with an idle GPU, and the "
+                         "overlapped launches' fill and drain — about one launch less one step — is spread over K "
+                         "steps: C2 0.884 ms per step at K = 20, 0.848-0.859 at K = 40, tools/RUNS.md r06 run 42)")
     ap.add_argument("--warmup", type=int, default=None,
-                    help="untimed steps (default 3; 5 for the streamed configs c4 / c5, whose first 4 launches time "
+                    help="untimed steps (default 10; 5 for the streamed configs c4 / c5, whose first 4 launches time "
                          "both camera-ray paths, DESIGN.md §3.5)")
     ap.add_argument("--config", default="c2")
     ap.add_argument("--spp", type=int, default=0,
@@ -131,7 +134,7 @@ def parse():
                     help="sample-parallel chains (iqpt_set_split, DESIGN.md §3.7)")
     args = ap.parse_args()
     if args.warmup is None:
-        args.warmup = 5 if args.config in STREAMED_CONFIGS else 3
+        args.warmup = 5 if args.config in STREAMED_CONFIGS else 10
     return args
 
 
