@@ -1,9 +1,14 @@
-# r06 run 38: PMC traffic and instruction mixes of the final kernels (kernel_sha16 3a8d33396bae8753): C2, the share-8
-# step, C4 (iqpt_anyhit_kernel), C5
+# r06 run 49: executed-work counts, PMC traffic and instruction mixes of the final kernels (the sky kernel in one-tile
+# blocks): C2, the share-8 step, C4 (iqpt_anyhit_kernel), C5
 mkdir -p gpurun_out
 O=gpurun_out
-R=r06_38
+R=r06_49
 export TMPDIR=/tmp
+for c in c2 c4 c5; do
+S=""; [ $c = c5 ] && S="--spp 16"; [ $c = c4 ] && S="--spp 16"
+timeout -k 10 300 python3 tools/work_counters.py --config $c $S --out $O/work_${c}_r06.json > $O/${R}_work_$c.log 2>&1 || { tail -20 $O/${R}_work_$c.log; exit 1; }
+python3 -c "import json; d=json.load(open('$O/work_${c}_r06.json')); print('$c', d['kernel_sha16'], d['per_ray'], d['flops_per_ray'])"
+done
 pmc() {  # name, counters, bench args
   timeout -s KILL 150 rocprofv3 --pmc $2 --kernel-trace --output-format csv -d $O/${R}_$1 -o run -- $B $3 > $O/${R}_$1.log 2>&1 || { tail -20 $O/${R}_$1.log; exit 1; }
   echo "pmc $1 done"
